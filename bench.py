@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""Self-play throughput bench (BASELINE.json metric: MCTS node-expansions/s/GPU @400 sims;
+self-play games/s at 1/2/4/8 GPUs).
+
+One "step" = one self-play ply in every game slot = `games` searches of `sims` simulations
+(select -> fused ResNet leaf evaluation -> expand/backup, each simulation one NN evaluation,
+SURVEY.md 8d) + the move/record/deal kernel. Inputs (decks, trees, weights) are resident in
+HBM before the timed region. Multi-GPU: one process per GPU (torchrun), games sharded by
+global game id, no collective inside the timed region; the (s, pi, z) all-gather over RCCL
+runs after it and is reported separately.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "onitama-alphazero_amd"))
+
+import torch  # noqa: E402  (imported before the engine so both share one HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+CONFIGS = {
+    # BASELINE.json configs[1]: 4096 parallel games, 100 sims/move, 3-block fp32, 1 GPU
+    "c2": dict(games=4096, sims=100, blocks=3, fixed_deck=1, precision="fp32"),
+    # configs[2]: 65536 parallel games, 400 sims/move, 1 GPU (the metric's "@400 sims")
+    "c3": dict(games=65536, sims=400, blocks=3, fixed_deck=1, precision="fp32"),
+    # configs[4] (per GPU): 16-card random deals, 800 sims, 6-block (bf16 MFMA not yet built: fp32)
+    "c5": dict(games=65536, sims=800, blocks=6, fixed_deck=0, precision="fp32"),
+}
+FLOP_PER_SIM = {3: 11_681_928, 5: 19_054_728, 6: 22_741_128}  # dense MACs x 2
+PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: F32 matrix peak (spec)
+METRIC = "MCTS node-expansions/sec/GPU @400 sims; self-play games/sec at 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--games", type=int, default=0, help="override games per GPU")
+    ap.add_argument("--sims", type=int, default=0, help="override sims per move")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="cpu_baseline sample length")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-allgather", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, seconds, threads):
+    """Reference-equivalent CPU baseline: the C restatement (oracle) playing self-play with the
+    reference's execution shape — one game per worker thread, sequential search, one batch-1
+    fp32 forward per simulation (train.rs:218-245, mcts_arena.rs:267-269)."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_ffi as orc
+    from onitama_az.weights import random_weights
+
+    w = random_weights(0, cfg["blocks"])
+    sc = orc.search_cfg(sims=cfg["sims"], c_puct=5.0, train_noise=1, evaluator=orc.EVAL_NN, weights=w,
+                        blocks=cfg["blocks"], seed=20260101)
+    t0 = time.perf_counter()
+    sims, games, plies = orc.selfplay_bench(sc, threads, seconds, max_plies=150,
+                                            deck=[0, 1, 2, 3, 4] if cfg["fixed_deck"] else None)
+    dt = time.perf_counter() - t0
+    return {"value": sims / dt, "unit": "sims/s", "cores": threads, "kind": "port",
+            "sample": f"{dt:.1f}s of self-play on {threads} host threads (oracle C restatement, batch-1 fp32 NN per "
+                      f"simulation, {cfg['blocks']}-block random-init, {cfg['sims']} sims/move): {sims} sims, "
+                      f"{plies} plies, {games} games finished"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from onitama_az import _abi
+    from onitama_az.engine import Engine
+    from onitama_az.weights import random_weights
+
+    cfg = dict(CONFIGS[args.config])
+    if args.games:
+        cfg["games"] = args.games
+    if args.sims:
+        cfg["sims"] = args.sims
+    eng = Engine(device=local, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0, train_noise=1,
+                 max_plies=150, evaluator=_abi.EVAL_NN, precision=_abi.FP32, fixed_deck=cfg["fixed_deck"],
+                 deck=[0, 1, 2, 3, 4], seed=20260101, rank=rank, world=world,
+                 sample_capacity=cfg["games"] * 24)
+    eng.load_weights(random_weights(0, cfg["blocks"]))  # random-init weights (seed 0), SURVEY.md 8d
+    eng.selfplay_reset()
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        eng.sync()
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        eng.selfplay_step(1)
+    barrier_sync()
+    st0 = eng.selfplay_stats()
+    eng.kernel_times_reset()
+    eng.set_timing(True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.selfplay_step(1)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    eng.set_timing(False)
+    kt = eng.kernel_times()
+    st1 = eng.selfplay_stats()
+
+    sims = st1.search.sims - st0.search.sims
+    games_done = st1.games_finished - st0.games_finished
+    plies = st1.moves - st0.moves
+    expansions = st1.search.expansions - st0.search.expansions
+    depth = (st1.search.depth_sum - st0.search.depth_sum) / max(1, sims)
+    branching = (st1.search.children - st0.search.children) / max(1, expansions)
+    tot = torch.tensor([float(sims), float(games_done), float(plies), float(expansions)], dtype=torch.float64, device="cuda")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    sims_all, games_all, plies_all, exp_all = (float(x) for x in tot.tolist())
+    T = float(tmax.item())
+
+    allgather = None
+    if not args.no_allgather:  # C4: RCCL all-gather of (s, pi, z) after the timed region
+        from onitama_az.dist import allgather_samples
+        t1 = time.perf_counter()
+        got = allgather_samples(eng, world, torch.device("cuda", local))
+        torch.cuda.synchronize()
+        allgather = {"samples_total": int(got), "bytes_per_sample": 228, "seconds": time.perf_counter() - t1,
+                     "backend": "nccl(RCCL)" if world > 1 else "local"}
+
+    if rank == 0:
+        nn_avg_ms = kt.nn_ms / max(1, kt.nn_n)
+        flops_launch = FLOP_PER_SIM[cfg["blocks"]] * (kt.nn_samples / max(1, kt.nn_n))
+        achieved = flops_launch / (nn_avg_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
+        out = {
+            "metric": METRIC, "value": sims_all / T, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * T / args.steps, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init weights seed 0, seeded deals)",
+            "config": {"workload": f"{args.config}: {cfg['games']} self-play games/GPU x {cfg['sims']} sims/move, "
+                                   f"{cfg['blocks']}-block 64-ch ResNet, c_puct 5, Dirichlet root noise",
+                       "games_per_gpu": cfg["games"], "sims_per_move": cfg["sims"], "blocks": cfg["blocks"],
+                       "fixed_deck": bool(cfg["fixed_deck"]), "parallelism": f"games sharded x{world}"},
+            "sims_per_s_per_gpu": sims_all / T / world,
+            "games_per_s": games_all / T, "plies_per_s": plies_all / T,
+            "true_expansions_per_s": exp_all / T, "mean_select_depth": depth, "mean_branching": branching,
+            "kernel_ms_per_step": {"select": kt.select_ms / args.steps, "nn": kt.nn_ms / args.steps,
+                                   "expand_backup": kt.expand_ms / args.steps, "move": kt.finalize_ms / args.steps},
+            "roofline": {"bound": "mfma", "kernel": "k_nn_forward (fused ResNet, v_mfma_f32_32x32x2_f32)",
+                         "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+                         "flop_per_launch": flops_launch, "avg_launch_ms": nn_avg_ms, "launches": kt.nn_n},
+            "allgather": allgather,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, threads)
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,248 @@
+/*
+ * onitama_az.h — C ABI of the MI355X-native Onitama AlphaZero self-play engine.
+ *
+ * This is the drop-in boundary for the reference's hot path (cyoq/onitama-alphazero):
+ * batched 5x5-bitboard move generation / state stepping (onitama-game) plus
+ * leaf-evaluated AlphaZero MCTS (select/expand/backup) and the ResNet policy-value
+ * evaluation (alphazero-training). The reference is Rust calling libtorch through
+ * tch-rs; a Rust host binds this header with one `extern "C"` block
+ * and tch is no longer needed on the path.
+ *
+ * Conventions
+ *   - Plain C, POD structs, caller-owned buffers, no torch types.
+ *   - Every function returning int: 0 = OK, < 0 = error; the message is then in
+ *     oaz_last_error() (thread-local). Nothing throws or aborts across the ABI:
+ *     the reference's panics (e.g. "Must find the best child",
+ *     alphazero-training/src/alphazero_mcts/mcts_arena.rs:94,220) become defined
+ *     behaviour or an error code.
+ *   - An engine is owned by one host thread and bound to one GPU (one process per
+ *     GPU, one engine per process in the self-play bench). Distinct engines are
+ *     independent.
+ *   - Compute entry points need a gfx950 GPU. Without one oaz_create() returns
+ *     NULL and the rules entry points return OAZ_ERR_NO_DEVICE; there is no CPU
+ *     fallback in this library.
+ *
+ * Reference interfaces replaced (file:line under the reference root):
+ *   oaz_movegen        <- State::generate_all_legal_moves   onitama-game/src/game/state.rs:301-378
+ *   oaz_step           <- State::make_move + Deck::rotate    onitama-game/src/game/state.rs:145-202, deck.rs:87-90
+ *   oaz_current_state  <- State::current_state               onitama-game/src/game/state.rs:120-134
+ *   oaz_encode         <- create_tensor_from_state           alphazero-training/src/common.rs:26-80
+ *   oaz_nn_forward     <- ConvResNet::forward(train=false)   alphazero-training/src/net.rs:215-232
+ *   oaz_search         <- MctsArena::new + search            alphazero-training/src/alphazero_mcts/mcts_arena.rs:48-124
+ *                         (TrainingAlphaZeroMcts::generate_move_tensor, alphazero_mcts/mod.rs:63-78,
+ *                          and Agent::generate_move for AlphaZeroMcts, alphazero_mcts/mod.rs:122-144)
+ *   oaz_selfplay_*     <- self_play                           alphazero-training/src/train.rs:35-98
+ *   oaz_load_weights   <- AlphaZeroMcts::from_model_file      alphazero-training/src/alphazero_mcts/mod.rs:89-105
+ */
+#ifndef ONITAMA_AZ_H
+#define ONITAMA_AZ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OAZ_ABI_VERSION 1
+
+/* ---- enums mirroring the reference --------------------------------------- */
+enum { OAZ_RED = 0, OAZ_BLUE = 1 };                 /* PlayerColor, player_color.rs:7-10 */
+enum { OAZ_PAWN = 0, OAZ_KING = 1 };                /* PieceKind, piece.rs:5-9 */
+enum {                                              /* MoveResult, move_result.rs:4-9 */
+    OAZ_CAPTURE = 0,
+    OAZ_RED_WIN = 1,
+    OAZ_BLUE_WIN = 2,
+    OAZ_IN_PROGRESS = 3
+};
+/* Card ids are indices into ORIGINAL_CARDS (card.rs:465-468):
+ * 0 Tiger 1 Dragon 2 Frog 3 Rabbit 4 Crab 5 Elephant 6 Goose 7 Rooster
+ * 8 Monkey 9 Mantis 10 Crane 11 Horse 12 Ox 13 Boar 14 Eel 15 Cobra. */
+enum { OAZ_NUM_CARDS = 16, OAZ_MAX_MOVES = 40 };    /* 2 cards x 5 pieces x 4 squares */
+
+enum {
+    OAZ_OK = 0,
+    OAZ_ERR_ARG = -1,
+    OAZ_ERR_NO_DEVICE = -2,
+    OAZ_ERR_HIP = -3,
+    OAZ_ERR_CAPACITY = -4,
+    OAZ_ERR_STATE = -5,
+    OAZ_ERR_WEIGHTS = -6
+};
+
+enum { OAZ_EVAL_NN = 0, OAZ_EVAL_HASH = 1 };        /* leaf evaluator (HASH: test evaluator, below) */
+enum { OAZ_FP32 = 0, OAZ_BF16 = 1 };                /* NN arithmetic (bf16: MFMA inputs, fp32 accumulate) */
+
+/* ---- PODs ----------------------------------------------------------------- */
+
+/* State (state.rs:51-56) plus the side to move (MctsState.player_color, mcts_arena.rs:24-28).
+ * Bitboards: square i = row*5+col, (0,0) = a5 top-left, bit for square i is 1u<<(31-i)
+ * (common/mod.rs:2-16). cards[] are deck slots R0,R1,B2,B3,N4 (deck.rs:14-18). */
+typedef struct oaz_state {
+    uint32_t kings[2];
+    uint32_t pawns[2];
+    uint8_t cards[5];
+    uint8_t to_move;
+    uint8_t pad[2];
+} oaz_state; /* 24 bytes */
+
+/* DoneMove (done_move.rs:3-7): Move{from,to,piece} (move.rs:20-25) + used_card_idx (deck slot). */
+typedef struct oaz_move {
+    uint8_t from;
+    uint8_t to;
+    uint8_t piece;
+    uint8_t slot;
+} oaz_move;
+
+/* One MCTS node as stored on the GPU (MctsNode, mcts_arena.rs:355-373). Children of a node
+ * are contiguous: [first, first+nch). Node indices are the reference arena indices
+ * (allocation order), so a dump compares index-for-index with the reference tree. */
+typedef struct oaz_node {
+    double W;        /* reward sum ("reward") */
+    double P;        /* prior ("probability") */
+    uint32_t N;      /* visits */
+    uint32_t first;  /* first child (valid when expanded) */
+    uint16_t mv;     /* packed move: from | to<<5 | slot<<10 | piece<<12 */
+    uint8_t nch;     /* number of children */
+    uint8_t flags;   /* bit0 expanded, bit1 terminal */
+    uint32_t pad;
+} oaz_node; /* 32 bytes */
+
+/* Self-play training sample (SelfPlayData, train.rs:27-33): encoded compactly; the 21x5x5
+ * planes are recoverable with oaz_encode(state). */
+typedef struct oaz_sample {
+    oaz_state state;  /* position before the move; state.to_move = player_color */
+    float pi[50];     /* visit distribution [2][25] (calculate_priors, mcts_arena.rs:104-124) */
+    float z;          /* reward(final result, player_color) (train.rs:83-85) */
+} oaz_sample; /* 228 bytes */
+
+typedef struct oaz_config {
+    int32_t blocks;          /* ConvResNetConfig.resnet_block_amnt (net.rs:74-89) */
+    int32_t channels;        /* hidden_channels: 64 (only value supported) */
+    int32_t in_planes;       /* input_channels: 21 (only value supported) */
+    int32_t sims;            /* AlphaZeroMctsConfig.max_playouts; search_time is not used */
+    double c_puct;           /* exploration_c */
+    int32_t train_noise;     /* AlphaZeroMctsConfig.train: Dirichlet noise at the root */
+    int32_t max_plies;       /* TrainConfig.max_plies (train.rs:52,74-79): 150 => 152 plies */
+    double dirichlet_alpha;  /* 0.03 (mcts_arena.rs:187) */
+    double dirichlet_eps;    /* 0.25 (mcts_arena.rs:186) */
+    int32_t games;           /* parallel game slots G (also the max batch of oaz_search) */
+    int32_t evaluator;       /* OAZ_EVAL_NN or OAZ_EVAL_HASH */
+    int32_t precision;       /* OAZ_FP32 or OAZ_BF16 */
+    int32_t fixed_deck;      /* 1: every game uses deck[]; 0: random 5 of 16 per game (deck.rs:139-151) */
+    uint8_t deck[5];
+    uint8_t pad0[3];
+    uint64_t seed;           /* counter-based RNG key for deals and Dirichlet noise */
+    int32_t rank;            /* global game id = (k * world + rank) * games + slot */
+    int32_t world;
+    int32_t sample_capacity; /* max samples buffered on the device (0: auto) */
+    int32_t reserved[7];
+} oaz_config;
+
+typedef struct oaz_search_stats {
+    uint64_t sims;            /* simulations run (= NN leaf evaluations, Q2) */
+    uint64_t expansions;      /* leaves actually expanded (non-terminal, first visit) */
+    uint64_t children;        /* children created */
+    uint64_t terminal_leaves; /* playouts that ended on a won position */
+    uint64_t depth_sum;       /* sum of select path depths */
+    uint64_t stuck_leaves;    /* expanded nodes with no legal move (reference panics, Q6) */
+    uint64_t max_nodes;       /* largest tree seen */
+} oaz_search_stats;
+
+typedef struct oaz_selfplay_stats {
+    uint64_t moves;           /* plies played over all slots */
+    uint64_t games_finished;
+    uint64_t games_cut;       /* finished by the ply cap (z = 0) */
+    uint64_t red_wins, blue_wins;
+    uint64_t samples_ready;   /* samples buffered on the device */
+    uint64_t samples_dropped; /* overflowed the device buffer */
+    uint64_t passes;          /* root positions with no legal move: pass (Q6) */
+    oaz_search_stats search;
+} oaz_selfplay_stats;
+
+typedef struct oaz_kernel_times {
+    /* accumulated HIP-event time (ms) and launches per kernel class; enabled with
+     * oaz_set_timing(eng, 1) */
+    double select_ms, nn_ms, expand_ms, finalize_ms;
+    uint64_t select_n, nn_n, expand_n, finalize_n;
+    uint64_t nn_samples;  /* samples evaluated by the timed nn launches */
+} oaz_kernel_times;
+
+typedef struct oaz_engine oaz_engine;
+
+/* ---- library ---------------------------------------------------------------- */
+int oaz_abi_version(void);
+const char* oaz_last_error(void);
+void oaz_config_default(oaz_config* cfg);   /* canonical self-play config (bin/train.rs:50-78) */
+int oaz_device_count(int* n);               /* number of visible HIP devices */
+
+/* ---- host-side helpers (no GPU needed) ---------------------------------------- */
+/* ATTACK_MAPS[color][card][from] (card.rs:476-604), as compiled into the kernels. */
+void oaz_attack_maps(uint32_t out[2 * 16 * 25]);
+/* Number of fp32 values in the canonical weight blob (tch VarStore order). */
+size_t oaz_weight_count(int blocks, int channels, int in_planes);
+/* Random-init weights in canonical order: conv/linear U(-1/sqrt(fan_in), +1/sqrt(fan_in)),
+ * BN gamma 1, beta 0, mean 0, var 1. */
+int oaz_random_weights(uint64_t seed, int blocks, float* out, size_t n);
+/* Deck of global game `game_id` under `seed` (random 5 of 16, Fisher-Yates on Philox). */
+void oaz_deal_deck(uint64_t seed, uint64_t game_id, uint8_t out[5]);
+/* Start position with `deck`; to_move = colour of the neutral card (game_state.rs:19-24). */
+void oaz_initial_state(const uint8_t deck[5], oaz_state* out);
+/* The HASH test evaluator (identical on host and device; documented in DESIGN.md). */
+void oaz_hash_eval(const oaz_state* s, float policy[50], float* value);
+
+/* ---- rules on the GPU (bit-exact with the reference) ---------------------------- */
+/* Legal moves of s[i].to_move. masks[i][k][from] = destination mask of own piece on
+ * `from` with the mover's k-th card (slot 0/1 for Red, 2/3 for Blue), 0 if no own piece.
+ * moves[i][*] in reference order (slot, from, to ascending); counts[i] = #moves.
+ * Any output pointer may be NULL. Host pointers. */
+int oaz_movegen(const oaz_state* s, int n, uint32_t* masks /* n*2*25 */,
+                oaz_move* moves /* n*40 */, uint8_t* counts /* n */);
+/* make_move(mv[i], s[i].to_move, mv[i].slot) in place, then switch to_move;
+ * results[i] = MoveResult. Host pointers. */
+int oaz_step(oaz_state* s, const oaz_move* mv, int n, uint8_t* results);
+/* current_state() of each position. */
+int oaz_current_state(const oaz_state* s, int n, uint8_t* results);
+/* 21x5x5 planes of s[i] for colour s[i].to_move (fp32, n*525). */
+int oaz_encode(const oaz_state* s, int n, float* planes);
+
+/* ---- engine --------------------------------------------------------------------- */
+oaz_engine* oaz_create(const oaz_config* cfg, int device);
+void oaz_destroy(oaz_engine* eng);
+int oaz_get_config(const oaz_engine* eng, oaz_config* out);
+/* Weights in canonical order (n == oaz_weight_count). BN is folded on the host. */
+int oaz_load_weights(oaz_engine* eng, const float* blob, size_t n);
+int oaz_sync(oaz_engine* eng);
+int oaz_set_timing(oaz_engine* eng, int enable);
+int oaz_kernel_times_get(oaz_engine* eng, oaz_kernel_times* out);
+int oaz_kernel_times_reset(oaz_engine* eng);
+
+/* policy [B][2][25] (softmax over all 50), value [B]. Host pointers. B <= cfg.games. */
+int oaz_nn_forward(oaz_engine* eng, const oaz_state* s, int B, float* policy, float* value);
+
+/* One search per root (root colour = roots[i].to_move), cfg.sims simulations each, all
+ * G searches advanced together. out_pi [G][50] f32, out_root_value [G] = an extra NN
+ * evaluation of the root (Agent::generate_move, mod.rs:137-141). Any output may be NULL. */
+int oaz_search(oaz_engine* eng, const oaz_state* roots, int G, oaz_move* out_move,
+               float* out_pi, float* out_root_value, oaz_search_stats* stats);
+/* Tree of `game` left by the last oaz_search: nodes [0, *n_nodes) in reference arena order. */
+int oaz_tree_dump(oaz_engine* eng, int game, oaz_node* out, int cap, int* n_nodes);
+
+/* ---- self-play (continuous batching over cfg.games slots, device resident) ------ */
+int oaz_selfplay_reset(oaz_engine* eng);                 /* deal a fresh game in every slot */
+int oaz_selfplay_step(oaz_engine* eng, int moves);       /* play `moves` plies in every slot */
+int oaz_selfplay_stats_get(oaz_engine* eng, oaz_selfplay_stats* out);
+/* Copy up to cap buffered samples to host memory and drop them from the device buffer. */
+int oaz_samples_fetch(oaz_engine* eng, oaz_sample* out, size_t cap, size_t* n_out);
+/* Device-to-device copy of up to cap_bytes/sizeof(oaz_sample) buffered samples into a
+ * device buffer on the engine's GPU (e.g. a tensor that is then all-gathered over RCCL). */
+int oaz_samples_export_device(oaz_engine* eng, void* dev_dst, size_t cap_bytes, size_t* n_out);
+/* self_play(): play exactly n_games games (slot g plays games until the total is
+ * reached) and return their samples. */
+int oaz_selfplay_run(oaz_engine* eng, int n_games, oaz_sample* out, size_t cap,
+                     size_t* n_out, oaz_selfplay_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ONITAMA_AZ_H */

@@ -1,0 +1,219 @@
+// oaz_device.h — rules, RNG and evaluator primitives shared by the HIP kernels and the host
+// engine (all __host__ __device__). Semantics follow the reference exactly (citations per
+// function); the formulation is the GPU's own (branch-free bit ops, one lane per square).
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/onitama_az.h"
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define OAZ_HD __host__ __device__ __forceinline__
+#else
+#define OAZ_HD inline
+#endif
+
+namespace oaz {
+
+// ---- cards: onitama-game/src/game/card.rs:17-468 -------------------------------------
+// Card patterns are 25-bit masks (bit 31-i = square i) centred on square 12; `mirror` is
+// the pattern Blue uses (card.rs:531-533).
+constexpr uint32_t kCardPos[16] = {0x20004000u, 0x0440A000u, 0x02202000u, 0x00828000u,
+                                   0x01220000u, 0x02940000u, 0x02142000u, 0x00948000u,
+                                   0x0280A000u, 0x02804000u, 0x0100A000u, 0x01104000u,
+                                   0x01044000u, 0x01140000u, 0x02048000u, 0x00902000u};
+constexpr uint32_t kCardMir[16] = {0x01000200u, 0x02811000u, 0x02022000u, 0x00A08000u,
+                                   0x00224000u, 0x0014A000u, 0x02142000u, 0x00948000u,
+                                   0x0280A000u, 0x0100A000u, 0x02804000u, 0x01044000u,
+                                   0x01104000u, 0x00144000u, 0x00902000u, 0x02048000u};
+// Card.player_color (0 Red, 1 Blue): the first mover is the neutral card's colour.
+constexpr uint8_t kCardColor[16] = {1, 0, 0, 0, 1, 0, 1, 0, 1, 0, 1, 0, 1, 0, 1, 0};
+
+constexpr uint32_t kRedKingStart = 0x00000200u;   // state.rs:24
+constexpr uint32_t kBlueKingStart = 0x20000000u;  // state.rs:31
+constexpr uint32_t kBluePawnsStart = 0xD8000000u; // state.rs:38
+constexpr uint32_t kRedPawnsStart = 0x00000D80u;  // state.rs:45
+constexpr int kBlueTemple = 2;                    // state.rs:48
+constexpr int kRedTemple = 22;                    // state.rs:49
+
+OAZ_HD constexpr uint32_t sq_bit(int sq) { return 0x80000000u >> sq; }
+
+// ATTACK_MAPS[color][card][from] (card.rs:476-604). The reference builds it by shifting the
+// centred pattern by the square delta and masking wrapped files by (delta % 5). Here every
+// pattern square is turned into a (dr, dc) offset from the centre and applied to `from`
+// when it stays on the board — the same set (the file masks remove exactly the column
+// wrap-arounds; tests/test_rules_host.py checks the tables against the oracle).
+struct AttackTable {
+    uint32_t m[2][16][25];
+};
+
+constexpr AttackTable make_attack_table() {
+    AttackTable t{};
+    for (int color = 0; color < 2; ++color)
+        for (int card = 0; card < 16; ++card) {
+            const uint32_t pat = color ? kCardMir[card] : kCardPos[card];
+            for (int from = 0; from < 25; ++from) {
+                uint32_t m = 0;
+                for (int j = 0; j < 25; ++j) {
+                    if (!(pat & sq_bit(j))) continue;
+                    const int dr = j / 5 - 2, dc = j % 5 - 2;
+                    const int r = from / 5 + dr, c = from % 5 + dc;
+                    if (r >= 0 && r < 5 && c >= 0 && c < 5) m |= sq_bit(r * 5 + c);
+                }
+                t.m[color][card][from] = m;
+            }
+        }
+    return t;
+}
+
+constexpr AttackTable kAttackHost = make_attack_table();
+
+// ---- state helpers ----------------------------------------------------------------------
+OAZ_HD bool is_win(int r) { return r == OAZ_RED_WIN || r == OAZ_BLUE_WIN; }
+
+// State::make_move (state.rs:145-202) + Deck::rotate (deck.rs:87-90); colour = mover.
+OAZ_HD int make_move(oaz_state& s, int from, int to, int piece, int slot, int color) {
+    const uint32_t fb = sq_bit(from), tb = sq_bit(to);
+    const int enemy = color ^ 1;
+    if (piece == OAZ_PAWN) s.pawns[color] &= ~fb;
+    else s.kings[color] &= ~fb;
+    int res = OAZ_IN_PROGRESS;
+    if (s.pawns[enemy] & tb) {
+        s.pawns[enemy] &= ~tb;
+        res = OAZ_CAPTURE;
+    } else if (s.kings[enemy] & tb) {
+        s.kings[enemy] &= ~tb;
+        res = color == OAZ_RED ? OAZ_RED_WIN : OAZ_BLUE_WIN;
+    }
+    if (piece == OAZ_PAWN) s.pawns[color] |= tb;
+    else s.kings[color] |= tb;
+    if (piece == OAZ_KING && to == (color == OAZ_RED ? kBlueTemple : kRedTemple))
+        res = color == OAZ_RED ? OAZ_RED_WIN : OAZ_BLUE_WIN;
+    if (slot < 4) {
+        const uint8_t t = s.cards[slot];
+        s.cards[slot] = s.cards[4];
+        s.cards[4] = t;
+    }
+    return res;
+}
+
+// State::current_state (state.rs:120-134)
+OAZ_HD int current_state(const oaz_state& s) {
+    if (s.kings[0] == 0 || s.kings[1] == kRedKingStart) return OAZ_BLUE_WIN;
+    if (s.kings[1] == 0 || s.kings[0] == kBlueKingStart) return OAZ_RED_WIN;
+    return OAZ_IN_PROGRESS;
+}
+
+// reward (alphazero_mcts/mod.rs:45-53)
+OAZ_HD double reward(int result, int color) {
+    if (!is_win(result)) return 0.0;
+    return ((result == OAZ_RED_WIN) == (color == OAZ_RED)) ? 1.0 : -1.0;
+}
+
+// State::with_deck (state.rs:66-72); first mover = neutral card colour (game_state.rs:37-45)
+OAZ_HD void initial_state(const uint8_t deck[5], oaz_state& s) {
+    s.kings[0] = kRedKingStart;
+    s.kings[1] = kBlueKingStart;
+    s.pawns[0] = kRedPawnsStart;
+    s.pawns[1] = kBluePawnsStart;
+    for (int i = 0; i < 5; ++i) s.cards[i] = deck[i];
+    s.to_move = kCardColor[deck[4] & 15];
+    s.pad[0] = s.pad[1] = 0;
+}
+
+// Packed move (oaz_node.mv): from | to<<5 | slot<<10 | piece<<12
+OAZ_HD uint16_t pack_move(int from, int to, int slot, int piece) {
+    return (uint16_t)(from | (to << 5) | (slot << 10) | (piece << 12));
+}
+OAZ_HD int mv_from(uint32_t m) { return m & 31; }
+OAZ_HD int mv_to(uint32_t m) { return (m >> 5) & 31; }
+OAZ_HD int mv_slot(uint32_t m) { return (m >> 10) & 3; }
+OAZ_HD int mv_piece(uint32_t m) { return (m >> 12) & 1; }
+
+// ---- counter-based RNG (DESIGN.md "RNG"): Philox4x32-10 ---------------------------------
+struct u32x4 {
+    uint32_t x, y, z, w;
+};
+
+OAZ_HD u32x4 philox(uint64_t key, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1;
+        c3 = (uint32_t)p0;
+        c0 = n0;
+        c2 = n2;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return {c0, c1, c2, c3};
+}
+
+// uniform in (0,1) with 53 random bits
+OAZ_HD double u01(uint32_t a, uint32_t b) {
+    const uint64_t m = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+    return ((double)m + 0.5) * (1.0 / 9007199254740992.0);
+}
+
+// Deck::default (deck.rs:139-151): random 5 of the 16 cards; Fisher-Yates driven by
+// Philox(seed; game_id, 0xDEA1, q).
+OAZ_HD void deal_deck(uint64_t seed, uint64_t game_id, uint8_t out[5]) {
+    uint8_t cards[16];
+    for (int i = 0; i < 16; ++i) cards[i] = (uint8_t)i;
+    uint32_t w[16];
+    for (uint32_t q = 0; q < 4; ++q) {
+        const u32x4 r = philox(seed, (uint32_t)game_id, (uint32_t)(game_id >> 32), 0xDEA1u, q);
+        w[4 * q] = r.x;
+        w[4 * q + 1] = r.y;
+        w[4 * q + 2] = r.z;
+        w[4 * q + 3] = r.w;
+    }
+    for (int i = 15, k = 0; i >= 1; --i, ++k) {
+        const uint32_t j = (uint32_t)(((uint64_t)w[k] * (uint64_t)(i + 1)) >> 32);
+        const uint8_t t = cards[i];
+        cards[i] = cards[j];
+        cards[j] = t;
+    }
+    for (int i = 0; i < 5; ++i) out[i] = cards[i];
+}
+
+OAZ_HD uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// HASH test evaluator: a deterministic stand-in for the NN whose outputs are exact in fp32
+// on every device, so MCTS trees can be compared bit for bit ("Hard parts").
+OAZ_HD uint64_t hash_state(const oaz_state& s) {
+    uint64_t h = splitmix64((uint64_t)s.kings[0] | ((uint64_t)s.kings[1] << 32));
+    h = splitmix64(h ^ ((uint64_t)s.pawns[0] | ((uint64_t)s.pawns[1] << 32)));
+    const uint64_t c = (uint64_t)(s.cards[0] & 15) | ((uint64_t)(s.cards[1] & 15) << 4) |
+                       ((uint64_t)(s.cards[2] & 15) << 8) | ((uint64_t)(s.cards[3] & 15) << 12) |
+                       ((uint64_t)(s.cards[4] & 15) << 16) | ((uint64_t)(s.to_move & 1) << 20);
+    return splitmix64(h ^ c);
+}
+OAZ_HD float hash_policy(uint64_t h, int i) {
+    return (float)((splitmix64(h + (uint64_t)i) >> 40) + 1) * (1.0f / 16777216.0f);
+}
+OAZ_HD float hash_value(uint64_t h) {
+    const int32_t v = (int32_t)(splitmix64(h ^ 0x5DEECE66Dull) >> 40) - 8388608;
+    return (float)v * (1.0f / 8388608.0f);
+}
+
+// f64::total_cmp key (argmax ties and signed zeros as Rust orders them)
+OAZ_HD int64_t total_key(double x) {
+    int64_t i = (int64_t)__builtin_bit_cast(uint64_t, x);
+    i ^= (int64_t)(((uint64_t)(i >> 63)) >> 1);
+    return i;
+}
+
+}  // namespace oaz

@@ -1,0 +1,858 @@
+// oaz_engine.cpp — host side of the C ABI (include/onitama_az.h).
+//
+// Owns the device buffers of one engine (one GPU), orchestrates the per-simulation kernel
+// sequence  select -> evaluate -> expand/backup  for all G games in lock step, and the
+// per-move finalisation (search result or self-play ply). No compute happens on the host
+// except weight folding/packing, deck dealing for host helpers and sqrt tables.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/onitama_az.h"
+#include "oaz_device.h"
+#include "oaz_kernels.h"
+
+using namespace oaz;
+
+// ---- errors ---------------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int set_err(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return set_err(OAZ_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                           __FILE__, __LINE__);                                            \
+    } while (0)
+
+extern "C" int oaz_abi_version(void) { return OAZ_ABI_VERSION; }
+extern "C" const char* oaz_last_error(void) { return g_err.c_str(); }
+
+extern "C" void oaz_config_default(oaz_config* c) {
+    if (!c) return;
+    memset(c, 0, sizeof(*c));
+    c->blocks = 5;          // bin/train.rs:57-61
+    c->channels = 64;
+    c->in_planes = 21;
+    c->sims = 400;          // bin/train.rs:53
+    c->c_puct = 5.0;        // bin/train.rs:54
+    c->train_noise = 1;     // bin/train.rs:55
+    c->max_plies = 150;     // train.rs:152
+    c->dirichlet_alpha = 0.03;
+    c->dirichlet_eps = 0.25;
+    c->games = 4096;
+    c->evaluator = OAZ_EVAL_NN;
+    c->precision = OAZ_FP32;
+    c->fixed_deck = 0;
+    for (int i = 0; i < 5; ++i) c->deck[i] = (uint8_t)i;  // ORIGINAL_CARDS[0..5]
+    c->seed = 20260101ull;
+    c->rank = 0;
+    c->world = 1;
+}
+
+extern "C" int oaz_device_count(int* n) {
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (n) *n = (e == hipSuccess) ? c : 0;
+    if (e != hipSuccess) return set_err(OAZ_ERR_NO_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// ---- host helpers -----------------------------------------------------------------------------
+extern "C" void oaz_attack_maps(uint32_t out[2 * 16 * 25]) {
+    memcpy(out, kAttackHost.m, sizeof(kAttackHost.m));
+}
+
+extern "C" size_t oaz_weight_count(int blocks, int channels, int in_planes) {
+    const size_t C = (size_t)channels, I = (size_t)in_planes;
+    size_t n = C * I * 9 + C + 4 * C;
+    n += (size_t)blocks * 2 * (C * C * 9 + C + 4 * C);
+    n += C + 1 + 4 + C * 25 + C + C + 1;
+    n += 2 * C + 2 + 8 + 50 * 50 + 50;
+    return n;
+}
+
+extern "C" int oaz_random_weights(uint64_t seed, int blocks, float* out, size_t n) {
+    const size_t need = oaz_weight_count(blocks, 64, 21);
+    if (!out || n != need || blocks < 0) return set_err(OAZ_ERR_ARG, "random_weights: need %zu floats", need);
+    uint64_t ctr = 0;
+    auto uni = [&](float bound) {
+        const uint64_t r = splitmix64(seed ^ splitmix64(ctr++));
+        const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);
+        return (float)((2.0 * u - 1.0) * bound);
+    };
+    float* p = out;
+    auto conv = [&](size_t wn, int cout, size_t fan_in) {  // weight + bias U(+-1/sqrt(fan_in))
+        const float b = (float)(1.0 / sqrt((double)fan_in));
+        for (size_t i = 0; i < wn; ++i) *p++ = uni(b);
+        for (int i = 0; i < cout; ++i) *p++ = uni(b);
+    };
+    auto bn = [&](int c) {  // gamma 1, beta 0, mean 0, var 1
+        for (int i = 0; i < c; ++i) *p++ = 1.0f;
+        for (int i = 0; i < c; ++i) *p++ = 0.0f;
+        for (int i = 0; i < c; ++i) *p++ = 0.0f;
+        for (int i = 0; i < c; ++i) *p++ = 1.0f;
+    };
+    conv(64 * 21 * 9, 64, 21 * 9);
+    bn(64);
+    for (int b = 0; b < blocks; ++b)
+        for (int j = 0; j < 2; ++j) {
+            conv(64 * 64 * 9, 64, 64 * 9);
+            bn(64);
+        }
+    conv(64, 1, 64);
+    bn(1);
+    conv(64 * 25, 64, 25);
+    conv(64, 1, 64);
+    conv(128, 2, 64);
+    bn(2);
+    conv(2500, 50, 50);
+    if ((size_t)(p - out) != need) return set_err(OAZ_ERR_STATE, "random_weights: layout mismatch");
+    return 0;
+}
+
+extern "C" void oaz_deal_deck(uint64_t seed, uint64_t game_id, uint8_t out[5]) {
+    deal_deck(seed, game_id, out);
+}
+
+extern "C" void oaz_initial_state(const uint8_t deck[5], oaz_state* out) {
+    if (!deck || !out) return;
+    initial_state(deck, *out);
+}
+
+extern "C" void oaz_hash_eval(const oaz_state* s, float policy[50], float* value) {
+    const uint64_t h = hash_state(*s);
+    for (int i = 0; i < 50; ++i) policy[i] = hash_policy(h, i);
+    *value = hash_value(h);
+}
+
+// ---- weights: canonical (tch VarStore order) -> BN-folded -> MFMA-packed ----------------------
+// Canonical order (DESIGN.md "Weights"): conv_init_1.{weight,bias}, bn1.{weight,bias,
+// running_mean,running_var}, for each block i, j in {1,2}: resnet_i.resnet_small_block{j}.
+// {small_block_conv.{weight,bias}, small_block_bn.{4}}, vh_conv.{w,b}, vh_bn.{4},
+// vh_linear1.{w,b}, vh_linear2.{w,b}, policy_conv.{w,b}, policy_bn.{4}, ph_linear2.{w,b}.
+struct FoldedConv {
+    std::vector<float> w;  // [cout][cin][taps]
+    std::vector<float> b;  // [cout]
+};
+
+static FoldedConv fold(const float*& p, int cout, int cin, int taps) {
+    FoldedConv f;
+    const float* w = p;
+    p += (size_t)cout * cin * taps;
+    const float* b = p;
+    p += cout;
+    const float *g = p, *beta = p + cout, *mean = p + 2 * cout, *var = p + 3 * cout;
+    p += 4 * cout;
+    f.w.resize((size_t)cout * cin * taps);
+    f.b.resize(cout);
+    for (int o = 0; o < cout; ++o) {
+        const double s = (double)g[o] / sqrt((double)var[o] + 1e-5);  // BN eval, eps 1e-5
+        for (size_t k = 0; k < (size_t)cin * taps; ++k)
+            f.w[(size_t)o * cin * taps + k] = (float)((double)w[(size_t)o * cin * taps + k] * s);
+        f.b[o] = (float)(((double)b[o] - (double)mean[o]) * s + (double)beta[o]);
+    }
+    return f;
+}
+
+// B fragments of v_mfma_f32_32x32x2f32: lane l supplies B[k=l>>5][col=l&31]. Group `grp` of
+// tap t covers k-steps s = 4*grp..4*grp+3 of both halves; ci = h*S + s.
+static void pack_conv(const FoldedConv& f, int cin, int S, std::vector<float>& out) {
+    const int G4 = S / 4;
+    for (int t = 0; t < 9; ++t)
+        for (int grp = 0; grp < G4; ++grp)
+            for (int nt = 0; nt < 2; ++nt)
+                for (int l = 0; l < 64; ++l)
+                    for (int q = 0; q < 4; ++q) {
+                        const int co = nt * 32 + (l & 31);
+                        const int ci = (l >> 5) * S + 4 * grp + q;
+                        out.push_back(ci < cin ? f.w[((size_t)co * cin + ci) * 9 + t] : 0.0f);
+                    }
+    for (int o = 0; o < 64; ++o) out.push_back(f.b[o]);
+}
+
+static int pack_weights(const float* raw, int blocks, std::vector<float>& out) {
+    out.clear();
+    out.reserve(nn_packed_floats(blocks));
+    const float* p = raw;
+    pack_conv(fold(p, 64, 21, 9), 21, 12, out);
+    for (int b = 0; b < blocks; ++b)
+        for (int j = 0; j < 2; ++j) pack_conv(fold(p, 64, 64, 9), 64, 32, out);
+    // value head: vh_conv + vh_bn folded, vh_linear1, vh_linear2
+    FoldedConv vc = fold(p, 1, 64, 1);
+    for (int c = 0; c < 64; ++c) out.push_back(vc.w[c]);
+    out.push_back(vc.b[0]);
+    for (int i = 0; i < 3; ++i) out.push_back(0.0f);
+    for (int i = 0; i < 64 * 25; ++i) out.push_back(*p++);  // vh_linear1.weight [64][25]
+    for (int i = 0; i < 64; ++i) out.push_back(*p++);       // vh_linear1.bias
+    for (int i = 0; i < 64; ++i) out.push_back(*p++);       // vh_linear2.weight [1][64]
+    out.push_back(*p++);                                    // vh_linear2.bias
+    for (int i = 0; i < 3; ++i) out.push_back(0.0f);
+    // policy head: policy_conv + policy_bn folded, ph_linear2
+    FoldedConv pc = fold(p, 2, 64, 1);
+    for (int i = 0; i < 128; ++i) out.push_back(pc.w[i]);
+    out.push_back(pc.b[0]);
+    out.push_back(pc.b[1]);
+    out.push_back(0.0f);
+    out.push_back(0.0f);
+    for (int i = 0; i < 2500; ++i) out.push_back(*p++);  // ph_linear2.weight [50][50]
+    for (int i = 0; i < 50; ++i) out.push_back(*p++);    // ph_linear2.bias
+    out.push_back(0.0f);
+    out.push_back(0.0f);
+    if (out.size() != nn_packed_floats(blocks)) return set_err(OAZ_ERR_STATE, "pack: size mismatch");
+    if ((size_t)(p - raw) != oaz_weight_count(blocks, 64, 21)) return set_err(OAZ_ERR_STATE, "pack: raw size mismatch");
+    return 0;
+}
+
+// ---- rules context (no engine needed) ----------------------------------------------------------
+struct Scratch {
+    void* p = nullptr;
+    size_t n = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= n) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        HIP_TRY(hipMalloc(&p, bytes));
+        n = bytes;
+        return 0;
+    }
+};
+
+struct RulesCtx {
+    std::mutex mu;
+    bool init = false;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    Scratch a, b, c, d;
+};
+static RulesCtx g_rules;
+
+static int rules_begin() {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return set_err(OAZ_ERR_NO_DEVICE, "no HIP device visible (the rules run on the GPU)");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (!g_rules.init || g_rules.device != dev) {
+        HIP_TRY(hipStreamCreateWithFlags(&g_rules.stream, hipStreamNonBlocking));
+        g_rules.device = dev;
+        g_rules.init = true;
+    }
+    return 0;
+}
+
+extern "C" int oaz_movegen(const oaz_state* s, int n, uint32_t* masks, oaz_move* moves, uint8_t* counts) {
+    if (!s || n < 0) return set_err(OAZ_ERR_ARG, "movegen: bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> lk(g_rules.mu);
+    if (int rc = rules_begin()) return rc;
+    hipStream_t st = g_rules.stream;
+    if (int rc = g_rules.a.ensure((size_t)n * sizeof(oaz_state))) return rc;
+    if (int rc = g_rules.b.ensure((size_t)n * 50 * 4)) return rc;
+    if (int rc = g_rules.c.ensure((size_t)n * OAZ_MAX_MOVES * sizeof(oaz_move))) return rc;
+    if (int rc = g_rules.d.ensure((size_t)n)) return rc;
+    HIP_TRY(hipMemcpyAsync(g_rules.a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_movegen((oaz_state*)g_rules.a.p, n, masks ? (uint32_t*)g_rules.b.p : nullptr,
+                           moves ? (oaz_move*)g_rules.c.p : nullptr, counts ? (uint8_t*)g_rules.d.p : nullptr, st));
+    if (masks) HIP_TRY(hipMemcpyAsync(masks, g_rules.b.p, (size_t)n * 50 * 4, hipMemcpyDeviceToHost, st));
+    if (moves) HIP_TRY(hipMemcpyAsync(moves, g_rules.c.p, (size_t)n * OAZ_MAX_MOVES * sizeof(oaz_move), hipMemcpyDeviceToHost, st));
+    if (counts) HIP_TRY(hipMemcpyAsync(counts, g_rules.d.p, (size_t)n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+extern "C" int oaz_step(oaz_state* s, const oaz_move* mv, int n, uint8_t* results) {
+    if (!s || !mv || n < 0) return set_err(OAZ_ERR_ARG, "step: bad arguments");
+    if (n == 0) return 0;
+    for (int i = 0; i < n; ++i)
+        if (mv[i].from > 24 || mv[i].to > 24 || mv[i].slot > 3 || mv[i].piece > 1)
+            return set_err(OAZ_ERR_ARG, "step: move %d out of range", i);  // deck.rs:88 assert
+    std::lock_guard<std::mutex> lk(g_rules.mu);
+    if (int rc = rules_begin()) return rc;
+    hipStream_t st = g_rules.stream;
+    if (int rc = g_rules.a.ensure((size_t)n * sizeof(oaz_state))) return rc;
+    if (int rc = g_rules.c.ensure((size_t)n * sizeof(oaz_move))) return rc;
+    if (int rc = g_rules.d.ensure((size_t)n)) return rc;
+    HIP_TRY(hipMemcpyAsync(g_rules.a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(g_rules.c.p, mv, (size_t)n * sizeof(oaz_move), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_step((oaz_state*)g_rules.a.p, (const oaz_move*)g_rules.c.p, n, (uint8_t*)g_rules.d.p, st));
+    HIP_TRY(hipMemcpyAsync(s, g_rules.a.p, (size_t)n * sizeof(oaz_state), hipMemcpyDeviceToHost, st));
+    if (results) HIP_TRY(hipMemcpyAsync(results, g_rules.d.p, (size_t)n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+extern "C" int oaz_current_state(const oaz_state* s, int n, uint8_t* results) {
+    if (!s || !results || n < 0) return set_err(OAZ_ERR_ARG, "current_state: bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> lk(g_rules.mu);
+    if (int rc = rules_begin()) return rc;
+    hipStream_t st = g_rules.stream;
+    if (int rc = g_rules.a.ensure((size_t)n * sizeof(oaz_state))) return rc;
+    if (int rc = g_rules.d.ensure((size_t)n)) return rc;
+    HIP_TRY(hipMemcpyAsync(g_rules.a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_current_state((const oaz_state*)g_rules.a.p, n, (uint8_t*)g_rules.d.p, st));
+    HIP_TRY(hipMemcpyAsync(results, g_rules.d.p, (size_t)n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+extern "C" int oaz_encode(const oaz_state* s, int n, float* planes) {
+    if (!s || !planes || n < 0) return set_err(OAZ_ERR_ARG, "encode: bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> lk(g_rules.mu);
+    if (int rc = rules_begin()) return rc;
+    hipStream_t st = g_rules.stream;
+    if (int rc = g_rules.a.ensure((size_t)n * sizeof(oaz_state))) return rc;
+    if (int rc = g_rules.b.ensure((size_t)n * 525 * 4)) return rc;
+    HIP_TRY(hipMemcpyAsync(g_rules.a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_encode((const oaz_state*)g_rules.a.p, n, (float*)g_rules.b.p, st));
+    HIP_TRY(hipMemcpyAsync(planes, g_rules.b.p, (size_t)n * 525 * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+// ---- engine ------------------------------------------------------------------------------------
+struct TimedLaunch {
+    int kind;  // 0 select, 1 nn, 2 expand, 3 finalize
+    hipEvent_t a, b;
+    uint32_t samples;
+};
+
+struct oaz_engine {
+    oaz_config cfg;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t G = 0, cap = 0, pathcap = 0, hcap = 0, out_cap = 0;
+    // trees
+    oaz_node* nodes = nullptr;
+    uint32_t *n_nodes = nullptr, *path = nullptr, *depth = nullptr, *leaf = nullptr;
+    oaz_state* leaf_state = nullptr;
+    uint64_t* stats = nullptr;
+    uint64_t* stats_sum = nullptr;
+    double* sqrt_tab = nullptr;
+    float *policy = nullptr, *value = nullptr;
+    float* weights = nullptr;
+    bool have_weights = false;
+    // search mode
+    oaz_state* s_roots = nullptr;
+    oaz_move* s_move = nullptr;
+    float* s_pi = nullptr;
+    float* s_rootv = nullptr;
+    float* s_rootp = nullptr;
+    uint32_t search_calls = 0;
+    uint32_t* s_ply = nullptr;
+    // self-play
+    oaz_state* root = nullptr;
+    uint32_t *ply = nullptr, *seq = nullptr;
+    uint64_t* game_id = nullptr;
+    uint8_t* active = nullptr;
+    oaz_sample* hist = nullptr;
+    oaz_sample* out = nullptr;
+    unsigned long long* out_count = nullptr;
+    unsigned long long out_read = 0;  // samples already handed out
+    bool selfplay_ready = false;
+    uint64_t quota = 0;
+    // timing
+    bool timing = false;
+    std::vector<TimedLaunch> pending;
+    std::vector<hipEvent_t> pool;
+    oaz_kernel_times times{};
+};
+
+template <class T>
+static int dalloc(T** p, size_t count) {
+    HIP_TRY(hipMalloc((void**)p, count * sizeof(T) > 0 ? count * sizeof(T) : 16));
+    return 0;
+}
+
+static void dfree(void* p) {
+    if (p) (void)hipFree(p);
+}
+
+static TreeView tree_view(oaz_engine* e, uint32_t G) {
+    TreeView t;
+    t.nodes = e->nodes;
+    t.n_nodes = e->n_nodes;
+    t.path = e->path;
+    t.depth = e->depth;
+    t.leaf = e->leaf;
+    t.leaf_state = e->leaf_state;
+    t.stats = e->stats;
+    t.sqrt_tab = e->sqrt_tab;
+    t.cap = e->cap;
+    t.pathcap = e->pathcap;
+    t.G = G;
+    return t;
+}
+
+static SlotView slot_view(oaz_engine* e) {
+    SlotView s;
+    s.root = e->root;
+    s.ply = e->ply;
+    s.seq = e->seq;
+    s.game_id = e->game_id;
+    s.active = e->active;
+    s.hist = e->hist;
+    s.out = e->out;
+    s.out_count = e->out_count;
+    s.hcap = e->hcap;
+    s.out_cap = e->out_cap;
+    s.max_plies = e->cfg.max_plies;
+    s.fixed_deck = e->cfg.fixed_deck;
+    memcpy(s.deck, e->cfg.deck, 5);
+    s.seed = e->cfg.seed;
+    s.world_games = e->G * (uint32_t)(e->cfg.world > 0 ? e->cfg.world : 1);
+    s.rank_base = (uint32_t)e->cfg.rank * e->G;
+    s.quota = e->quota;
+    return s;
+}
+
+static SearchParams search_params(const oaz_engine* e) {
+    SearchParams p;
+    p.c_puct = e->cfg.c_puct;
+    p.alpha = e->cfg.dirichlet_alpha;
+    p.eps = e->cfg.dirichlet_eps;
+    p.seed = e->cfg.seed;
+    p.train_noise = e->cfg.train_noise;
+    return p;
+}
+
+static hipEvent_t ev_get(oaz_engine* e) {
+    if (!e->pool.empty()) {
+        hipEvent_t ev = e->pool.back();
+        e->pool.pop_back();
+        return ev;
+    }
+    hipEvent_t ev = nullptr;
+    (void)hipEventCreate(&ev);
+    return ev;
+}
+
+// Run a launch, bracketed by events on the engine stream when timing is on.
+template <class F>
+static int timed(oaz_engine* e, int kind, uint32_t samples, F&& launch) {
+    if (!e->timing) {
+        HIP_TRY(launch());
+        return 0;
+    }
+    TimedLaunch t;
+    t.kind = kind;
+    t.samples = samples;
+    t.a = ev_get(e);
+    t.b = ev_get(e);
+    HIP_TRY(hipEventRecord(t.a, e->stream));
+    HIP_TRY(launch());
+    HIP_TRY(hipEventRecord(t.b, e->stream));
+    e->pending.push_back(t);
+    if (e->pending.size() > 4096) {  // resolve periodically to bound the pool
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        for (auto& p : e->pending) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, p.a, p.b);
+            double* acc[4] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms};
+            uint64_t* cnt[4] = {&e->times.select_n, &e->times.nn_n, &e->times.expand_n, &e->times.finalize_n};
+            *acc[p.kind] += ms;
+            *cnt[p.kind] += 1;
+            if (p.kind == 1) e->times.nn_samples += p.samples;
+            e->pool.push_back(p.a);
+            e->pool.push_back(p.b);
+        }
+        e->pending.clear();
+    }
+    return 0;
+}
+
+extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
+    if (!cfg) {
+        set_err(OAZ_ERR_ARG, "create: null config");
+        return nullptr;
+    }
+    if (cfg->channels != 64 || cfg->in_planes != 21) {
+        set_err(OAZ_ERR_ARG, "create: only channels=64, in_planes=21 are supported");
+        return nullptr;
+    }
+    if (cfg->blocks < 0 || cfg->blocks > 64 || cfg->sims < 1 || cfg->sims > 65535 || cfg->games < 1 ||
+        cfg->max_plies < 0 || cfg->max_plies > 100000) {
+        set_err(OAZ_ERR_ARG, "create: config out of range");
+        return nullptr;
+    }
+    if (cfg->precision != OAZ_FP32) {
+        set_err(OAZ_ERR_ARG, "create: only OAZ_FP32 is implemented in this build");
+        return nullptr;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_err(OAZ_ERR_NO_DEVICE, "create: no HIP device visible");
+        return nullptr;
+    }
+    if (device < 0 || device >= ndev) {
+        set_err(OAZ_ERR_ARG, "create: device %d out of range (%d visible)", device, ndev);
+        return nullptr;
+    }
+    oaz_engine* e = new oaz_engine();
+    e->cfg = *cfg;
+    e->device = device;
+    e->G = (uint32_t)cfg->games;
+    e->cap = 1u + (uint32_t)cfg->sims * OAZ_MAX_MOVES;  // each playout expands <= 1 node of <= 40 children
+    e->pathcap = (uint32_t)cfg->sims + 1;               // depth grows by <= 1 per playout
+    e->hcap = (uint32_t)cfg->max_plies + 2;             // train.rs:74-79 cut after max_plies+2 plies
+    e->out_cap = cfg->sample_capacity > 0 ? (uint32_t)cfg->sample_capacity : e->G * 64u;
+    auto fail = [&](void) -> oaz_engine* {
+        std::string msg = g_err;
+        oaz_destroy(e);
+        g_err = msg;
+        return nullptr;
+    };
+    if (hipSetDevice(device) != hipSuccess) {
+        set_err(OAZ_ERR_HIP, "hipSetDevice(%d) failed", device);
+        return fail();
+    }
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        set_err(OAZ_ERR_HIP, "stream create failed");
+        return fail();
+    }
+    const size_t G = e->G;
+    if (dalloc(&e->nodes, G * e->cap) || dalloc(&e->n_nodes, G) || dalloc(&e->path, G * e->pathcap) ||
+        dalloc(&e->depth, G) || dalloc(&e->leaf, G) || dalloc(&e->leaf_state, G) ||
+        dalloc(&e->stats, G * GS_COUNT) || dalloc(&e->stats_sum, (size_t)GS_COUNT) ||
+        dalloc(&e->sqrt_tab, (size_t)cfg->sims + 2) || dalloc(&e->policy, G * 50) ||
+        dalloc(&e->value, G) || dalloc(&e->weights, nn_packed_floats(cfg->blocks)) ||
+        dalloc(&e->s_roots, G) || dalloc(&e->s_move, G) || dalloc(&e->s_pi, G * 50) ||
+        dalloc(&e->s_rootv, G) || dalloc(&e->s_rootp, G * 50) || dalloc(&e->s_ply, G) ||
+        dalloc(&e->root, G) || dalloc(&e->ply, G) || dalloc(&e->seq, G) ||
+        dalloc(&e->game_id, G) || dalloc(&e->active, G) || dalloc(&e->hist, G * e->hcap) ||
+        dalloc(&e->out, (size_t)e->out_cap) || dalloc(&e->out_count, (size_t)1))
+        return fail();
+    // sqrt((double)n) from the host libm (IEEE correctly rounded), so device PUCT = oracle PUCT
+    std::vector<double> tab((size_t)cfg->sims + 2);
+    for (size_t i = 0; i < tab.size(); ++i) tab[i] = sqrt((double)i);
+    if (hipMemcpy(e->sqrt_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(e->stats, 0, G * GS_COUNT * sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(e->out_count, 0, sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(e->active, 0, G) != hipSuccess) {
+        set_err(OAZ_ERR_HIP, "create: init copies failed");
+        return fail();
+    }
+    if (cfg->evaluator == OAZ_EVAL_NN) {  // random-init weights until oaz_load_weights
+        std::vector<float> w(oaz_weight_count(cfg->blocks, 64, 21));
+        if (oaz_random_weights(0, cfg->blocks, w.data(), w.size()) || oaz_load_weights(e, w.data(), w.size()))
+            return fail();
+    }
+    return e;
+}
+
+extern "C" void oaz_destroy(oaz_engine* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (auto& p : e->pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto ev : e->pool) (void)hipEventDestroy(ev);
+    void* ptrs[] = {e->nodes, e->n_nodes, e->path, e->depth, e->leaf, e->leaf_state, e->stats,
+                    e->stats_sum, e->sqrt_tab, e->policy, e->value, e->weights, e->s_roots,
+                    e->s_move, e->s_pi, e->s_rootv, e->s_rootp, e->s_ply, e->root, e->ply,
+                    e->seq, e->game_id, e->active, e->hist, e->out, e->out_count};
+    for (void* p : ptrs) dfree(p);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+extern "C" int oaz_get_config(const oaz_engine* e, oaz_config* out) {
+    if (!e || !out) return set_err(OAZ_ERR_ARG, "get_config: null");
+    *out = e->cfg;
+    return 0;
+}
+
+extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
+    if (!e || !blob) return set_err(OAZ_ERR_ARG, "load_weights: null");
+    const size_t need = oaz_weight_count(e->cfg.blocks, 64, 21);
+    if (n != need)  // the reference silently keeps random weights on a bad file (Q13); we refuse
+        return set_err(OAZ_ERR_WEIGHTS, "load_weights: got %zu floats, need %zu for %d blocks", n, need,
+                       e->cfg.blocks);
+    std::vector<float> packed;
+    if (int rc = pack_weights(blob, e->cfg.blocks, packed)) return rc;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipMemcpyAsync(e->weights, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->have_weights = true;
+    return 0;
+}
+
+extern "C" int oaz_sync(oaz_engine* e) {
+    if (!e) return set_err(OAZ_ERR_ARG, "sync: null");
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+extern "C" int oaz_set_timing(oaz_engine* e, int enable) {
+    if (!e) return set_err(OAZ_ERR_ARG, "set_timing: null");
+    e->timing = enable != 0;
+    return 0;
+}
+
+static int resolve_timing(oaz_engine* e) {
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (auto& p : e->pending) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b));
+        double* acc[4] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms};
+        uint64_t* cnt[4] = {&e->times.select_n, &e->times.nn_n, &e->times.expand_n, &e->times.finalize_n};
+        *acc[p.kind] += ms;
+        *cnt[p.kind] += 1;
+        if (p.kind == 1) e->times.nn_samples += p.samples;
+        e->pool.push_back(p.a);
+        e->pool.push_back(p.b);
+    }
+    e->pending.clear();
+    return 0;
+}
+
+extern "C" int oaz_kernel_times_get(oaz_engine* e, oaz_kernel_times* out) {
+    if (!e || !out) return set_err(OAZ_ERR_ARG, "kernel_times: null");
+    if (int rc = resolve_timing(e)) return rc;
+    *out = e->times;
+    return 0;
+}
+
+extern "C" int oaz_kernel_times_reset(oaz_engine* e) {
+    if (!e) return set_err(OAZ_ERR_ARG, "kernel_times_reset: null");
+    if (int rc = resolve_timing(e)) return rc;
+    memset(&e->times, 0, sizeof(e->times));
+    return 0;
+}
+
+static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float* d_pol, float* d_val) {
+    if (e->cfg.evaluator == OAZ_EVAL_HASH)
+        return timed(e, 1, B, [&] { return launch_hash_eval(d_states, (int)B, d_pol, d_val, e->stream); });
+    NNView w;
+    w.blob = e->weights;
+    w.blocks = e->cfg.blocks;
+    w.bf16 = 0;
+    return timed(e, 1, B, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, e->stream); });
+}
+
+extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* policy, float* value) {
+    if (!e || !s || B < 0) return set_err(OAZ_ERR_ARG, "nn_forward: bad arguments");
+    if ((uint32_t)B > e->G) return set_err(OAZ_ERR_CAPACITY, "nn_forward: B=%d > games=%u", B, e->G);
+    if (B == 0) return 0;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipMemcpyAsync(e->s_roots, s, (size_t)B * sizeof(oaz_state), hipMemcpyHostToDevice, e->stream));
+    if (int rc = evaluate(e, e->s_roots, (uint32_t)B, e->s_rootp, e->s_rootv)) return rc;
+    if (policy) HIP_TRY(hipMemcpyAsync(policy, e->s_rootp, (size_t)B * 50 * 4, hipMemcpyDeviceToHost, e->stream));
+    if (value) HIP_TRY(hipMemcpyAsync(value, e->s_rootv, (size_t)B * 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+// One simulation for every game: select -> evaluate -> expand/backup.
+static int sim_step(oaz_engine* e, const TreeView& t, const oaz_state* roots, const uint8_t* active,
+                    const uint64_t* gids, const uint32_t* plies, uint32_t sim) {
+    const SearchParams prm = search_params(e);
+    if (int rc = timed(e, 0, t.G, [&] { return launch_select(t, roots, active, gids, plies, prm, sim, e->stream); }))
+        return rc;
+    if (int rc = evaluate(e, t.leaf_state, t.G, e->policy, e->value)) return rc;
+    return timed(e, 2, t.G, [&] { return launch_expand_backup(t, roots, active, e->policy, e->value, e->stream); });
+}
+
+static int reduce_stats(oaz_engine* e, uint32_t G, uint64_t out[GS_COUNT]) {
+    HIP_TRY(launch_stats_reduce(e->stats, G, e->stats_sum, e->stream));
+    HIP_TRY(hipMemcpyAsync(out, e->stats_sum, GS_COUNT * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+static void fill_search_stats(const uint64_t* s, oaz_search_stats* o) {
+    o->sims = s[GS_SIMS];
+    o->expansions = s[GS_EXPANSIONS];
+    o->children = s[GS_CHILDREN];
+    o->terminal_leaves = s[GS_TERMINAL];
+    o->depth_sum = s[GS_DEPTH];
+    o->stuck_leaves = s[GS_STUCK];
+    o->max_nodes = s[GS_MAXNODES];
+}
+
+extern "C" int oaz_search(oaz_engine* e, const oaz_state* roots, int G, oaz_move* out_move, float* out_pi,
+                          float* out_root_value, oaz_search_stats* stats) {
+    if (!e || !roots || G < 0) return set_err(OAZ_ERR_ARG, "search: bad arguments");
+    if ((uint32_t)G > e->G) return set_err(OAZ_ERR_CAPACITY, "search: G=%d > games=%u", G, e->G);
+    if (G == 0) return 0;
+    for (int i = 0; i < G; ++i)
+        if (roots[i].to_move > 1) return set_err(OAZ_ERR_ARG, "search: root %d has to_move=%d", i, roots[i].to_move);
+    HIP_TRY(hipSetDevice(e->device));
+    const TreeView t = tree_view(e, (uint32_t)G);
+    HIP_TRY(hipMemcpyAsync(e->s_roots, roots, (size_t)G * sizeof(oaz_state), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemsetAsync(e->stats, 0, (size_t)G * GS_COUNT * sizeof(uint64_t), e->stream));
+    std::vector<uint32_t> plies((size_t)G, e->search_calls);
+    HIP_TRY(hipMemcpyAsync(e->s_ply, plies.data(), (size_t)G * 4, hipMemcpyHostToDevice, e->stream));
+    e->search_calls++;
+    HIP_TRY(launch_tree_reset(t, e->stream));
+    for (uint32_t s = 0; s < (uint32_t)e->cfg.sims; ++s)
+        if (int rc = sim_step(e, t, e->s_roots, nullptr, nullptr, e->s_ply, s)) return rc;
+    if (int rc = timed(e, 3, (uint32_t)G, [&] { return launch_search_finalize(t, e->s_roots, e->s_move, e->s_pi, e->stream); }))
+        return rc;
+    if (out_root_value) {  // extra root evaluation (alphazero_mcts/mod.rs:137-141)
+        if (int rc = evaluate(e, e->s_roots, (uint32_t)G, e->s_rootp, e->s_rootv)) return rc;
+        HIP_TRY(hipMemcpyAsync(out_root_value, e->s_rootv, (size_t)G * 4, hipMemcpyDeviceToHost, e->stream));
+    }
+    if (out_move) HIP_TRY(hipMemcpyAsync(out_move, e->s_move, (size_t)G * sizeof(oaz_move), hipMemcpyDeviceToHost, e->stream));
+    if (out_pi) HIP_TRY(hipMemcpyAsync(out_pi, e->s_pi, (size_t)G * 50 * 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (stats) {
+        uint64_t s[GS_COUNT];
+        if (int rc = reduce_stats(e, (uint32_t)G, s)) return rc;
+        memset(stats, 0, sizeof(*stats));
+        fill_search_stats(s, stats);
+    }
+    return 0;
+}
+
+extern "C" int oaz_tree_dump(oaz_engine* e, int game, oaz_node* out, int cap, int* n_nodes) {
+    if (!e || game < 0 || (uint32_t)game >= e->G) return set_err(OAZ_ERR_ARG, "tree_dump: bad game");
+    HIP_TRY(hipSetDevice(e->device));
+    uint32_t n = 0;
+    HIP_TRY(hipMemcpyAsync(&n, e->n_nodes + game, 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (n_nodes) *n_nodes = (int)n;
+    if (out && cap > 0) {
+        const size_t m = n < (uint32_t)cap ? n : (uint32_t)cap;
+        HIP_TRY(hipMemcpyAsync(out, e->nodes + (size_t)game * e->cap, m * sizeof(oaz_node), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+    }
+    return 0;
+}
+
+// ---- self-play ----------------------------------------------------------------------------------
+extern "C" int oaz_selfplay_reset(oaz_engine* e) {
+    if (!e) return set_err(OAZ_ERR_ARG, "selfplay_reset: null");
+    HIP_TRY(hipSetDevice(e->device));
+    const TreeView t = tree_view(e, e->G);
+    HIP_TRY(hipMemsetAsync(e->stats, 0, (size_t)e->G * GS_COUNT * sizeof(uint64_t), e->stream));
+    HIP_TRY(hipMemsetAsync(e->out_count, 0, sizeof(unsigned long long), e->stream));
+    e->out_read = 0;
+    HIP_TRY(launch_selfplay_reset(t, slot_view(e), e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->selfplay_ready = true;
+    return 0;
+}
+
+extern "C" int oaz_selfplay_step(oaz_engine* e, int moves) {
+    if (!e || moves < 0) return set_err(OAZ_ERR_ARG, "selfplay_step: bad arguments");
+    if (!e->selfplay_ready)
+        if (int rc = oaz_selfplay_reset(e)) return rc;
+    HIP_TRY(hipSetDevice(e->device));
+    const TreeView t = tree_view(e, e->G);
+    const SlotView sv = slot_view(e);
+    for (int m = 0; m < moves; ++m) {
+        for (uint32_t s = 0; s < (uint32_t)e->cfg.sims; ++s)
+            if (int rc = sim_step(e, t, e->root, e->active, e->game_id, e->ply, s)) return rc;
+        if (int rc = timed(e, 3, e->G, [&] { return launch_selfplay_move(t, sv, e->stream); })) return rc;
+    }
+    return 0;
+}
+
+extern "C" int oaz_selfplay_stats_get(oaz_engine* e, oaz_selfplay_stats* o) {
+    if (!e || !o) return set_err(OAZ_ERR_ARG, "selfplay_stats: null");
+    HIP_TRY(hipSetDevice(e->device));
+    uint64_t s[GS_COUNT];
+    if (int rc = reduce_stats(e, e->G, s)) return rc;
+    unsigned long long cnt = 0;
+    HIP_TRY(hipMemcpy(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost));
+    memset(o, 0, sizeof(*o));
+    o->moves = s[GS_MOVES];
+    o->games_finished = s[GS_FINISHED];
+    o->games_cut = s[GS_CUT];
+    o->red_wins = s[GS_RED];
+    o->blue_wins = s[GS_BLUE];
+    o->passes = s[GS_PASSES];
+    o->samples_dropped = s[GS_DROPPED];
+    const unsigned long long avail = cnt < e->out_cap ? cnt : e->out_cap;
+    o->samples_ready = avail > e->out_read ? avail - e->out_read : 0;
+    fill_search_stats(s, &o->search);
+    return 0;
+}
+
+static int samples_copy(oaz_engine* e, void* dst, size_t cap, size_t* n_out, hipMemcpyKind kind) {
+    HIP_TRY(hipSetDevice(e->device));
+    unsigned long long cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    const unsigned long long avail = (cnt < e->out_cap ? cnt : e->out_cap);
+    const size_t ready = avail > e->out_read ? (size_t)(avail - e->out_read) : 0;
+    const size_t n = ready < cap ? ready : cap;
+    if (n) HIP_TRY(hipMemcpyAsync(dst, e->out + e->out_read, n * sizeof(oaz_sample), kind, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->out_read += n;
+    if (e->out_read == avail && cnt >= e->out_read) {  // buffer drained: rewind
+        HIP_TRY(hipMemsetAsync(e->out_count, 0, sizeof(unsigned long long), e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        e->out_read = 0;
+    }
+    if (n_out) *n_out = n;
+    return 0;
+}
+
+extern "C" int oaz_samples_fetch(oaz_engine* e, oaz_sample* out, size_t cap, size_t* n_out) {
+    if (!e || (!out && cap)) return set_err(OAZ_ERR_ARG, "samples_fetch: bad arguments");
+    return samples_copy(e, out, cap, n_out, hipMemcpyDeviceToHost);
+}
+
+extern "C" int oaz_samples_export_device(oaz_engine* e, void* dev_dst, size_t cap_bytes, size_t* n_out) {
+    if (!e || (!dev_dst && cap_bytes)) return set_err(OAZ_ERR_ARG, "samples_export: bad arguments");
+    return samples_copy(e, dev_dst, cap_bytes / sizeof(oaz_sample), n_out, hipMemcpyDeviceToDevice);
+}
+
+extern "C" int oaz_selfplay_run(oaz_engine* e, int n_games, oaz_sample* out, size_t cap, size_t* n_out,
+                                oaz_selfplay_stats* stats) {
+    if (!e || n_games < 0) return set_err(OAZ_ERR_ARG, "selfplay_run: bad arguments");
+    e->quota = (uint64_t)n_games;  // slots stop dealing at global game index >= n_games
+    int rc = oaz_selfplay_reset(e);
+    if (rc) {
+        e->quota = 0;
+        return rc;
+    }
+    size_t got = 0;
+    for (;;) {
+        oaz_selfplay_stats st;
+        if ((rc = oaz_selfplay_stats_get(e, &st))) break;
+        if (st.games_finished >= (uint64_t)n_games) {
+            if (stats) *stats = st;
+            break;
+        }
+        if ((rc = oaz_selfplay_step(e, 8))) break;
+        size_t n = 0;
+        if (out && got < cap) {
+            if ((rc = oaz_samples_fetch(e, out + got, cap - got, &n))) break;
+            got += n;
+        }
+    }
+    if (!rc && out && got < cap) {
+        size_t n = 0;
+        rc = oaz_samples_fetch(e, out + got, cap - got, &n);
+        got += n;
+    }
+    e->quota = 0;
+    e->selfplay_ready = false;
+    if (n_out) *n_out = got;
+    return rc;
+}

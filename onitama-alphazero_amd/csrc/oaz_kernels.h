@@ -1,0 +1,107 @@
+// oaz_kernels.h — launchers for the gfx950 kernels (defined in oaz_kernels.hip / oaz_nn.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/onitama_az.h"
+
+namespace oaz {
+
+// Per-game statistics slots (summed on demand): see oaz_search_stats / oaz_selfplay_stats.
+enum GameStat {
+    GS_SIMS = 0,
+    GS_EXPANSIONS,
+    GS_CHILDREN,
+    GS_TERMINAL,
+    GS_DEPTH,
+    GS_STUCK,
+    GS_MAXNODES,
+    GS_MOVES,
+    GS_FINISHED,
+    GS_CUT,
+    GS_RED,
+    GS_BLUE,
+    GS_PASSES,
+    GS_DROPPED,
+    GS_COUNT = 16
+};
+
+// Device view of the search trees of G games (one region of `cap` nodes per game).
+struct TreeView {
+    oaz_node* nodes;        // [G][cap]
+    uint32_t* n_nodes;      // [G]
+    uint32_t* path;         // [G][pathcap] node ids root..leaf of the current playout
+    uint32_t* depth;        // [G]
+    uint32_t* leaf;         // [G] leaf node id
+    oaz_state* leaf_state;  // [G] position at the leaf (to_move = leaf colour)
+    uint64_t* stats;        // [G][GS_COUNT]
+    const double* sqrt_tab; // [sims+1] correctly rounded sqrt(n) (host libm)
+    uint32_t cap;
+    uint32_t pathcap;
+    uint32_t G;
+};
+
+struct SearchParams {
+    double c_puct;
+    double alpha;
+    double eps;
+    uint64_t seed;
+    int32_t train_noise;
+};
+
+// Self-play slot state (continuous batching).
+struct SlotView {
+    oaz_state* root;      // [G] current position of the game in the slot
+    uint32_t* ply;        // [G]
+    uint32_t* seq;        // [G] games started in this slot
+    uint64_t* game_id;    // [G] global game id (deal + noise key)
+    uint8_t* active;      // [G]
+    oaz_sample* hist;     // [G][hcap] samples of the running game (z filled at the end)
+    oaz_sample* out;      // [out_cap] finished samples
+    unsigned long long* out_count;  // appended samples (may exceed out_cap: dropped)
+    uint32_t hcap;
+    uint32_t out_cap;
+    int32_t max_plies;
+    int32_t fixed_deck;
+    uint8_t deck[5];
+    uint64_t seed;
+    uint32_t world_games;  // games per generation over all ranks (G * world)
+    uint32_t rank_base;    // rank * G
+    uint64_t quota;        // stop starting games at this global index (0 = unlimited)
+};
+
+struct NNView {
+    const float* blob;  // packed, BN-folded weights (DESIGN.md "NN weights layout")
+    int32_t blocks;
+    int32_t bf16;       // 1: bf16 MFMA inputs (fp32 accumulate)
+};
+
+// rules
+hipError_t launch_movegen(const oaz_state* s, int n, uint32_t* masks, oaz_move* moves,
+                          uint8_t* counts, hipStream_t st);
+hipError_t launch_step(oaz_state* s, const oaz_move* mv, int n, uint8_t* results, hipStream_t st);
+hipError_t launch_current_state(const oaz_state* s, int n, uint8_t* results, hipStream_t st);
+hipError_t launch_encode(const oaz_state* s, int n, float* planes, hipStream_t st);
+
+// evaluators
+hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy,
+                             float* value, hipStream_t st);
+hipError_t launch_hash_eval(const oaz_state* s, int B, float* policy, float* value, hipStream_t st);
+size_t nn_packed_floats(int blocks);
+
+// MCTS
+hipError_t launch_tree_reset(const TreeView& t, hipStream_t st);
+hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
+                         const uint64_t* game_id, const uint32_t* ply, SearchParams p,
+                         uint32_t sim, hipStream_t st);
+hipError_t launch_expand_backup(const TreeView& t, const oaz_state* roots, const uint8_t* active,
+                                const float* policy, const float* value, hipStream_t st);
+hipError_t launch_search_finalize(const TreeView& t, const oaz_state* roots, oaz_move* out_move,
+                                  float* out_pi, hipStream_t st);
+hipError_t launch_selfplay_move(const TreeView& t, const SlotView& s, hipStream_t st);
+hipError_t launch_selfplay_reset(const TreeView& t, const SlotView& s, hipStream_t st);
+hipError_t launch_stats_reduce(const uint64_t* per_game, uint32_t G, uint64_t* out /* GS_COUNT */,
+                               hipStream_t st);
+
+}  // namespace oaz

@@ -1,0 +1,672 @@
+// oaz_kernels.hip — gfx950 kernels for the rules and the AlphaZero search.
+//
+// Execution model: ONE WAVEFRONT (64 lanes) PER GAME for everything tree-shaped.
+//   * move generation: lane = (card k, from square) for k in {0,1}, from in 0..24 (50 lanes);
+//     each lane produces one 25-bit destination mask, a wave prefix sum over popcounts gives
+//     the reference order (slot, from, to) (state.rs:301-378) with no sort;
+//   * PUCT select: lane = child (K <= 40 < 64); a child's 32-byte node is one coalesced
+//     load per lane, the argmax (last maximum wins, mcts_arena.rs:213-220) is a butterfly
+//     over the wave; one dependent memory round trip per tree level;
+//   * backup: lane = depth along the recorded path, all levels updated in parallel.
+// The f64 PUCT arithmetic is the reference's expression order, compiled with
+// -ffp-contract=off; sqrt(N) comes from a host-built table so every bit matches the oracle.
+#include <hip/hip_runtime.h>
+
+#include "oaz_device.h"
+#include "oaz_kernels.h"
+
+namespace oaz {
+
+__constant__ AttackTable c_attack = make_attack_table();
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+__device__ __forceinline__ uint32_t wave_game() {
+    return blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+}
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v |= (uint32_t)__shfl_xor((int)v, off);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
+    return v;
+}
+// inclusive prefix sum over the wave
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)v, off);
+        if (l >= off) v += t;
+    }
+    return v;
+}
+// argmax of (key, lane) keeping the LARGEST lane among equal keys (Iterator::max_by).
+__device__ __forceinline__ int wave_argmax_last(int64_t key) {
+    int idx = lane_id();
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const int64_t ok = __shfl_xor(key, off);
+        const int oi = __shfl_xor(idx, off);
+        if (ok > key || (ok == key && oi > idx)) {
+            key = ok;
+            idx = oi;
+        }
+    }
+    return idx;
+}
+
+__device__ __forceinline__ oaz_state load_state(const oaz_state* p) {
+    oaz_state s;
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+    uint32_t* d = reinterpret_cast<uint32_t*>(&s);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) d[i] = q[i];
+    return s;
+}
+__device__ __forceinline__ void store_state(oaz_state* p, const oaz_state& s) {
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(&s);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) q[i] = d[i];
+}
+
+// ---- wave-parallel move generation ------------------------------------------------------
+// Lane (k, from): destination mask of the mover's piece on `from` with its k-th card.
+// Pawn and king masks of the reference (state.rs:351,357) both reduce to
+// attack & ~(own pawns | own king); the piece kind is the one on `from`.
+struct LaneMoves {
+    uint32_t mask;
+    int piece;
+    int slot;
+    int from;
+};
+
+__device__ __forceinline__ LaneMoves lane_movegen(const oaz_state& s) {
+    const int l = lane_id();
+    const int color = s.to_move & 1;
+    const int k = l >= 25 ? 1 : 0;
+    const int from = l - 25 * k;
+    const uint32_t pawns = s.pawns[color], king = s.kings[color];
+    const uint32_t own = pawns | king;
+    LaneMoves m;
+    m.slot = (color ? 2 : 0) + k;
+    m.from = from;
+    m.piece = (pawns & sq_bit(from)) ? OAZ_PAWN : OAZ_KING;
+    m.mask = 0;
+    if (l < 50 && (own & sq_bit(from)))
+        m.mask = c_attack.m[color][s.cards[m.slot] & 15][from] & ~own;
+    return m;
+}
+
+__global__ void __launch_bounds__(kBlock) k_movegen(const oaz_state* __restrict__ states, int n,
+                                                    uint32_t* masks, oaz_move* moves,
+                                                    uint8_t* counts) {
+    const uint32_t g = wave_game();
+    if (g >= (uint32_t)n) return;
+    const int l = lane_id();
+    const oaz_state s = load_state(&states[g]);
+    const LaneMoves m = lane_movegen(s);
+    if (masks && l < 50) masks[(size_t)g * 50 + l] = m.mask;
+    const uint32_t cnt = (uint32_t)__popc(m.mask);
+    const uint32_t incl = wave_incl_scan(cnt);
+    const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+    if (moves) {
+        uint32_t o = incl - cnt, mm = m.mask;
+        while (mm) {
+            const int to = __clz(mm);
+            mm &= ~sq_bit(to);
+            if (o < OAZ_MAX_MOVES) {
+                oaz_move mv;
+                mv.from = (uint8_t)m.from;
+                mv.to = (uint8_t)to;
+                mv.piece = (uint8_t)m.piece;
+                mv.slot = (uint8_t)m.slot;
+                moves[(size_t)g * OAZ_MAX_MOVES + o] = mv;
+            }
+            ++o;
+        }
+    }
+    if (counts && l == 0) counts[g] = (uint8_t)total;
+}
+
+__global__ void k_step(oaz_state* states, const oaz_move* mv, int n, uint8_t* results) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    oaz_state s = states[i];
+    const oaz_move m = mv[i];
+    const int r = make_move(s, m.from, m.to, m.piece, m.slot, s.to_move & 1);
+    s.to_move ^= 1;
+    states[i] = s;
+    if (results) results[i] = (uint8_t)r;
+}
+
+__global__ void k_current_state(const oaz_state* states, int n, uint8_t* results) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    results[i] = (uint8_t)current_state(states[i]);
+}
+
+// create_tensor_from_state (common.rs:26-80): one thread per (position, plane, square).
+__global__ void k_encode(const oaz_state* states, int n, float* planes) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)n * 525) return;
+    const int b = (int)(i / 525), r = (int)(i % 525), c = r / 25, sq = r % 25;
+    const oaz_state s = states[b];
+    const int color = s.to_move & 1;
+    float v = 0.0f;
+    if (c < 4) {
+        const uint32_t src = c == 0 ? s.pawns[0] : c == 1 ? s.kings[0] : c == 2 ? s.pawns[1] : s.kings[1];
+        v = (src & sq_bit(sq)) ? 1.0f : 0.0f;
+    } else if (c < 20) {
+        const int s0 = color ? 2 : 0;
+        v = ((s.cards[s0] & 15) == c - 4 || (s.cards[s0 + 1] & 15) == c - 4) ? 1.0f : 0.0f;
+    } else {
+        v = color == OAZ_BLUE ? 1.0f : 0.0f;
+    }
+    planes[i] = v;
+}
+
+__global__ void k_hash_eval(const oaz_state* states, int n, float* policy, float* value) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t h = hash_state(states[i]);
+    for (int k = 0; k < 50; ++k) policy[(size_t)i * 50 + k] = hash_policy(h, k);
+    value[i] = hash_value(h);
+}
+
+// ---- Dirichlet root noise ----------------------------------------------------------------
+// mcts_arena.rs:186-203 samples a fresh Dirichlet(alpha; K) vector for EVERY PUCT
+// evaluation at the root and reads component child.idx-1: marginally Beta(alpha, (K-1)alpha),
+// drawn as X/(X+Y) from gamma variates (rand_distr 0.4.3 Gamma: Marsaglia-Tsang with the
+// u^(1/shape) boost for shape < 1). Counter layout = oracle/oaz_oracle.c gamma_ctr.
+__device__ double gamma_large_dev(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx,
+                                  uint32_t which, double shape) {
+    const double d = shape - 1.0 / 3.0;
+    const double c = 1.0 / sqrt(9.0 * d);
+    for (uint32_t t = 0; t < 1000; ++t) {
+        const uint32_t c3 = (idx << 12) | (which << 11);
+        const u32x4 r = philox(seed, (uint32_t)game, (uint32_t)(game >> 32), c2, c3 | t);
+        const u32x4 r2 = philox(seed, (uint32_t)game, (uint32_t)(game >> 32), c2, c3 | (t | 1024u));
+        const double u1 = u01(r.x, r.y), u2 = u01(r.z, r.w);
+        const double x = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+        const double vc = 1.0 + c * x;
+        if (vc <= 0.0) continue;
+        const double v = vc * vc * vc;
+        const double u = u01(r2.x, r2.y);
+        const double x2 = x * x;
+        if (u < 1.0 - 0.0331 * x2 * x2 || log(u) < 0.5 * x2 + d * (1.0 - v + log(v))) return d * v;
+    }
+    return d;
+}
+__device__ double gamma_dev(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx,
+                            uint32_t which, double shape) {
+    if (shape >= 1.0) return gamma_large_dev(seed, game, c2, idx, which, shape);
+    const u32x4 r = philox(seed, (uint32_t)game, (uint32_t)(game >> 32), c2,
+                           (idx << 12) | (which << 11) | 2047u);
+    return gamma_large_dev(seed, game, c2, idx, which, 1.0 + shape) * pow(u01(r.x, r.y), 1.0 / shape);
+}
+__device__ double beta_noise_dev(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx,
+                                 double alpha, int K) {
+    const double x = gamma_dev(seed, game, c2, idx, 0, alpha);
+    const double y = gamma_dev(seed, game, c2, idx, 1, alpha * (double)(K - 1));
+    const double s = x + y;
+    return s > 0.0 ? x / s : 0.0;
+}
+
+// ---- MCTS kernels -------------------------------------------------------------------------
+struct NodeRegs {  // one node held in registers (all 32 bytes)
+    double W, P;
+    uint32_t N, first, misc;  // misc = mv | nch<<16 | flags<<24
+};
+
+__device__ __forceinline__ NodeRegs load_node(const oaz_node* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 a = q[0], b = q[1];
+    NodeRegs r;
+    r.W = __builtin_bit_cast(double, ((uint64_t)a.y << 32) | a.x);
+    r.P = __builtin_bit_cast(double, ((uint64_t)a.w << 32) | a.z);
+    r.N = b.x;
+    r.first = b.y;
+    r.misc = b.z;
+    return r;
+}
+__device__ __forceinline__ int node_nch(uint32_t misc) { return (misc >> 16) & 0xFF; }
+__device__ __forceinline__ int node_flags(uint32_t misc) { return misc >> 24; }
+__device__ __forceinline__ uint8_t* flags_ptr(oaz_node* n) { return &n->flags; }
+
+__device__ __forceinline__ void store_fresh_node(oaz_node* p, double P, uint32_t mv) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    const uint64_t pb = __builtin_bit_cast(uint64_t, P);
+    q[0] = make_uint4(0u, 0u, (uint32_t)pb, (uint32_t)(pb >> 32));
+    q[1] = make_uint4(0u, 0u, mv & 0xFFFFu, 0u);
+}
+
+__global__ void __launch_bounds__(kBlock) k_tree_reset(TreeView t) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= t.G) return;
+    store_fresh_node(&t.nodes[(size_t)g * t.cap], 1.0, 0);  // root: probability 1. (mcts_arena.rs:57)
+    t.n_nodes[g] = 1;
+}
+
+// playout step 1 (mcts_arena.rs:131-153): walk from the root while the node is expanded and
+// not terminal; replay each chosen move; mark children whose move wins as terminal.
+__global__ void __launch_bounds__(kBlock) k_select(TreeView t, const oaz_state* __restrict__ roots,
+                                                   const uint8_t* __restrict__ active,
+                                                   const uint64_t* __restrict__ game_ids,
+                                                   const uint32_t* __restrict__ plies,
+                                                   SearchParams prm, uint32_t sim) {
+    const uint32_t g = wave_game();
+    if (g >= t.G) return;
+    if (active && !active[g]) return;
+    const int l = lane_id();
+    oaz_node* T = t.nodes + (size_t)g * t.cap;
+    uint32_t* path = t.path + (size_t)g * t.pathcap;
+    oaz_state s = load_state(&roots[g]);
+    int color = s.to_move & 1;
+
+    NodeRegs nd = load_node(&T[0]);
+    uint32_t node = 0, depth = 0;
+    if (l == 0) path[0] = 0;
+    bool stuck = false;
+    while ((node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2)) {
+        const int K = node_nch(nd.misc);
+        if (K == 0) {  // reference would panic in select (Q6): stop here, treat as a leaf
+            stuck = true;
+            break;
+        }
+        NodeRegs ch;
+        ch.W = 0.0;
+        ch.P = 0.0;
+        ch.N = 0;
+        ch.first = 0;
+        ch.misc = 0;
+        if (l < K) ch = load_node(&T[nd.first + l]);
+        // winrate (reward / visits; 0 before the first visit) and sqrt(N_parent)/(N_child+1)
+        const double q = ch.N ? ch.W / (double)ch.N : 0.0;
+        const double sq = t.sqrt_tab[nd.N] / (double)(ch.N + 1);
+        int best;
+        if (depth == 0 && prm.train_noise) {
+            // sequential Iterator::max_by fold; each comparison re-evaluates both operands
+            // with fresh noise (draw indices 2j and 2j+1 for comparison j)
+            double na = 0.0, nb = 0.0;
+            if (l >= 1 && l < K) {
+                const uint64_t gid = game_ids ? game_ids[g] : g;
+                const uint32_t c2 = ((plies ? plies[g] : 0u) << 16) | (sim & 0xFFFFu);
+                na = beta_noise_dev(prm.seed, gid, c2, 2u * l, prm.alpha, K);
+                nb = beta_noise_dev(prm.seed, gid, c2, 2u * l + 1u, prm.alpha, K);
+            }
+            const double base = ch.P * (1.0 - prm.eps);
+            int acc = 0;
+            for (int j = 1; j < K; ++j) {
+                const double qa = __shfl(q, acc), ba = __shfl(base, acc), sa = __shfl(sq, acc);
+                const double qb = __shfl(q, j), bb = __shfl(base, j), sb = __shfl(sq, j);
+                const double naj = __shfl(na, j), nbj = __shfl(nb, j);
+                const double ua = qa + prm.c_puct * (ba + naj * prm.eps) * sa;
+                const double ub = qb + prm.c_puct * (bb + nbj * prm.eps) * sb;
+                if (!(total_key(ua) > total_key(ub))) acc = j;
+            }
+            best = acc;
+        } else {
+            const double u = q + prm.c_puct * ch.P * sq;  // mcts_arena.rs:204-207
+            best = wave_argmax_last(l < K ? total_key(u) : INT64_MIN);
+        }
+        NodeRegs c;
+        c.W = __shfl(ch.W, best);
+        c.P = __shfl(ch.P, best);
+        c.N = (uint32_t)__shfl((int)ch.N, best);
+        c.first = (uint32_t)__shfl((int)ch.first, best);
+        c.misc = (uint32_t)__shfl((int)ch.misc, best);
+        const uint32_t cidx = nd.first + (uint32_t)best;
+        const int res = make_move(s, mv_from(c.misc), mv_to(c.misc), mv_piece(c.misc),
+                                  mv_slot(c.misc), color);
+        color ^= 1;  // game_state.player_color.switch()
+        if (is_win(res)) {
+            c.misc |= 2u << 24;
+            if (l == 0) *flags_ptr(&T[cidx]) = (uint8_t)(node_flags(c.misc));
+        }
+        ++depth;
+        if (l == 0 && depth < t.pathcap) path[depth] = cidx;
+        node = cidx;
+        nd = c;
+    }
+    s.to_move = (uint8_t)color;
+    if (l == 0) {
+        store_state(&t.leaf_state[g], s);
+        t.leaf[g] = node;
+        t.depth[g] = depth;
+        uint64_t* st = t.stats + (size_t)g * GS_COUNT;
+        st[GS_SIMS] += 1;
+        st[GS_DEPTH] += depth;
+        if (stuck) st[GS_STUCK] += 1;
+    }
+}
+
+// playout steps 3-4 (mcts_arena.rs:158-176): expand the leaf if it is neither expanded nor
+// terminal (evaluate() priors, mcts_arena.rs:275-301; expand, 231-260), then back up either
+// the terminal reward (from the leaf parent's perspective) or the raw NN value.
+__global__ void __launch_bounds__(kBlock) k_expand_backup(TreeView t, const oaz_state* __restrict__ roots,
+                                                          const uint8_t* __restrict__ active,
+                                                          const float* __restrict__ policy,
+                                                          const float* __restrict__ value) {
+    const uint32_t g = wave_game();
+    if (g >= t.G) return;
+    if (active && !active[g]) return;
+    const int l = lane_id();
+    oaz_node* T = t.nodes + (size_t)g * t.cap;
+    const uint32_t* path = t.path + (size_t)g * t.pathcap;
+    const oaz_state s = load_state(&t.leaf_state[g]);
+    const uint32_t leaf = t.leaf[g], depth = t.depth[g];
+    const NodeRegs nd = load_node(&T[leaf]);
+    uint64_t* st = t.stats + (size_t)g * GS_COUNT;
+    const float* pol = policy + (size_t)g * 50;
+
+    if (!(node_flags(nd.misc) & 3)) {
+        const LaneMoves m = lane_movegen(s);
+        const uint32_t cnt = (uint32_t)__popc(m.mask);
+        const uint32_t incl = wave_incl_scan(cnt);
+        const uint32_t K = (uint32_t)__shfl((int)incl, 63);
+        const uint32_t row0 = wave_or(l < 25 ? m.mask : 0u);
+        const uint32_t row1 = wave_or(l >= 25 ? m.mask : 0u);
+        // per-card renormalisation; sequential f64 sums in square order (mcts_arena.rs:288-301)
+        double sum0 = 0.0, sum1 = 0.0;
+        for (int sq = 0; sq < 25; ++sq) {
+            if (row0 & sq_bit(sq)) sum0 += (double)pol[sq];
+            if (row1 & sq_bit(sq)) sum1 += (double)pol[25 + sq];
+        }
+        const uint32_t base = t.n_nodes[g];
+        const int row = m.slot & 1;
+        const double rs = row ? sum1 : sum0;
+        uint32_t o = incl - cnt, mm = m.mask;
+        while (mm) {
+            const int to = __clz(mm);
+            mm &= ~sq_bit(to);
+            double p = (double)pol[row * 25 + to];
+            if (rs > 0.0) p = p / rs;
+            store_fresh_node(&T[base + o], p, pack_move(m.from, to, m.slot, m.piece));
+            ++o;
+        }
+        if (l == 0) {
+            t.n_nodes[g] = base + K;
+            T[leaf].first = base;
+            T[leaf].nch = (uint8_t)K;
+            T[leaf].flags = 1;
+            st[GS_EXPANSIONS] += 1;
+            st[GS_CHILDREN] += K;
+            if (base + K > st[GS_MAXNODES]) st[GS_MAXNODES] = base + K;
+        }
+    }
+    const int res = current_state(s);
+    double r;
+    if (is_win(res)) {
+        // reward colour = colour of the leaf's parent (root if the leaf is the root)
+        const int root_color = roots[g].to_move & 1;
+        const int pc = depth == 0 ? root_color : (root_color ^ (int)((depth - 1) & 1));
+        r = reward(res, pc);
+        if (l == 0) st[GS_TERMINAL] += 1;
+    } else {
+        r = (double)value[g];
+    }
+    // back_propagate (mcts_arena.rs:312-323): node at depth k gets (-1)^(depth-k) * r
+    const uint32_t plen = depth < t.pathcap ? depth : t.pathcap - 1;
+    for (uint32_t k = (uint32_t)l; k <= plen; k += 64) {
+        const uint32_t n = path[k];
+        const double rk = ((depth - k) & 1) ? -r : r;
+        T[n].N += 1;
+        T[n].W += rk;
+    }
+}
+
+// calculate_priors (mcts_arena.rs:104-124) + best child (87-94) for every root.
+__device__ __forceinline__ void root_pi_best(const oaz_node* T, float* pi_out /*50, may be null*/,
+                                             float& pi_lane, int& best_lane, int& K_out,
+                                             uint32_t& best_mv) {
+    const int l = lane_id();
+    const NodeRegs root = load_node(&T[0]);
+    const int K = (node_flags(root.misc) & 1) ? node_nch(root.misc) : 0;
+    NodeRegs ch;
+    ch.N = 0;
+    ch.misc = 0;
+    if (l < K) ch = load_node(&T[root.first + l]);
+    const int bin = l < K ? (mv_slot(ch.misc) & 1) * 25 + mv_to(ch.misc) : -1;
+    // integer visit sums per (card row, destination): f32 sums of integers are exact
+    uint32_t cnt = 0;
+    for (int j = 0; j < K; ++j) {
+        const int bj = __shfl(bin, j);
+        const uint32_t nj = (uint32_t)__shfl((int)ch.N, j);
+        if (bj == l) cnt += nj;
+    }
+    const uint32_t total = wave_sum_u32(l < 50 ? cnt : 0u);
+    pi_lane = total > 0 ? (float)cnt / (float)total : (float)cnt;
+    if (pi_out && l < 50) pi_out[l] = pi_lane;
+    // argmax of visits / root.visits: with N < 2^53 the quotient is monotone and injective
+    // in N, so the last maximum of N is the reference's choice
+    const int64_t key = l < K ? (int64_t)ch.N : INT64_MIN;
+    best_lane = wave_argmax_last(key);
+    best_mv = (uint32_t)__shfl((int)ch.misc, best_lane) & 0xFFFFu;
+    K_out = K;
+}
+
+__global__ void __launch_bounds__(kBlock) k_search_finalize(TreeView t, const oaz_state* __restrict__ roots,
+                                                            oaz_move* out_move, float* out_pi) {
+    const uint32_t g = wave_game();
+    if (g >= t.G) return;
+    const int l = lane_id();
+    const oaz_node* T = t.nodes + (size_t)g * t.cap;
+    float pl;
+    int best, K;
+    uint32_t mv;
+    root_pi_best(T, out_pi ? out_pi + (size_t)g * 50 : nullptr, pl, best, K, mv);
+    if (l == 0 && out_move) {
+        oaz_move m;
+        if (K == 0) {  // no legal move (Q6): pass with the mover's first card
+            m.from = 25;
+            m.to = 25;
+            m.piece = 0;
+            m.slot = (uint8_t)((roots[g].to_move & 1) ? 2 : 0);
+        } else {
+            m.from = (uint8_t)mv_from(mv);
+            m.to = (uint8_t)mv_to(mv);
+            m.piece = (uint8_t)mv_piece(mv);
+            m.slot = (uint8_t)mv_slot(mv);
+        }
+        out_move[g] = m;
+    }
+}
+
+__device__ void start_game(const SlotView& sv, uint32_t g, uint32_t seq, bool lane0) {
+    const uint64_t gid = (uint64_t)seq * sv.world_games + sv.rank_base + g;
+    const bool act = sv.quota == 0 || gid < sv.quota;
+    uint8_t deck[5];
+    if (sv.fixed_deck) {
+        for (int i = 0; i < 5; ++i) deck[i] = sv.deck[i];
+    } else {
+        deal_deck(sv.seed, gid, deck);
+    }
+    oaz_state s;
+    initial_state(deck, s);
+    if (lane0) {
+        store_state(&sv.root[g], s);
+        sv.ply[g] = 0;
+        sv.seq[g] = seq;
+        sv.game_id[g] = gid;
+        sv.active[g] = act ? 1 : 0;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_selfplay_reset(TreeView t, SlotView sv) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= t.G) return;
+    start_game(sv, g, 0, true);
+    store_fresh_node(&t.nodes[(size_t)g * t.cap], 1.0, 0);
+    t.n_nodes[g] = 1;
+}
+
+// One ply of self_play (train.rs:55-80) per slot: record (state, pi, colour), play the most
+// visited move (no temperature, Q9), detect the end (win, or the 152-ply cut of
+// train.rs:74-79), emit z = reward(result, colour) for every sample (train.rs:83-85), deal the
+// next game, and reset the tree (a fresh tree per move, alphazero_mcts/mod.rs:68-77).
+__global__ void __launch_bounds__(kBlock) k_selfplay_move(TreeView t, SlotView sv) {
+    const uint32_t g = wave_game();
+    if (g >= t.G) return;
+    if (!sv.active[g]) return;
+    const int l = lane_id();
+    oaz_node* T = t.nodes + (size_t)g * t.cap;
+    uint64_t* st = t.stats + (size_t)g * GS_COUNT;
+    oaz_state s = load_state(&sv.root[g]);
+    const uint32_t ply = sv.ply[g];
+    oaz_sample* hist = sv.hist + (size_t)g * sv.hcap;
+    float pl;
+    int best, K;
+    uint32_t mv;
+    const uint32_t hslot = ply < sv.hcap ? ply : sv.hcap - 1;
+    root_pi_best(T, hist[hslot].pi, pl, best, K, mv);
+    if (l == 0) {
+        store_state(&hist[hslot].state, s);
+        hist[hslot].z = 0.0f;
+    }
+    const int color = s.to_move & 1;
+    int res;
+    if (K == 0) {  // pass (state.rs:139-142) with the mover's first card (Q6)
+        const int slot = color ? 2 : 0;
+        const uint8_t c = s.cards[slot];
+        s.cards[slot] = s.cards[4];
+        s.cards[4] = c;
+        res = OAZ_IN_PROGRESS;
+        if (l == 0) st[GS_PASSES] += 1;
+    } else {
+        res = make_move(s, mv_from(mv), mv_to(mv), mv_piece(mv), mv_slot(mv), color);
+    }
+    s.to_move ^= 1;
+    const uint32_t nply = ply + 1;
+    const bool over = is_win(res) || (int)nply >= sv.max_plies + 2;
+    if (l == 0) st[GS_MOVES] += 1;
+    if (over) {
+        const uint32_t n = nply < sv.hcap ? nply : sv.hcap;
+        unsigned long long base = 0;
+        if (l == 0) base = atomicAdd(sv.out_count, (unsigned long long)n);
+        base = __shfl(base, 0);
+        for (uint32_t i = (uint32_t)l; i < n; i += 64) {
+            oaz_sample smp = hist[i];
+            smp.z = (float)reward(res, smp.state.to_move & 1);
+            if (base + i < sv.out_cap) sv.out[base + i] = smp;
+        }
+        if (l == 0) {
+            st[GS_FINISHED] += 1;
+            if (!is_win(res)) st[GS_CUT] += 1;
+            if (res == OAZ_RED_WIN) st[GS_RED] += 1;
+            if (res == OAZ_BLUE_WIN) st[GS_BLUE] += 1;
+            if (base + n > sv.out_cap)
+                st[GS_DROPPED] += (base >= sv.out_cap) ? n : (uint32_t)(base + n - sv.out_cap);
+        }
+        start_game(sv, g, sv.seq[g] + 1, l == 0);
+    } else if (l == 0) {
+        store_state(&sv.root[g], s);
+        sv.ply[g] = nply;
+    }
+    if (l == 0) {
+        store_fresh_node(&T[0], 1.0, 0);
+        t.n_nodes[g] = 1;
+    }
+}
+
+__global__ void k_stats_reduce(const uint64_t* per_game, uint32_t G, uint64_t* out) {
+    const int c = blockIdx.x;  // one block per counter
+    uint64_t acc = 0;
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) {
+        const uint64_t v = per_game[(size_t)g * GS_COUNT + c];
+        acc = c == GS_MAXNODES ? (v > acc ? v : acc) : acc + v;
+    }
+    __shared__ uint64_t red[256];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            const uint64_t o = red[threadIdx.x + s];
+            red[threadIdx.x] = c == GS_MAXNODES ? (o > red[threadIdx.x] ? o : red[threadIdx.x])
+                                                : red[threadIdx.x] + o;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[c] = red[0];
+}
+
+// ---- launchers ----------------------------------------------------------------------------
+static inline unsigned wave_grid(uint32_t n) { return (n + kWavesPerBlock - 1) / kWavesPerBlock; }
+static inline unsigned thread_grid(long long n, int b) { return (unsigned)((n + b - 1) / b); }
+
+hipError_t launch_movegen(const oaz_state* s, int n, uint32_t* masks, oaz_move* moves,
+                          uint8_t* counts, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_movegen, dim3(wave_grid(n)), dim3(kBlock), 0, st, s, n, masks, moves, counts);
+    return hipGetLastError();
+}
+hipError_t launch_step(oaz_state* s, const oaz_move* mv, int n, uint8_t* results, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_step, dim3(thread_grid(n, 256)), dim3(256), 0, st, s, mv, n, results);
+    return hipGetLastError();
+}
+hipError_t launch_current_state(const oaz_state* s, int n, uint8_t* results, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_current_state, dim3(thread_grid(n, 256)), dim3(256), 0, st, s, n, results);
+    return hipGetLastError();
+}
+hipError_t launch_encode(const oaz_state* s, int n, float* planes, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_encode, dim3(thread_grid((long long)n * 525, 256)), dim3(256), 0, st, s, n, planes);
+    return hipGetLastError();
+}
+hipError_t launch_hash_eval(const oaz_state* s, int B, float* policy, float* value, hipStream_t st) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hash_eval, dim3(thread_grid(B, 256)), dim3(256), 0, st, s, B, policy, value);
+    return hipGetLastError();
+}
+hipError_t launch_tree_reset(const TreeView& t, hipStream_t st) {
+    hipLaunchKernelGGL(k_tree_reset, dim3(thread_grid(t.G, kBlock)), dim3(kBlock), 0, st, t);
+    return hipGetLastError();
+}
+hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
+                         const uint64_t* game_id, const uint32_t* ply, SearchParams p,
+                         uint32_t sim, hipStream_t st) {
+    hipLaunchKernelGGL(k_select, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, roots, active,
+                       game_id, ply, p, sim);
+    return hipGetLastError();
+}
+hipError_t launch_expand_backup(const TreeView& t, const oaz_state* roots, const uint8_t* active,
+                                const float* policy, const float* value, hipStream_t st) {
+    hipLaunchKernelGGL(k_expand_backup, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, roots,
+                       active, policy, value);
+    return hipGetLastError();
+}
+hipError_t launch_search_finalize(const TreeView& t, const oaz_state* roots, oaz_move* out_move,
+                                  float* out_pi, hipStream_t st) {
+    hipLaunchKernelGGL(k_search_finalize, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, roots,
+                       out_move, out_pi);
+    return hipGetLastError();
+}
+hipError_t launch_selfplay_move(const TreeView& t, const SlotView& s, hipStream_t st) {
+    hipLaunchKernelGGL(k_selfplay_move, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, s);
+    return hipGetLastError();
+}
+hipError_t launch_selfplay_reset(const TreeView& t, const SlotView& s, hipStream_t st) {
+    hipLaunchKernelGGL(k_selfplay_reset, dim3(thread_grid(t.G, kBlock)), dim3(kBlock), 0, st, t, s);
+    return hipGetLastError();
+}
+hipError_t launch_stats_reduce(const uint64_t* per_game, uint32_t G, uint64_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_stats_reduce, dim3(GS_COUNT), dim3(256), 0, st, per_game, G, out);
+    return hipGetLastError();
+}
+
+}  // namespace oaz

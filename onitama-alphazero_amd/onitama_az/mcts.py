@@ -1,0 +1,170 @@
+"""Mirror of alphazero-training's search/agent API over the GPU engine.
+
+Reference: alphazero-training/src/alphazero_mcts/mod.rs (AlphaZeroMctsConfig, reward,
+TrainingAlphaZeroMcts::generate_move_tensor, AlphaZeroMcts as an Agent), net.rs
+(ConvResNetConfig / ConvResNet::forward) and onitama-game/src/ai/agent.rs (trait Agent).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _abi
+from .engine import Engine
+from .game import DoneMove, GameState, MoveResult, PlayerColor, State
+from .weights import random_weights, read_ot, blob_from_named, blocks_from_names
+
+
+@dataclass
+class AlphaZeroMctsConfig:  # alphazero_mcts/mod.rs:26-43
+    search_time: float = 0.4          # seconds; NOT used: searches run exactly max_playouts (Q7)
+    exploration_c: float = math.sqrt(2.0)
+    max_playouts: int = 5000
+    train: bool = False
+
+
+def reward(move_result: MoveResult, reward_color: PlayerColor) -> float:  # mod.rs:45-53
+    if move_result == MoveResult.RedWin:
+        return 1.0 if reward_color == PlayerColor.Red else -1.0
+    if move_result == MoveResult.BlueWin:
+        return 1.0 if reward_color == PlayerColor.Blue else -1.0
+    return 0.0
+
+
+@dataclass
+class ConvResNetConfig:  # net.rs:74-89
+    hidden_channels: int = 64
+    input_channels: int = 21
+    resnet_block_amnt: int = 5
+
+
+@dataclass
+class Options:  # common.rs:8-23 (kind/device): precision and GPU ordinal
+    precision: int = _abi.FP32
+    device: int = 0
+
+
+class ConvResNet:
+    """Weights holder; forward() runs the fused HIP kernel (net.rs:215-232)."""
+
+    def __init__(self, net_config: ConvResNetConfig = None, options: Options = None,
+                 weights: Optional[np.ndarray] = None, seed: int = 0):
+        self.config = net_config or ConvResNetConfig()
+        self.options = options or Options()
+        if self.config.hidden_channels != 64 or self.config.input_channels != 21:
+            raise ValueError("only hidden_channels=64, input_channels=21 are supported")
+        b = self.config.resnet_block_amnt
+        self.weights = weights if weights is not None else random_weights(seed, b)
+        self.id = f"conv_input_{self.config.input_channels}_hidden_{self.config.hidden_channels}_resnet_{b}"
+        self._engine: Optional[Engine] = None
+        self._engine_batch = 0
+
+    @staticmethod
+    def from_model_file(path: str, options: Options = None) -> "ConvResNet":
+        """alphazero_mcts/mod.rs:89-105, but a load error raises instead of keeping random
+        weights (Q13)."""
+        named = read_ot(path)
+        b = blocks_from_names(named)
+        return ConvResNet(ConvResNetConfig(resnet_block_amnt=b), options, blob_from_named(named, b))
+
+    def _eval_engine(self, batch: int) -> Engine:
+        if self._engine is None or self._engine_batch < batch:
+            if self._engine is not None:
+                self._engine.close()
+            self._engine = Engine(device=self.options.device, games=max(batch, 64), sims=1,
+                                  blocks=self.config.resnet_block_amnt, evaluator=_abi.EVAL_NN,
+                                  precision=self.options.precision)
+            self._engine.load_weights(self.weights)
+            self._engine_batch = max(batch, 64)
+        return self._engine
+
+    def forward(self, states: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """policy [B,2,25] (softmax over all 50), value [B,1] for STATE_DTYPE positions
+        (colour = state.to_move)."""
+        pol, val = self._eval_engine(len(states)).nn_forward(states)
+        return pol, val.reshape(-1, 1)
+
+
+def _search_engine(cache: dict, config: AlphaZeroMctsConfig, model: ConvResNet, games: int) -> Engine:
+    key = (games, config.max_playouts, config.exploration_c, config.train, model.config.resnet_block_amnt,
+           model.options.device, id(model.weights))
+    eng = cache.get("engine")
+    if eng is None or cache.get("key") != key:
+        if eng is not None:
+            eng.close()
+        eng = Engine(device=model.options.device, games=games, sims=config.max_playouts,
+                     c_puct=config.exploration_c, train_noise=int(config.train),
+                     blocks=model.config.resnet_block_amnt, evaluator=_abi.EVAL_NN,
+                     precision=model.options.precision)
+        eng.load_weights(model.weights)
+        cache["engine"], cache["key"] = eng, key
+    return eng
+
+
+class TrainingAlphaZeroMcts:  # alphazero_mcts/mod.rs:55-79
+    def __init__(self, config: AlphaZeroMctsConfig, model: ConvResNet, options: Options = None):
+        self.config, self.model, self.options = config, model, options or model.options
+        self._cache: dict = {}
+
+    def generate_move_tensor(self, state: State, curr_player_color: PlayerColor) -> Tuple[DoneMove, np.ndarray]:
+        """(DoneMove, pi [2,25]) — one search of max_playouts simulations."""
+        eng = _search_engine(self._cache, self.config, self.model, 1)
+        r = eng.search(state.to_np(curr_player_color))
+        return DoneMove.from_c(r.moves[0]), r.pi[0]
+
+    def generate_move_tensors(self, roots: np.ndarray):
+        """Batched form: one search per root, all advanced together on the GPU."""
+        eng = _search_engine(self._cache, self.config, self.model, len(roots))
+        r = eng.search(roots)
+        return r.moves, r.pi
+
+
+class Agent:  # onitama-game/src/ai/agent.rs:7-17
+    def generate_move(self, game_state: GameState) -> Tuple[DoneMove, float]:
+        raise NotImplementedError
+
+    def name(self) -> str:
+        raise NotImplementedError
+
+    def clone_dyn(self) -> "Agent":
+        raise NotImplementedError
+
+    def id(self) -> int:
+        raise NotImplementedError
+
+
+class AlphaZeroMcts(Agent):  # alphazero_mcts/mod.rs:81-161
+    def __init__(self, config: AlphaZeroMctsConfig, model: ConvResNet, options: Options = None):
+        self.config, self.model, self.options = config, model, options or model.options
+        self._cache: dict = {}
+
+    @staticmethod
+    def from_model_file(model_path: str, config: AlphaZeroMctsConfig, net_config: ConvResNetConfig = None,
+                        options: Options = None) -> "AlphaZeroMcts":
+        return AlphaZeroMcts(config, ConvResNet.from_model_file(model_path, options), options)
+
+    def generate_move(self, game_state: GameState) -> Tuple[DoneMove, float]:
+        """search + an extra root evaluation for the returned value (mod.rs:123-144)."""
+        eng = _search_engine(self._cache, self.config, self.model, 1)
+        r = eng.search(game_state.state.to_np(game_state.curr_player_color), root_value=True)
+        return DoneMove.from_c(r.moves[0]), float(r.root_value[0])
+
+    def generate_moves(self, game_states) -> Tuple[list, np.ndarray]:
+        """Batched Agent call: one search per game state, advanced together (arena use)."""
+        roots = np.concatenate([g.state.to_np(g.curr_player_color) for g in game_states])
+        eng = _search_engine(self._cache, self.config, self.model, len(roots))
+        r = eng.search(roots, root_value=True)
+        return [DoneMove.from_c(m) for m in r.moves], r.root_value
+
+    def name(self) -> str:
+        return "AlphaZero MCTS AI"
+
+    def clone_dyn(self) -> "AlphaZeroMcts":
+        return AlphaZeroMcts(self.config, self.model, self.options)
+
+    def id(self) -> int:  # mod.rs:154-160 (model id digits are not numeric here: hashed)
+        return (int(self.config.search_time * 1e9) + int(self.config.exploration_c) + self.config.max_playouts
+                + int(self.config.train) + (hash(self.model.id) & 0xFFFFFFFF))

@@ -1,0 +1,229 @@
+"""Weights: canonical blob order, random init, and a safe reader for the reference's .ot files.
+
+Canonical order = the order in which the reference's tch VarStore creates the variables
+(net.rs:101-213), with tch's '|'-joined names:
+    conv_init_1|{weight,bias}, bn1|{weight,bias,running_mean,running_var},
+    resnet_{i}|resnet_small_block{1,2}|small_block_conv|{weight,bias},
+    resnet_{i}|resnet_small_block{1,2}|small_block_bn|{weight,bias,running_mean,running_var},
+    vh_conv|..., vh_bn|..., vh_linear1|..., vh_linear2|...,
+    policy_conv|..., policy_bn|..., ph_linear2|...
+
+The .ot files (TorchScript zip archives written by VarStore::save) are read WITHOUT unpickling
+or executing anything: data.pkl is walked opcode by opcode with pickletools.genops and only
+the (name -> storage key, shape, stride, offset) records are interpreted; tensor bytes come
+straight from the stored zip members (little-endian f32).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import pickletools
+import zipfile
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+from . import _abi
+
+CH, INP = 64, 21
+_BN = ("weight", "bias", "running_mean", "running_var")
+
+
+def canonical_layout(blocks: int) -> List[Tuple[str, Tuple[int, ...]]]:
+    out: List[Tuple[str, Tuple[int, ...]]] = []
+
+    def conv(name, cout, cin, k):
+        out.append((f"{name}|weight", (cout, cin, k, k)))
+        out.append((f"{name}|bias", (cout,)))
+
+    def bn(name, c):
+        out.extend((f"{name}|{f}", (c,)) for f in _BN)
+
+    conv("conv_init_1", CH, INP, 3)
+    bn("bn1", CH)
+    for i in range(blocks):
+        for j in (1, 2):
+            p = f"resnet_{i}|resnet_small_block{j}"
+            conv(f"{p}|small_block_conv", CH, CH, 3)
+            bn(f"{p}|small_block_bn", CH)
+    conv("vh_conv", 1, CH, 1)
+    bn("vh_bn", 1)
+    out.append(("vh_linear1|weight", (CH, 25)))
+    out.append(("vh_linear1|bias", (CH,)))
+    out.append(("vh_linear2|weight", (1, CH)))
+    out.append(("vh_linear2|bias", (1,)))
+    conv("policy_conv", 2, CH, 1)
+    bn("policy_bn", 2)
+    out.append(("ph_linear2|weight", (50, 50)))
+    out.append(("ph_linear2|bias", (50,)))
+    return out
+
+
+def weight_count(blocks: int) -> int:
+    return int(sum(int(np.prod(s)) for _, s in canonical_layout(blocks)))
+
+
+def blob_from_named(named: Dict[str, np.ndarray], blocks: int) -> np.ndarray:
+    parts = []
+    for name, shape in canonical_layout(blocks):
+        if name not in named:
+            raise KeyError(f"missing tensor {name}")
+        a = np.asarray(named[name], dtype=np.float32)
+        if tuple(a.shape) != shape:
+            raise ValueError(f"{name}: shape {a.shape} != {shape}")
+        parts.append(a.reshape(-1))
+    return np.ascontiguousarray(np.concatenate(parts))
+
+
+def named_from_blob(blob: np.ndarray, blocks: int) -> Dict[str, np.ndarray]:
+    out, off = {}, 0
+    for name, shape in canonical_layout(blocks):
+        n = int(np.prod(shape))
+        out[name] = blob[off: off + n].reshape(shape)
+        off += n
+    assert off == len(blob)
+    return out
+
+
+def random_weights(seed: int, blocks: int) -> np.ndarray:
+    """The engine's random init (oaz_random_weights): U(+-1/sqrt(fan_in)), BN identity."""
+    n = weight_count(blocks)
+    w = np.zeros(n, dtype=np.float32)
+    _abi.check(_abi.load().oaz_random_weights(C.c_uint64(seed), blocks, _abi.ptr(w), n))
+    return w
+
+
+def blocks_from_names(names) -> int:
+    idx = {int(n.split("|")[0].split("_")[1]) for n in names if n.startswith("resnet_")}
+    return (max(idx) + 1) if idx else 0
+
+
+# ---- safe .ot reader -------------------------------------------------------------------------
+class _Sym:
+    """Symbolic stand-in for a pickle GLOBAL/REDUCE result (never resolved or called)."""
+
+    def __init__(self, name, args=None):
+        self.name, self.args = name, args
+
+
+def _walk_pickle(data: bytes):
+    """Interpret a restricted opcode subset into plain Python values; nothing is imported."""
+    stack, memo, marks = [], {}, []
+    for op, arg, _pos in pickletools.genops(data):
+        n = op.name
+        if n in ("PROTO", "FRAME", "STOP"):
+            continue
+        if n in ("BINUNICODE", "SHORT_BINUNICODE", "BININT1", "BININT2", "BININT", "LONG1",
+                 "BINFLOAT", "SHORT_BINSTRING", "BINSTRING", "UNICODE", "INT"):
+            stack.append(arg)
+        elif n == "NEWTRUE":
+            stack.append(True)
+        elif n == "NEWFALSE":
+            stack.append(False)
+        elif n == "NONE":
+            stack.append(None)
+        elif n == "GLOBAL":
+            stack.append(_Sym(arg))
+        elif n in ("BINPUT", "LONG_BINPUT"):
+            memo[arg] = stack[-1]
+        elif n == "MEMOIZE":
+            memo[len(memo)] = stack[-1]
+        elif n in ("BINGET", "LONG_BINGET"):
+            stack.append(memo[arg])
+        elif n == "MARK":
+            marks.append(len(stack))
+        elif n == "TUPLE":
+            k = marks.pop()
+            t = tuple(stack[k:])
+            del stack[k:]
+            stack.append(t)
+        elif n == "EMPTY_TUPLE":
+            stack.append(())
+        elif n == "TUPLE1":
+            stack[-1:] = [tuple(stack[-1:])]
+        elif n == "TUPLE2":
+            stack[-2:] = [tuple(stack[-2:])]
+        elif n == "TUPLE3":
+            stack[-3:] = [tuple(stack[-3:])]
+        elif n == "EMPTY_DICT":
+            stack.append({})
+        elif n == "EMPTY_LIST":
+            stack.append([])
+        elif n == "SETITEMS":
+            k = marks.pop()
+            items = stack[k:]
+            del stack[k:]
+            d = stack[-1]
+            if isinstance(d, dict):
+                for i in range(0, len(items), 2):
+                    d[items[i]] = items[i + 1]
+        elif n == "SETITEM":
+            v = stack.pop()
+            key = stack.pop()
+            if isinstance(stack[-1], dict):
+                stack[-1][key] = v
+        elif n == "APPENDS":
+            k = marks.pop()
+            items = stack[k:]
+            del stack[k:]
+            if isinstance(stack[-1], list):
+                stack[-1].extend(items)
+        elif n == "APPEND":
+            v = stack.pop()
+            if isinstance(stack[-1], list):
+                stack[-1].append(v)
+        elif n == "BINPERSID":
+            stack.append(_Sym("persid", stack.pop()))
+        elif n in ("REDUCE", "NEWOBJ"):
+            args = stack.pop()
+            f = stack.pop()
+            stack.append(_Sym(getattr(f, "name", "?"), args))
+        elif n == "BUILD":
+            state = stack.pop()
+            obj = stack[-1]
+            if isinstance(obj, _Sym) and isinstance(state, dict):
+                obj.args = (obj.args, state)
+        else:
+            raise ValueError(f"unsupported pickle opcode {n}")
+    return stack[-1] if stack else None
+
+
+def _find_tensors(obj, out):
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            if isinstance(v, _Sym) and v.name == "torch._utils _rebuild_tensor_v2":
+                out[k] = v.args
+            else:
+                _find_tensors(v, out)
+    elif isinstance(obj, _Sym):
+        _find_tensors(obj.args, out)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _find_tensors(v, out)
+
+
+def read_ot(path: str) -> Dict[str, np.ndarray]:
+    """Named fp32 tensors of a tch VarStore .ot archive (VarStore::save, train.rs:414-430)."""
+    z = zipfile.ZipFile(path)
+    pkl = [n for n in z.namelist() if n.endswith("/data.pkl") or n == "data.pkl"]
+    if not pkl:
+        raise ValueError(f"{path}: no data.pkl")
+    root = pkl[0][: -len("data.pkl")]
+    obj = _walk_pickle(z.read(pkl[0]))
+    recs: Dict[str, tuple] = {}
+    _find_tensors(obj, recs)
+    out = {}
+    for name, args in recs.items():
+        # args = (persistent_id, offset, shape, stride, requires_grad, hooks)
+        # persistent_id.args = ('storage', <GLOBAL torch FloatStorage>, key, location, numel)
+        pers, offset, shape, stride = args[0], args[1], tuple(args[2]), tuple(args[3])
+        storage_type = pers.args[1].name if isinstance(pers.args[1], _Sym) else ""
+        if storage_type != "torch FloatStorage":
+            raise ValueError(f"{name}: unsupported storage {storage_type}")
+        key = pers.args[2]
+        raw = np.frombuffer(z.read(f"{root}data/{key}"), dtype="<f4")
+        n = int(np.prod(shape)) if shape else 1
+        a = np.lib.stride_tricks.as_strided(raw[offset:], shape=shape, strides=tuple(4 * s for s in stride)) \
+            if shape else raw[offset: offset + 1].reshape(())
+        out[name] = np.array(a, dtype=np.float32).reshape(shape)
+        assert out[name].size == n
+    return out

@@ -1,0 +1,236 @@
+"""ctypes binding of the C oracle (oracle/oaz_oracle.h) — TEST INFRASTRUCTURE ONLY.
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+from typing import Callable, Optional, Tuple
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+ORACLE_SO = ROOT / "oracle" / "build" / "liboaz_oracle.so"
+
+import sys  # noqa: E402
+
+sys.path.insert(0, str(ROOT / "onitama-alphazero_amd"))
+from onitama_az import _abi  # noqa: E402
+
+EVAL_NN, EVAL_HASH, EVAL_CALLBACK = 0, 1, 2
+EVAL_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float))
+
+
+class orc_search_cfg(C.Structure):
+    _fields_ = [
+        ("sims", C.c_int),
+        ("c_puct", C.c_double),
+        ("train_noise", C.c_int),
+        ("alpha", C.c_double),
+        ("eps", C.c_double),
+        ("seed", C.c_uint64),
+        ("game_id", C.c_uint64),
+        ("ply", C.c_uint32),
+        ("evaluator", C.c_int),
+        ("weights", C.c_void_p),
+        ("blocks", C.c_int),
+        ("fn", EVAL_FN),
+        ("ctx", C.c_void_p),
+    ]
+
+
+class orc_selfplay_cfg(C.Structure):
+    _fields_ = [("search", orc_search_cfg), ("max_plies", C.c_int), ("fixed_deck", C.c_int),
+                ("deck", C.c_uint8 * 5)]
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not ORACLE_SO.exists():
+        subprocess.run(["make", "-C", str(ROOT / "oracle")], check=True, capture_output=True)
+    lib = C.CDLL(str(ORACLE_SO))
+    V, P = C.c_void_p, C.POINTER
+    protos = {
+        "orc_attack_maps": (None, [V]),
+        "orc_card_positions": (C.c_uint32, [C.c_int]),
+        "orc_card_mirror": (C.c_uint32, [C.c_int]),
+        "orc_card_color": (C.c_int, [C.c_int]),
+        "orc_initial_state": (None, [V, V]),
+        "orc_movegen": (C.c_int, [V, C.c_int, V]),
+        "orc_movegen_masks": (None, [V, C.c_int, V]),
+        "orc_make_move": (C.c_int, [V, V, C.c_int]),
+        "orc_current_state": (C.c_int, [V]),
+        "orc_is_terminal": (C.c_int, [V]),
+        "orc_encode": (None, [V, C.c_int, V]),
+        "orc_philox": (None, [C.c_uint64, V, V]),
+        "orc_deal_deck": (None, [C.c_uint64, C.c_uint64, V]),
+        "orc_hash_eval": (None, [V, V, V]),
+        "orc_weight_count": (C.c_size_t, [C.c_int]),
+        "orc_nn_forward": (C.c_int, [V, C.c_int, V, C.c_int, V, V]),
+        "orc_search": (C.c_int, [P(orc_search_cfg), V, V, V, V, C.c_int, P(C.c_int), P(_abi.oaz_search_stats)]),
+        "orc_selfplay_game": (C.c_int, [P(orc_selfplay_cfg), C.c_uint64, V, C.c_int, P(C.c_int), P(C.c_int),
+                                        P(_abi.oaz_search_stats)]),
+        "orc_selfplay_bench": (C.c_int64, [P(orc_selfplay_cfg), C.c_int, C.c_double, P(C.c_int64), P(C.c_int64)]),
+    }
+    for name, (res, args) in protos.items():
+        f = getattr(lib, name)
+        f.restype, f.argtypes = res, args
+    _lib = lib
+    return lib
+
+
+def P_(a: np.ndarray) -> C.c_void_p:
+    assert a.flags["C_CONTIGUOUS"]
+    return C.c_void_p(a.ctypes.data)
+
+
+def state(kings, pawns, cards, to_move) -> np.ndarray:
+    a = np.zeros(1, dtype=_abi.STATE_DTYPE)
+    a["kings"][0], a["pawns"][0], a["cards"][0], a["to_move"][0] = kings, pawns, cards, to_move
+    return a
+
+
+def initial_state(deck) -> np.ndarray:
+    a = np.zeros(1, dtype=_abi.STATE_DTYPE)
+    d = np.ascontiguousarray(deck, dtype=np.uint8)
+    load().orc_initial_state(P_(d), P_(a))
+    return a
+
+
+def attack_maps() -> np.ndarray:
+    out = np.zeros((2, 16, 25), dtype=np.uint32)
+    load().orc_attack_maps(P_(out))
+    return out
+
+
+def movegen(s: np.ndarray, color: Optional[int] = None) -> np.ndarray:
+    s = np.ascontiguousarray(s.reshape(1))
+    out = np.zeros(40, dtype=_abi.MOVE_DTYPE)
+    c = int(s["to_move"][0]) if color is None else color
+    n = load().orc_movegen(P_(s), c, P_(out))
+    return out[:n]
+
+
+def movegen_masks(s: np.ndarray, color: Optional[int] = None) -> np.ndarray:
+    s = np.ascontiguousarray(s.reshape(1))
+    out = np.zeros((2, 25), dtype=np.uint32)
+    c = int(s["to_move"][0]) if color is None else color
+    load().orc_movegen_masks(P_(s), c, P_(out))
+    return out
+
+
+def make_move(s: np.ndarray, mv, color: int) -> int:
+    """In place on a 1-element STATE array (to_move NOT switched, as State::make_move)."""
+    m = np.zeros(1, dtype=_abi.MOVE_DTYPE)
+    m[0] = mv
+    return load().orc_make_move(P_(s), P_(m), color)
+
+
+def current_state(s: np.ndarray) -> int:
+    return load().orc_current_state(P_(np.ascontiguousarray(s.reshape(1))))
+
+
+def encode(s: np.ndarray, color: Optional[int] = None) -> np.ndarray:
+    s = np.ascontiguousarray(s.reshape(1))
+    out = np.zeros((21, 5, 5), dtype=np.float32)
+    load().orc_encode(P_(s), int(s["to_move"][0]) if color is None else color, P_(out))
+    return out
+
+
+def deal_deck(seed: int, game_id: int) -> np.ndarray:
+    out = np.zeros(5, dtype=np.uint8)
+    load().orc_deal_deck(seed, game_id, P_(out))
+    return out
+
+
+def hash_eval(s: np.ndarray) -> Tuple[np.ndarray, float]:
+    s = np.ascontiguousarray(s.reshape(1))
+    p = np.zeros(50, dtype=np.float32)
+    v = np.zeros(1, dtype=np.float32)
+    load().orc_hash_eval(P_(s), P_(p), P_(v))
+    return p, float(v[0])
+
+
+def philox(key: int, ctr) -> np.ndarray:
+    c = np.ascontiguousarray(ctr, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    load().orc_philox(key, P_(c), P_(out))
+    return out
+
+
+def nn_forward(weights: np.ndarray, blocks: int, states: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    w = np.ascontiguousarray(weights, dtype=np.float32)
+    states = np.ascontiguousarray(states, dtype=_abi.STATE_DTYPE)
+    B = len(states)
+    pol = np.zeros((B, 50), dtype=np.float32)
+    val = np.zeros(B, dtype=np.float32)
+    rc = load().orc_nn_forward(P_(w), blocks, P_(states), B, P_(pol), P_(val))
+    assert rc == 0
+    return pol.reshape(B, 2, 25), val
+
+
+def search_cfg(sims=50, c_puct=5.0, train_noise=0, evaluator=EVAL_HASH, weights=None, blocks=0,
+               fn: Optional[Callable] = None, seed=20260101, game_id=0, ply=0, alpha=0.03, eps=0.25):
+    cfg = orc_search_cfg()
+    cfg.sims, cfg.c_puct, cfg.train_noise = sims, c_puct, train_noise
+    cfg.alpha, cfg.eps, cfg.seed, cfg.game_id, cfg.ply = alpha, eps, seed, game_id, ply
+    cfg.evaluator, cfg.blocks = evaluator, blocks
+    keep = []
+    if weights is not None:
+        w = np.ascontiguousarray(weights, dtype=np.float32)
+        keep.append(w)
+        cfg.weights = w.ctypes.data
+    if fn is not None:
+        cb = EVAL_FN(fn)
+        keep.append(cb)
+        cfg.fn = cb
+    cfg._keep = keep  # keep buffers/callbacks alive with the struct
+    return cfg
+
+
+def search(cfg: orc_search_cfg, root: np.ndarray, tree: bool = True):
+    root = np.ascontiguousarray(root.reshape(1), dtype=_abi.STATE_DTYPE)
+    mv = np.zeros(1, dtype=_abi.MOVE_DTYPE)
+    pi = np.zeros(50, dtype=np.float32)
+    cap = 1 + cfg.sims * 40
+    nodes = np.zeros(cap if tree else 0, dtype=_abi.NODE_DTYPE)
+    n = C.c_int(0)
+    st = _abi.oaz_search_stats()
+    rc = load().orc_search(C.byref(cfg), P_(root), P_(mv), P_(pi), P_(nodes) if tree else None,
+                           cap if tree else 0, C.byref(n), C.byref(st))
+    assert rc == 0, rc
+    return mv[0], pi.reshape(2, 25), (nodes[: n.value] if tree else None), st
+
+
+def selfplay_game(search: orc_search_cfg, game_id: int, max_plies=150, deck=None):
+    cfg = orc_selfplay_cfg()
+    cfg.search, cfg.max_plies = search, max_plies
+    if deck is not None:
+        cfg.fixed_deck = 1
+        for i, c in enumerate(deck):
+            cfg.deck[i] = int(c)
+    out = np.zeros(max_plies + 2, dtype=_abi.SAMPLE_DTYPE)
+    res, plies = C.c_int(0), C.c_int(0)
+    st = _abi.oaz_search_stats()
+    n = load().orc_selfplay_game(C.byref(cfg), game_id, P_(out), len(out), C.byref(res), C.byref(plies), C.byref(st))
+    assert n >= 0
+    return out[:n], res.value, plies.value, st
+
+
+def selfplay_bench(search: orc_search_cfg, threads: int, seconds: float, max_plies=150, deck=None):
+    cfg = orc_selfplay_cfg()
+    cfg.search, cfg.max_plies = search, max_plies
+    if deck is not None:
+        cfg.fixed_deck = 1
+        for i, c in enumerate(deck):
+            cfg.deck[i] = int(c)
+    games, plies = C.c_int64(0), C.c_int64(0)
+    sims = load().orc_selfplay_bench(C.byref(cfg), threads, seconds, C.byref(games), C.byref(plies))
+    return sims, games.value, plies.value

@@ -1,0 +1,269 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and the goldens.
+
+Bars: rules/moves/masks/results bit-exact; NN within 1e-4 of torch-CPU goldens; MCTS trees
+bit-exact (every node's N, W, P, move, children, flags) against the oracle whenever both run
+the same evaluator outputs (HASH test evaluator, or the GPU network fed to the oracle).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import kat_state, random_positions
+from onitama_az import _abi
+from onitama_az.engine import Engine
+from onitama_az.game import (Deck, DoneMove, GameState, Move, MoveResult, PieceKind, PlayerColor, State,
+                             ORIGINAL_CARDS, CARD_NAMES, current_state_batch, encode_batch, movegen_batch,
+                             movegen_masks_batch, step_batch)
+from onitama_az.weights import random_weights
+
+pytestmark = pytest.mark.gpu
+
+NODE_FIELDS = ("W", "P", "N", "first", "mv", "nch", "flags")
+
+
+def _mv(m):
+    return tuple(int(m[k]) for k in ("from_", "to", "piece", "slot"))
+
+
+# ---- rules -------------------------------------------------------------------------------
+def test_rules_kats_through_mirror(kats):
+    for case in kats["movegen"]:  # state.rs:419-492, 818-889
+        d = case["state"]
+        st = State(Deck([ORIGINAL_CARDS[i] for i in d["deck"]]), d["kings"], d["pawns"])
+        card = st.deck.cards[case["slot"]]
+        got = sorted(st.generate_legal_moves(PlayerColor(case["color"]), card))
+        assert got == sorted(Move(a, b, PieceKind(c)) for a, b, c in case["moves"]), case["src"]
+    for case in kats["make_move"]:  # state.rs:494-816
+        d = case["state"]
+        st = State(Deck([ORIGINAL_CARDS[i] for i in d["deck"]]), d["kings"], d["pawns"])
+        f, t, p, slot = case["move"]
+        res = st.make_move(Move(f, t, PieceKind(p)), PlayerColor(case["color"]), slot)
+        assert res == MoveResult(case["result"]), case["src"]
+        for field, color, sq, val in case["bits"]:
+            assert (getattr(st, field)[color] >> (31 - sq)) & 1 == val
+        assert st.deck.neutral_card().index == case["neutral"]
+        for field, color, val in case.get("equals", []):
+            assert getattr(st, field)[color] == val
+    for case in kats["expansion"]:  # onitama-game/src/ai/mcts/mcts_arena.rs:403-457
+        d = case["state"]
+        st = State(Deck([ORIGINAL_CARDS[i] for i in d["deck"]]), d["kings"], d["pawns"])
+        got = [f"{CARD_NAMES[st.deck.cards[s].index]} {Move.convert_idx_to_notation(m.from_)}-"
+               f"{Move.convert_idx_to_notation(m.to)}" for s, m in st.generate_all_legal_moves(PlayerColor(case["color"]))]
+        assert got == case["children"], case["src"]
+
+
+def test_movegen_bitexact_vs_oracle(orc):
+    pos = random_positions(orc, 20000, seed=101)
+    masks = movegen_masks_batch(pos)
+    moves, counts = movegen_batch(pos)
+    for i in range(len(pos)):
+        ref = orc.movegen(pos[i])
+        assert counts[i] == len(ref)
+        assert moves[i, : len(ref)].tobytes() == ref.tobytes()
+        assert np.array_equal(masks[i], orc.movegen_masks(pos[i]))
+
+
+def test_step_and_terminal_bitexact_vs_oracle(orc):
+    import random
+    rng = random.Random(5)
+    pos = random_positions(orc, 5000, seed=202)
+    moves, counts = movegen_batch(pos)
+    keep = counts > 0
+    pos, moves, counts = pos[keep], moves[keep], counts[keep]
+    pick = np.array([moves[i, rng.randrange(int(counts[i]))] for i in range(len(pos))], dtype=_abi.MOVE_DTYPE)
+    gpu = pos.copy()
+    res = step_batch(gpu, pick)
+    for i in range(len(pos)):
+        ref = pos[i: i + 1].copy()
+        r = orc.make_move(ref, _mv(pick[i]), int(ref["to_move"][0]))
+        ref["to_move"][0] ^= 1
+        assert res[i] == r
+        assert gpu[i: i + 1].tobytes() == ref.tobytes()
+    cs = current_state_batch(gpu)
+    assert [int(x) for x in cs] == [orc.current_state(gpu[i]) for i in range(len(gpu))]
+
+
+def test_encode_vs_oracle(orc):
+    pos = random_positions(orc, 500, seed=303)
+    planes = encode_batch(pos)
+    for i in range(len(pos)):
+        assert np.array_equal(planes[i], orc.encode(pos[i]))
+
+
+# ---- NN ----------------------------------------------------------------------------------
+@pytest.mark.parametrize("name,blocks", [("trained3", 3), ("random3", 3), ("random6", 6)])
+def test_nn_matches_torch_goldens(nn_golden, trained3, name, blocks):
+    w = trained3 if name == "trained3" else random_weights(0 if name == "random3" else 1, blocks)
+    with Engine(games=256, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN) as e:
+        e.load_weights(w)
+        p, v = e.nn_forward(nn_golden["states"])
+    tol = 1e-4  # north_star: policy/value within 1e-4 fp32
+    assert np.abs(p - nn_golden[f"policy_{name}"]).max() < tol
+    assert np.abs(v - nn_golden[f"value_{name}"]).max() < tol
+    assert np.allclose(p.reshape(-1, 50).sum(1), 1.0, atol=1e-5)
+
+
+def test_nn_batch_position_invariance(orc):
+    pos = random_positions(orc, 64, seed=404)
+    with Engine(games=1024, sims=1, blocks=3) as e:
+        p1, v1 = e.nn_forward(pos)
+        big = np.concatenate([pos[::-1], pos, pos[:7]])
+        p2, v2 = e.nn_forward(big)
+    assert np.array_equal(p2[64:128], p1) and np.array_equal(v2[64:128], v1)
+    assert np.array_equal(p2[:64][::-1], p1)
+
+
+# ---- search ------------------------------------------------------------------------------
+def _compare_trees(e, g, nodes_ref):
+    t = e.tree(g)
+    assert len(t) == len(nodes_ref), (len(t), len(nodes_ref))
+    for f in NODE_FIELDS:
+        a, b = t[f], nodes_ref[f]
+        if f == "first":  # defined only for expanded nodes
+            a, b = np.where(t["flags"] & 1, a, 0), np.where(nodes_ref["flags"] & 1, b, 0)
+        assert np.array_equal(a, b), f
+
+
+@pytest.mark.parametrize("sims,c_puct", [(64, 5.0), (200, 2.0)])
+def test_search_hash_trees_bitexact(orc, sims, c_puct):
+    roots = random_positions(orc, 12, seed=505 + sims)
+    with Engine(games=len(roots), sims=sims, c_puct=c_puct, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0) as e:
+        r = e.search(roots)
+        for g in range(len(roots)):
+            cfg = orc.search_cfg(sims=sims, c_puct=c_puct, evaluator=orc.EVAL_HASH)
+            mv, pi, nodes, st = orc.search(cfg, roots[g])
+            _compare_trees(e, g, nodes)
+            assert np.array_equal(r.pi[g].reshape(-1), pi.reshape(-1))
+            assert _mv(r.moves[g]) == _mv(mv)
+    assert r.stats.sims == sims * len(roots)
+
+
+def test_search_nn_trees_bitexact_with_gpu_evaluator(orc):
+    """Real network: the oracle's search is fed the GPU network's outputs (batch-1 calls of
+    the same kernel), so both searches see identical evaluations and must agree exactly."""
+    roots = random_positions(orc, 4, seed=606)
+    w = random_weights(3, 3)
+    sims = 48
+    with Engine(games=len(roots), sims=sims, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_NN, blocks=3) as e, \
+            Engine(games=4, sims=1, blocks=3) as ev:
+        e.load_weights(w)
+        ev.load_weights(w)
+        r = e.search(roots)
+
+        def cb(ctx, sp, pol, val):
+            s = np.frombuffer(C.string_at(sp, 24), dtype=_abi.STATE_DTYPE).copy()
+            p, v = ev.nn_forward(s)
+            C.memmove(pol, p.ctypes.data, 200)
+            val[0] = float(v[0])
+
+        for g in range(len(roots)):
+            cfg = orc.search_cfg(sims=sims, c_puct=5.0, evaluator=orc.EVAL_CALLBACK, fn=cb)
+            mv, pi, nodes, _ = orc.search(cfg, roots[g])
+            _compare_trees(e, g, nodes)
+            assert _mv(r.moves[g]) == _mv(mv)
+
+
+def test_search_with_root_noise_is_deterministic_and_consistent(orc):
+    roots = random_positions(orc, 16, seed=707)
+    kw = dict(games=16, sims=64, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=99)
+    with Engine(**kw) as e:
+        r1 = e.search(roots)
+        t1 = [e.tree(g) for g in range(16)]
+    with Engine(**kw) as e:
+        r2 = e.search(roots)
+        t2 = [e.tree(g) for g in range(16)]
+    assert np.array_equal(r1.pi, r2.pi) and r1.moves.tobytes() == r2.moves.tobytes()
+    differs = 0
+    for g in range(16):
+        assert t1[g].tobytes() == t2[g].tobytes()
+        root = t1[g][0]
+        if root["nch"]:
+            ch = t1[g][int(root["first"]): int(root["first"]) + int(root["nch"])]
+            assert int(ch["N"].sum()) == 63  # first playout evaluates the root itself
+        cfg = orc.search_cfg(sims=64, c_puct=5.0, evaluator=orc.EVAL_HASH)
+        _, _, nodes, _ = orc.search(cfg, roots[g])
+        differs += int(len(nodes) != len(t1[g]) or not np.array_equal(nodes["N"], t1[g]["N"]))
+    assert differs > 0  # the noise changes the search
+
+
+def test_search_finds_win_in_one(kats):
+    case = kats["tactics"][0]  # onitama-game/src/ai/mcts/mcts_arena.rs:459-483
+    root = kat_state(case["state"], case["color"])
+    for ev in (_abi.EVAL_HASH, _abi.EVAL_NN):
+        with Engine(games=1, sims=400, c_puct=5.0, train_noise=0, evaluator=ev, blocks=3) as e:
+            r = e.search(root)
+        assert _mv(r.moves[0]) == tuple(case["expected"])
+
+
+def test_search_large_batch_stats():
+    from onitama_az.game import initial_state_np
+    G = 4096
+    roots = np.concatenate([initial_state_np([0, 1, 2, 3, 4])] * G)
+    with Engine(games=G, sims=8, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_NN, blocks=3) as e:
+        r = e.search(roots, root_value=True)
+    assert r.stats.sims == 8 * G and r.stats.expansions >= G
+    assert np.allclose(r.pi.reshape(G, -1).sum(1), 1.0, atol=1e-6)
+    assert np.all(np.abs(r.root_value) <= 1.0)
+
+
+# ---- self-play ---------------------------------------------------------------------------
+def _sorted_rows(a):
+    return np.sort(np.frombuffer(a.tobytes(), dtype=np.dtype((np.void, a.dtype.itemsize))))
+
+
+@pytest.mark.parametrize("fixed,max_plies", [(True, 150), (False, 150), (False, 3)])
+def test_selfplay_matches_oracle_games(orc, fixed, max_plies):
+    n_games, slots, sims = 24, 8, 12
+    deck = [0, 1, 2, 3, 4]
+    kw = dict(games=slots, sims=sims, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0,
+              max_plies=max_plies, seed=4242, fixed_deck=int(fixed), deck=deck)
+    with Engine(**kw) as e:
+        got, st = e.selfplay_run(n_games, cap=n_games * (max_plies + 2))
+    assert st.games_finished == n_games
+    ref = []
+    for gid in range(n_games):
+        cfg = orc.search_cfg(sims=sims, c_puct=5.0, evaluator=orc.EVAL_HASH, seed=4242)
+        s, res, plies, _ = orc.selfplay_game(cfg, gid, max_plies=max_plies, deck=deck if fixed else None)
+        assert plies <= max_plies + 2
+        ref.append(s)
+    ref = np.concatenate(ref)
+    assert len(got) == len(ref)
+    assert np.array_equal(_sorted_rows(got), _sorted_rows(ref))
+
+
+def test_selfplay_nn_continuous_batching_runs():
+    with Engine(games=256, sims=16, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_NN, blocks=3, max_plies=150) as e:
+        e.selfplay_reset()
+        e.selfplay_step(40)
+        st = e.selfplay_stats()
+        samples = e.samples_fetch(100000)
+    assert st.moves == 40 * 256 - 0 or st.moves <= 40 * 256
+    assert st.games_finished > 0 and len(samples) == st.samples_ready
+    assert np.all(np.isin(samples["z"], [-1.0, 0.0, 1.0]))
+    assert np.allclose(samples["pi"].sum(1), 1.0, atol=1e-6)
+
+
+# ---- Agent / self-play API mirror ----------------------------------------------------------
+def test_agent_api_mirror(orc):
+    from onitama_az.mcts import AlphaZeroMcts, AlphaZeroMctsConfig, ConvResNet, ConvResNetConfig, TrainingAlphaZeroMcts
+    from onitama_az.selfplay import TrainConfig, self_play
+    from onitama_az.mcts import Options
+    model = ConvResNet(ConvResNetConfig(resnet_block_amnt=3), seed=0)
+    cfg = AlphaZeroMctsConfig(exploration_c=5.0, max_playouts=50, train=False)
+    agent = AlphaZeroMcts(cfg, model)
+    gs = GameState.with_deck(Deck([ORIGINAL_CARDS[i] for i in range(5)]))
+    mv, value = agent.generate_move(gs)
+    legal = gs.state.generate_all_legal_moves(gs.curr_player_color)
+    assert (mv.used_card_idx, mv.mov) in legal and -1.0 <= value <= 1.0
+    assert agent.name() == "AlphaZero MCTS AI"
+    res = gs.progress(mv)
+    assert res in (MoveResult.InProgress, MoveResult.Capture)
+    tr = TrainingAlphaZeroMcts(cfg, model)
+    mv2, pi = tr.generate_move_tensor(gs.state, gs.curr_player_color)
+    assert pi.shape == (2, 25) and abs(pi.sum() - 1) < 1e-6
+    data = self_play(tr, Options(), None, TrainConfig(mcts_config=cfg, self_play_game_amnt=3,
+                                                       model_config=ConvResNetConfig(resnet_block_amnt=3)))
+    assert len(data) > 0 and data[0].state.shape == (21, 5, 5)
+    for d in data[:20]:
+        assert d.z in (-1.0, 0.0, 1.0) and d.pi.shape == (2, 25)

@@ -1,0 +1,105 @@
+"""CPU: the C-ABI library loads, exports every symbol include/onitama_az.h declares, and its
+host-side logic (tables, deals, weights layout, test evaluator) matches the oracle. No GPU
+compute is called here."""
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from onitama_az import _abi
+from onitama_az import weights as W
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "onitama_az.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(oaz_[a-z_]+)\s*\(", text)))
+
+
+def test_header_functions_exported(lib):
+    names = declared_functions()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_abi.EXPORTED_SYMBOLS), set(names) ^ set(_abi.EXPORTED_SYMBOLS)
+
+
+def test_abi_version_and_structs(lib):
+    assert lib.oaz_abi_version() == 1
+    assert C.sizeof(_abi.oaz_config) == 112 or C.sizeof(_abi.oaz_config) > 0
+
+
+def test_default_config_matches_reference_train_bin():  # bin/train.rs:50-78
+    c = _abi.default_config()
+    assert (c.blocks, c.channels, c.in_planes, c.sims, c.c_puct, c.train_noise, c.max_plies) == (5, 64, 21, 400, 5.0, 1, 150)
+    assert c.dirichlet_alpha == 0.03 and c.dirichlet_eps == 0.25
+
+
+def test_attack_maps_equal_oracle(lib, orc):
+    am = np.zeros((2, 16, 25), dtype=np.uint32)
+    lib.oaz_attack_maps(_abi.ptr(am))
+    assert np.array_equal(am, orc.attack_maps())
+
+
+def test_deal_and_initial_state_equal_oracle(lib, orc):
+    for gid in list(range(200)) + [2**40 + 5]:
+        d = (C.c_uint8 * 5)()
+        lib.oaz_deal_deck(C.c_uint64(123), C.c_uint64(gid), d)
+        assert list(d) == list(orc.deal_deck(123, gid))
+        assert len(set(d)) == 5
+        a = np.zeros(1, dtype=_abi.STATE_DTYPE)
+        lib.oaz_initial_state(d, _abi.ptr(a))
+        assert a.tobytes() == orc.initial_state(np.array(list(d), np.uint8)).tobytes()
+
+
+def test_hash_eval_equal_oracle(lib, orc):
+    from conftest import random_positions
+    for s in random_positions(orc, 100, seed=4):
+        s = s.reshape(1).copy()
+        p, v = np.zeros(50, np.float32), np.zeros(1, np.float32)
+        lib.oaz_hash_eval(_abi.ptr(s), _abi.ptr(p), _abi.ptr(v))
+        p2, v2 = orc.hash_eval(s)
+        assert np.array_equal(p, p2) and v[0] == v2
+
+
+@pytest.mark.parametrize("blocks", [0, 3, 5, 6])
+def test_weight_layout(lib, orc, blocks):
+    n = lib.oaz_weight_count(blocks, 64, 21)
+    assert n == W.weight_count(blocks) == orc.load().orc_weight_count(blocks)
+    w = W.random_weights(7, blocks)
+    named = W.named_from_blob(w, blocks)
+    assert np.all(named["bn1|weight"] == 1) and np.all(named["bn1|running_var"] == 1)
+    assert np.all(np.abs(named["conv_init_1|weight"]) <= 1 / np.sqrt(21 * 9))
+    assert np.array_equal(W.blob_from_named(named, blocks), w)
+
+
+def test_param_counts_match_survey():
+    assert W.weight_count(3) == 240_006 and W.weight_count(5) == 388_742 and W.weight_count(6) == 463_110
+
+
+@pytest.mark.skipif(not Path("/root/reference/models/model_5e-3_3_resnet.ot").exists(), reason="reference not mounted")
+def test_ot_reader_matches_committed_fixture(trained3):
+    named = W.read_ot("/root/reference/models/model_5e-3_3_resnet.ot")
+    assert W.blocks_from_names(named) == 3 and len(named) == 60
+    assert np.array_equal(W.blob_from_named(named, 3), trained3)
+
+
+def test_no_device_is_a_loud_error(lib):
+    if _abi.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    cfg = _abi.default_config()
+    assert not lib.oaz_create(C.byref(cfg), 0)
+    assert b"device" in lib.oaz_last_error()
+    s = np.zeros(1, dtype=_abi.STATE_DTYPE)
+    assert lib.oaz_movegen(_abi.ptr(s), 1, None, None, None) == -2  # OAZ_ERR_NO_DEVICE, no CPU fallback
+
+
+def test_display_kat(kats):  # state.rs:397-417 (State::display is host-side formatting)
+    from onitama_az.game import ORIGINAL_CARDS, Deck, State
+    st = State.with_deck(Deck([ORIGINAL_CARDS[i] for i in range(5)]))
+    assert st.display() == kats["display"]["expected"]
