@@ -1,0 +1,63 @@
+"""A/B the NN kernel variants in one process (interleaved rounds): parity vs the torch goldens
+and per-launch time at a given batch. Usage: python tools/nn_ab.py [--batch 65536] [--variants 1,2,3]"""
+import argparse
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "onitama-alphazero_amd"))
+from onitama_az import _abi  # noqa: E402
+from onitama_az.engine import Engine  # noqa: E402
+from onitama_az.weights import random_weights  # noqa: E402
+
+FLOP = {3: 11_681_928, 5: 19_054_728, 6: 22_741_128}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--variants", default="1,2,3")
+    ap.add_argument("--blocks", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    g = np.load(ROOT / "tests/golden/nn_golden.npz")
+    w3 = np.load(ROOT / "tests/golden/weights_3block_trained.npy")
+    engines = {}
+    for v in [int(x) for x in a.variants.split(",")]:
+        os.environ["OAZ_NN_VARIANT"] = str(v)
+        e = Engine(games=a.batch, sims=1, blocks=a.blocks, evaluator=_abi.EVAL_NN)
+        if a.blocks == 3:
+            e.load_weights(w3)
+            p, val = e.nn_forward(g["states"])
+            err = float(max(np.abs(p - g["policy_trained3"]).max(), np.abs(val - g["value_trained3"]).max()))
+        else:
+            err = None
+        e.load_weights(random_weights(0, a.blocks))
+        engines[v] = (e, err)
+    states = np.concatenate([g["states"]] * (a.batch // len(g["states"]) + 1))[: a.batch]
+    res = {v: [] for v in engines}
+    for _ in range(a.rounds):
+        for v, (e, _) in engines.items():
+            e.nn_forward(states[:1024])
+            e.kernel_times_reset()
+            e.set_timing(True)
+            for _ in range(a.reps):
+                e.nn_forward(states)
+            e.set_timing(False)
+            t = e.kernel_times()
+            res[v].append(t.nn_ms / t.nn_n)
+    out = {}
+    for v, ts in res.items():
+        ms = float(np.median(ts))
+        out[v] = {"median_ms": ms, "min_ms": float(min(ts)), "tflops": FLOP[a.blocks] * a.batch / ms / 1e9,
+                  "sims_per_s": a.batch / ms * 1e3, "max_err_vs_torch": engines[v][1]}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
