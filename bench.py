@@ -158,8 +158,9 @@ def main():
             "games_per_s": games_all / T, "plies_per_s": plies_all / T,
             "true_expansions_per_s": exp_all / T, "mean_select_depth": depth, "mean_branching": branching,
             "kernel_ms_per_step": {"select": kt.select_ms / args.steps, "nn": kt.nn_ms / args.steps,
-                                   "expand_backup": kt.expand_ms / args.steps, "move": kt.finalize_ms / args.steps},
-            "roofline": {"bound": "mfma", "kernel": "k_nn_forward (fused ResNet, v_mfma_f32_32x32x2_f32)",
+                                   "expand_backup": kt.expand_ms / args.steps, "move": kt.finalize_ms / args.steps,
+                                   "root_noise_stream2": kt.noise_ms / args.steps},
+            "roofline": {"bound": "mfma", "kernel": "k_nn_sq16 (fused ResNet, v_mfma_f32_16x16x4_f32)",
                          "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
                          "flop_per_launch": flops_launch, "avg_launch_ms": nn_avg_ms, "launches": kt.nn_n},

@@ -166,6 +166,8 @@ typedef struct oaz_kernel_times {
     double select_ms, nn_ms, expand_ms, finalize_ms;
     uint64_t select_n, nn_n, expand_n, finalize_n;
     uint64_t nn_samples;  /* samples evaluated by the timed nn launches */
+    double noise_ms;      /* Dirichlet root-noise producer (second stream, overlaps the NN) */
+    uint64_t noise_n;
 } oaz_kernel_times;
 
 typedef struct oaz_engine oaz_engine;

@@ -353,7 +353,7 @@ extern "C" int oaz_encode(const oaz_state* s, int n, float* planes) {
 
 // ---- engine ------------------------------------------------------------------------------------
 struct TimedLaunch {
-    int kind;  // 0 select, 1 nn, 2 expand, 3 finalize
+    int kind;  // 0 select, 1 nn, 2 expand, 3 finalize, 4 root noise (second stream)
     hipEvent_t a, b;
     uint32_t samples;
 };
@@ -362,6 +362,9 @@ struct oaz_engine {
     oaz_config cfg;
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;       // root-noise producer, overlaps the NN kernel
+    hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_consumed[2] = {nullptr, nullptr};
+    double* noise = nullptr;             // [2][kNoiseChunk][G][kNoiseStride]
     uint32_t G = 0, cap = 0, pathcap = 0, hcap = 0, out_cap = 0;
     // trees
     oaz_node* nodes = nullptr;
@@ -471,8 +474,21 @@ static hipEvent_t ev_get(oaz_engine* e) {
 }
 
 // Run a launch, bracketed by events on the engine stream when timing is on.
+static constexpr uint32_t kNoiseChunk = 8;  // simulations of root noise produced per launch
+
+static void accumulate(oaz_engine* e, const TimedLaunch& p, float ms) {
+    double* acc[5] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms,
+                      &e->times.noise_ms};
+    uint64_t* cnt[5] = {&e->times.select_n, &e->times.nn_n, &e->times.expand_n, &e->times.finalize_n,
+                        &e->times.noise_n};
+    *acc[p.kind] += ms;
+    *cnt[p.kind] += 1;
+    if (p.kind == 1) e->times.nn_samples += p.samples;
+}
+
 template <class F>
-static int timed(oaz_engine* e, int kind, uint32_t samples, F&& launch) {
+static int timed(oaz_engine* e, int kind, uint32_t samples, F&& launch, hipStream_t st = nullptr) {
+    if (!st) st = e->stream;
     if (!e->timing) {
         HIP_TRY(launch());
         return 0;
@@ -482,20 +498,17 @@ static int timed(oaz_engine* e, int kind, uint32_t samples, F&& launch) {
     t.samples = samples;
     t.a = ev_get(e);
     t.b = ev_get(e);
-    HIP_TRY(hipEventRecord(t.a, e->stream));
+    HIP_TRY(hipEventRecord(t.a, st));
     HIP_TRY(launch());
-    HIP_TRY(hipEventRecord(t.b, e->stream));
+    HIP_TRY(hipEventRecord(t.b, st));
     e->pending.push_back(t);
     if (e->pending.size() > 4096) {  // resolve periodically to bound the pool
         HIP_TRY(hipStreamSynchronize(e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream2));
         for (auto& p : e->pending) {
             float ms = 0.f;
             (void)hipEventElapsedTime(&ms, p.a, p.b);
-            double* acc[4] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms};
-            uint64_t* cnt[4] = {&e->times.select_n, &e->times.nn_n, &e->times.expand_n, &e->times.finalize_n};
-            *acc[p.kind] += ms;
-            *cnt[p.kind] += 1;
-            if (p.kind == 1) e->times.nn_samples += p.samples;
+            accumulate(e, p, ms);
             e->pool.push_back(p.a);
             e->pool.push_back(p.b);
         }
@@ -550,10 +563,17 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         set_err(OAZ_ERR_HIP, "hipSetDevice(%d) failed", device);
         return fail();
     }
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) {
         set_err(OAZ_ERR_HIP, "stream create failed");
         return fail();
     }
+    for (int i = 0; i < 2; ++i)
+        if (hipEventCreateWithFlags(&e->ev_ready[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_consumed[i], hipEventDisableTiming) != hipSuccess) {
+            set_err(OAZ_ERR_HIP, "event create failed");
+            return fail();
+        }
     const size_t G = e->G;
     if (dalloc(&e->nodes, G * e->cap) || dalloc(&e->n_nodes, G) || dalloc(&e->path, G * e->pathcap) ||
         dalloc(&e->depth, G) || dalloc(&e->leaf, G) || dalloc(&e->leaf_state, G) ||
@@ -565,7 +585,8 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         dalloc(&e->s_rootv, G) || dalloc(&e->s_rootp, G * 50) || dalloc(&e->s_ply, G) ||
         dalloc(&e->root, G) || dalloc(&e->ply, G) || dalloc(&e->seq, G) ||
         dalloc(&e->game_id, G) || dalloc(&e->active, G) || dalloc(&e->hist, G * e->hcap) ||
-        dalloc(&e->out, (size_t)e->out_cap) || dalloc(&e->out_count, (size_t)1))
+        dalloc(&e->out, (size_t)e->out_cap) || dalloc(&e->out_count, (size_t)1) ||
+        (cfg->train_noise && dalloc(&e->noise, 2 * kNoiseChunk * G * kNoiseStride)))
         return fail();
     // sqrt((double)n) from the host libm (IEEE correctly rounded), so device PUCT = oracle PUCT
     std::vector<double> tab((size_t)cfg->sims + 2);
@@ -589,6 +610,11 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->stream2) (void)hipStreamSynchronize(e->stream2);
+    for (int i = 0; i < 2; ++i) {
+        if (e->ev_ready[i]) (void)hipEventDestroy(e->ev_ready[i]);
+        if (e->ev_consumed[i]) (void)hipEventDestroy(e->ev_consumed[i]);
+    }
     for (auto& p : e->pending) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -597,9 +623,10 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     void* ptrs[] = {e->nodes, e->n_nodes, e->path, e->depth, e->leaf, e->leaf_state, e->stats,
                     e->stats_sum, e->sqrt_tab, e->policy, e->value, e->weights, e->weights2, e->s_roots,
                     e->s_move, e->s_pi, e->s_rootv, e->s_rootp, e->s_ply, e->root, e->ply,
-                    e->seq, e->game_id, e->active, e->hist, e->out, e->out_count};
+                    e->seq, e->game_id, e->active, e->hist, e->out, e->out_count, e->noise};
     for (void* p : ptrs) dfree(p);
     if (e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->stream2) (void)hipStreamDestroy(e->stream2);
     delete e;
 }
 
@@ -629,6 +656,7 @@ extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
 extern "C" int oaz_sync(oaz_engine* e) {
     if (!e) return set_err(OAZ_ERR_ARG, "sync: null");
     HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream2));
     return 0;
 }
 
@@ -640,14 +668,11 @@ extern "C" int oaz_set_timing(oaz_engine* e, int enable) {
 
 static int resolve_timing(oaz_engine* e) {
     HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream2));
     for (auto& p : e->pending) {
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b));
-        double* acc[4] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms};
-        uint64_t* cnt[4] = {&e->times.select_n, &e->times.nn_n, &e->times.expand_n, &e->times.finalize_n};
-        *acc[p.kind] += ms;
-        *cnt[p.kind] += 1;
-        if (p.kind == 1) e->times.nn_samples += p.samples;
+        accumulate(e, p, ms);
         e->pool.push_back(p.a);
         e->pool.push_back(p.b);
     }
@@ -694,14 +719,52 @@ extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* p
     return 0;
 }
 
-// One simulation for every game: select -> evaluate -> expand/backup.
-static int sim_step(oaz_engine* e, const TreeView& t, const oaz_state* roots, const uint8_t* active,
-                    const uint64_t* gids, const uint32_t* plies, uint32_t sim) {
+// All cfg.sims simulations of one move for every game: select -> evaluate -> expand/backup,
+// in lock step. With root noise, k_root_noise fills chunk c+1 of the double-buffered noise
+// ring on stream2 while stream 1 runs chunk c (events order the two ring slots).
+static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, const uint8_t* active,
+                    const uint64_t* gids, const uint32_t* plies) {
     const SearchParams prm = search_params(e);
-    if (int rc = timed(e, 0, t.G, [&] { return launch_select(t, roots, active, gids, plies, prm, sim, e->stream); }))
-        return rc;
-    if (int rc = evaluate(e, t.leaf_state, t.G, e->policy, e->value)) return rc;
-    return timed(e, 2, t.G, [&] { return launch_expand_backup(t, roots, active, e->policy, e->value, e->stream); });
+    const uint32_t sims = (uint32_t)e->cfg.sims;
+    const bool noise = e->cfg.train_noise && e->noise;
+    const size_t slot_elems = (size_t)kNoiseChunk * t.G * kNoiseStride;
+    const uint32_t nchunks = (sims + kNoiseChunk - 1) / kNoiseChunk;
+    auto produce = [&](uint32_t c) -> int {
+        if (c >= 2) HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[c & 1], 0));
+        const uint32_t s0 = c * kNoiseChunk, n = sims - s0 < kNoiseChunk ? sims - s0 : kNoiseChunk;
+        double* buf = e->noise + (c & 1) * slot_elems;
+        if (int rc = timed(e, 4, t.G * n, [&] {
+                return launch_root_noise(roots, active, gids, plies, prm, t.G, s0, n, buf, e->stream2);
+            }, e->stream2))
+            return rc;
+        HIP_TRY(hipEventRecord(e->ev_ready[c & 1], e->stream2));
+        return 0;
+    };
+    if (noise) {
+        HIP_TRY(hipEventRecord(e->ev_consumed[0], e->stream));  // stream2 starts after prior work
+        HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[0], 0));
+        if (int rc = produce(0)) return rc;
+    }
+    for (uint32_t c = 0; c < nchunks; ++c) {
+        if (noise) {
+            if (c + 1 < nchunks)
+                if (int rc = produce(c + 1)) return rc;
+            HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_ready[c & 1], 0));
+        }
+        const uint32_t s0 = c * kNoiseChunk, s1 = s0 + kNoiseChunk < sims ? s0 + kNoiseChunk : sims;
+        for (uint32_t s = s0; s < s1; ++s) {
+            const double* nz = noise ? e->noise + (c & 1) * slot_elems + (size_t)(s - s0) * t.G * kNoiseStride : nullptr;
+            if (int rc = timed(e, 0, t.G, [&] { return launch_select(t, roots, active, nz, prm, e->stream); }))
+                return rc;
+            if (int rc = evaluate(e, t.leaf_state, t.G, e->policy, e->value)) return rc;
+            if (int rc = timed(e, 2, t.G, [&] {
+                    return launch_expand_backup(t, roots, active, e->policy, e->value, e->stream);
+                }))
+                return rc;
+        }
+        if (noise) HIP_TRY(hipEventRecord(e->ev_consumed[c & 1], e->stream));
+    }
+    return 0;
 }
 
 static int reduce_stats(oaz_engine* e, uint32_t G, uint64_t out[GS_COUNT]) {
@@ -736,8 +799,7 @@ extern "C" int oaz_search(oaz_engine* e, const oaz_state* roots, int G, oaz_move
     HIP_TRY(hipMemcpyAsync(e->s_ply, plies.data(), (size_t)G * 4, hipMemcpyHostToDevice, e->stream));
     e->search_calls++;
     HIP_TRY(launch_tree_reset(t, e->stream));
-    for (uint32_t s = 0; s < (uint32_t)e->cfg.sims; ++s)
-        if (int rc = sim_step(e, t, e->s_roots, nullptr, nullptr, e->s_ply, s)) return rc;
+    if (int rc = run_sims(e, t, e->s_roots, nullptr, nullptr, e->s_ply)) return rc;
     if (int rc = timed(e, 3, (uint32_t)G, [&] { return launch_search_finalize(t, e->s_roots, e->s_move, e->s_pi, e->stream); }))
         return rc;
     if (out_root_value) {  // extra root evaluation (alphazero_mcts/mod.rs:137-141)
@@ -793,8 +855,7 @@ extern "C" int oaz_selfplay_step(oaz_engine* e, int moves) {
     const TreeView t = tree_view(e, e->G);
     const SlotView sv = slot_view(e);
     for (int m = 0; m < moves; ++m) {
-        for (uint32_t s = 0; s < (uint32_t)e->cfg.sims; ++s)
-            if (int rc = sim_step(e, t, e->root, e->active, e->game_id, e->ply, s)) return rc;
+        if (int rc = run_sims(e, t, e->root, e->active, e->game_id, e->ply)) return rc;
         if (int rc = timed(e, 3, e->G, [&] { return launch_selfplay_move(t, sv, e->stream); })) return rc;
     }
     return 0;

@@ -226,6 +226,35 @@ __device__ double beta_noise_dev(uint64_t seed, uint64_t game, uint32_t c2, uint
     return s > 0.0 ? x / s : 0.0;
 }
 
+// Dirichlet draws of nsims consecutive simulations for every root: out[(k*G + g)*80 + 2j + {0,1}]
+// holds the noise for comparison j (operand a, operand b) of simulation sim0+k. They depend only
+// on (root position, game id, ply, sim), so they are produced off the critical path (second
+// stream) instead of inside the latency-bound select walk. One wave per game covers all
+// nsims * 2(K-1) draws of the chunk with every lane busy.
+__global__ void __launch_bounds__(kBlock) k_root_noise(const oaz_state* __restrict__ roots,
+                                                       const uint8_t* __restrict__ active,
+                                                       const uint64_t* __restrict__ game_ids,
+                                                       const uint32_t* __restrict__ plies, SearchParams prm,
+                                                       uint32_t G, uint32_t sim0, uint32_t nsims, double* out) {
+    const uint32_t g = wave_game();
+    if (g >= G) return;
+    if (active && !active[g]) return;
+    const int l = lane_id();
+    const oaz_state s = load_state(&roots[g]);
+    const LaneMoves m = lane_movegen(s);
+    const int K = (int)wave_sum_u32((uint32_t)__popc(m.mask));  // = root children (expand order)
+    if (K < 2) return;
+    const uint64_t gid = game_ids ? game_ids[g] : g;
+    const uint32_t ply = plies ? plies[g] : 0u;
+    const int per_sim = 2 * (K - 1);
+    for (int idx = l; idx < (int)nsims * per_sim; idx += 64) {
+        const int k = idx / per_sim, r = idx - k * per_sim;
+        const uint32_t d = 2u + (uint32_t)r;  // draw index 2j + which, j = 1 + r/2
+        const uint32_t c2 = (ply << 16) | ((sim0 + k) & 0xFFFFu);
+        out[((size_t)k * G + g) * kNoiseStride + d] = beta_noise_dev(prm.seed, gid, c2, d, prm.alpha, K);
+    }
+}
+
 // ---- MCTS kernels -------------------------------------------------------------------------
 struct NodeRegs {  // one node held in registers (all 32 bytes)
     double W, P;
@@ -265,9 +294,8 @@ __global__ void __launch_bounds__(kBlock) k_tree_reset(TreeView t) {
 // not terminal; replay each chosen move; mark children whose move wins as terminal.
 __global__ void __launch_bounds__(kBlock) k_select(TreeView t, const oaz_state* __restrict__ roots,
                                                    const uint8_t* __restrict__ active,
-                                                   const uint64_t* __restrict__ game_ids,
-                                                   const uint32_t* __restrict__ plies,
-                                                   SearchParams prm, uint32_t sim) {
+                                                   const double* __restrict__ noise,
+                                                   SearchParams prm) {
     const uint32_t g = wave_game();
     if (g >= t.G) return;
     if (active && !active[g]) return;
@@ -298,15 +326,14 @@ __global__ void __launch_bounds__(kBlock) k_select(TreeView t, const oaz_state* 
         const double q = ch.N ? ch.W / (double)ch.N : 0.0;
         const double sq = t.sqrt_tab[nd.N] / (double)(ch.N + 1);
         int best;
-        if (depth == 0 && prm.train_noise) {
+        if (depth == 0 && prm.train_noise && noise) {
             // sequential Iterator::max_by fold; each comparison re-evaluates both operands
             // with fresh noise (draw indices 2j and 2j+1 for comparison j)
+            // draws precomputed by k_root_noise (same root, game id, ply and sim)
             double na = 0.0, nb = 0.0;
             if (l >= 1 && l < K) {
-                const uint64_t gid = game_ids ? game_ids[g] : g;
-                const uint32_t c2 = ((plies ? plies[g] : 0u) << 16) | (sim & 0xFFFFu);
-                na = beta_noise_dev(prm.seed, gid, c2, 2u * l, prm.alpha, K);
-                nb = beta_noise_dev(prm.seed, gid, c2, 2u * l + 1u, prm.alpha, K);
+                na = noise[(size_t)g * kNoiseStride + 2 * l];
+                nb = noise[(size_t)g * kNoiseStride + 2 * l + 1];
             }
             const double base = ch.P * (1.0 - prm.eps);
             int acc = 0;
@@ -638,10 +665,15 @@ hipError_t launch_tree_reset(const TreeView& t, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
-                         const uint64_t* game_id, const uint32_t* ply, SearchParams p,
-                         uint32_t sim, hipStream_t st) {
-    hipLaunchKernelGGL(k_select, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, roots, active,
-                       game_id, ply, p, sim);
+                         const double* noise, SearchParams p, hipStream_t st) {
+    hipLaunchKernelGGL(k_select, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, roots, active, noise, p);
+    return hipGetLastError();
+}
+hipError_t launch_root_noise(const oaz_state* roots, const uint8_t* active, const uint64_t* game_id,
+                             const uint32_t* ply, SearchParams p, uint32_t G, uint32_t sim0, uint32_t nsims,
+                             double* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_root_noise, dim3(wave_grid(G)), dim3(kBlock), 0, st, roots, active, game_id, ply, p, G,
+                       sim0, nsims, out);
     return hipGetLastError();
 }
 hipError_t launch_expand_backup(const TreeView& t, const oaz_state* roots, const uint8_t* active,

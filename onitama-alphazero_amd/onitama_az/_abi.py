@@ -119,6 +119,8 @@ class oaz_kernel_times(C.Structure):
         ("expand_n", C.c_uint64),
         ("finalize_n", C.c_uint64),
         ("nn_samples", C.c_uint64),
+        ("noise_ms", C.c_double),
+        ("noise_n", C.c_uint64),
     ]
 
 
