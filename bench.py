@@ -12,9 +12,14 @@ runs after it and is reported separately.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5]
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -33,6 +38,13 @@ CONFIGS = {
     "c5": dict(games=65536, sims=800, blocks=6, fixed_deck=0, precision="fp32"),
 }
 FLOP_PER_SIM = {3: 11_681_928, 5: 19_054_728, 6: 22_741_128}  # dense MACs x 2
+
+
+def nonzero_flop_per_sim(blocks):
+    """FLOPs excluding products with the 3x3 convs' zero padding: 169 on-board (square, tap)
+    pairs of 225 (what k_nn_sq16 executes)."""
+    macs = 169 * 21 * 64 + blocks * 2 * 169 * 64 * 64 + (1600 + 1600 + 64 + 3200 + 2500)
+    return 2 * macs
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: F32 matrix peak (spec)
 METRIC = "MCTS node-expansions/sec/GPU @400 sims; self-play games/sec at 1/2/4/8 GPU"
 
@@ -40,8 +52,10 @@ METRIC = "MCTS node-expansions/sec/GPU @400 sims; self-play games/sec at 1/2/4/8
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=14)
+    ap.add_argument("--stagger", type=int, default=12,
+                    help="slot g starts after g %% stagger plies so game ages reach steady state in warmup")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--games", type=int, default=0, help="override games per GPU")
     ap.add_argument("--sims", type=int, default=0, help="override sims per move")
@@ -49,7 +63,40 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+def pmc_traffic(args, cfg):
+    """HBM bytes per k_nn_sq16 launch from rocprofv3 PMC counters, one counter per pass (TCC slots:
+    FETCH_SIZE and WRITE_SIZE do not fit one pass). Runs as child processes BEFORE this process
+    touches the GPU. gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half the
+    bytes of wide (16 B/lane) coalesced reads -> doubled; WRITE_SIZE is taken as reported."""
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    kb = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        with tempfile.TemporaryDirectory() as d:
+            cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
+                   str(Path(__file__).resolve()), "--pmc-child", "--config", args.config, "--games", str(cfg["games"]),
+                   "--sims", "2"]
+            try:
+                subprocess.run(cmd, timeout=600, capture_output=True, check=True)
+            except (subprocess.SubprocessError, OSError):
+                return None
+            vals = []
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                for r in csv.DictReader(open(f)):
+                    if "k_nn_sq16" in r["Kernel_Name"] and r["Counter_Name"] == ctr:
+                        vals.append(float(r["Counter_Value"]))
+            if not vals:
+                return None
+            kb[ctr] = sum(vals) / len(vals)
+    fetch, write = 2.0 * kb["FETCH_SIZE"] * 1024.0, kb["WRITE_SIZE"] * 1024.0
+    return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+            "raw_kb": kb, "note": "rocprofv3 --pmc, separate passes; FETCH_SIZE x2 (gfx950 wide-read correction)"}
 
 
 def cpu_baseline(cfg, seconds, threads):
@@ -90,12 +137,20 @@ def main():
         cfg["games"] = args.games
     if args.sims:
         cfg["sims"] = args.sims
+    traffic = None
+    if not args.pmc_child and not args.no_pmc and world == 1:
+        traffic = pmc_traffic(args, cfg)  # child processes; this process has not touched the GPU yet
     eng = Engine(device=local, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0, train_noise=1,
                  max_plies=150, evaluator=_abi.EVAL_NN, precision=_abi.FP32, fixed_deck=cfg["fixed_deck"],
                  deck=[0, 1, 2, 3, 4], seed=20260101, rank=rank, world=world,
-                 sample_capacity=cfg["games"] * 24)
+                 sample_capacity=cfg["games"] * 24, stagger=0 if args.pmc_child else args.stagger)
     eng.load_weights(random_weights(0, cfg["blocks"]))  # random-init weights (seed 0), SURVEY.md 8d
     eng.selfplay_reset()
+    if args.pmc_child:  # profiled pass: one move of a couple of simulations, NN launches at full batch
+        eng.selfplay_step(1)
+        eng.sync()
+        eng.close()
+        return
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -146,6 +201,10 @@ def main():
         nn_avg_ms = kt.nn_ms / max(1, kt.nn_n)
         flops_launch = FLOP_PER_SIM[cfg["blocks"]] * (kt.nn_samples / max(1, kt.nn_n))
         achieved = flops_launch / (nn_avg_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
+        nz = nonzero_flop_per_sim(cfg["blocks"]) * (kt.nn_samples / max(1, kt.nn_n))
+        achieved_nz = nz / (nn_avg_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
+        positions = kt.nn_samples / max(1, kt.nn_n)
+        alg_bytes = 0.96e6 + positions * (24 + 204)  # weights once + states in + policy/value out
         out = {
             "metric": METRIC, "value": sims_all / T, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * T / args.steps, "higher_is_better": True, "scaling": "weak",
@@ -154,7 +213,7 @@ def main():
                                    f"{cfg['blocks']}-block 64-ch ResNet, c_puct 5, Dirichlet root noise",
                        "games_per_gpu": cfg["games"], "sims_per_move": cfg["sims"], "blocks": cfg["blocks"],
                        "fixed_deck": bool(cfg["fixed_deck"]), "parallelism": f"games sharded x{world}"},
-            "sims_per_s_per_gpu": sims_all / T / world,
+            "sims_per_s_per_gpu": sims_all / T / world, "stagger": args.stagger,
             "games_per_s": games_all / T, "plies_per_s": plies_all / T,
             "true_expansions_per_s": exp_all / T, "mean_select_depth": depth, "mean_branching": branching,
             "kernel_ms_per_step": {"select": kt.select_ms / args.steps, "nn": kt.nn_ms / args.steps,
@@ -162,8 +221,12 @@ def main():
                                    "root_noise_stream2": kt.noise_ms / args.steps},
             "roofline": {"bound": "mfma", "kernel": "k_nn_sq16 (fused ResNet, v_mfma_f32_16x16x4_f32)",
                          "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
-                         "flop_per_launch": flops_launch, "avg_launch_ms": nn_avg_ms, "launches": kt.nn_n},
+                         "frac": achieved / PEAK_FP32_MFMA_TFLOPS,
+                         "traffic": traffic["bytes_per_launch"] if traffic else None,
+                         "flop_per_launch": flops_launch, "avg_launch_ms": nn_avg_ms, "launches": kt.nn_n,
+                         "positions_per_launch": positions, "flop_accounting": "SURVEY 8d dense MACs x2 per sim",
+                         "achieved_nonzero": achieved_nz, "frac_nonzero": achieved_nz / PEAK_FP32_MFMA_TFLOPS,
+                         "algorithmic_bytes_per_launch": alg_bytes, "traffic_detail": traffic},
             "allgather": allgather,
         }
         if not args.no_cpu_baseline and world == 1:

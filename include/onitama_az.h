@@ -136,7 +136,9 @@ typedef struct oaz_config {
     int32_t rank;            /* global game id = (k * world + rank) * games + slot */
     int32_t world;
     int32_t sample_capacity; /* max samples buffered on the device (0: auto) */
-    int32_t reserved[7];
+    int32_t stagger;         /* self-play: slot g starts playing after g % stagger plies (steady-state
+                                game ages for throughput measurement); 0 = all slots start at once */
+    int32_t reserved[6];
 } oaz_config;
 
 typedef struct oaz_search_stats {

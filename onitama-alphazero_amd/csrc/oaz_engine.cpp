@@ -449,6 +449,7 @@ static SlotView slot_view(oaz_engine* e) {
     s.world_games = e->G * (uint32_t)(e->cfg.world > 0 ? e->cfg.world : 1);
     s.rank_base = (uint32_t)e->cfg.rank * e->G;
     s.quota = e->quota;
+    s.stagger = e->quota ? 0u : (uint32_t)(e->cfg.stagger > 0 ? e->cfg.stagger : 0);
     return s;
 }
 

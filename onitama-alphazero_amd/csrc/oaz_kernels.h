@@ -56,7 +56,7 @@ struct SlotView {
     uint32_t* ply;        // [G]
     uint32_t* seq;        // [G] games started in this slot
     uint64_t* game_id;    // [G] global game id (deal + noise key)
-    uint8_t* active;      // [G]
+    uint8_t* active;      // [G] 1 = playing, 0 = done (quota), k > 1 = starts in k-1 plies
     oaz_sample* hist;     // [G][hcap] samples of the running game (z filled at the end)
     oaz_sample* out;      // [out_cap] finished samples
     unsigned long long* out_count;  // appended samples (may exceed out_cap: dropped)
@@ -69,6 +69,7 @@ struct SlotView {
     uint32_t world_games;  // games per generation over all ranks (G * world)
     uint32_t rank_base;    // rank * G
     uint64_t quota;        // stop starting games at this global index (0 = unlimited)
+    uint32_t stagger;      // slot g waits g % stagger plies before its first game (0: none)
 };
 
 struct NNView {

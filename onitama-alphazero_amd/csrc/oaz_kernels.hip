@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(kBlock) k_root_noise(const oaz_state* __restri
                                                        uint32_t G, uint32_t sim0, uint32_t nsims, double* out) {
     const uint32_t g = wave_game();
     if (g >= G) return;
-    if (active && !active[g]) return;
+    if (active && active[g] != 1) return;
     const int l = lane_id();
     const oaz_state s = load_state(&roots[g]);
     const LaneMoves m = lane_movegen(s);
@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(kBlock) k_select(TreeView t, const oaz_state* 
                                                    SearchParams prm) {
     const uint32_t g = wave_game();
     if (g >= t.G) return;
-    if (active && !active[g]) return;
+    if (active && active[g] != 1) return;
     const int l = lane_id();
     oaz_node* T = t.nodes + (size_t)g * t.cap;
     uint32_t* path = t.path + (size_t)g * t.pathcap;
@@ -390,7 +390,7 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup(TreeView t, const oaz_
                                                           const float* __restrict__ value) {
     const uint32_t g = wave_game();
     if (g >= t.G) return;
-    if (active && !active[g]) return;
+    if (active && active[g] != 1) return;
     const int l = lane_id();
     oaz_node* T = t.nodes + (size_t)g * t.cap;
     const uint32_t* path = t.path + (size_t)g * t.pathcap;
@@ -537,6 +537,7 @@ __global__ void __launch_bounds__(kBlock) k_selfplay_reset(TreeView t, SlotView 
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= t.G) return;
     start_game(sv, g, 0, true);
+    if (sv.stagger > 1 && sv.active[g] == 1) sv.active[g] = (uint8_t)(1 + g % (sv.stagger > 255 ? 255 : sv.stagger));
     store_fresh_node(&t.nodes[(size_t)g * t.cap], 1.0, 0);
     t.n_nodes[g] = 1;
 }
@@ -548,7 +549,11 @@ __global__ void __launch_bounds__(kBlock) k_selfplay_reset(TreeView t, SlotView 
 __global__ void __launch_bounds__(kBlock) k_selfplay_move(TreeView t, SlotView sv) {
     const uint32_t g = wave_game();
     if (g >= t.G) return;
-    if (!sv.active[g]) return;
+    const uint8_t act = sv.active[g];
+    if (act != 1) {  // finished (0) or still waiting for its staggered start (> 1)
+        if (act > 1 && lane_id() == 0) sv.active[g] = act - 1;
+        return;
+    }
     const int l = lane_id();
     oaz_node* T = t.nodes + (size_t)g * t.cap;
     uint64_t* st = t.stats + (size_t)g * GS_COUNT;

@@ -78,7 +78,8 @@ class oaz_config(C.Structure):
         ("rank", C.c_int32),
         ("world", C.c_int32),
         ("sample_capacity", C.c_int32),
-        ("reserved", C.c_int32 * 7),
+        ("stagger", C.c_int32),
+        ("reserved", C.c_int32 * 6),
     ]
 
 

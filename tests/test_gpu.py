@@ -244,6 +244,16 @@ def test_selfplay_nn_continuous_batching_runs():
     assert np.allclose(samples["pi"].sum(1), 1.0, atol=1e-6)
 
 
+def test_selfplay_stagger_delays_slots():
+    G, S = 64, 4
+    with Engine(games=G, sims=4, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0, stagger=S) as e:
+        e.selfplay_reset()
+        e.selfplay_step(6)
+        st = e.selfplay_stats()
+    # slot g plays 6 - (g % S) plies
+    assert st.moves == sum(6 - (g % S) for g in range(G))
+
+
 # ---- Agent / self-play API mirror ----------------------------------------------------------
 def test_agent_api_mirror(orc):
     from onitama_az.mcts import AlphaZeroMcts, AlphaZeroMctsConfig, ConvResNet, ConvResNetConfig, TrainingAlphaZeroMcts
