@@ -137,13 +137,15 @@ def main():
         cfg["games"] = args.games
     if args.sims:
         cfg["sims"] = args.sims
+    # staggered starts must be over before the timed region (every slot playing)
+    stagger = min(args.stagger, args.warmup) if args.stagger > 1 else 0
     traffic = None
     if not args.pmc_child and not args.no_pmc and world == 1:
         traffic = pmc_traffic(args, cfg)  # child processes; this process has not touched the GPU yet
     eng = Engine(device=local, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0, train_noise=1,
                  max_plies=150, evaluator=_abi.EVAL_NN, precision=_abi.FP32, fixed_deck=cfg["fixed_deck"],
                  deck=[0, 1, 2, 3, 4], seed=20260101, rank=rank, world=world,
-                 sample_capacity=cfg["games"] * 24, stagger=0 if args.pmc_child else args.stagger)
+                 sample_capacity=cfg["games"] * 24, stagger=0 if args.pmc_child else stagger)
     eng.load_weights(random_weights(0, cfg["blocks"]))  # random-init weights (seed 0), SURVEY.md 8d
     eng.selfplay_reset()
     if args.pmc_child:  # profiled pass: one move of a couple of simulations, NN launches at full batch
@@ -213,7 +215,7 @@ def main():
                                    f"{cfg['blocks']}-block 64-ch ResNet, c_puct 5, Dirichlet root noise",
                        "games_per_gpu": cfg["games"], "sims_per_move": cfg["sims"], "blocks": cfg["blocks"],
                        "fixed_deck": bool(cfg["fixed_deck"]), "parallelism": f"games sharded x{world}"},
-            "sims_per_s_per_gpu": sims_all / T / world, "stagger": args.stagger,
+            "sims_per_s_per_gpu": sims_all / T / world, "stagger": stagger,
             "games_per_s": games_all / T, "plies_per_s": plies_all / T,
             "true_expansions_per_s": exp_all / T, "mean_select_depth": depth, "mean_branching": branching,
             "kernel_ms_per_step": {"select": kt.select_ms / args.steps, "nn": kt.nn_ms / args.steps,

@@ -173,49 +173,52 @@ static FoldedConv fold(const float*& p, int cout, int cin, int taps) {
     return f;
 }
 
-// B fragments of v_mfma_f32_32x32x2f32: lane l supplies B[k=l>>5][col=l&31]. Group `grp` of
-// tap t covers k-steps s = 4*grp..4*grp+3 of both halves; ci = h*S + s.
-static void pack_conv(const FoldedConv& f, int cin, int S, std::vector<float>& out) {
-    const int G4 = S / 4;
+// B fragments of v_mfma_f32_16x16x4f32 for a 64->64 conv: lane l supplies B[k=l>>4][col=l&15];
+// k-group g of tap t covers channels ci = 16g + 4(l>>4) + q, q = 0..3; N-tile nt = 16 columns.
+static void pack_conv64(const FoldedConv& f, std::vector<float>& out) {
     for (int t = 0; t < 9; ++t)
-        for (int grp = 0; grp < G4; ++grp)
-            for (int nt = 0; nt < 2; ++nt)
-                for (int l = 0; l < 64; ++l)
-                    for (int q = 0; q < 4; ++q) {
-                        const int co = nt * 32 + (l & 31);
-                        const int ci = (l >> 5) * S + 4 * grp + q;
-                        out.push_back(ci < cin ? f.w[((size_t)co * cin + ci) * 9 + t] : 0.0f);
-                    }
-    for (int o = 0; o < 64; ++o) out.push_back(f.b[o]);
-}
-
-// v2 (k_nn_tower16) B fragments of v_mfma_f32_16x16x4f32: lane l supplies B[k=l>>4][col=l&15];
-// group g of tap t covers channels ci = 16g + 4(l>>4) + q, q = 0..3; N-tile nt = 16 columns.
-static void pack_conv2(const FoldedConv& f, int cin, int G, std::vector<float>& out) {
-    for (int t = 0; t < 9; ++t)
-        for (int g = 0; g < G; ++g)
+        for (int g = 0; g < 4; ++g)
             for (int nt = 0; nt < 4; ++nt)
                 for (int l = 0; l < 64; ++l)
                     for (int q = 0; q < 4; ++q) {
                         const int co = nt * 16 + (l & 15);
                         const int ci = 16 * g + 4 * (l >> 4) + q;
-                        out.push_back(ci < cin ? f.w[((size_t)co * cin + ci) * 9 + t] : 0.0f);
+                        out.push_back(f.w[((size_t)co * 64 + ci) * 9 + t]);
                     }
     for (int o = 0; o < 64; ++o) out.push_back(f.b[o]);
 }
 
-static int pack_weights(const float* raw, int blocks, int variant, std::vector<float>& out) {
-    out.clear();
-    const size_t expect = variant == 2 ? nn2_packed_floats(blocks) : nn_packed_floats(blocks);
-    out.reserve(expect);
-    const float* p = raw;
-    if (variant == 2) pack_conv2(fold(p, 64, 21, 9), 21, 2, out);
-    else pack_conv(fold(p, 64, 21, 9), 21, 12, out);
-    for (int b = 0; b < blocks; ++b)
-        for (int j = 0; j < 2; ++j) {
-            if (variant == 2) pack_conv2(fold(p, 64, 64, 9), 64, 4, out);
-            else pack_conv(fold(p, 64, 64, 9), 64, 32, out);
+// First layer (k_nn_sq16): the 4 bitboard planes go through MFMA (lane l supplies
+// W[co = 16nt + (l&15)][plane l>>4][tap t]); the 16 card planes and the blue-to-move plane
+// (constant over the board, common.rs:68-77,32-37) become T[square][c][co] = sum over the
+// on-board taps of W[co][plane][tap], with c = card index or 16 for the colour plane.
+static void pack_first_layer(const FoldedConv& f, std::vector<float>& out) {
+    for (int t = 0; t < 9; ++t)
+        for (int nt = 0; nt < 4; ++nt)
+            for (int l = 0; l < 64; ++l) out.push_back(f.w[((size_t)(nt * 16 + (l & 15)) * 21 + (l >> 4)) * 9 + t]);
+    for (int o = 0; o < 64; ++o) out.push_back(f.b[o]);
+    for (int sq = 0; sq < 25; ++sq)
+        for (int c = 0; c < 17; ++c) {
+            const int plane = c < 16 ? 4 + c : 20;
+            for (int co = 0; co < 64; ++co) {
+                double acc = 0.0;
+                for (int t = 0; t < 9; ++t) {
+                    const int r = sq / 5 + t / 3 - 1, cc = sq % 5 + t % 3 - 1;
+                    if (r < 0 || r > 4 || cc < 0 || cc > 4) continue;
+                    acc += (double)f.w[((size_t)co * 21 + plane) * 9 + t];
+                }
+                out.push_back((float)acc);
+            }
         }
+}
+
+static int pack_weights(const float* raw, int blocks, std::vector<float>& out) {
+    out.clear();
+    out.reserve(nn_packed_floats(blocks));
+    const float* p = raw;
+    pack_first_layer(fold(p, 64, 21, 9), out);
+    for (int b = 0; b < blocks; ++b)
+        for (int j = 0; j < 2; ++j) pack_conv64(fold(p, 64, 64, 9), out);
     // value head: vh_conv + vh_bn folded, vh_linear1, vh_linear2
     FoldedConv vc = fold(p, 1, 64, 1);
     for (int c = 0; c < 64; ++c) out.push_back(vc.w[c]);
@@ -237,7 +240,7 @@ static int pack_weights(const float* raw, int blocks, int variant, std::vector<f
     for (int i = 0; i < 50; ++i) out.push_back(*p++);    // ph_linear2.bias
     out.push_back(0.0f);
     out.push_back(0.0f);
-    if (out.size() != expect) return set_err(OAZ_ERR_STATE, "pack: size mismatch");
+    if (out.size() != nn_packed_floats(blocks)) return set_err(OAZ_ERR_STATE, "pack: size mismatch");
     if ((size_t)(p - raw) != oaz_weight_count(blocks, 64, 21)) return set_err(OAZ_ERR_STATE, "pack: raw size mismatch");
     return 0;
 }
@@ -375,8 +378,6 @@ struct oaz_engine {
     double* sqrt_tab = nullptr;
     float *policy = nullptr, *value = nullptr;
     float* weights = nullptr;
-    float* weights2 = nullptr;
-    int nn_variant = 2;
     bool have_weights = false;
     // search mode
     oaz_state* s_roots = nullptr;
@@ -553,7 +554,6 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
     e->pathcap = (uint32_t)cfg->sims + 1;               // depth grows by <= 1 per playout
     e->hcap = (uint32_t)cfg->max_plies + 2;             // train.rs:74-79 cut after max_plies+2 plies
     e->out_cap = cfg->sample_capacity > 0 ? (uint32_t)cfg->sample_capacity : e->G * 64u;
-    if (const char* v = getenv("OAZ_NN_VARIANT")) e->nn_variant = atoi(v) == 1 ? 1 : 2;
     auto fail = [&](void) -> oaz_engine* {
         std::string msg = g_err;
         oaz_destroy(e);
@@ -581,7 +581,6 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         dalloc(&e->stats, G * GS_COUNT) || dalloc(&e->stats_sum, (size_t)GS_COUNT) ||
         dalloc(&e->sqrt_tab, (size_t)cfg->sims + 2) || dalloc(&e->policy, G * 50) ||
         dalloc(&e->value, G) || dalloc(&e->weights, nn_packed_floats(cfg->blocks)) ||
-        dalloc(&e->weights2, nn2_packed_floats(cfg->blocks)) ||
         dalloc(&e->s_roots, G) || dalloc(&e->s_move, G) || dalloc(&e->s_pi, G * 50) ||
         dalloc(&e->s_rootv, G) || dalloc(&e->s_rootp, G * 50) || dalloc(&e->s_ply, G) ||
         dalloc(&e->root, G) || dalloc(&e->ply, G) || dalloc(&e->seq, G) ||
@@ -622,7 +621,7 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     }
     for (auto ev : e->pool) (void)hipEventDestroy(ev);
     void* ptrs[] = {e->nodes, e->n_nodes, e->path, e->depth, e->leaf, e->leaf_state, e->stats,
-                    e->stats_sum, e->sqrt_tab, e->policy, e->value, e->weights, e->weights2, e->s_roots,
+                    e->stats_sum, e->sqrt_tab, e->policy, e->value, e->weights, e->s_roots,
                     e->s_move, e->s_pi, e->s_rootv, e->s_rootp, e->s_ply, e->root, e->ply,
                     e->seq, e->game_id, e->active, e->hist, e->out, e->out_count, e->noise};
     for (void* p : ptrs) dfree(p);
@@ -643,12 +642,10 @@ extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
     if (n != need)  // the reference silently keeps random weights on a bad file (Q13); we refuse
         return set_err(OAZ_ERR_WEIGHTS, "load_weights: got %zu floats, need %zu for %d blocks", n, need,
                        e->cfg.blocks);
-    std::vector<float> packed, packed2;
-    if (int rc = pack_weights(blob, e->cfg.blocks, 1, packed)) return rc;
-    if (int rc = pack_weights(blob, e->cfg.blocks, 2, packed2)) return rc;
+    std::vector<float> packed;
+    if (int rc = pack_weights(blob, e->cfg.blocks, packed)) return rc;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipMemcpyAsync(e->weights, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
-    HIP_TRY(hipMemcpyAsync(e->weights2, packed2.data(), packed2.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->have_weights = true;
     return 0;
@@ -702,8 +699,6 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
     w.blob = e->weights;
     w.blocks = e->cfg.blocks;
     w.bf16 = 0;
-    w.blob2 = e->weights2;
-    w.variant = e->nn_variant;
     return timed(e, 1, B, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, e->stream); });
 }
 

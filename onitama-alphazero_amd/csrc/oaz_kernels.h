@@ -76,8 +76,6 @@ struct NNView {
     const float* blob;  // packed, BN-folded weights (DESIGN.md "NN weights layout")
     int32_t blocks;
     int32_t bf16;       // 1: bf16 MFMA inputs (fp32 accumulate)
-    const float* blob2; // packed for the v2 kernel (k_nn_tower16)
-    int32_t variant;    // 1: k_nn_forward (32-row tiles), 2: k_nn_tower16 (16 positions / WG)
 };
 
 // rules
@@ -92,7 +90,6 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
                              float* value, hipStream_t st);
 hipError_t launch_hash_eval(const oaz_state* s, int B, float* policy, float* value, hipStream_t st);
 size_t nn_packed_floats(int blocks);
-size_t nn2_packed_floats(int blocks);
 
 // MCTS
 hipError_t launch_tree_reset(const TreeView& t, hipStream_t st);

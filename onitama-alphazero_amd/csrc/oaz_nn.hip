@@ -1,17 +1,29 @@
-// oaz_nn.hip — ConvResNet policy-value forward (alphazero-training/src/net.rs:101-232), fused.
+// oaz_nn.hip — ConvResNet policy-value forward (alphazero-training/src/net.rs:101-232), fused
+// into one kernel: encoder -> conv3x3(21->64)+BN+ReLU -> blocks x [conv3x3+BN+ReLU ->
+// conv3x3+BN -> +skip -> ReLU] -> value head (1x1 conv, MLP, tanh) -> policy head (1x1 conv,
+// linear, softmax over 50).
 //
-// One wavefront evaluates SPW positions end to end: encoder -> conv3x3(21->64) -> blocks x
-// [conv3x3 -> relu -> conv3x3 -> +skip -> relu] -> value head -> policy head + softmax.
-//   * 3x3 convs are implicit GEMMs on v_mfma_f32_32x32x2_f32 (exact f32 MFMA, no xf32 on
-//     gfx950): M = one position's 25 squares padded to 32 rows, N = 64 output channels
-//     (two 32-column tiles), K = 9 taps x Cin. A rows are gathered from the LDS activation
-//     image through a per-lane neighbour index (off-board taps read a zero row); B fragments
-//     are pre-packed on the host so each k-group is one coalesced 1 KiB dwordx4 load.
-//   * BN (eval mode) is folded into the conv weights/bias on the host.
-//   * activations never leave LDS (7 KB per position); the skip connection lives in
-//     registers, so one LDS image per position suffices and convs write in place.
-//   * the first layer never materialises the 21 planes: A values are computed from the
-//     24-byte compact state (common.rs:26-80 semantics).
+// Geometry (k_nn_sq16)
+//   * A workgroup evaluates 16 positions. The 3x3 convs are implicit GEMMs on
+//     v_mfma_f32_16x16x4_f32 (exact fp32 MFMA; gfx950 has no xf32) whose 400 rows are ordered
+//     SQUARE-MAJOR (row = square*16 + position): an M-tile is one board square of all 16
+//     positions. For a tap, a tile's neighbour square is on the board for the whole tile or off
+//     it for the whole tile, so off-board products are skipped instead of multiplied by zero
+//     padding: 169 of the 225 (square, tap) products of a 5x5 board are computed.
+//   * 8 waves: wave w owns output channels 16*(w&3)..+15 and square group w>>2. The two groups
+//     (4 corners + 4 edges + 5 interior | 8 edges + 4 interior) carry 85 and 84 on-board
+//     (square, tap) pairs, and waves w, w+4 share a SIMD, so SIMDs are balanced.
+//   * Activations stay in LDS for the whole tower (row stride 72 floats, channel order
+//     16g + 4*(lane>>4) + q: the ds_read_b128 A gathers are bank-conflict free); the residual
+//     skip is kept in registers; each conv writes its output in place between barriers.
+//   * BN (eval) is folded on the host; B fragments are packed so that each k-group is one
+//     coalesced 1 KiB dwordx4 load per wave.
+//   * First layer: of the 21 input planes (common.rs:26-80) only the 4 bitboards vary across
+//     the board; the 16 card planes and the side-to-move plane are constant over all squares,
+//     so their contribution is the host-precomputed table T[square][card][channel] (sum of the
+//     folded weights over the on-board taps) added in the epilogue. The MFMA part of the first
+//     layer is therefore one k-step (4 bitboards) per (square, tap), with A values taken
+//     straight from the state's bits: the 21 planes are never materialised.
 #include <hip/hip_runtime.h>
 
 #include "oaz_device.h"
@@ -19,137 +31,41 @@
 
 namespace oaz {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+namespace nn {
 constexpr int kCh = 64;
-constexpr int kRS = 68;                      // LDS row stride (floats): 64 + 4 pad, no bank conflicts
-constexpr int kRows = 26;                    // 25 squares + zero row
-constexpr int kSampleFloats = kRows * kRS;   // 1768 floats = 7072 B
-constexpr int kInitS = 12;                   // first layer: Cin 21 padded to 24, k-steps per tap per half
-constexpr int kInitG = kInitS / 4;           // dwordx4 groups per tap
-constexpr int kConvS = 32;                   // 64-channel layers: k-steps per tap per half
-constexpr int kConvG = kConvS / 4;
-
-// Packed blob layout (floats), built by pack_weights() in oaz_engine.cpp:
-//   [init W: 9*3*2*64*4][init b: 64]
-//   blocks x 2 x [W: 9*8*2*64*4][b: 64]
-//   value:  wv[64] bv[1] pad[3] l1w[64*25] l1b[64] l2w[64] l2b[1] pad[3]
-//   policy: wp[2*64] bp[2] pad[2] plw[50*50] plb[50] pad[2]
-constexpr size_t kInitW = 9 * kInitG * 2 * 64 * 4;
-constexpr size_t kConvW = 9 * kConvG * 2 * 64 * 4;
+constexpr int kSB = 16;      // positions per workgroup (= rows per M-tile)
+constexpr int kWaves = 8;
+constexpr int kTPW = 13;     // squares per wave group (group 1: 12)
+constexpr int kRS = 72;      // LDS row stride (floats)
+constexpr int kScratch = 128;  // per-wave head scratch (floats)
+constexpr int kLdsFloats = kSB * 25 * kRS + kWaves * kScratch;  // 29824 floats = 119,296 B
+// Packed blob (floats), built by pack_weights() in oaz_engine.cpp:
+//   [L1 B: 9 taps x 4 N-tiles x 64 lanes][L1 bias 64][L1 table: 25 squares x 17 x 64]
+//   blocks x 2 x [W: 9 taps x 4 groups x 4 N-tiles x 64 lanes x 4][bias 64]
+//   value head:  wv[64] bv pad[3] l1w[64*25] l1b[64] l2w[64] l2b pad[3]
+//   policy head: wp[2*64] bp[2] pad[2] plw[50*50] plb[50] pad[2]
+constexpr size_t kL1B = 9 * 4 * 64;
+constexpr size_t kL1Table = 25 * 17 * kCh;
+constexpr size_t kW64 = 9 * 4 * 4 * 64 * 4;
 constexpr size_t kValueF = 64 + 4 + 64 * 25 + 64 + 64 + 4;
 constexpr size_t kPolicyF = 128 + 4 + 2500 + 52;
+}  // namespace nn
 
 size_t nn_packed_floats(int blocks) {
-    return kInitW + kCh + (size_t)blocks * 2 * (kConvW + kCh) + kValueF + kPolicyF;
+    return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (nn::kW64 + nn::kCh) + nn::kValueF +
+           nn::kPolicyF;
 }
 
-__device__ __forceinline__ int nbr_index(int i, int t) {
-    // square i (row-major 5x5) shifted by tap t = (dy, dx) in {-1,0,1}^2; 25 = off board
-    if (i >= 25) return 25;
-    const int r = i / 5 + t / 3 - 1, c = i % 5 + t % 3 - 1;
+// Square groups: 4 corners + 4 edges + 5 interior (85 on-board taps) | 8 edges + 4 interior (84).
+__constant__ int8_t c_sq_order[25] = {0, 4, 20, 24, 1, 3, 21, 23, 6, 8, 12, 16, 18,
+                                      2, 5, 10, 15, 9, 14, 19, 22, 7, 11, 13, 17};
+
+__device__ __forceinline__ int nbr_index(int sq, int t) {
+    // square sq (row-major 5x5) shifted by tap t = (dy, dx) in {-1,0,1}^2; 25 = off board
+    const int r = sq / 5 + t / 3 - 1, c = sq % 5 + t % 3 - 1;
     return (r >= 0 && r < 5 && c >= 0 && c < 5) ? r * 5 + c : 25;
-}
-
-// Input plane `ci` (0..23, 21..23 zero padding) of state s at square sq (25 = off board).
-__device__ __forceinline__ float plane_value(const oaz_state& s, int ci, int sq) {
-    if (sq >= 25) return 0.0f;
-    const int color = s.to_move & 1;
-    if (ci < 4) {
-        const uint32_t src = ci == 0 ? s.pawns[0] : ci == 1 ? s.kings[0] : ci == 2 ? s.pawns[1] : s.kings[1];
-        return (src & sq_bit(sq)) ? 1.0f : 0.0f;
-    }
-    if (ci < 20) {  // the mover's two cards (static indices: no local-array promotion)
-        const int c0 = (color ? s.cards[2] : s.cards[0]) & 15, c1 = (color ? s.cards[3] : s.cards[1]) & 15;
-        return (c0 == ci - 4 || c1 == ci - 4) ? 1.0f : 0.0f;
-    }
-    if (ci == 20) return color ? 1.0f : 0.0f;
-    return 0.0f;
-}
-
-template <int SPW>
-__device__ __forceinline__ void zero_acc(f32x16 (&acc)[SPW][2]) {
-#pragma unroll
-    for (int sp = 0; sp < SPW; ++sp) {
-        acc[sp][0] = f32x16{};
-        acc[sp][1] = f32x16{};
-    }
-}
-
-// acc += conv3x3(act) over 64 input channels; ci = h*32 + 4*grp + q.
-template <int SPW>
-__device__ __forceinline__ void conv64(f32x16 (&acc)[SPW][2], const float* act, const float4* W,
-                                       int lane) {
-    const int i = lane & 31, h = lane >> 5;
-    float4 b0 = W[0 * 64 + lane], b1 = W[1 * 64 + lane];
-    for (int t = 0; t < 9; ++t) {
-        const int row = nbr_index(i, t);
-        const float* arow = act + row * kRS + h * 32;
-#pragma unroll 2
-        for (int grp = 0; grp < kConvG; ++grp) {
-            const int gi = t * kConvG + grp;
-            float4 n0 = b0, n1 = b1;
-            if (gi + 1 < 9 * kConvG) {
-                n0 = W[((gi + 1) * 2 + 0) * 64 + lane];
-                n1 = W[((gi + 1) * 2 + 1) * 64 + lane];
-            }
-            float4 a[SPW];
-#pragma unroll
-            for (int sp = 0; sp < SPW; ++sp)
-                a[sp] = *reinterpret_cast<const float4*>(arow + sp * kSampleFloats + 4 * grp);
-#pragma unroll
-            for (int sp = 0; sp < SPW; ++sp) {
-                acc[sp][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[sp].x, b0.x, acc[sp][0], 0, 0, 0);
-                acc[sp][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[sp].x, b1.x, acc[sp][1], 0, 0, 0);
-            }
-#pragma unroll
-            for (int sp = 0; sp < SPW; ++sp) {
-                acc[sp][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[sp].y, b0.y, acc[sp][0], 0, 0, 0);
-                acc[sp][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[sp].y, b1.y, acc[sp][1], 0, 0, 0);
-            }
-#pragma unroll
-            for (int sp = 0; sp < SPW; ++sp) {
-                acc[sp][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[sp].z, b0.z, acc[sp][0], 0, 0, 0);
-                acc[sp][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[sp].z, b1.z, acc[sp][1], 0, 0, 0);
-            }
-#pragma unroll
-            for (int sp = 0; sp < SPW; ++sp) {
-                acc[sp][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[sp].w, b0.w, acc[sp][0], 0, 0, 0);
-                acc[sp][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[sp].w, b1.w, acc[sp][1], 0, 0, 0);
-            }
-            b0 = n0;
-            b1 = n1;
-        }
-    }
-}
-
-// C/D layout of v_mfma_f32_32x32x2f32: reg r of lane l holds row (r&3)+8*(r>>2)+4*(l>>5),
-// column l&31. Rows are squares (>=25: padding), columns output channels.
-__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
-
-template <int SPW>
-__device__ __forceinline__ void epilogue(const f32x16 (&acc)[SPW][2], float* act, const float* bias,
-                                         const f32x16 (*skip)[2], int lane) {
-    const int i = lane & 31;
-    const float bb0 = bias[i], bb1 = bias[32 + i];
-#pragma unroll
-    for (int sp = 0; sp < SPW; ++sp) {
-        float* a = act + sp * kSampleFloats;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = acc_row(r, lane);
-            if (row < 25) {
-                float v0 = acc[sp][0][r] + bb0;
-                float v1 = acc[sp][1][r] + bb1;
-                if (skip) {
-                    v0 += skip[sp][0][r];
-                    v1 += skip[sp][1][r];
-                }
-                a[row * kRS + i] = v0 > 0.0f ? v0 : 0.0f;
-                a[row * kRS + 32 + i] = v1 > 0.0f ? v1 : 0.0f;
-            }
-        }
-    }
 }
 
 __device__ __forceinline__ float wave_sum_f(float v) {
@@ -163,193 +79,41 @@ __device__ __forceinline__ float wave_max_f(float v) {
     return v;
 }
 
-template <int SPW, int WPB>
-__global__ void __launch_bounds__(64 * WPB) k_nn_forward(const oaz_state* __restrict__ states, int B,
-                                                         const float* __restrict__ blob, int blocks,
-                                                         float* __restrict__ policy,
-                                                         float* __restrict__ value) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int i = lane & 31, h = lane >> 5;
-    float* act = smem + (size_t)wave * SPW * kSampleFloats;
-    const int b0 = (blockIdx.x * WPB + wave) * SPW;
-    if (b0 >= B) return;  // whole wave idle (no block-level barriers in this kernel)
-
-    oaz_state st[SPW];
-#pragma unroll
-    for (int sp = 0; sp < SPW; ++sp) {
-        const int b = b0 + sp < B ? b0 + sp : b0;
-        st[sp] = states[b];
-        act[sp * kSampleFloats + 25 * kRS + lane] = 0.0f;  // zero row (64 channels)
-    }
-
-    // ---- initial block: conv3x3(21->64)+BN+ReLU (net.rs:119-136) ----
-    f32x16 acc[SPW][2];
-    zero_acc<SPW>(acc);
-    const float* p = blob;
-    {
-        const float4* W = reinterpret_cast<const float4*>(p);
-        for (int t = 0; t < 9; ++t) {
-            const int sq = nbr_index(i, t);
-#pragma unroll
-            for (int grp = 0; grp < kInitG; ++grp) {
-                const float4 w0 = W[((t * kInitG + grp) * 2 + 0) * 64 + lane];
-                const float4 w1 = W[((t * kInitG + grp) * 2 + 1) * 64 + lane];
-                const float wb0[4] = {w0.x, w0.y, w0.z, w0.w};
-                const float wb1[4] = {w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int ci = h * kInitS + 4 * grp + q;
-#pragma unroll
-                    for (int sp = 0; sp < SPW; ++sp) {
-                        const float av = plane_value(st[sp], ci, sq);
-                        acc[sp][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wb0[q], acc[sp][0], 0, 0, 0);
-                        acc[sp][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wb1[q], acc[sp][1], 0, 0, 0);
-                    }
-                }
-            }
-        }
-        p += kInitW;
-        epilogue<SPW>(acc, act, p, nullptr, lane);
-        p += kCh;
-    }
-
-    // ---- residual tower (net.rs:39-66, 138-147) ----
-    for (int blk = 0; blk < blocks; ++blk) {
-        f32x16 skip[SPW][2];
-#pragma unroll
-        for (int sp = 0; sp < SPW; ++sp)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = acc_row(r, lane);
-                const float* a = act + sp * kSampleFloats + (row < 25 ? row : 25) * kRS;
-                skip[sp][0][r] = a[i];
-                skip[sp][1][r] = a[32 + i];
-            }
-        zero_acc<SPW>(acc);
-        conv64<SPW>(acc, act, reinterpret_cast<const float4*>(p), lane);
-        p += kConvW;
-        epilogue<SPW>(acc, act, p, nullptr, lane);
-        p += kCh;
-        zero_acc<SPW>(acc);
-        conv64<SPW>(acc, act, reinterpret_cast<const float4*>(p), lane);
-        p += kConvW;
-        epilogue<SPW>(acc, act, p, skip, lane);
-        p += kCh;
-    }
-
-    // ---- heads (net.rs:152-213), per position ----
-    const float* vw = p;
-    const float vb = p[64];
-    const float* l1w = p + 68;
-    const float* l1b = l1w + 64 * 25;
-    const float* l2w = l1b + 64;
-    const float l2b = l2w[64];
-    const float* pp = p + kValueF;
-    const float* pw = pp;
-    const float pb0 = pp[128], pb1 = pp[129];
-    const float* plw = pp + 132;
-    const float* plb = plw + 2500;
-    for (int sp = 0; sp < SPW; ++sp) {
-        float* a = act + sp * kSampleFloats;
-        // 1x1 convs (value 64->1, policy 64->2) with folded BN, ReLU; lane = square
-        float v1 = 0.0f, c0 = 0.0f, c1 = 0.0f;
-        if (lane < 25) {
-            float sv = vb, s0 = pb0, s1 = pb1;
-            const float* row = a + lane * kRS;
-            for (int c = 0; c < kCh; c += 4) {
-                const float4 x = *reinterpret_cast<const float4*>(row + c);
-                sv += vw[c] * x.x + vw[c + 1] * x.y + vw[c + 2] * x.z + vw[c + 3] * x.w;
-                s0 += pw[c] * x.x + pw[c + 1] * x.y + pw[c + 2] * x.z + pw[c + 3] * x.w;
-                s1 += pw[64 + c] * x.x + pw[65 + c] * x.y + pw[66 + c] * x.z + pw[67 + c] * x.w;
-            }
-            v1 = sv > 0.0f ? sv : 0.0f;
-            c0 = s0 > 0.0f ? s0 : 0.0f;
-            c1 = s1 > 0.0f ? s1 : 0.0f;
-        }
-        // stage the flattened head inputs in the (now free) first rows of the image
-        if (lane < 25) {
-            a[lane] = v1;          // value features [25]
-            a[32 + lane] = c0;     // policy features [o*25+p] at 32..81
-            a[57 + lane] = c1;
-        }
-        // value: linear 25->64, ReLU, linear 64->1, tanh
-        float hj = l1b[lane];
-        for (int q = 0; q < 25; ++q) hj += l1w[lane * 25 + q] * a[q];
-        hj = hj > 0.0f ? hj : 0.0f;
-        const float vsum = wave_sum_f(l2w[lane] * hj);
-        // policy: linear 50->50, softmax over all 50 (net.rs:205-212)
-        float lg = -INFINITY;
-        if (lane < 50) {
-            lg = plb[lane];
-            for (int f = 0; f < 50; ++f) lg += plw[lane * 50 + f] * a[32 + f];
-        }
-        const float mx = wave_max_f(lg);
-        const float e = lane < 50 ? expf(lg - mx) : 0.0f;
-        const float den = wave_sum_f(e);
-        const int b = b0 + sp;
-        if (b < B) {
-            if (lane < 50) policy[(size_t)b * 50 + lane] = e / den;
-            if (lane == 0) value[b] = tanhf(vsum + l2b);
-        }
-    }
-}
-
-// ===========================================================================================
-// v2: square-major tiles, off-board taps skipped.
-//   A workgroup evaluates 16 positions. Its 400 GEMM rows are ordered square-major
-//   (row = square*16 + position), so M-tile m is "square m of all 16 positions". For tap t the
-//   neighbour of square m is either on the board for the whole tile or off it for the whole
-//   tile: off-board tiles are skipped instead of multiplied by a zero row — 169 of the 225
-//   (tile, tap) products of a 5x5 board are computed, the dense GEMM's padding work is gone.
-//   8 waves: wave w owns output channels 16*(w&3)..+15 and square group w>>2; the two groups
-//   (13 and 12 squares) carry 85 and 84 on-board (square, tap) pairs, so the two waves that
-//   share a SIMD are balanced. Two waves per SIMD (<= 256 VGPRs). Layers are separated by
-//   workgroup barriers (every wave reads all input channels of its squares' neighbours).
-// ===========================================================================================
-namespace v2 {
-constexpr int kSB = 16;                  // positions per workgroup (= rows per M-tile)
-constexpr int kWaves = 8;
-constexpr int kTPW = 13;                 // squares per wave group (group 1: 12)
-// Row stride 72 floats and channel order ci = 16g + 4kq + q: the 16-lane groups of a
-// ds_read_b128 (lanes = 16 consecutive rows x 4 channel quarters) hit 16 distinct 16-byte
-// bank slots (row*18 + kq mod 16), so the A gathers are conflict-free.
-constexpr int kRS2 = 72;
-constexpr int kScratch = 128;            // per-wave head scratch (floats)
-constexpr int kLdsFloats = kSB * 25 * kRS2 + kWaves * kScratch;  // 29824 floats = 119,296 B
-constexpr size_t kW0 = 9 * 2 * 4 * 64 * 4;   // first layer, Cin padded 21 -> 32
-constexpr size_t kW64 = 9 * 4 * 4 * 64 * 4;  // 64 -> 64
-}  // namespace v2
-
-// Square groups: 4 corners + 4 edges + 5 interior (85 on-board taps) | 8 edges + 4 interior (84).
-__constant__ int8_t c_sq_order[25] = {0, 4, 20, 24, 1, 3, 21, 23, 6, 8, 12, 16, 18,
-                                      2, 5, 10, 15, 9, 14, 19, 22, 7, 11, 13, 17};
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-size_t nn2_packed_floats(int blocks) {
-    return v2::kW0 + kCh + (size_t)blocks * 2 * (v2::kW64 + kCh) + kValueF + kPolicyF;
-}
-
-// acc[j] += conv3x3 over CIN = 16*G input channels for square sq[j] (j < ntiles).
-// K order per tap: at k-step (g, q) lane group kq = lane>>4 supplies channel 16g + 4kq + q.
-template <int G>
-__device__ __forceinline__ void conv_sq(f32x4 (&acc)[v2::kTPW], const float* act, const float4* W,
-                                        const int (&sq)[v2::kTPW], int lane, int nt, int ntiles) {
-    const int i = lane & 15, kq = lane >> 4;
-    const float* base = act + i * v2::kRS2 + 4 * kq;
+// First layer, bitboard part: acc[j] += sum over on-board taps of bit(plane kq, neighbour) *
+// W[co][kq][tap] — one v_mfma_f32_16x16x4_f32 per (square, tap), K = the 4 bitboards.
+__device__ __forceinline__ void conv_l1(f32x4 (&acc)[nn::kTPW], uint32_t bb, const float* W,
+                                        const int (&sq)[nn::kTPW], int lane, int nt, int ntiles) {
     for (int t = 0; t < 9; ++t) {
-        int off[v2::kTPW];  // wave-uniform: row offset of the neighbour square, -1 if off board
+        const float b = W[(t * 4 + nt) * 64 + lane];
 #pragma unroll
-        for (int j = 0; j < v2::kTPW; ++j) {
+        for (int j = 0; j < nn::kTPW; ++j) {
             const int nb = nbr_index(sq[j], t);
-            off[j] = (j < ntiles && nb < 25) ? nb * v2::kSB * v2::kRS2 : -1;
+            if (j < ntiles && nb < 25) {
+                const float a = (float)((bb >> (31 - nb)) & 1u);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+            }
+        }
+    }
+}
+
+// acc[j] += conv3x3 over 64 input channels for square sq[j] (j < ntiles).
+// K order per tap: at k-step (g, q) lane group kq = lane>>4 supplies channel 16g + 4kq + q.
+__device__ __forceinline__ void conv64(f32x4 (&acc)[nn::kTPW], const float* act, const float4* W,
+                                       const int (&sq)[nn::kTPW], int lane, int nt, int ntiles) {
+    const int i = lane & 15, kq = lane >> 4;
+    const float* base = act + i * nn::kRS + 4 * kq;
+    for (int t = 0; t < 9; ++t) {
+        int off[nn::kTPW];  // wave-uniform: row offset of the neighbour square, -1 if off board
+#pragma unroll
+        for (int j = 0; j < nn::kTPW; ++j) {
+            const int nb = nbr_index(sq[j], t);
+            off[j] = (j < ntiles && nb < 25) ? nb * nn::kSB * nn::kRS : -1;
         }
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const float4 b = W[((t * G + g) * 4 + nt) * 64 + lane];
+        for (int g = 0; g < 4; ++g) {
+            const float4 b = W[((t * 4 + g) * 4 + nt) * 64 + lane];
 #pragma unroll
-            for (int j = 0; j < v2::kTPW; ++j)
+            for (int j = 0; j < nn::kTPW; ++j)
                 if (off[j] >= 0) {
                     const float4 a = *reinterpret_cast<const float4*>(base + off[j] + 16 * g);
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc[j], 0, 0, 0);
@@ -363,50 +127,70 @@ __device__ __forceinline__ void conv_sq(f32x4 (&acc)[v2::kTPW], const float* act
 
 // C/D of v_mfma_f32_16x16x4_f32: reg r of lane l = (row (l>>4)*4 + r, col l&15) of the tile,
 // i.e. position (l>>4)*4 + r at square sq[j]; LDS row = square*16 + position.
-__device__ __forceinline__ void epilogue_sq(const f32x4 (&acc)[v2::kTPW], float* act, const float* bias,
-                                            const f32x4* skip, const int (&sq)[v2::kTPW], int lane, int nt,
-                                            int ntiles) {
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[nn::kTPW], float* act, const float* bias,
+                                         const f32x4* skip, const int (&sq)[nn::kTPW], int lane, int nt,
+                                         int ntiles) {
     const int co = nt * 16 + (lane & 15);
     const float bb = bias[co];
 #pragma unroll
-    for (int j = 0; j < v2::kTPW; ++j)
+    for (int j = 0; j < nn::kTPW; ++j)
         if (j < ntiles)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = sq[j] * v2::kSB + (lane >> 4) * 4 + r;
+                const int row = sq[j] * nn::kSB + (lane >> 4) * 4 + r;
                 float v = acc[j][r] + bb;
                 if (skip) v += skip[j][r];
-                act[row * v2::kRS2 + co] = v > 0.0f ? v : 0.0f;
+                act[row * nn::kRS + co] = v > 0.0f ? v : 0.0f;
             }
 }
 
-__device__ __forceinline__ void read_skip_sq(f32x4 (&skip)[v2::kTPW], const float* act, const int (&sq)[v2::kTPW],
-                                             int lane, int nt, int ntiles) {
+// First-layer epilogue: bias + constant-plane table (the mover's two cards, blue-to-move).
+__device__ __forceinline__ void epilogue_l1(const f32x4 (&acc)[nn::kTPW], float* act, const float* bias,
+                                            const float* table, const int* pinfo, const int (&sq)[nn::kTPW],
+                                            int lane, int nt, int ntiles) {
     const int co = nt * 16 + (lane & 15);
+    const float bb = bias[co];
 #pragma unroll
-    for (int j = 0; j < v2::kTPW; ++j)
+    for (int j = 0; j < nn::kTPW; ++j)
         if (j < ntiles)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) skip[j][r] = act[(sq[j] * v2::kSB + (lane >> 4) * 4 + r) * v2::kRS2 + co];
+            for (int r = 0; r < 4; ++r) {
+                const int pos = (lane >> 4) * 4 + r;
+                const int info = pinfo[pos];
+                const float* ts = table + (size_t)sq[j] * 17 * nn::kCh + co;
+                float v = acc[j][r] + bb + ts[(info & 15) * nn::kCh] + ts[((info >> 4) & 15) * nn::kCh];
+                if (info & 0x100) v += ts[16 * nn::kCh];
+                act[(sq[j] * nn::kSB + pos) * nn::kRS + co] = v > 0.0f ? v : 0.0f;
+            }
+}
+
+__device__ __forceinline__ void read_skip(f32x4 (&skip)[nn::kTPW], const float* act, const int (&sq)[nn::kTPW],
+                                          int lane, int nt, int ntiles) {
+    const int co = nt * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < nn::kTPW; ++j)
+        if (j < ntiles)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) skip[j][r] = act[(sq[j] * nn::kSB + (lane >> 4) * 4 + r) * nn::kRS + co];
 }
 
 // value + policy heads (net.rs:152-213) for position `s` of the workgroup (one wave).
-__device__ __forceinline__ void heads_sq(const float* act, float* scratch, int s, const float* p, int lane, int b,
-                                         int B, float* policy, float* value) {
+__device__ __forceinline__ void heads(const float* act, float* scratch, int s, const float* p, int lane, int b, int B,
+                                      float* policy, float* value) {
     const float* vw = p;
     const float vb = p[64];
     const float* l1w = p + 68;
     const float* l1b = l1w + 64 * 25;
     const float* l2w = l1b + 64;
     const float l2b = l2w[64];
-    const float* pp = p + kValueF;
+    const float* pp = p + nn::kValueF;
     const float pb0 = pp[128], pb1 = pp[129];
     const float* plw = pp + 132;
     const float* plb = plw + 2500;
     if (lane < 25) {  // 1x1 convs (value 64->1, policy 64->2) with folded BN, ReLU; lane = square
         float sv = vb, s0 = pb0, s1 = pb1;
-        const float* row = act + (lane * v2::kSB + s) * v2::kRS2;
-        for (int c = 0; c < kCh; c += 4) {
+        const float* row = act + (lane * nn::kSB + s) * nn::kRS;
+        for (int c = 0; c < nn::kCh; c += 4) {
             const float4 x = *reinterpret_cast<const float4*>(row + c);
             sv += vw[c] * x.x + vw[c + 1] * x.y + vw[c + 2] * x.z + vw[c + 3] * x.w;
             s0 += pp[c] * x.x + pp[c + 1] * x.y + pp[c + 2] * x.z + pp[c + 3] * x.w;
@@ -434,89 +218,75 @@ __device__ __forceinline__ void heads_sq(const float* act, float* scratch, int s
     }
 }
 
-__global__ void __launch_bounds__(64 * v2::kWaves) k_nn_sq16(const oaz_state* __restrict__ states, int B,
+__global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __restrict__ states, int B,
                                                              const float* __restrict__ blob, int blocks,
                                                              float* __restrict__ policy,
                                                              float* __restrict__ value) {
-    __shared__ __attribute__((aligned(16))) float act[v2::kLdsFloats];
+    __shared__ __attribute__((aligned(16))) float act[nn::kLdsFloats];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nt = wave & 3, grp = wave >> 2;
-    const int ntiles = grp == 0 ? v2::kTPW : 25 - v2::kTPW;
-    int sq[v2::kTPW];
+    const int ntiles = grp == 0 ? nn::kTPW : 25 - nn::kTPW;
+    int sq[nn::kTPW];
 #pragma unroll
-    for (int j = 0; j < v2::kTPW; ++j) sq[j] = (j < ntiles) ? c_sq_order[grp * v2::kTPW + j] : 0;
-    const int b0 = blockIdx.x * v2::kSB;
+    for (int j = 0; j < nn::kTPW; ++j) sq[j] = (j < ntiles) ? c_sq_order[grp * nn::kTPW + j] : 0;
+    const int b0 = blockIdx.x * nn::kSB;
+    // per-position card/colour info for the first-layer table; the area is wave 0's head
+    // scratch, free until the heads run
+    int* pinfo = reinterpret_cast<int*>(act + nn::kSB * 25 * nn::kRS);
 
-    // encoder (common.rs:26-80): 21 planes, zero-padded to 32 channels, from the 24-byte state
-    if (tid < v2::kSB * 25) {
-        const int sqr = tid / v2::kSB, pos = tid - v2::kSB * sqr;
+    // encoder (common.rs:26-80): lane = (position lane&15, bitboard lane>>4: red pawns, red
+    // king, blue pawns, blue king); the cards / colour of each position go to LDS
+    {
+        const int pos = lane & 15, kq = lane >> 4;
         const int b = b0 + pos < B ? b0 + pos : b0;
-        const oaz_state st = states[b];
-        float* row = act + tid * v2::kRS2;
-#pragma unroll
-        for (int c = 0; c < 32; c += 4) {
-            float4 v;
-            v.x = plane_value(st, c, sqr);
-            v.y = plane_value(st, c + 1, sqr);
-            v.z = plane_value(st, c + 2, sqr);
-            v.w = plane_value(st, c + 3, sqr);
-            *reinterpret_cast<float4*>(row + c) = v;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
+        const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
+        if (tid < nn::kSB) {
+            const oaz_state st = states[b];
+            const int blue = st.to_move & 1;
+            const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
+            pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
         }
-    }
-    __syncthreads();
-
-    f32x4 acc[v2::kTPW];
-    f32x4 skip[v2::kTPW];
-    const float* p = blob;
+        __syncthreads();
+        f32x4 acc[nn::kTPW];
 #pragma unroll
-    for (int j = 0; j < v2::kTPW; ++j) acc[j] = f32x4{};
-    conv_sq<2>(acc, act, reinterpret_cast<const float4*>(p), sq, lane, nt, ntiles);
-    p += v2::kW0;
-    __syncthreads();
-    epilogue_sq(acc, act, p, nullptr, sq, lane, nt, ntiles);
-    p += kCh;
-    __syncthreads();
+        for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
+        conv_l1(acc, bb, blob, sq, lane, nt, ntiles);
+        epilogue_l1(acc, act, blob + nn::kL1B, blob + nn::kL1B + nn::kCh, pinfo, sq, lane, nt, ntiles);
+        __syncthreads();
+    }
 
+    const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
+    f32x4 acc[nn::kTPW];
+    f32x4 skip[nn::kTPW];
     for (int blk = 0; blk < blocks; ++blk) {
-        read_skip_sq(skip, act, sq, lane, nt, ntiles);
+        read_skip(skip, act, sq, lane, nt, ntiles);
 #pragma unroll
-        for (int j = 0; j < v2::kTPW; ++j) acc[j] = f32x4{};
-        conv_sq<4>(acc, act, reinterpret_cast<const float4*>(p), sq, lane, nt, ntiles);
-        p += v2::kW64;
+        for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
+        conv64(acc, act, reinterpret_cast<const float4*>(p), sq, lane, nt, ntiles);
+        p += nn::kW64;
         __syncthreads();
-        epilogue_sq(acc, act, p, nullptr, sq, lane, nt, ntiles);
-        p += kCh;
+        epilogue(acc, act, p, nullptr, sq, lane, nt, ntiles);
+        p += nn::kCh;
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < v2::kTPW; ++j) acc[j] = f32x4{};
-        conv_sq<4>(acc, act, reinterpret_cast<const float4*>(p), sq, lane, nt, ntiles);
-        p += v2::kW64;
+        for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
+        conv64(acc, act, reinterpret_cast<const float4*>(p), sq, lane, nt, ntiles);
+        p += nn::kW64;
         __syncthreads();
-        epilogue_sq(acc, act, p, skip, sq, lane, nt, ntiles);
-        p += kCh;
+        epilogue(acc, act, p, skip, sq, lane, nt, ntiles);
+        p += nn::kCh;
         __syncthreads();
     }
-    float* scratch = act + v2::kSB * 25 * v2::kRS2 + wave * v2::kScratch;
-    for (int s = wave; s < v2::kSB; s += v2::kWaves) heads_sq(act, scratch, s, p, lane, b0 + s, B, policy, value);
+    float* scratch = act + nn::kSB * 25 * nn::kRS + wave * nn::kScratch;
+    for (int s = wave; s < nn::kSB; s += nn::kWaves) heads(act, scratch, s, p, lane, b0 + s, B, policy, value);
 }
 
-constexpr int kSPW = 2;
-constexpr int kWPB = 4;
-
-hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy,
-                             float* value, hipStream_t st) {
+hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy, float* value,
+                             hipStream_t st) {
     if (B <= 0) return hipSuccess;
-    if (w.variant == 2) {
-        const unsigned grid2 = (unsigned)((B + v2::kSB - 1) / v2::kSB);
-        hipLaunchKernelGGL(k_nn_sq16, dim3(grid2), dim3(64 * v2::kWaves), 0, st, s, B, w.blob2, w.blocks, policy,
-                           value);
-        return hipGetLastError();
-    }
-    const int per_block = kSPW * kWPB;
-    const unsigned grid = (unsigned)((B + per_block - 1) / per_block);
-    const size_t lds = (size_t)kWPB * kSPW * kSampleFloats * sizeof(float);
-    hipLaunchKernelGGL((k_nn_forward<kSPW, kWPB>), dim3(grid), dim3(64 * kWPB), lds, st, s, B,
-                       w.blob, w.blocks, policy, value);
+    const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
+    hipLaunchKernelGGL(k_nn_sq16, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy, value);
     return hipGetLastError();
 }
 

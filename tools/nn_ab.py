@@ -1,5 +1,5 @@
-"""A/B the NN kernel variants in one process (interleaved rounds): parity vs the torch goldens
-and per-launch time at a given batch. Usage: python tools/nn_ab.py [--batch 65536] [--variants 1,2,3]"""
+"""NN kernel microbench: parity vs the torch goldens and per-launch time at a given batch, over
+interleaved rounds of one or more engines (block counts). Usage: python tools/nn_ab.py [--batch 65536] [--blocks 3,6]"""
 import argparse
 import json
 import os
@@ -20,24 +20,22 @@ FLOP = {3: 11_681_928, 5: 19_054_728, 6: 22_741_128}
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
-    ap.add_argument("--variants", default="1,2,3")
-    ap.add_argument("--blocks", type=int, default=3)
+    ap.add_argument("--blocks", default="3")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     g = np.load(ROOT / "tests/golden/nn_golden.npz")
     w3 = np.load(ROOT / "tests/golden/weights_3block_trained.npy")
     engines = {}
-    for v in [int(x) for x in a.variants.split(",")]:
-        os.environ["OAZ_NN_VARIANT"] = str(v)
-        e = Engine(games=a.batch, sims=1, blocks=a.blocks, evaluator=_abi.EVAL_NN)
-        if a.blocks == 3:
+    for v in [int(x) for x in a.blocks.split(",")]:
+        e = Engine(games=a.batch, sims=1, blocks=v, evaluator=_abi.EVAL_NN)
+        if v == 3:
             e.load_weights(w3)
             p, val = e.nn_forward(g["states"])
             err = float(max(np.abs(p - g["policy_trained3"]).max(), np.abs(val - g["value_trained3"]).max()))
         else:
             err = None
-        e.load_weights(random_weights(0, a.blocks))
+        e.load_weights(random_weights(0, v))
         engines[v] = (e, err)
     states = np.concatenate([g["states"]] * (a.batch // len(g["states"]) + 1))[: a.batch]
     res = {v: [] for v in engines}
@@ -54,7 +52,7 @@ def main():
     out = {}
     for v, ts in res.items():
         ms = float(np.median(ts))
-        out[v] = {"median_ms": ms, "min_ms": float(min(ts)), "tflops": FLOP[a.blocks] * a.batch / ms / 1e9,
+        out[v] = {"median_ms": ms, "min_ms": float(min(ts)), "tflops": FLOP[v] * a.batch / ms / 1e9,
                   "sims_per_s": a.batch / ms * 1e3, "max_err_vs_torch": engines[v][1]}
     print(json.dumps(out, indent=1))
 
