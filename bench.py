@@ -34,8 +34,8 @@ CONFIGS = {
     "c2": dict(games=4096, sims=100, blocks=3, fixed_deck=1, precision="fp32"),
     # configs[2]: 65536 parallel games, 400 sims/move, 1 GPU (the metric's "@400 sims")
     "c3": dict(games=65536, sims=400, blocks=3, fixed_deck=1, precision="fp32"),
-    # configs[4] (per GPU): 16-card random deals, 800 sims, 6-block (bf16 MFMA not yet built: fp32)
-    "c5": dict(games=65536, sims=800, blocks=6, fixed_deck=0, precision="fp32"),
+    # configs[4] (per GPU): 16-card random deals, 800 sims, 6-block, bf16 MFMA inputs / fp32 accumulate
+    "c5": dict(games=65536, sims=800, blocks=6, fixed_deck=0, precision="bf16"),
 }
 FLOP_PER_SIM = {3: 11_681_928, 5: 19_054_728, 6: 22_741_128}  # dense MACs x 2
 
@@ -45,7 +45,7 @@ def nonzero_flop_per_sim(blocks):
     pairs of 225 (what k_nn_sq16 executes)."""
     macs = 169 * 21 * 64 + blocks * 2 * 169 * 64 * 64 + (1600 + 1600 + 64 + 3200 + 2500)
     return 2 * macs
-PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: F32 matrix peak (spec)
+PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: F32 matrix / BF16 dense MFMA peaks (spec)
 METRIC = "MCTS node-expansions/sec/GPU @400 sims; self-play games/sec at 1/2/4/8 GPU"
 
 
@@ -143,7 +143,8 @@ def main():
     if not args.pmc_child and not args.no_pmc and world == 1:
         traffic = pmc_traffic(args, cfg)  # child processes; this process has not touched the GPU yet
     eng = Engine(device=local, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0, train_noise=1,
-                 max_plies=150, evaluator=_abi.EVAL_NN, precision=_abi.FP32, fixed_deck=cfg["fixed_deck"],
+                 max_plies=150, evaluator=_abi.EVAL_NN,
+                 precision=_abi.BF16 if cfg["precision"] == "bf16" else _abi.FP32, fixed_deck=cfg["fixed_deck"],
                  deck=[0, 1, 2, 3, 4], seed=20260101, rank=rank, world=world,
                  sample_capacity=cfg["games"] * 24, stagger=0 if args.pmc_child else stagger)
     eng.load_weights(random_weights(0, cfg["blocks"]))  # random-init weights (seed 0), SURVEY.md 8d
@@ -210,7 +211,7 @@ def main():
         out = {
             "metric": METRIC, "value": sims_all / T, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * T / args.steps, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init weights seed 0, seeded deals)",
+            "vs_baseline": None, "dtype": cfg["precision"], "data": "synthetic (random-init weights seed 0, seeded deals)",
             "config": {"workload": f"{args.config}: {cfg['games']} self-play games/GPU x {cfg['sims']} sims/move, "
                                    f"{cfg['blocks']}-block 64-ch ResNet, c_puct 5, Dirichlet root noise",
                        "games_per_gpu": cfg["games"], "sims_per_move": cfg["sims"], "blocks": cfg["blocks"],
@@ -221,13 +222,15 @@ def main():
             "kernel_ms_per_step": {"select": kt.select_ms / args.steps, "nn": kt.nn_ms / args.steps,
                                    "expand_backup": kt.expand_ms / args.steps, "move": kt.finalize_ms / args.steps,
                                    "root_noise_stream2": kt.noise_ms / args.steps},
-            "roofline": {"bound": "mfma", "kernel": "k_nn_sq16 (fused ResNet, v_mfma_f32_16x16x4_f32)",
-                         "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_MFMA_TFLOPS,
+            "roofline": {"bound": "mfma",
+                         "kernel": "k_nn_sq16<fp32> (fused ResNet, v_mfma_f32_16x16x4_f32)" if cfg["precision"] == "fp32"
+                         else "k_nn_sq16<bf16> (fused ResNet, v_mfma_f32_16x16x32_bf16)",
+                         "achieved": achieved, "peak": PEAK_TFLOPS[cfg["precision"]], "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_TFLOPS[cfg["precision"]],
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
                          "flop_per_launch": flops_launch, "avg_launch_ms": nn_avg_ms, "launches": kt.nn_n,
                          "positions_per_launch": positions, "flop_accounting": "SURVEY 8d dense MACs x2 per sim",
-                         "achieved_nonzero": achieved_nz, "frac_nonzero": achieved_nz / PEAK_FP32_MFMA_TFLOPS,
+                         "achieved_nonzero": achieved_nz, "frac_nonzero": achieved_nz / PEAK_TFLOPS[cfg["precision"]],
                          "algorithmic_bytes_per_launch": alg_bytes, "traffic_detail": traffic},
             "allgather": allgather,
         }

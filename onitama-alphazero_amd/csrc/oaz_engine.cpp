@@ -188,6 +188,34 @@ static void pack_conv64(const FoldedConv& f, std::vector<float>& out) {
     for (int o = 0; o < 64; ++o) out.push_back(f.b[o]);
 }
 
+// bf16 B fragments of v_mfma_f32_16x16x32_bf16: for K-half m, lane l supplies
+// B[k = 8(l>>4) + e][col l&15] = W[co = 16nt + (l&15)][ci = 32m + 8(l>>4) + e][tap t].
+static uint16_t f32_to_bf16(float f) {  // round to nearest even
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+static void pack_conv64_bf16(const FoldedConv& f, std::vector<float>& out) {
+    std::vector<uint16_t> h;
+    h.reserve(9 * 2 * 4 * 64 * 8);
+    for (int t = 0; t < 9; ++t)
+        for (int m = 0; m < 2; ++m)
+            for (int nt = 0; nt < 4; ++nt)
+                for (int l = 0; l < 64; ++l)
+                    for (int e = 0; e < 8; ++e) {
+                        const int co = nt * 16 + (l & 15);
+                        const int ci = 32 * m + 8 * (l >> 4) + e;
+                        h.push_back(f32_to_bf16(f.w[((size_t)co * 64 + ci) * 9 + t]));
+                    }
+    const size_t base = out.size();
+    out.resize(base + h.size() / 2);
+    memcpy(out.data() + base, h.data(), h.size() * sizeof(uint16_t));
+    for (int o = 0; o < 64; ++o) out.push_back(f.b[o]);
+}
+
 // First layer (k_nn_sq16): the 4 bitboard planes go through MFMA (lane l supplies
 // W[co = 16nt + (l&15)][plane l>>4][tap t]); the 16 card planes and the blue-to-move plane
 // (constant over the board, common.rs:68-77,32-37) become T[square][c][co] = sum over the
@@ -212,13 +240,16 @@ static void pack_first_layer(const FoldedConv& f, std::vector<float>& out) {
         }
 }
 
-static int pack_weights(const float* raw, int blocks, std::vector<float>& out) {
+static int pack_weights(const float* raw, int blocks, int bf16, std::vector<float>& out) {
     out.clear();
-    out.reserve(nn_packed_floats(blocks));
+    out.reserve(nn_packed_floats(blocks, bf16));
     const float* p = raw;
     pack_first_layer(fold(p, 64, 21, 9), out);
     for (int b = 0; b < blocks; ++b)
-        for (int j = 0; j < 2; ++j) pack_conv64(fold(p, 64, 64, 9), out);
+        for (int j = 0; j < 2; ++j) {
+            if (bf16) pack_conv64_bf16(fold(p, 64, 64, 9), out);
+            else pack_conv64(fold(p, 64, 64, 9), out);
+        }
     // value head: vh_conv + vh_bn folded, vh_linear1, vh_linear2
     FoldedConv vc = fold(p, 1, 64, 1);
     for (int c = 0; c < 64; ++c) out.push_back(vc.w[c]);
@@ -240,7 +271,7 @@ static int pack_weights(const float* raw, int blocks, std::vector<float>& out) {
     for (int i = 0; i < 50; ++i) out.push_back(*p++);    // ph_linear2.bias
     out.push_back(0.0f);
     out.push_back(0.0f);
-    if (out.size() != nn_packed_floats(blocks)) return set_err(OAZ_ERR_STATE, "pack: size mismatch");
+    if (out.size() != nn_packed_floats(blocks, bf16)) return set_err(OAZ_ERR_STATE, "pack: size mismatch");
     if ((size_t)(p - raw) != oaz_weight_count(blocks, 64, 21)) return set_err(OAZ_ERR_STATE, "pack: raw size mismatch");
     return 0;
 }
@@ -533,8 +564,8 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         set_err(OAZ_ERR_ARG, "create: config out of range");
         return nullptr;
     }
-    if (cfg->precision != OAZ_FP32) {
-        set_err(OAZ_ERR_ARG, "create: only OAZ_FP32 is implemented in this build");
+    if (cfg->precision != OAZ_FP32 && cfg->precision != OAZ_BF16) {
+        set_err(OAZ_ERR_ARG, "create: precision must be OAZ_FP32 or OAZ_BF16");
         return nullptr;
     }
     int ndev = 0;
@@ -580,7 +611,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         dalloc(&e->depth, G) || dalloc(&e->leaf, G) || dalloc(&e->leaf_state, G) ||
         dalloc(&e->stats, G * GS_COUNT) || dalloc(&e->stats_sum, (size_t)GS_COUNT) ||
         dalloc(&e->sqrt_tab, (size_t)cfg->sims + 2) || dalloc(&e->policy, G * 50) ||
-        dalloc(&e->value, G) || dalloc(&e->weights, nn_packed_floats(cfg->blocks)) ||
+        dalloc(&e->value, G) || dalloc(&e->weights, nn_packed_floats(cfg->blocks, cfg->precision == OAZ_BF16)) ||
         dalloc(&e->s_roots, G) || dalloc(&e->s_move, G) || dalloc(&e->s_pi, G * 50) ||
         dalloc(&e->s_rootv, G) || dalloc(&e->s_rootp, G * 50) || dalloc(&e->s_ply, G) ||
         dalloc(&e->root, G) || dalloc(&e->ply, G) || dalloc(&e->seq, G) ||
@@ -643,7 +674,7 @@ extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
         return set_err(OAZ_ERR_WEIGHTS, "load_weights: got %zu floats, need %zu for %d blocks", n, need,
                        e->cfg.blocks);
     std::vector<float> packed;
-    if (int rc = pack_weights(blob, e->cfg.blocks, packed)) return rc;
+    if (int rc = pack_weights(blob, e->cfg.blocks, e->cfg.precision == OAZ_BF16, packed)) return rc;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipMemcpyAsync(e->weights, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -698,7 +729,7 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
     NNView w;
     w.blob = e->weights;
     w.blocks = e->cfg.blocks;
-    w.bf16 = 0;
+    w.bf16 = e->cfg.precision == OAZ_BF16;
     return timed(e, 1, B, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, e->stream); });
 }
 

@@ -89,7 +89,7 @@ hipError_t launch_encode(const oaz_state* s, int n, float* planes, hipStream_t s
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy,
                              float* value, hipStream_t st);
 hipError_t launch_hash_eval(const oaz_state* s, int B, float* policy, float* value, hipStream_t st);
-size_t nn_packed_floats(int blocks);
+size_t nn_packed_floats(int blocks, int bf16);
 
 // MCTS
 hipError_t launch_tree_reset(const TreeView& t, hipStream_t st);

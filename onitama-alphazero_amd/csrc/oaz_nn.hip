@@ -24,6 +24,11 @@
 //     folded weights over the on-board taps) added in the epilogue. The MFMA part of the first
 //     layer is therefore one k-step (4 bitboards) per (square, tap), with A values taken
 //     straight from the state's bits: the 21 planes are never materialised.
+//   * bf16 variant (OAZ_BF16, BASELINE C5): activations are stored in LDS as bf16 (row stride
+//     80 elements = 160 B: with the natural channel order the 16-lane ds_read_b128 groups hit
+//     16 distinct bank slots), 64->64 convs use v_mfma_f32_16x16x32_bf16 (K = 32: two MFMAs per
+//     (square, tap, N-tile) instead of sixteen), accumulation, skip, bias and heads stay fp32;
+//     the first layer keeps the exact fp32 MFMA on 0/1 inputs.
 #include <hip/hip_runtime.h>
 
 #include "oaz_device.h"
@@ -32,6 +37,7 @@
 namespace oaz {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace nn {
 constexpr int kCh = 64;
@@ -51,11 +57,33 @@ constexpr size_t kL1Table = 25 * 17 * kCh;
 constexpr size_t kW64 = 9 * 4 * 4 * 64 * 4;
 constexpr size_t kValueF = 64 + 4 + 64 * 25 + 64 + 64 + 4;
 constexpr size_t kPolicyF = 128 + 4 + 2500 + 52;
+// bf16 variant: 64->64 conv B fragments are bf16 [9 taps][2 K-halves][4 N-tiles][64 lanes][8],
+// stored in the float blob as 9*2*4*64*4 floats; LDS rows hold 80 bf16 (64 + 16 pad)
+constexpr size_t kW64h = 9 * 2 * 4 * 64 * 4;
+constexpr int kRSh = 80;
+constexpr int kLdsFloatsH = kSB * 25 * kRSh / 2 + kWaves * kScratch;  // 17024 floats = 68,096 B
+
+// Element type of the LDS activation image.
+template <bool BF16> struct Act;
+template <> struct Act<false> {
+    using T = float;
+    static constexpr int kRS = nn::kRS;
+    static constexpr size_t kW = nn::kW64;
+    static __device__ __forceinline__ float load(const T* p) { return *p; }
+    static __device__ __forceinline__ void store(T* p, float v) { *p = v; }
+};
+template <> struct Act<true> {
+    using T = __bf16;
+    static constexpr int kRS = nn::kRSh;
+    static constexpr size_t kW = nn::kW64h;
+    static __device__ __forceinline__ float load(const T* p) { return (float)*p; }
+    static __device__ __forceinline__ void store(T* p, float v) { *p = (__bf16)v; }
+};
 }  // namespace nn
 
-size_t nn_packed_floats(int blocks) {
-    return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (nn::kW64 + nn::kCh) + nn::kValueF +
-           nn::kPolicyF;
+size_t nn_packed_floats(int blocks, int bf16) {
+    return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * ((bf16 ? nn::kW64h : nn::kW64) + nn::kCh) +
+           nn::kValueF + nn::kPolicyF;
 }
 
 // Square groups: 4 corners + 4 edges + 5 interior (85 on-board taps) | 8 edges + 4 interior (84).
@@ -125,11 +153,36 @@ __device__ __forceinline__ void conv64(f32x4 (&acc)[nn::kTPW], const float* act,
     }
 }
 
+// bf16: acc[j] += conv3x3 over 64 channels with v_mfma_f32_16x16x32_bf16. For K-half m, lane
+// l supplies A[row l&15][k = 8(l>>4) + e] = channel 32m + 8(l>>4) + e (natural order).
+__device__ __forceinline__ void conv64_bf16(f32x4 (&acc)[nn::kTPW], const __bf16* act, const bf16x8* W,
+                                            const int (&sq)[nn::kTPW], int lane, int nt, int ntiles) {
+    const int i = lane & 15, kq = lane >> 4;
+    const __bf16* base = act + i * nn::kRSh + 8 * kq;
+    for (int t = 0; t < 9; ++t) {
+        const bf16x8 b0 = W[((t * 2 + 0) * 4 + nt) * 64 + lane];
+        const bf16x8 b1 = W[((t * 2 + 1) * 4 + nt) * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < nn::kTPW; ++j) {
+            const int nb = nbr_index(sq[j], t);
+            if (j < ntiles && nb < 25) {
+                const __bf16* a = base + nb * nn::kSB * nn::kRSh;
+                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(a);
+                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(a + 32);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc[j], 0, 0, 0);
+            }
+        }
+    }
+}
+
 // C/D of v_mfma_f32_16x16x4_f32: reg r of lane l = (row (l>>4)*4 + r, col l&15) of the tile,
 // i.e. position (l>>4)*4 + r at square sq[j]; LDS row = square*16 + position.
-__device__ __forceinline__ void epilogue(const f32x4 (&acc)[nn::kTPW], float* act, const float* bias,
-                                         const f32x4* skip, const int (&sq)[nn::kTPW], int lane, int nt,
-                                         int ntiles) {
+template <bool BF16>
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[nn::kTPW], typename nn::Act<BF16>::T* act,
+                                         const float* bias, const f32x4* skip, const int (&sq)[nn::kTPW],
+                                         int lane, int nt, int ntiles) {
+    using A = nn::Act<BF16>;
     const int co = nt * 16 + (lane & 15);
     const float bb = bias[co];
 #pragma unroll
@@ -140,14 +193,16 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[nn::kTPW], float* ac
                 const int row = sq[j] * nn::kSB + (lane >> 4) * 4 + r;
                 float v = acc[j][r] + bb;
                 if (skip) v += skip[j][r];
-                act[row * nn::kRS + co] = v > 0.0f ? v : 0.0f;
+                A::store(act + row * A::kRS + co, v > 0.0f ? v : 0.0f);
             }
 }
 
 // First-layer epilogue: bias + constant-plane table (the mover's two cards, blue-to-move).
-__device__ __forceinline__ void epilogue_l1(const f32x4 (&acc)[nn::kTPW], float* act, const float* bias,
-                                            const float* table, const int* pinfo, const int (&sq)[nn::kTPW],
-                                            int lane, int nt, int ntiles) {
+template <bool BF16>
+__device__ __forceinline__ void epilogue_l1(const f32x4 (&acc)[nn::kTPW], typename nn::Act<BF16>::T* act,
+                                            const float* bias, const float* table, const int* pinfo,
+                                            const int (&sq)[nn::kTPW], int lane, int nt, int ntiles) {
+    using A = nn::Act<BF16>;
     const int co = nt * 16 + (lane & 15);
     const float bb = bias[co];
 #pragma unroll
@@ -160,23 +215,27 @@ __device__ __forceinline__ void epilogue_l1(const f32x4 (&acc)[nn::kTPW], float*
                 const float* ts = table + (size_t)sq[j] * 17 * nn::kCh + co;
                 float v = acc[j][r] + bb + ts[(info & 15) * nn::kCh] + ts[((info >> 4) & 15) * nn::kCh];
                 if (info & 0x100) v += ts[16 * nn::kCh];
-                act[(sq[j] * nn::kSB + pos) * nn::kRS + co] = v > 0.0f ? v : 0.0f;
+                A::store(act + (sq[j] * nn::kSB + pos) * A::kRS + co, v > 0.0f ? v : 0.0f);
             }
 }
 
-__device__ __forceinline__ void read_skip(f32x4 (&skip)[nn::kTPW], const float* act, const int (&sq)[nn::kTPW],
-                                          int lane, int nt, int ntiles) {
+template <bool BF16>
+__device__ __forceinline__ void read_skip(f32x4 (&skip)[nn::kTPW], const typename nn::Act<BF16>::T* act,
+                                          const int (&sq)[nn::kTPW], int lane, int nt, int ntiles) {
+    using A = nn::Act<BF16>;
     const int co = nt * 16 + (lane & 15);
 #pragma unroll
     for (int j = 0; j < nn::kTPW; ++j)
         if (j < ntiles)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) skip[j][r] = act[(sq[j] * nn::kSB + (lane >> 4) * 4 + r) * nn::kRS + co];
+            for (int r = 0; r < 4; ++r) skip[j][r] = A::load(act + (sq[j] * nn::kSB + (lane >> 4) * 4 + r) * A::kRS + co);
 }
 
 // value + policy heads (net.rs:152-213) for position `s` of the workgroup (one wave).
-__device__ __forceinline__ void heads(const float* act, float* scratch, int s, const float* p, int lane, int b, int B,
-                                      float* policy, float* value) {
+template <bool BF16>
+__device__ __forceinline__ void heads(const typename nn::Act<BF16>::T* act, float* scratch, int s, const float* p,
+                                      int lane, int b, int B, float* policy, float* value) {
+    using A = nn::Act<BF16>;
     const float* vw = p;
     const float vb = p[64];
     const float* l1w = p + 68;
@@ -189,9 +248,13 @@ __device__ __forceinline__ void heads(const float* act, float* scratch, int s, c
     const float* plb = plw + 2500;
     if (lane < 25) {  // 1x1 convs (value 64->1, policy 64->2) with folded BN, ReLU; lane = square
         float sv = vb, s0 = pb0, s1 = pb1;
-        const float* row = act + (lane * nn::kSB + s) * nn::kRS;
+        const typename A::T* row = act + (lane * nn::kSB + s) * A::kRS;
         for (int c = 0; c < nn::kCh; c += 4) {
-            const float4 x = *reinterpret_cast<const float4*>(row + c);
+            float4 x;
+            x.x = A::load(row + c);
+            x.y = A::load(row + c + 1);
+            x.z = A::load(row + c + 2);
+            x.w = A::load(row + c + 3);
             sv += vw[c] * x.x + vw[c + 1] * x.y + vw[c + 2] * x.z + vw[c + 3] * x.w;
             s0 += pp[c] * x.x + pp[c + 1] * x.y + pp[c + 2] * x.z + pp[c + 3] * x.w;
             s1 += pp[64 + c] * x.x + pp[65 + c] * x.y + pp[66 + c] * x.z + pp[67 + c] * x.w;
@@ -218,11 +281,15 @@ __device__ __forceinline__ void heads(const float* act, float* scratch, int s, c
     }
 }
 
+template <bool BF16>
 __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __restrict__ states, int B,
                                                              const float* __restrict__ blob, int blocks,
                                                              float* __restrict__ policy,
                                                              float* __restrict__ value) {
-    __shared__ __attribute__((aligned(16))) float act[nn::kLdsFloats];
+    using A = nn::Act<BF16>;
+    constexpr int kImageFloats = BF16 ? nn::kSB * 25 * nn::kRSh / 2 : nn::kSB * 25 * nn::kRS;
+    __shared__ __attribute__((aligned(16))) float lds[BF16 ? nn::kLdsFloatsH : nn::kLdsFloats];
+    typename A::T* act = reinterpret_cast<typename A::T*>(lds);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nt = wave & 3, grp = wave >> 2;
     const int ntiles = grp == 0 ? nn::kTPW : 25 - nn::kTPW;
@@ -232,7 +299,7 @@ __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __
     const int b0 = blockIdx.x * nn::kSB;
     // per-position card/colour info for the first-layer table; the area is wave 0's head
     // scratch, free until the heads run
-    int* pinfo = reinterpret_cast<int*>(act + nn::kSB * 25 * nn::kRS);
+    int* pinfo = reinterpret_cast<int*>(lds + kImageFloats);
 
     // encoder (common.rs:26-80): lane = (position lane&15, bitboard lane>>4: red pawns, red
     // king, blue pawns, blue king); the cards / colour of each position go to LDS
@@ -252,41 +319,50 @@ __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __
 #pragma unroll
         for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
         conv_l1(acc, bb, blob, sq, lane, nt, ntiles);
-        epilogue_l1(acc, act, blob + nn::kL1B, blob + nn::kL1B + nn::kCh, pinfo, sq, lane, nt, ntiles);
+        epilogue_l1<BF16>(acc, act, blob + nn::kL1B, blob + nn::kL1B + nn::kCh, pinfo, sq, lane, nt, ntiles);
         __syncthreads();
     }
 
     const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
     f32x4 acc[nn::kTPW];
     f32x4 skip[nn::kTPW];
-    for (int blk = 0; blk < blocks; ++blk) {
-        read_skip(skip, act, sq, lane, nt, ntiles);
+    auto conv = [&](const float* w) {
 #pragma unroll
         for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
-        conv64(acc, act, reinterpret_cast<const float4*>(p), sq, lane, nt, ntiles);
-        p += nn::kW64;
+        if constexpr (BF16)
+            conv64_bf16(acc, act, reinterpret_cast<const bf16x8*>(w), sq, lane, nt, ntiles);
+        else
+            conv64(acc, act, reinterpret_cast<const float4*>(w), sq, lane, nt, ntiles);
+    };
+    for (int blk = 0; blk < blocks; ++blk) {
+        read_skip<BF16>(skip, act, sq, lane, nt, ntiles);
+        conv(p);  // small block 1: conv + BN + ReLU
+        p += A::kW;
         __syncthreads();
-        epilogue(acc, act, p, nullptr, sq, lane, nt, ntiles);
+        epilogue<BF16>(acc, act, p, nullptr, sq, lane, nt, ntiles);
         p += nn::kCh;
         __syncthreads();
-#pragma unroll
-        for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
-        conv64(acc, act, reinterpret_cast<const float4*>(p), sq, lane, nt, ntiles);
-        p += nn::kW64;
+        conv(p);  // small block 2: conv + BN, + skip, ReLU
+        p += A::kW;
         __syncthreads();
-        epilogue(acc, act, p, skip, sq, lane, nt, ntiles);
+        epilogue<BF16>(acc, act, p, skip, sq, lane, nt, ntiles);
         p += nn::kCh;
         __syncthreads();
     }
-    float* scratch = act + nn::kSB * 25 * nn::kRS + wave * nn::kScratch;
-    for (int s = wave; s < nn::kSB; s += nn::kWaves) heads(act, scratch, s, p, lane, b0 + s, B, policy, value);
+    float* scratch = lds + kImageFloats + wave * nn::kScratch;
+    for (int s = wave; s < nn::kSB; s += nn::kWaves) heads<BF16>(act, scratch, s, p, lane, b0 + s, B, policy, value);
 }
 
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy, float* value,
                              hipStream_t st) {
     if (B <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
-    hipLaunchKernelGGL(k_nn_sq16, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy, value);
+    if (w.bf16)
+        hipLaunchKernelGGL(k_nn_sq16<true>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
+                           value);
+    else
+        hipLaunchKernelGGL(k_nn_sq16<false>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
+                           value);
     return hipGetLastError();
 }
 

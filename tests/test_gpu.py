@@ -104,6 +104,19 @@ def test_nn_matches_torch_goldens(nn_golden, trained3, name, blocks):
     assert np.allclose(p.reshape(-1, 50).sum(1), 1.0, atol=1e-5)
 
 
+@pytest.mark.parametrize("name,blocks", [("trained3", 3), ("random3", 3), ("random6", 6)])
+def test_nn_bf16_mode_close_to_fp32_goldens(nn_golden, trained3, name, blocks):
+    """OAZ_BF16 (BASELINE C5: bf16 MFMA inputs, fp32 accumulation) is a throughput mode, not the
+    parity path: it must stay close to the fp32 torch goldens (tolerance 3e-2 absolute)."""
+    w = trained3 if name == "trained3" else random_weights(0 if name == "random3" else 1, blocks)
+    with Engine(games=256, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN, precision=_abi.BF16) as e:
+        e.load_weights(w)
+        p, v = e.nn_forward(nn_golden["states"])
+    assert np.abs(p - nn_golden[f"policy_{name}"]).max() < 3e-2
+    assert np.abs(v - nn_golden[f"value_{name}"]).max() < 3e-2
+    assert np.allclose(p.reshape(-1, 50).sum(1), 1.0, atol=1e-5)
+
+
 def test_nn_batch_position_invariance(orc):
     pos = random_positions(orc, 64, seed=404)
     with Engine(games=1024, sims=1, blocks=3) as e:
@@ -232,8 +245,10 @@ def test_selfplay_matches_oracle_games(orc, fixed, max_plies):
     assert np.array_equal(_sorted_rows(got), _sorted_rows(ref))
 
 
-def test_selfplay_nn_continuous_batching_runs():
-    with Engine(games=256, sims=16, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_NN, blocks=3, max_plies=150) as e:
+@pytest.mark.parametrize("precision,blocks", [(_abi.FP32, 3), (_abi.BF16, 6)])
+def test_selfplay_nn_continuous_batching_runs(precision, blocks):
+    with Engine(games=256, sims=16, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_NN, blocks=blocks, max_plies=150,
+                precision=precision, fixed_deck=0) as e:
         e.selfplay_reset()
         e.selfplay_step(40)
         st = e.selfplay_stats()

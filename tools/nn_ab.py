@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--blocks", default="3")
+    ap.add_argument("--precision", default="fp32,bf16")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
@@ -28,19 +29,24 @@ def main():
     w3 = np.load(ROOT / "tests/golden/weights_3block_trained.npy")
     engines = {}
     for v in [int(x) for x in a.blocks.split(",")]:
-        e = Engine(games=a.batch, sims=1, blocks=v, evaluator=_abi.EVAL_NN)
-        if v == 3:
-            e.load_weights(w3)
-            p, val = e.nn_forward(g["states"])
-            err = float(max(np.abs(p - g["policy_trained3"]).max(), np.abs(val - g["value_trained3"]).max()))
-        else:
-            err = None
-        e.load_weights(random_weights(0, v))
-        engines[v] = (e, err)
+        for prec in a.precision.split(","):
+            e = Engine(games=a.batch, sims=1, blocks=v, evaluator=_abi.EVAL_NN,
+                       precision=_abi.BF16 if prec == "bf16" else _abi.FP32)
+            err = {}
+            for name, blob, nb in (("trained3", w3, 3), ("random3", random_weights(0, 3), 3),
+                                   ("random6", random_weights(1, 6), 6)):
+                if nb != v:
+                    continue
+                e.load_weights(blob)
+                p, val = e.nn_forward(g["states"])
+                err[name] = {"policy": float(np.abs(p - g[f"policy_{name}"]).max()),
+                             "value": float(np.abs(val - g[f"value_{name}"]).max())}
+            e.load_weights(random_weights(0, v))
+            engines[f"{v}-{prec}"] = (e, err, v)
     states = np.concatenate([g["states"]] * (a.batch // len(g["states"]) + 1))[: a.batch]
     res = {v: [] for v in engines}
     for _ in range(a.rounds):
-        for v, (e, _) in engines.items():
+        for v, (e, _, _) in engines.items():
             e.nn_forward(states[:1024])
             e.kernel_times_reset()
             e.set_timing(True)
@@ -52,7 +58,8 @@ def main():
     out = {}
     for v, ts in res.items():
         ms = float(np.median(ts))
-        out[v] = {"median_ms": ms, "min_ms": float(min(ts)), "tflops": FLOP[v] * a.batch / ms / 1e9,
+        nb = engines[v][2]
+        out[v] = {"median_ms": ms, "min_ms": float(min(ts)), "tflops": FLOP[nb] * a.batch / ms / 1e9,
                   "sims_per_s": a.batch / ms * 1e3, "max_err_vs_torch": engines[v][1]}
     print(json.dumps(out, indent=1))
 
