@@ -200,6 +200,74 @@ def test_search_with_root_noise_is_deterministic_and_consistent(orc):
     assert differs > 0  # the noise changes the search
 
 
+def test_search_no_legal_move_root_passes(orc, kats):
+    """state.rs:852-889: Blue has no legal move. The reference's AZ search panics ("Must find the
+    best child"); the engine returns a pass with the mover's first card and pi = 0 (Q6)."""
+    case = [c for c in kats["movegen"] if "no_legal_moves_at_all" in c["src"]][0]
+    root = kat_state(case["state"], 1)
+    with Engine(games=1, sims=20, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0) as e:
+        r = e.search(root)
+        t = e.tree(0)
+    assert _mv(r.moves[0]) == (25, 25, 0, 2) and np.all(r.pi == 0)
+    mv, pi, nodes, st = orc.search(orc.search_cfg(sims=20, c_puct=5.0, evaluator=orc.EVAL_HASH), root)
+    assert _mv(mv) == (25, 25, 0, 2) and st.stuck_leaves == 19
+    assert r.stats.stuck_leaves == 19 and t.tobytes() == nodes.tobytes()
+
+
+def test_search_stuck_leaves_inside_tree_match_oracle(orc, kats):
+    """Red to move in the no-move KAT position: Red moves that leave Blue without a move create
+    expanded-but-childless nodes inside the tree (Q6); both searches must treat them alike."""
+    case = [c for c in kats["movegen"] if "no_legal_moves_at_all" in c["src"]][0]
+    root = kat_state(case["state"], 0)
+    with Engine(games=1, sims=300, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0) as e:
+        r = e.search(root)
+        mv, pi, nodes, st = orc.search(orc.search_cfg(sims=300, c_puct=5.0, evaluator=orc.EVAL_HASH), root)
+        _compare_trees(e, 0, nodes)
+    assert r.stats.stuck_leaves == st.stuck_leaves
+
+
+@pytest.mark.parametrize("sims", [1, 2, 3])
+def test_search_tiny_budgets(orc, sims):
+    roots = random_positions(orc, 5, seed=808)
+    with Engine(games=5, sims=sims, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0) as e:
+        r = e.search(roots)
+        for g in range(5):
+            mv, pi, nodes, _ = orc.search(orc.search_cfg(sims=sims, c_puct=5.0, evaluator=orc.EVAL_HASH), roots[g])
+            _compare_trees(e, g, nodes)
+            assert _mv(r.moves[g]) == _mv(mv) and np.array_equal(r.pi[g].reshape(-1), pi.reshape(-1))
+
+
+def test_empty_and_single_inputs(orc):
+    empty = np.zeros(0, dtype=_abi.STATE_DTYPE)
+    moves, counts = movegen_batch(empty)
+    assert moves.shape == (0, 40) and counts.shape == (0,)
+    one = random_positions(orc, 1, seed=909)
+    with Engine(games=4, sims=10, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0) as e:
+        assert len(e.search(empty).moves) == 0
+        r = e.search(one)
+        mv, _, _, _ = orc.search(orc.search_cfg(sims=10, c_puct=5.0, evaluator=orc.EVAL_HASH), one[0])
+        assert _mv(r.moves[0]) == _mv(mv)
+        with pytest.raises(_abi.OazError):
+            e.search(np.concatenate([one] * 5))  # more roots than game slots
+
+
+def test_search_root_noise_matches_oracle(orc):
+    """Noise on: both sides draw the same Philox streams and run the same f64 gamma/Beta
+    algorithm (device ocml vs host libm), so trees agree unless a last-bit libm difference flips
+    a near-tie."""
+    roots = random_positions(orc, 24, seed=1010)
+    sims = 48
+    with Engine(games=24, sims=sims, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=77) as e:
+        e.search(roots)
+        same = 0
+        for g in range(24):
+            cfg = orc.search_cfg(sims=sims, c_puct=5.0, evaluator=orc.EVAL_HASH, train_noise=1, seed=77, game_id=g, ply=0)
+            _, _, nodes, _ = orc.search(cfg, roots[g])
+            t = e.tree(g)
+            same += int(len(t) == len(nodes) and t.tobytes() == nodes.tobytes())
+    assert same >= 20, same
+
+
 def test_search_finds_win_in_one(kats):
     case = kats["tactics"][0]  # onitama-game/src/ai/mcts/mcts_arena.rs:459-483
     root = kat_state(case["state"], case["color"])
