@@ -12,10 +12,13 @@ from .game import (CARD_NAMES, ORIGINAL_CARDS, Card, Deck, DoneMove, GameState, 
 from .mcts import (AlphaZeroMcts, AlphaZeroMctsConfig, ConvResNet, ConvResNetConfig, Options,
                    TrainingAlphaZeroMcts, reward)
 from .selfplay import SelfPlayData, TrainConfig, self_play
+from .evaluator import (AlphaZeroAgent, EloRating, Evaluator, EvaluatorConfig, FightStatistics, PitStatistics,
+                        RandomAgent, fight)
 
 __all__ = [
     "_abi", "OazError", "load", "Engine", "SearchResult", "CARD_NAMES", "ORIGINAL_CARDS", "Card", "Deck",
     "DoneMove", "GameState", "Move", "MoveResult", "PieceKind", "PlayerColor", "State", "AlphaZeroMcts",
     "AlphaZeroMctsConfig", "ConvResNet", "ConvResNetConfig", "Options", "TrainingAlphaZeroMcts", "reward",
-    "SelfPlayData", "TrainConfig", "self_play",
+    "SelfPlayData", "TrainConfig", "self_play", "AlphaZeroAgent", "EloRating", "Evaluator", "EvaluatorConfig",
+    "FightStatistics", "PitStatistics", "RandomAgent", "fight",
 ]
