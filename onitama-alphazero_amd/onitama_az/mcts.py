@@ -70,6 +70,11 @@ class ConvResNet:
         b = blocks_from_names(named)
         return ConvResNet(ConvResNetConfig(resnet_block_amnt=b), options, blob_from_named(named, b))
 
+    def save(self, path: str) -> None:
+        """VarStore::save of the model's variables (train.rs:414-430)."""
+        from .weights import save_blob_ot
+        save_blob_ot(path, self.weights, self.config.resnet_block_amnt)
+
     def _eval_engine(self, batch: int) -> Engine:
         if self._engine is None or self._engine_batch < batch:
             if self._engine is not None:

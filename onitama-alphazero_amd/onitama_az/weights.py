@@ -227,3 +227,101 @@ def read_ot(path: str) -> Dict[str, np.ndarray]:
         out[name] = np.array(a, dtype=np.float32).reshape(shape)
         assert out[name].size == n
     return out
+
+
+# ---- .ot writer (train.rs:414-430 save_vs) -------------------------------------------------------
+def _pk_str(s: str) -> bytes:
+    b = s.encode("utf-8")
+    return b"X" + len(b).to_bytes(4, "little") + b
+
+
+def _pk_int(v: int) -> bytes:
+    if 0 <= v < 256:
+        return b"K" + bytes([v])
+    if 0 <= v < 65536:
+        return b"M" + v.to_bytes(2, "little")
+    return b"J" + int(v).to_bytes(4, "little", signed=True)
+
+
+def _pk_tuple(items) -> bytes:
+    return b"(" + b"".join(items) + b"t"
+
+
+def _data_pkl(entries: List[Tuple[str, Tuple[int, ...]]]) -> bytes:
+    """The TorchScript module pickle of a tch VarStore (protocol 2): a `__torch__ Module` whose
+    state dict maps each '|' name to torch._utils._rebuild_tensor_v2(storage '<i>', 0, shape,
+    contiguous stride, False, OrderedDict())."""
+    out = [b"\x80\x02", b"c__torch__\nModule\n", b")\x81}("]
+    for i, (name, shape) in enumerate(entries):
+        numel = int(np.prod(shape)) if shape else 1
+        stride, acc = [], 1
+        for d in reversed(shape):
+            stride.append(acc)
+            acc *= d
+        stride.reverse()
+        pers = _pk_tuple([_pk_str("storage"), b"ctorch\nFloatStorage\n", _pk_str(str(i)), _pk_str("cpu"),
+                          _pk_int(numel)]) + b"Q"
+        args = _pk_tuple([pers, _pk_int(0), _pk_tuple([_pk_int(d) for d in shape]),
+                          _pk_tuple([_pk_int(s) for s in stride]), b"\x89",
+                          b"ccollections\nOrderedDict\n)R"])
+        out.append(_pk_str(name) + b"ctorch._utils\n_rebuild_tensor_v2\n" + args + b"R")
+    out.append(b"ub.")
+    return b"".join(out)
+
+
+def _torch_py(names: List[str]) -> bytes:
+    lines = ["class Module(Module):",
+             "  __parameters__ = [" + "".join(f'"{n}", ' for n in names) + "]",
+             "  __buffers__ = []",
+             "  __annotations__ = []"]
+    lines += [f'  __annotations__["{n}"] = Tensor' for n in names]
+    return ("\n".join(lines) + "\n").encode()
+
+
+class _AlignedZip:
+    """Stored zip members whose data start on 64-byte boundaries (the torch archive convention,
+    padding carried in an 'FB' extra field), so readers may mmap the tensors."""
+
+    def __init__(self, path: str):
+        self.z = zipfile.ZipFile(path, "w", compression=zipfile.ZIP_STORED)
+
+    def add(self, name: str, data: bytes, deflate: bool = False):
+        info = zipfile.ZipInfo(name, date_time=(1980, 1, 1, 0, 0, 0))
+        info.compress_type = zipfile.ZIP_DEFLATED if deflate else zipfile.ZIP_STORED
+        if not deflate:
+            start = self.z.fp.tell() + 30 + len(name.encode())
+            pad = (-(start + 4)) % 64
+            info.extra = b"FB" + pad.to_bytes(2, "little") + b"Z" * pad
+        self.z.writestr(info, data)
+
+    def close(self):
+        self.z.close()
+
+
+def write_ot(path: str, named: Dict[str, np.ndarray], archive: str = None) -> None:
+    """Write named fp32 tensors as a tch VarStore .ot archive (TorchScript zip: data.pkl,
+    data/<i>, code/__torch__.py, constants.pkl, version), the format read_ot and the reference's
+    VarStore::load read."""
+    import os
+    archive = archive or os.path.splitext(os.path.basename(path))[0]
+    names = list(named)
+    entries = [(n, tuple(np.asarray(named[n]).shape)) for n in names]
+    z = _AlignedZip(path)
+    try:
+        for i, n in enumerate(names):
+            z.add(f"{archive}/data/{i}", np.ascontiguousarray(named[n], dtype="<f4").tobytes())
+        z.add(f"{archive}/data.pkl", _data_pkl(entries))
+        z.add(f"{archive}/code/__torch__.py", _torch_py(names), deflate=True)
+        z.add(f"{archive}/constants.pkl", b"\x80\x02).")
+        z.add(f"{archive}/version", b"3\n")
+    finally:
+        z.close()
+
+
+def checkpoint_path(folder: str, iteration: int, is_best: bool, stamp: str) -> str:
+    """save_vs naming (train.rs:414-422): <folder>/[best_]model_<iter>_<YYYYmmdd_HHMMSS>.ot"""
+    return f"{folder}/{'best_' if is_best else ''}model_{iteration}_{stamp}.ot"
+
+
+def save_blob_ot(path: str, blob: np.ndarray, blocks: int) -> None:
+    write_ot(path, named_from_blob(blob, blocks))

@@ -89,6 +89,31 @@ def test_ot_reader_matches_committed_fixture(trained3):
     assert np.array_equal(W.blob_from_named(named, 3), trained3)
 
 
+def test_ot_writer_round_trip(trained3, tmp_path):
+    """save_vs format (train.rs:414-430): read back by the safe reader and by TorchScript's own
+    loader (the loader tch's VarStore::load drives), tensors stored 64-byte aligned."""
+    import struct
+    import zipfile
+    p = W.checkpoint_path(str(tmp_path), 7, True, "20260101_120000")
+    assert p.endswith("/best_model_7_20260101_120000.ot")
+    W.save_blob_ot(p, trained3, 3)
+    assert np.array_equal(W.blob_from_named(W.read_ot(p), 3), trained3)
+    raw = open(p, "rb").read()
+    z = zipfile.ZipFile(p)
+    assert z.testzip() is None
+    for info in z.infolist():
+        if "/data/" in info.filename:
+            n, e = struct.unpack("<HH", raw[info.header_offset + 26: info.header_offset + 30])
+            assert (info.header_offset + 30 + n + e) % 64 == 0
+    import torch
+    m = torch.jit.load(p)
+    params = dict(m.named_parameters())
+    named = W.named_from_blob(trained3, 3)
+    assert set(params) == set(named)
+    for k, v in named.items():
+        assert np.array_equal(params[k].detach().numpy(), v), k
+
+
 def test_no_device_is_a_loud_error(lib):
     if _abi.device_count() > 0:
         pytest.skip("a GPU is visible")
