@@ -33,6 +33,9 @@
  *                          and Agent::generate_move for AlphaZeroMcts, alphazero_mcts/mod.rs:122-144)
  *   oaz_selfplay_*     <- self_play                           alphazero-training/src/train.rs:35-98
  *   oaz_load_weights   <- AlphaZeroMcts::from_model_file      alphazero-training/src/alphazero_mcts/mod.rs:89-105
+ *   oaz_trainer_*      <- the training loop body               alphazero-training/src/train.rs:264-313
+ *                         (ConvResNet::forward(train=true) net.rs:215-232, alphaloss net.rs:234-243,
+ *                          nn::Sgd{momentum 0.9} + set_weight_decay train.rs:181-186, opt.backward_step)
  */
 #ifndef ONITAMA_AZ_H
 #define ONITAMA_AZ_H
@@ -245,6 +248,59 @@ int oaz_samples_export_device(oaz_engine* eng, void* dev_dst, size_t cap_bytes, 
  * reached) and return their samples. */
 int oaz_selfplay_run(oaz_engine* eng, int n_games, oaz_sample* out, size_t cap,
                      size_t* n_out, oaz_selfplay_stats* stats);
+
+/* ---- training step ---------------------------------
+ * One trainer = one GPU. Parameters live on the device in the canonical blob
+ * layout (the VarStore order, see oaz_weight_count); BN running statistics are
+ * part of the blob and are updated by the train-mode forward (momentum 0.1,
+ * unbiased variance), as tch's batch_norm2d does. A step is
+ *   gather batch -> forward(train=true) -> alphaloss -> backward -> SGD
+ * with the reference's optimiser: d = g + wd*p; buf = momentum*buf + d; p -= lr*buf
+ * over the trainable variables (weights, biases, BN gamma/beta). */
+typedef struct oaz_train_config {
+    int32_t blocks;               /* residual blocks (ConvResNetConfig::resnet_block_amnt) */
+    int32_t max_batch;            /* largest batch (multiple of 16); train_batch_size 512 (train.rs:142) */
+    double learning_rate;         /* 5e-3 (bin/train.rs:69) */
+    double momentum;              /* 0.9 (train.rs:182) */
+    double weight_decay;          /* l2_const 1e-4 (train.rs:139,186) */
+    double bn_momentum;           /* 0.1 (tch BatchNormConfig default) */
+    double bn_eps;                /* 1e-5 */
+    int32_t value_loss_broadcast; /* 1 = reference (Q16: z[B] - v[B,1] broadcasts to [B,B]), 0 = elementwise */
+    int32_t reserved[7];
+} oaz_train_config;
+
+typedef struct oaz_trainer oaz_trainer;
+
+void oaz_train_config_default(oaz_train_config* cfg);
+oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int device);  /* NULL on error */
+void oaz_trainer_destroy(oaz_trainer* t);
+/* Run the trainer's kernels on `stream` (a hipStream_t; NULL = the trainer's own stream). */
+int oaz_trainer_set_stream(oaz_trainer* t, void* stream);
+/* Parameters + running stats, canonical blob (n = oaz_weight_count(blocks, 64, 21)).
+ * set_weights also clears the momentum buffers (a fresh nn::Sgd). */
+int oaz_trainer_set_weights(oaz_trainer* t, const float* blob, size_t n);
+int oaz_trainer_get_weights(oaz_trainer* t, float* blob, size_t n);
+/* The replay buffer: copy n host samples to the device (owned), or bind n samples already
+ * resident on this GPU (e.g. oaz_samples_export_device; not owned, must outlive use). */
+int oaz_trainer_load_samples(oaz_trainer* t, const oaz_sample* samples, size_t n);
+int oaz_trainer_bind_device_samples(oaz_trainer* t, const oaz_sample* dev_samples, size_t n);
+/* Upload batch indices (n_batches x batch int32 into the replay buffer), e.g. one epoch of
+ * choose_multiple draws (train.rs:272-276). */
+int oaz_trainer_set_batches(oaz_trainer* t, const int32_t* idx, int n_batches, int batch);
+/* Forward + loss + backward for batch `b` of the uploaded indices: gradients land in the
+ * device gradient buffer (oaz_trainer_grads); no parameter changes except BN running stats. */
+int oaz_trainer_backward(oaz_trainer* t, int b);
+/* Device gradient buffer (canonical blob layout; running-stat slots unused) for an external
+ * all-reduce between backward and apply (data-parallel training). */
+int oaz_trainer_grads(oaz_trainer* t, float** dev_grads, size_t* n);
+int oaz_trainer_get_grads(oaz_trainer* t, float* host, size_t n);
+/* SGD step on the gradient buffer (scaled by grad_scale, e.g. 1/world after a sum all-reduce). */
+int oaz_trainer_apply(oaz_trainer* t, float grad_scale);
+/* backward(b) + apply(1) for batches [first, first+count). */
+int oaz_trainer_train(oaz_trainer* t, int first, int count);
+/* Loss sums since the last call: out[0] value loss, out[1] policy loss, out[2] steps. */
+int oaz_trainer_losses(oaz_trainer* t, double out[3]);
+int oaz_trainer_sync(oaz_trainer* t);
 
 #ifdef __cplusplus
 }

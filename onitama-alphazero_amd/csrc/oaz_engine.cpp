@@ -18,6 +18,7 @@
 
 #include "../../include/onitama_az.h"
 #include "oaz_device.h"
+#include "oaz_host.h"
 #include "oaz_kernels.h"
 
 using namespace oaz;
@@ -25,7 +26,7 @@ using namespace oaz;
 // ---- errors ---------------------------------------------------------------------------------
 static thread_local std::string g_err;
 
-static int set_err(int code, const char* fmt, ...) {
+int oaz_set_err(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -34,14 +35,6 @@ static int set_err(int code, const char* fmt, ...) {
     g_err = buf;
     return code;
 }
-
-#define HIP_TRY(expr)                                                                      \
-    do {                                                                                   \
-        hipError_t e_ = (expr);                                                            \
-        if (e_ != hipSuccess)                                                              \
-            return set_err(OAZ_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
-                           __FILE__, __LINE__);                                            \
-    } while (0)
 
 extern "C" int oaz_abi_version(void) { return OAZ_ABI_VERSION; }
 extern "C" const char* oaz_last_error(void) { return g_err.c_str(); }
@@ -72,7 +65,7 @@ extern "C" int oaz_device_count(int* n) {
     int c = 0;
     hipError_t e = hipGetDeviceCount(&c);
     if (n) *n = (e == hipSuccess) ? c : 0;
-    if (e != hipSuccess) return set_err(OAZ_ERR_NO_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    if (e != hipSuccess) return oaz_set_err(OAZ_ERR_NO_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
     return 0;
 }
 
@@ -92,7 +85,7 @@ extern "C" size_t oaz_weight_count(int blocks, int channels, int in_planes) {
 
 extern "C" int oaz_random_weights(uint64_t seed, int blocks, float* out, size_t n) {
     const size_t need = oaz_weight_count(blocks, 64, 21);
-    if (!out || n != need || blocks < 0) return set_err(OAZ_ERR_ARG, "random_weights: need %zu floats", need);
+    if (!out || n != need || blocks < 0) return oaz_set_err(OAZ_ERR_ARG, "random_weights: need %zu floats", need);
     uint64_t ctr = 0;
     auto uni = [&](float bound) {
         const uint64_t r = splitmix64(seed ^ splitmix64(ctr++));
@@ -125,7 +118,7 @@ extern "C" int oaz_random_weights(uint64_t seed, int blocks, float* out, size_t 
     conv(128, 2, 64);
     bn(2);
     conv(2500, 50, 50);
-    if ((size_t)(p - out) != need) return set_err(OAZ_ERR_STATE, "random_weights: layout mismatch");
+    if ((size_t)(p - out) != need) return oaz_set_err(OAZ_ERR_STATE, "random_weights: layout mismatch");
     return 0;
 }
 
@@ -271,8 +264,8 @@ static int pack_weights(const float* raw, int blocks, int bf16, std::vector<floa
     for (int i = 0; i < 50; ++i) out.push_back(*p++);    // ph_linear2.bias
     out.push_back(0.0f);
     out.push_back(0.0f);
-    if (out.size() != nn_packed_floats(blocks, bf16)) return set_err(OAZ_ERR_STATE, "pack: size mismatch");
-    if ((size_t)(p - raw) != oaz_weight_count(blocks, 64, 21)) return set_err(OAZ_ERR_STATE, "pack: raw size mismatch");
+    if (out.size() != nn_packed_floats(blocks, bf16)) return oaz_set_err(OAZ_ERR_STATE, "pack: size mismatch");
+    if ((size_t)(p - raw) != oaz_weight_count(blocks, 64, 21)) return oaz_set_err(OAZ_ERR_STATE, "pack: raw size mismatch");
     return 0;
 }
 
@@ -303,7 +296,7 @@ static RulesCtx g_rules;
 static int rules_begin() {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
-        return set_err(OAZ_ERR_NO_DEVICE, "no HIP device visible (the rules run on the GPU)");
+        return oaz_set_err(OAZ_ERR_NO_DEVICE, "no HIP device visible (the rules run on the GPU)");
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     if (!g_rules.init || g_rules.device != dev) {
@@ -315,7 +308,7 @@ static int rules_begin() {
 }
 
 extern "C" int oaz_movegen(const oaz_state* s, int n, uint32_t* masks, oaz_move* moves, uint8_t* counts) {
-    if (!s || n < 0) return set_err(OAZ_ERR_ARG, "movegen: bad arguments");
+    if (!s || n < 0) return oaz_set_err(OAZ_ERR_ARG, "movegen: bad arguments");
     if (n == 0) return 0;
     std::lock_guard<std::mutex> lk(g_rules.mu);
     if (int rc = rules_begin()) return rc;
@@ -335,11 +328,11 @@ extern "C" int oaz_movegen(const oaz_state* s, int n, uint32_t* masks, oaz_move*
 }
 
 extern "C" int oaz_step(oaz_state* s, const oaz_move* mv, int n, uint8_t* results) {
-    if (!s || !mv || n < 0) return set_err(OAZ_ERR_ARG, "step: bad arguments");
+    if (!s || !mv || n < 0) return oaz_set_err(OAZ_ERR_ARG, "step: bad arguments");
     if (n == 0) return 0;
     for (int i = 0; i < n; ++i)
         if (mv[i].from > 24 || mv[i].to > 24 || mv[i].slot > 3 || mv[i].piece > 1)
-            return set_err(OAZ_ERR_ARG, "step: move %d out of range", i);  // deck.rs:88 assert
+            return oaz_set_err(OAZ_ERR_ARG, "step: move %d out of range", i);  // deck.rs:88 assert
     std::lock_guard<std::mutex> lk(g_rules.mu);
     if (int rc = rules_begin()) return rc;
     hipStream_t st = g_rules.stream;
@@ -356,7 +349,7 @@ extern "C" int oaz_step(oaz_state* s, const oaz_move* mv, int n, uint8_t* result
 }
 
 extern "C" int oaz_current_state(const oaz_state* s, int n, uint8_t* results) {
-    if (!s || !results || n < 0) return set_err(OAZ_ERR_ARG, "current_state: bad arguments");
+    if (!s || !results || n < 0) return oaz_set_err(OAZ_ERR_ARG, "current_state: bad arguments");
     if (n == 0) return 0;
     std::lock_guard<std::mutex> lk(g_rules.mu);
     if (int rc = rules_begin()) return rc;
@@ -371,7 +364,7 @@ extern "C" int oaz_current_state(const oaz_state* s, int n, uint8_t* results) {
 }
 
 extern "C" int oaz_encode(const oaz_state* s, int n, float* planes) {
-    if (!s || !planes || n < 0) return set_err(OAZ_ERR_ARG, "encode: bad arguments");
+    if (!s || !planes || n < 0) return oaz_set_err(OAZ_ERR_ARG, "encode: bad arguments");
     if (n == 0) return 0;
     std::lock_guard<std::mutex> lk(g_rules.mu);
     if (int rc = rules_begin()) return rc;
@@ -552,29 +545,29 @@ static int timed(oaz_engine* e, int kind, uint32_t samples, F&& launch, hipStrea
 
 extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
     if (!cfg) {
-        set_err(OAZ_ERR_ARG, "create: null config");
+        oaz_set_err(OAZ_ERR_ARG, "create: null config");
         return nullptr;
     }
     if (cfg->channels != 64 || cfg->in_planes != 21) {
-        set_err(OAZ_ERR_ARG, "create: only channels=64, in_planes=21 are supported");
+        oaz_set_err(OAZ_ERR_ARG, "create: only channels=64, in_planes=21 are supported");
         return nullptr;
     }
     if (cfg->blocks < 0 || cfg->blocks > 64 || cfg->sims < 1 || cfg->sims > 65535 || cfg->games < 1 ||
         cfg->max_plies < 0 || cfg->max_plies > 100000) {
-        set_err(OAZ_ERR_ARG, "create: config out of range");
+        oaz_set_err(OAZ_ERR_ARG, "create: config out of range");
         return nullptr;
     }
     if (cfg->precision != OAZ_FP32 && cfg->precision != OAZ_BF16) {
-        set_err(OAZ_ERR_ARG, "create: precision must be OAZ_FP32 or OAZ_BF16");
+        oaz_set_err(OAZ_ERR_ARG, "create: precision must be OAZ_FP32 or OAZ_BF16");
         return nullptr;
     }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
-        set_err(OAZ_ERR_NO_DEVICE, "create: no HIP device visible");
+        oaz_set_err(OAZ_ERR_NO_DEVICE, "create: no HIP device visible");
         return nullptr;
     }
     if (device < 0 || device >= ndev) {
-        set_err(OAZ_ERR_ARG, "create: device %d out of range (%d visible)", device, ndev);
+        oaz_set_err(OAZ_ERR_ARG, "create: device %d out of range (%d visible)", device, ndev);
         return nullptr;
     }
     oaz_engine* e = new oaz_engine();
@@ -592,18 +585,18 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         return nullptr;
     };
     if (hipSetDevice(device) != hipSuccess) {
-        set_err(OAZ_ERR_HIP, "hipSetDevice(%d) failed", device);
+        oaz_set_err(OAZ_ERR_HIP, "hipSetDevice(%d) failed", device);
         return fail();
     }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) {
-        set_err(OAZ_ERR_HIP, "stream create failed");
+        oaz_set_err(OAZ_ERR_HIP, "stream create failed");
         return fail();
     }
     for (int i = 0; i < 2; ++i)
         if (hipEventCreateWithFlags(&e->ev_ready[i], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&e->ev_consumed[i], hipEventDisableTiming) != hipSuccess) {
-            set_err(OAZ_ERR_HIP, "event create failed");
+            oaz_set_err(OAZ_ERR_HIP, "event create failed");
             return fail();
         }
     const size_t G = e->G;
@@ -626,7 +619,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         hipMemset(e->stats, 0, G * GS_COUNT * sizeof(uint64_t)) != hipSuccess ||
         hipMemset(e->out_count, 0, sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(e->active, 0, G) != hipSuccess) {
-        set_err(OAZ_ERR_HIP, "create: init copies failed");
+        oaz_set_err(OAZ_ERR_HIP, "create: init copies failed");
         return fail();
     }
     if (cfg->evaluator == OAZ_EVAL_NN) {  // random-init weights until oaz_load_weights
@@ -662,16 +655,16 @@ extern "C" void oaz_destroy(oaz_engine* e) {
 }
 
 extern "C" int oaz_get_config(const oaz_engine* e, oaz_config* out) {
-    if (!e || !out) return set_err(OAZ_ERR_ARG, "get_config: null");
+    if (!e || !out) return oaz_set_err(OAZ_ERR_ARG, "get_config: null");
     *out = e->cfg;
     return 0;
 }
 
 extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
-    if (!e || !blob) return set_err(OAZ_ERR_ARG, "load_weights: null");
+    if (!e || !blob) return oaz_set_err(OAZ_ERR_ARG, "load_weights: null");
     const size_t need = oaz_weight_count(e->cfg.blocks, 64, 21);
     if (n != need)  // the reference silently keeps random weights on a bad file (Q13); we refuse
-        return set_err(OAZ_ERR_WEIGHTS, "load_weights: got %zu floats, need %zu for %d blocks", n, need,
+        return oaz_set_err(OAZ_ERR_WEIGHTS, "load_weights: got %zu floats, need %zu for %d blocks", n, need,
                        e->cfg.blocks);
     std::vector<float> packed;
     if (int rc = pack_weights(blob, e->cfg.blocks, e->cfg.precision == OAZ_BF16, packed)) return rc;
@@ -683,14 +676,14 @@ extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
 }
 
 extern "C" int oaz_sync(oaz_engine* e) {
-    if (!e) return set_err(OAZ_ERR_ARG, "sync: null");
+    if (!e) return oaz_set_err(OAZ_ERR_ARG, "sync: null");
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream2));
     return 0;
 }
 
 extern "C" int oaz_set_timing(oaz_engine* e, int enable) {
-    if (!e) return set_err(OAZ_ERR_ARG, "set_timing: null");
+    if (!e) return oaz_set_err(OAZ_ERR_ARG, "set_timing: null");
     e->timing = enable != 0;
     return 0;
 }
@@ -710,14 +703,14 @@ static int resolve_timing(oaz_engine* e) {
 }
 
 extern "C" int oaz_kernel_times_get(oaz_engine* e, oaz_kernel_times* out) {
-    if (!e || !out) return set_err(OAZ_ERR_ARG, "kernel_times: null");
+    if (!e || !out) return oaz_set_err(OAZ_ERR_ARG, "kernel_times: null");
     if (int rc = resolve_timing(e)) return rc;
     *out = e->times;
     return 0;
 }
 
 extern "C" int oaz_kernel_times_reset(oaz_engine* e) {
-    if (!e) return set_err(OAZ_ERR_ARG, "kernel_times_reset: null");
+    if (!e) return oaz_set_err(OAZ_ERR_ARG, "kernel_times_reset: null");
     if (int rc = resolve_timing(e)) return rc;
     memset(&e->times, 0, sizeof(e->times));
     return 0;
@@ -734,8 +727,8 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
 }
 
 extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* policy, float* value) {
-    if (!e || !s || B < 0) return set_err(OAZ_ERR_ARG, "nn_forward: bad arguments");
-    if ((uint32_t)B > e->G) return set_err(OAZ_ERR_CAPACITY, "nn_forward: B=%d > games=%u", B, e->G);
+    if (!e || !s || B < 0) return oaz_set_err(OAZ_ERR_ARG, "nn_forward: bad arguments");
+    if ((uint32_t)B > e->G) return oaz_set_err(OAZ_ERR_CAPACITY, "nn_forward: B=%d > games=%u", B, e->G);
     if (B == 0) return 0;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipMemcpyAsync(e->s_roots, s, (size_t)B * sizeof(oaz_state), hipMemcpyHostToDevice, e->stream));
@@ -813,11 +806,11 @@ static void fill_search_stats(const uint64_t* s, oaz_search_stats* o) {
 
 extern "C" int oaz_search(oaz_engine* e, const oaz_state* roots, int G, oaz_move* out_move, float* out_pi,
                           float* out_root_value, oaz_search_stats* stats) {
-    if (!e || !roots || G < 0) return set_err(OAZ_ERR_ARG, "search: bad arguments");
-    if ((uint32_t)G > e->G) return set_err(OAZ_ERR_CAPACITY, "search: G=%d > games=%u", G, e->G);
+    if (!e || !roots || G < 0) return oaz_set_err(OAZ_ERR_ARG, "search: bad arguments");
+    if ((uint32_t)G > e->G) return oaz_set_err(OAZ_ERR_CAPACITY, "search: G=%d > games=%u", G, e->G);
     if (G == 0) return 0;
     for (int i = 0; i < G; ++i)
-        if (roots[i].to_move > 1) return set_err(OAZ_ERR_ARG, "search: root %d has to_move=%d", i, roots[i].to_move);
+        if (roots[i].to_move > 1) return oaz_set_err(OAZ_ERR_ARG, "search: root %d has to_move=%d", i, roots[i].to_move);
     HIP_TRY(hipSetDevice(e->device));
     const TreeView t = tree_view(e, (uint32_t)G);
     HIP_TRY(hipMemcpyAsync(e->s_roots, roots, (size_t)G * sizeof(oaz_state), hipMemcpyHostToDevice, e->stream));
@@ -846,7 +839,7 @@ extern "C" int oaz_search(oaz_engine* e, const oaz_state* roots, int G, oaz_move
 }
 
 extern "C" int oaz_tree_dump(oaz_engine* e, int game, oaz_node* out, int cap, int* n_nodes) {
-    if (!e || game < 0 || (uint32_t)game >= e->G) return set_err(OAZ_ERR_ARG, "tree_dump: bad game");
+    if (!e || game < 0 || (uint32_t)game >= e->G) return oaz_set_err(OAZ_ERR_ARG, "tree_dump: bad game");
     HIP_TRY(hipSetDevice(e->device));
     uint32_t n = 0;
     HIP_TRY(hipMemcpyAsync(&n, e->n_nodes + game, 4, hipMemcpyDeviceToHost, e->stream));
@@ -862,7 +855,7 @@ extern "C" int oaz_tree_dump(oaz_engine* e, int game, oaz_node* out, int cap, in
 
 // ---- self-play ----------------------------------------------------------------------------------
 extern "C" int oaz_selfplay_reset(oaz_engine* e) {
-    if (!e) return set_err(OAZ_ERR_ARG, "selfplay_reset: null");
+    if (!e) return oaz_set_err(OAZ_ERR_ARG, "selfplay_reset: null");
     HIP_TRY(hipSetDevice(e->device));
     const TreeView t = tree_view(e, e->G);
     HIP_TRY(hipMemsetAsync(e->stats, 0, (size_t)e->G * GS_COUNT * sizeof(uint64_t), e->stream));
@@ -875,7 +868,7 @@ extern "C" int oaz_selfplay_reset(oaz_engine* e) {
 }
 
 extern "C" int oaz_selfplay_step(oaz_engine* e, int moves) {
-    if (!e || moves < 0) return set_err(OAZ_ERR_ARG, "selfplay_step: bad arguments");
+    if (!e || moves < 0) return oaz_set_err(OAZ_ERR_ARG, "selfplay_step: bad arguments");
     if (!e->selfplay_ready)
         if (int rc = oaz_selfplay_reset(e)) return rc;
     HIP_TRY(hipSetDevice(e->device));
@@ -889,7 +882,7 @@ extern "C" int oaz_selfplay_step(oaz_engine* e, int moves) {
 }
 
 extern "C" int oaz_selfplay_stats_get(oaz_engine* e, oaz_selfplay_stats* o) {
-    if (!e || !o) return set_err(OAZ_ERR_ARG, "selfplay_stats: null");
+    if (!e || !o) return oaz_set_err(OAZ_ERR_ARG, "selfplay_stats: null");
     HIP_TRY(hipSetDevice(e->device));
     uint64_t s[GS_COUNT];
     if (int rc = reduce_stats(e, e->G, s)) return rc;
@@ -930,18 +923,18 @@ static int samples_copy(oaz_engine* e, void* dst, size_t cap, size_t* n_out, hip
 }
 
 extern "C" int oaz_samples_fetch(oaz_engine* e, oaz_sample* out, size_t cap, size_t* n_out) {
-    if (!e || (!out && cap)) return set_err(OAZ_ERR_ARG, "samples_fetch: bad arguments");
+    if (!e || (!out && cap)) return oaz_set_err(OAZ_ERR_ARG, "samples_fetch: bad arguments");
     return samples_copy(e, out, cap, n_out, hipMemcpyDeviceToHost);
 }
 
 extern "C" int oaz_samples_export_device(oaz_engine* e, void* dev_dst, size_t cap_bytes, size_t* n_out) {
-    if (!e || (!dev_dst && cap_bytes)) return set_err(OAZ_ERR_ARG, "samples_export: bad arguments");
+    if (!e || (!dev_dst && cap_bytes)) return oaz_set_err(OAZ_ERR_ARG, "samples_export: bad arguments");
     return samples_copy(e, dev_dst, cap_bytes / sizeof(oaz_sample), n_out, hipMemcpyDeviceToDevice);
 }
 
 extern "C" int oaz_selfplay_run(oaz_engine* e, int n_games, oaz_sample* out, size_t cap, size_t* n_out,
                                 oaz_selfplay_stats* stats) {
-    if (!e || n_games < 0) return set_err(OAZ_ERR_ARG, "selfplay_run: bad arguments");
+    if (!e || n_games < 0) return oaz_set_err(OAZ_ERR_ARG, "selfplay_run: bad arguments");
     e->quota = (uint64_t)n_games;  // slots stop dealing at global game index >= n_games
     int rc = oaz_selfplay_reset(e);
     if (rc) {

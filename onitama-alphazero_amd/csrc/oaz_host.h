@@ -1,0 +1,17 @@
+// oaz_host.h — host-side helpers shared by the C-ABI translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/onitama_az.h"
+
+// Records the thread-local error message returned by oaz_last_error(); returns `code`.
+int oaz_set_err(int code, const char* fmt, ...);
+
+#define HIP_TRY(expr)                                                                           \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return oaz_set_err(OAZ_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                               __FILE__, __LINE__);                                             \
+    } while (0)

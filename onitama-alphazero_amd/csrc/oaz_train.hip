@@ -1,0 +1,1056 @@
+// oaz_train.hip — the training step on gfx950: gather a batch from the
+// replay buffer, ConvResNet::forward(train=true) (net.rs:215-232, BN on batch statistics),
+// alphaloss (net.rs:234-243), backward, and tch's SGD (train.rs:181-186, 309).
+//
+// Layout. Activations are square-major rows: row = sq * B + b (sq = board square, b = sample),
+// 64 fp32 channels per row (the first layer's 21 input planes padded to 32). A 3x3 conv over
+// 16 rows of one square reads, for each on-board tap, the 16 contiguous rows of the neighbour
+// square, so off-board taps are skipped outright (169 of 225 (square, tap) pairs do work).
+//
+// Kernels per step (N residual blocks, L = 1 + 2N convs):
+//   gather                      samples[idx] -> X0 [R][32], pi [B][50], z [B]
+//   per conv: conv_fwd (MFMA 16x16x4 f32, + per-16-row BN partial sums) -> bn_fwd_fin -> bn_act
+//   heads: head_conv (1x1, 3 channels) -> bn_fwd_fin x2 -> head_sample (value MLP, policy
+//          linear + softmax, loss, their backward, per-sample) -> head_bwd_fin -> head_bwd_rows
+//   per conv, last to first: bn_bwd_fin -> bn_bwd_apply -> wgrad (MFMA, per (tap, square)
+//          partials) -> wgrad_reduce -> conv_dgrad (the same conv kernel on flipped/transposed
+//          weights, epilogue = skip add + ReLU mask + BN-backward partial sums of the layer below)
+//   sgd (+ repack of the conv weights for the next step)
+// All reductions are two-stage with fixed order (deterministic; no float atomics).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/onitama_az.h"
+#include "oaz_device.h"
+#include "oaz_host.h"
+
+using namespace oaz;
+
+namespace tr {
+
+constexpr int kC = 64;       // hidden channels
+constexpr int kIn = 21;      // input planes
+constexpr int kInPad = 32;   // padded input row stride
+constexpr int kMaxConv = 1 + 2 * 16;
+constexpr int kHeadW = 64 * 25 + 64 + 64 + 1 + 2500 + 50;  // value MLP + policy linear grads
+constexpr int kHeadVW = 64 * 25 + 64 + 64 + 1;              // vh_linear1 w,b + vh_linear2 w,b
+constexpr int kHConvW = 64 + 1 + 128 + 2;                   // vh_conv w,b + policy_conv w,b
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int nbr(int sq, int t) {
+    const int y = sq / 5 + t / 3 - 1, x = sq % 5 + t % 3 - 1;
+    return (y >= 0 && y < 5 && x >= 0 && x < 5) ? y * 5 + x : -1;
+}
+
+__device__ __forceinline__ float wave_sum16(float v) {  // sum over the 4 lane groups (lane>>4)
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// ---- gather: create_tensor_from_state (common.rs:26-80) for samples[idx[b]] ----------------------
+__global__ void k_gather(const oaz_sample* samples, const int32_t* idx, int B, float* X0, float* pi, float* z) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * 25) return;
+    const int b = t % B, sq = t / B;
+    const oaz_sample* s = samples + idx[b];
+    const oaz_state st = s->state;
+    const int color = st.to_move & 1;
+    const uint32_t bit = sq_bit(sq);
+    float* row = X0 + (size_t)(sq * B + b) * kInPad;
+    float v[kInPad];
+#pragma unroll
+    for (int c = 0; c < kInPad; ++c) v[c] = 0.0f;
+    v[0] = (st.pawns[0] & bit) ? 1.0f : 0.0f;
+    v[1] = (st.kings[0] & bit) ? 1.0f : 0.0f;
+    v[2] = (st.pawns[1] & bit) ? 1.0f : 0.0f;
+    v[3] = (st.kings[1] & bit) ? 1.0f : 0.0f;
+    const int c0 = st.cards[color ? 2 : 0] & 15, c1 = st.cards[color ? 3 : 1] & 15;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[4 + c] = (c == c0 || c == c1) ? 1.0f : 0.0f;
+    v[20] = color == OAZ_BLUE ? 1.0f : 0.0f;
+#pragma unroll
+    for (int c = 0; c < kInPad; c += 4) *reinterpret_cast<float4*>(row + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
+    if (sq == 0) {
+        for (int k = 0; k < 50; ++k) pi[b * 50 + k] = s->pi[k];
+        z[b] = s->z;
+    }
+}
+
+// ---- 3x3 conv (forward, and dgrad on flipped weights) ------------------------------------------
+enum { CONV_FWD = 0, CONV_DGRAD = 1 };
+
+struct ConvArgs {
+    const float* in;      // [R][16*chunks]
+    const float4* w;      // packed [9][chunks][4 nt][64 lanes]
+    const float* bias;    // FWD
+    float* out;           // FWD: Z ; DGRAD: m = (dgrad + skip) * (act > 0)
+    float* part;          // [nwg][2][64]: FWD sum, sumsq ; DGRAD sum m, sum m*xhat
+    const float* act;     // DGRAD: activation of the layer below (ReLU output)
+    const float* zprev;   // DGRAD: its pre-BN conv output
+    const float* mean;    // DGRAD: its BN batch mean / invstd
+    const float* invstd;
+    const float* skip;    // DGRAD: residual gradient to add (or null)
+    int chunks;           // input channels / 16
+    int B;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+    const int sq = blockIdx.y, b0 = blockIdx.x * 16, B = a.B;
+    const int rs = 16 * a.chunks;
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int t = 0; t < 9; ++t) {
+        const int nb = nbr(sq, t);
+        if (nb < 0) continue;
+        const float* base = a.in + (size_t)(nb * B + b0 + i) * rs + 4 * kq;
+        const float4* wt = a.w + (size_t)t * a.chunks * 256 + wave * 64 + lane;
+        for (int g = 0; g < a.chunks; ++g) {
+            const float4 av = *reinterpret_cast<const float4*>(base + 16 * g);
+            const float4 bv = wt[g * 256];
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
+        }
+    }
+    // C/D layout: reg r of lane l = (row 4*(l>>4) + r, col l&15)
+    const int co = wave * 16 + i;
+    float s1 = 0.0f, s2 = 0.0f;
+    if (MODE == CONV_FWD) {
+        const float bb = a.bias[co];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const size_t o = (size_t)(sq * B + b0 + kq * 4 + r) * kC + co;
+            const float v = acc[r] + bb;
+            a.out[o] = v;
+            s1 += v;
+            s2 += v * v;
+        }
+    } else {
+        const float mu = a.mean[co], is = a.invstd[co];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const size_t o = (size_t)(sq * B + b0 + kq * 4 + r) * kC + co;
+            float d = acc[r];
+            if (a.skip) d += a.skip[o];
+            const float m = a.act[o] > 0.0f ? d : 0.0f;
+            a.out[o] = m;
+            s1 += m;
+            s2 += m * ((a.zprev[o] - mu) * is);
+        }
+    }
+    s1 = wave_sum16(s1);
+    s2 = wave_sum16(s2);
+    if (kq == 0) {
+        const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+        a.part[wg * 128 + co] = s1;
+        a.part[wg * 128 + 64 + co] = s2;
+    }
+}
+
+// ---- BN finalisation (forward): batch mean / biased var, running stats update ----------------------
+// part [nwg][2][pstride] (sum, sumsq) columns coff..coff+C-1; torch batch_norm(training=True):
+// y = (x - mean) * invstd * gamma + beta, invstd = 1/sqrt(var_biased + eps);
+// running = (1 - m) * running + m * {mean, var_unbiased}.
+__global__ void k_bn_fwd_fin(const float* part, int nwg, int pstride, int coff, int C, double N,
+                             float* rmean, float* rvar, float bn_mom, float eps, float* mean, float* invstd) {
+    __shared__ double sh[2][4][64];
+    const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+    double s1 = 0.0, s2 = 0.0;
+    if (c < C)
+        for (int w = q; w < nwg; w += 4) {
+            s1 += part[(size_t)w * 2 * pstride + coff + c];
+            s2 += part[(size_t)w * 2 * pstride + pstride + coff + c];
+        }
+    sh[0][q][c] = s1;
+    sh[1][q][c] = s2;
+    __syncthreads();
+    if (q == 0 && c < C) {
+        s1 = sh[0][0][c] + sh[0][1][c] + sh[0][2][c] + sh[0][3][c];
+        s2 = sh[1][0][c] + sh[1][1][c] + sh[1][2][c] + sh[1][3][c];
+        const double mu = s1 / N;
+        double var = s2 / N - mu * mu;
+        if (var < 0.0) var = 0.0;
+        mean[c] = (float)mu;
+        invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+        rmean[c] = (float)((1.0 - bn_mom) * rmean[c] + bn_mom * mu);
+        rvar[c] = (float)((1.0 - bn_mom) * rvar[c] + bn_mom * var * N / (N - 1.0));
+    }
+}
+
+// A = relu((Z - mean) * invstd * gamma + beta [+ skip])
+__global__ void k_bn_act(const float* Z, const float* mean, const float* invstd, const float* gamma,
+                         const float* beta, const float* skip, float* A, long long n) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t * 4 >= n) return;
+    const int c = (int)((t * 4) & 63);
+    const float4 z = reinterpret_cast<const float4*>(Z)[t];
+    float v[4] = {z.x, z.y, z.z, z.w};
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (skip) s = reinterpret_cast<const float4*>(skip)[t];
+    const float sk[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float y = (v[k] - mean[c + k]) * invstd[c + k] * gamma[c + k] + beta[c + k];
+        if (skip) y += sk[k];
+        v[k] = y > 0.0f ? y : 0.0f;
+    }
+    reinterpret_cast<float4*>(A)[t] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// ---- BN backward finalisation: dgamma = sum m*xhat, dbeta = sum m; dx coefficients -----------------
+__global__ void k_bn_bwd_fin(const float* part, int nwg, int pstride, int coff, int C, double N,
+                             const float* gamma, const float* invstd, float* ggamma, float* gbeta,
+                             float* c1, float* mm, float* mx) {
+    __shared__ double sh[2][4][64];
+    const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+    double s1 = 0.0, s2 = 0.0;
+    if (c < C)
+        for (int w = q; w < nwg; w += 4) {
+            s1 += part[(size_t)w * 2 * pstride + coff + c];
+            s2 += part[(size_t)w * 2 * pstride + pstride + coff + c];
+        }
+    sh[0][q][c] = s1;
+    sh[1][q][c] = s2;
+    __syncthreads();
+    if (q == 0 && c < C) {
+        s1 = sh[0][0][c] + sh[0][1][c] + sh[0][2][c] + sh[0][3][c];
+        s2 = sh[1][0][c] + sh[1][1][c] + sh[1][2][c] + sh[1][3][c];
+        gbeta[c] = (float)s1;
+        ggamma[c] = (float)s2;
+        c1[c] = gamma[c] * invstd[c];
+        mm[c] = (float)(s1 / N);
+        mx[c] = (float)(s2 / N);
+    }
+}
+
+// dZ = gamma*invstd * (m - mean(m) - xhat * mean(m*xhat)); per-64-row partial sums of dZ (conv bias grad)
+__global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* M, const float* Z, const float* mean,
+                                                      const float* invstd, const float* c1, const float* mm,
+                                                      const float* mx, float* dZ, float* part, int R) {
+    __shared__ float sh[4][64];
+    const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int r0 = blockIdx.x * 64;
+    const float mu = mean[c], is = invstd[c], k1 = c1[c], k2 = mm[c], k3 = mx[c];
+    float s = 0.0f;
+    for (int r = r0 + q; r < min(r0 + 64, R); r += 4) {
+        const size_t o = (size_t)r * kC + c;
+        const float xh = (Z[o] - mu) * is;
+        const float d = k1 * (M[o] - k2 - xh * k3);
+        dZ[o] = d;
+        s += d;
+    }
+    sh[q][c] = s;
+    __syncthreads();
+    if (q == 0) part[(size_t)blockIdx.x * 64 + c] = sh[0][c] + sh[1][c] + sh[2][c] + sh[3][c];
+}
+
+// ---- weight gradient: per (tap, square) partial D[co][ci] = sum_b dZ[sq,b][co] * X[nbr,b][ci] ------
+template <int NCT>  // input channel tiles of 16 (4 for 64 channels, 2 for the padded 32)
+__global__ __launch_bounds__(256) void k_wgrad(const float* dZ, const float* X, int B, float* part) {
+    const int sq = blockIdx.x, t = blockIdx.y;
+    const int nb = nbr(sq, t);
+    if (nb < 0) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+    const int xrs = NCT * 16;
+    f32x4 acc[NCT];
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const float* pa = dZ + (size_t)(sq * B + kq) * kC + wave * 16 + i;  // A[m = co][k = b]
+    const float* pb = X + (size_t)(nb * B + kq) * xrs + i;              // B[k = b][n = ci]
+    for (int b = 0; b < B; b += 4) {
+        const float av = pa[(size_t)b * kC];
+#pragma unroll
+        for (int j = 0; j < NCT; ++j) {
+            const float bv = pb[(size_t)b * xrs + 16 * j];
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
+        }
+    }
+    float* out = part + (size_t)(t * 25 + sq) * kC * xrs;
+#pragma unroll
+    for (int j = 0; j < NCT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(wave * 16 + kq * 4 + r) * xrs + 16 * j + i] = acc[j][r];
+}
+
+// grad_w[co][ci][tap] (canonical [co][cin][3][3]) = sum over on-board squares; grad_b = sum of dZ partials
+__global__ void k_wgrad_reduce(const float* part, int xrs, int cin, const float* bpart, int nbw,
+                               float* gw, float* gb) {
+    const int id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= 9 * kC * cin) return;
+    const int t = id % 9, ci = (id / 9) % cin, co = id / (9 * cin);
+    float s = 0.0f;
+    for (int sq = 0; sq < 25; ++sq)
+        if (nbr(sq, t) >= 0) s += part[((size_t)(t * 25 + sq) * kC + co) * xrs + ci];
+    gw[id] = s;
+    if (t == 0 && ci == 0) {
+        float sb = 0.0f;
+        for (int w = 0; w < nbw; ++w) sb += bpart[(size_t)w * 64 + co];
+        gb[co] = sb;
+    }
+}
+
+// ---- heads -------------------------------------------------------------------------------------
+struct HeadOff {  // float offsets into the parameter / gradient blob
+    int vcw, vcb, vg, vb, vrm, vrv, l1w, l1b, l2w, l2b;
+    int pcw, pcb, pg, pb, prm, prv, plw, plb;
+};
+
+// zv = vh_conv(A) (1x1, 64 -> 1), zp = policy_conv(A) (64 -> 2); per-256-row BN partials
+__global__ __launch_bounds__(256) void k_head_conv(const float* A, const float* P, HeadOff o, float* hz,
+                                                   float* part, int R) {
+    __shared__ float sh[4][6];
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    float v[3] = {0.0f, 0.0f, 0.0f};
+    if (r < R) {
+        const float4* row = reinterpret_cast<const float4*>(A + (size_t)r * kC);
+        float a0 = P[o.vcb], a1 = P[o.pcb], a2 = P[o.pcb + 1];
+        for (int k = 0; k < 16; ++k) {
+            const float4 x = row[k];
+            const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = 4 * k + j;
+                a0 += P[o.vcw + c] * xs[j];
+                a1 += P[o.pcw + c] * xs[j];
+                a2 += P[o.pcw + 64 + c] * xs[j];
+            }
+        }
+        v[0] = a0;
+        v[1] = a1;
+        v[2] = a2;
+        *reinterpret_cast<float4*>(hz + (size_t)r * 4) = make_float4(a0, a1, a2, 0.0f);
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const float s1 = wave_sum(v[j]), s2 = wave_sum(v[j] * v[j]);
+        if (lane == 0) {
+            sh[wave][j] = s1;
+            sh[wave][3 + j] = s2;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int j = threadIdx.x;
+        const float s = sh[0][j] + sh[1][j] + sh[2][j] + sh[3][j];
+        part[(size_t)blockIdx.x * 8 + (j < 3 ? j : 4 + j - 3)] = s;  // [nwg][2][4]
+    }
+}
+
+struct HeadStats {  // head BN batch statistics (channel 0 = value, 1..2 = policy)
+    float mean[3], invstd[3];
+    float c1[3], mm[3], mx[3];
+};
+
+// One thread per sample: value MLP (25 -> 64 -> 1, tanh), policy linear (50 -> 50) + softmax,
+// alphaloss terms (net.rs:234-243) and their backward down to the head BN outputs.
+// Q16: with value_loss_broadcast the value loss is mean_{i,j} (z_j - v_i)^2 over [B,B].
+constexpr int kHS = 64;  // samples per workgroup
+__global__ __launch_bounds__(64) void k_head_sample(const float* hz, const float* hst_mean, const float* hst_inv,
+                                                    const float* P, HeadOff o, const float* pi, const float* z,
+                                                    int B, int broadcast, float* g3, float* part_bn,
+                                                    float* part_w, float* part_loss) {
+    __shared__ float lds[kHeadW + 254 * kHS];  // 82 KB (a workgroup may hold up to 160 KB)
+    float* W = lds;                        // kHeadW floats: l1w[64][25] l1b[64] l2w[64] l2b plw[50][50] plb[50]
+    float* hv = W + kHeadW;                // [25][kHS]
+    float* dh1 = hv + 25 * kHS;            // [64][kHS]
+    float* h1 = dh1 + 64 * kHS;            // [64][kHS]
+    float* hp = h1 + 64 * kHS;             // [50][kHS]
+    float* dl = hp + 50 * kHS;             // [50][kHS]
+    float* du = dl + 50 * kHS;             // [kHS]
+    const int lane = threadIdx.x;
+    for (int k = lane; k < kHeadVW; k += 64) W[k] = P[o.l1w + k];
+    for (int k = lane; k < 2550; k += 64) W[kHeadVW + k] = P[o.plw + k];
+    __syncthreads();
+    const float* l1w = W;
+    const float* l1b = W + 1600;
+    const float* l2w = W + 1664;
+    const float l2b = W[1728];
+    const float* plw = W + kHeadVW;
+    const float* plb = plw + 2500;
+    // batch sums of z for the broadcast value loss
+    float sz = 0.0f, sz2 = 0.0f;
+    if (broadcast) {
+        for (int k = lane; k < B; k += 64) {
+            sz += z[k];
+            sz2 += z[k] * z[k];
+        }
+        sz = wave_sum(sz);
+        sz2 = wave_sum(sz2);
+    }
+    const int b = blockIdx.x * kHS + lane;
+    const bool ok = b < B;
+    float bnp[3][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+    float lv = 0.0f, lp = 0.0f;
+    float xh_v[25];
+    if (ok) {
+        for (int sq = 0; sq < 25; ++sq) {
+            const float x = (hz[(size_t)(sq * B + b) * 4] - hst_mean[0]) * hst_inv[0];
+            xh_v[sq] = x;
+            const float y = x * P[o.vg] + P[o.vb];
+            hv[sq * kHS + lane] = y > 0.0f ? y : 0.0f;
+        }
+        float u = l2b;
+        for (int oo = 0; oo < 64; ++oo) {
+            float a = l1b[oo];
+            for (int sq = 0; sq < 25; ++sq) a += l1w[oo * 25 + sq] * hv[sq * kHS + lane];
+            a = a > 0.0f ? a : 0.0f;
+            h1[oo * kHS + lane] = a;
+            u += l2w[oo] * a;
+        }
+        const float v = tanhf(u);
+        for (int c = 0; c < 2; ++c)
+            for (int sq = 0; sq < 25; ++sq) {
+                const float x = (hz[(size_t)(sq * B + b) * 4 + 1 + c] - hst_mean[1 + c]) * hst_inv[1 + c];
+                const float y = x * P[o.pg + c] + P[o.pb + c];
+                hp[(c * 25 + sq) * kHS + lane] = y > 0.0f ? y : 0.0f;
+            }
+        float mxl = -INFINITY;
+        for (int j = 0; j < 50; ++j) {
+            float a = plb[j];
+            for (int k = 0; k < 50; ++k) a += plw[j * 50 + k] * hp[k * kHS + lane];
+            dl[j * kHS + lane] = a;  // logits for now
+            mxl = fmaxf(mxl, a);
+        }
+        float se = 0.0f;
+        for (int j = 0; j < 50; ++j) {
+            const float e = expf(dl[j * kHS + lane] - mxl);
+            dl[j * kHS + lane] = e;
+            se += e;
+        }
+        const float inv25B = 1.0f / (25.0f * (float)B);
+        float spi = 0.0f;
+        for (int j = 0; j < 50; ++j) spi += pi[(size_t)b * 50 + j];
+        for (int j = 0; j < 50; ++j) {
+            const float p = dl[j * kHS + lane] / se;
+            const float t = pi[(size_t)b * 50 + j];
+            lp -= t * logf(p);
+            dl[j * kHS + lane] = (p * spi - t) * inv25B;
+        }
+        lp *= inv25B;
+        const float fB = (float)B;
+        float dv;
+        if (broadcast) {
+            lv = (sz2 - 2.0f * v * sz + fB * v * v) / (fB * fB);
+            dv = 2.0f * (fB * v - sz) / (fB * fB);
+        } else {
+            const float d = v - z[b];
+            lv = d * d / fB;
+            dv = 2.0f * d / fB;
+        }
+        const float duv = dv * (1.0f - v * v);
+        du[lane] = duv;
+        for (int oo = 0; oo < 64; ++oo) dh1[oo * kHS + lane] = h1[oo * kHS + lane] > 0.0f ? duv * l2w[oo] : 0.0f;
+        for (int sq = 0; sq < 25; ++sq) {
+            float d = 0.0f;
+            for (int oo = 0; oo < 64; ++oo) d += l1w[oo * 25 + sq] * dh1[oo * kHS + lane];
+            const float g = hv[sq * kHS + lane] > 0.0f ? d : 0.0f;
+            g3[(size_t)(sq * B + b) * 4] = g;
+            bnp[0][0] += g;
+            bnp[0][1] += g * xh_v[sq];
+        }
+        for (int k = 0; k < 50; ++k) {
+            float d = 0.0f;
+            for (int j = 0; j < 50; ++j) d += plw[j * 50 + k] * dl[j * kHS + lane];
+            const float g = hp[k * kHS + lane] > 0.0f ? d : 0.0f;
+            const int c = k / 25, sq = k % 25;
+            const size_t r = (size_t)(sq * B + b);
+            g3[r * 4 + 1 + c] = g;
+            const float x = (hz[r * 4 + 1 + c] - hst_mean[1 + c]) * hst_inv[1 + c];
+            bnp[1 + c][0] += g;
+            bnp[1 + c][1] += g * x;
+        }
+    } else {
+        for (int sq = 0; sq < 25; ++sq) hv[sq * kHS + lane] = 0.0f;
+        for (int oo = 0; oo < 64; ++oo) {
+            h1[oo * kHS + lane] = 0.0f;
+            dh1[oo * kHS + lane] = 0.0f;
+        }
+        for (int j = 0; j < 50; ++j) {
+            hp[j * kHS + lane] = 0.0f;
+            dl[j * kHS + lane] = 0.0f;
+        }
+        du[lane] = 0.0f;
+    }
+    // per-workgroup partials: head BN backward sums, losses
+    for (int c = 0; c < 3; ++c) {
+        const float s1 = wave_sum(bnp[c][0]), s2 = wave_sum(bnp[c][1]);
+        if (lane == 0) {
+            part_bn[(size_t)blockIdx.x * 8 + c] = s1;
+            part_bn[(size_t)blockIdx.x * 8 + 4 + c] = s2;
+        }
+    }
+    lv = wave_sum(lv);
+    lp = wave_sum(lp);
+    if (lane == 0) {
+        part_loss[blockIdx.x * 2] = lv;
+        part_loss[blockIdx.x * 2 + 1] = lp;
+    }
+    __syncthreads();
+    // weight-gradient partials over this workgroup's samples
+    float* pw = part_w + (size_t)blockIdx.x * kHeadW;
+    for (int e = lane; e < kHeadW; e += 64) {
+        float s = 0.0f;
+        if (e < 1600) {  // vh_linear1.weight [64][25]
+            const int oo = e / 25, sq = e % 25;
+            for (int k = 0; k < kHS; ++k) s += dh1[oo * kHS + k] * hv[sq * kHS + k];
+        } else if (e < 1664) {  // vh_linear1.bias
+            const int oo = e - 1600;
+            for (int k = 0; k < kHS; ++k) s += dh1[oo * kHS + k];
+        } else if (e < 1728) {  // vh_linear2.weight [1][64]
+            const int oo = e - 1664;
+            for (int k = 0; k < kHS; ++k) s += du[k] * h1[oo * kHS + k];
+        } else if (e == 1728) {  // vh_linear2.bias
+            for (int k = 0; k < kHS; ++k) s += du[k];
+        } else if (e < kHeadVW + 2500) {  // ph_linear2.weight [50][50]
+            const int j = (e - kHeadVW) / 50, kk = (e - kHeadVW) % 50;
+            for (int k = 0; k < kHS; ++k) s += dl[j * kHS + k] * hp[kk * kHS + k];
+        } else {  // ph_linear2.bias
+            const int j = e - kHeadVW - 2500;
+            for (int k = 0; k < kHS; ++k) s += dl[j * kHS + k];
+        }
+        pw[e] = s;
+    }
+}
+
+// out[j] = sum_w part[w*pstride + src + j], j < width
+__global__ void k_colsum(const float* part, int nwg, int pstride, int src, int width, float* out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= width) return;
+    float s = 0.0f;
+    for (int w = 0; w < nwg; ++w) s += part[(size_t)w * pstride + src + j];
+    out[j] = s;
+}
+
+// Loss accumulators (double) += this step's sums
+__global__ void k_loss_acc(const float* part_loss, int nwg, double* acc) {
+    if (threadIdx.x != 0) return;
+    double v = 0.0, p = 0.0;
+    for (int w = 0; w < nwg; ++w) {
+        v += part_loss[2 * w];
+        p += part_loss[2 * w + 1];
+    }
+    acc[0] += v;
+    acc[1] += p;
+    acc[2] += 1.0;
+}
+
+// Per trunk row: head BN backward -> dA = wv * dzv + wp0 * dzp0 + wp1 * dzp1; m = dA * (A > 0);
+// partials: sum m, sum m*xhat (last trunk BN), head conv weight/bias grads.
+__global__ __launch_bounds__(256) void k_head_bwd_rows(const float* A, const float* Z, const float* mean,
+                                                       const float* invstd, const float* hz, const float* g3,
+                                                       const float* hst_mean, const float* hst_inv,
+                                                       const float* hc1, const float* hmm, const float* hmx,
+                                                       const float* P, HeadOff o, float* M, float* part_bn,
+                                                       float* part_hc, int R) {
+    __shared__ float sh[4][8][64];
+    const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int r0 = blockIdx.x * 64;
+    const float wv = P[o.vcw + c], wp0 = P[o.pcw + c], wp1 = P[o.pcw + 64 + c];
+    const float mu = mean[c], is = invstd[c];
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // sum m, sum m*xh, dwv, dwp0, dwp1, dbv, dbp0, dbp1
+    for (int r = r0 + q; r < min(r0 + 64, R); r += 4) {
+        float dz[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float xh = (hz[(size_t)r * 4 + k] - hst_mean[k]) * hst_inv[k];
+            dz[k] = hc1[k] * (g3[(size_t)r * 4 + k] - hmm[k] - xh * hmx[k]);
+        }
+        const size_t off = (size_t)r * kC + c;
+        const float a = A[off];
+        const float dA = wv * dz[0] + wp0 * dz[1] + wp1 * dz[2];
+        const float m = a > 0.0f ? dA : 0.0f;
+        M[off] = m;
+        acc[0] += m;
+        acc[1] += m * ((Z[off] - mu) * is);
+        acc[2] += dz[0] * a;
+        acc[3] += dz[1] * a;
+        acc[4] += dz[2] * a;
+        acc[5] += dz[0];
+        acc[6] += dz[1];
+        acc[7] += dz[2];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sh[q][k][c] = acc[k];
+    __syncthreads();
+    if (q == 0) {
+        float s[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] = sh[0][k][c] + sh[1][k][c] + sh[2][k][c] + sh[3][k][c];
+        part_bn[(size_t)blockIdx.x * 128 + c] = s[0];
+        part_bn[(size_t)blockIdx.x * 128 + 64 + c] = s[1];
+        float* ph = part_hc + (size_t)blockIdx.x * kHConvW;  // vh_conv w[64] b | policy_conv w[2][64] b[2]
+        ph[c] = s[2];
+        ph[65 + c] = s[3];
+        ph[65 + 64 + c] = s[4];
+        if (c == 0) {
+            ph[64] = s[5];
+            ph[65 + 128] = s[6];
+            ph[65 + 129] = s[7];
+        }
+    }
+}
+
+// ---- optimiser + weight packing -------------------------------------------------------------------
+__global__ void k_sgd(float* p, const float* g, float* buf, const uint8_t* mask, long long n, float lr,
+                      float mom, float wd, float scale) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !mask[i]) return;
+    const float d = g[i] * scale + wd * p[i];
+    const float bb = mom * buf[i] + d;
+    buf[i] = bb;
+    p[i] = p[i] - lr * bb;
+}
+
+// Packed conv weights: float4 index ((t*chunks + g)*4 + nt)*64 + lane holds, for output channel
+// nt*16 + (lane&15), input channels 16g + 4*(lane>>4) + {0..3}.
+//   fwd:   W[co][ci][t]            (co = output, ci = input; ci >= cin -> 0)
+//   dgrad: W[ci'][co'][8 - t]      (output = original input channel, input = original output)
+__global__ void k_pack(const float* W, int cin, int chunks, float4* wf, float4* wd) {
+    const int id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= 9 * chunks * 256) return;
+    const int lane = id & 63, nt = (id >> 6) & 3, g = (id >> 8) % chunks, t = (id >> 8) / chunks;
+    const int oc = nt * 16 + (lane & 15), ic0 = 16 * g + 4 * (lane >> 4);
+    float v[4], d[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ic = ic0 + j;
+        v[j] = ic < cin ? W[((size_t)oc * cin + ic) * 9 + t] : 0.0f;
+        d[j] = (wd && oc < cin) ? W[((size_t)ic * cin + oc) * 9 + (8 - t)] : 0.0f;
+    }
+    wf[id] = make_float4(v[0], v[1], v[2], v[3]);
+    if (wd) wd[id] = make_float4(d[0], d[1], d[2], d[3]);
+}
+
+}  // namespace tr
+
+using namespace tr;
+
+// ---- host trainer ---------------------------------------------------------------------------------
+struct Layout {
+    size_t cw[kMaxConv], cb[kMaxConv], bg[kMaxConv], bb[kMaxConv], brm[kMaxConv], brv[kMaxConv];
+    HeadOff h;
+    size_t total;
+};
+
+static Layout make_layout(int blocks) {  // weights.py canonical_layout / VarStore order
+    Layout L{};
+    size_t p = 0;
+    const int nconv = 1 + 2 * blocks;
+    for (int l = 0; l < nconv; ++l) {
+        const size_t cin = l == 0 ? kIn : kC;
+        L.cw[l] = p; p += kC * cin * 9;
+        L.cb[l] = p; p += kC;
+        L.bg[l] = p; p += kC;
+        L.bb[l] = p; p += kC;
+        L.brm[l] = p; p += kC;
+        L.brv[l] = p; p += kC;
+    }
+    HeadOff& h = L.h;
+    h.vcw = (int)p; p += 64;
+    h.vcb = (int)p; p += 1;
+    h.vg = (int)p; p += 1;
+    h.vb = (int)p; p += 1;
+    h.vrm = (int)p; p += 1;
+    h.vrv = (int)p; p += 1;
+    h.l1w = (int)p; p += 64 * 25;
+    h.l1b = (int)p; p += 64;
+    h.l2w = (int)p; p += 64;
+    h.l2b = (int)p; p += 1;
+    h.pcw = (int)p; p += 128;
+    h.pcb = (int)p; p += 2;
+    h.pg = (int)p; p += 2;
+    h.pb = (int)p; p += 2;
+    h.prm = (int)p; p += 2;
+    h.prv = (int)p; p += 2;
+    h.plw = (int)p; p += 2500;
+    h.plb = (int)p; p += 50;
+    L.total = p;
+    return L;
+}
+
+struct oaz_trainer {
+    oaz_train_config cfg{};
+    int device = 0;
+    hipStream_t own = nullptr, st = nullptr;
+    Layout L{};
+    int nconv = 0, maxB = 0;
+    size_t nparam = 0;
+    std::vector<void*> allocs;
+    float *P = nullptr, *G = nullptr, *MOM = nullptr;
+    uint8_t* mask = nullptr;
+    float4 *wf[kMaxConv] = {}, *wd[kMaxConv] = {};
+    float *X0 = nullptr, *Z[kMaxConv] = {}, *A[kMaxConv] = {}, *M[kMaxConv] = {}, *DZ = nullptr;
+    float *mean[kMaxConv] = {}, *invstd[kMaxConv] = {}, *bcoef = nullptr;  // bcoef: c1, mm, mx [3][64]
+    float *part = nullptr, *bpart = nullptr, *wpart = nullptr;
+    float *hz = nullptr, *g3 = nullptr, *hstat = nullptr;  // hstat: mean[3] invstd[3] c1[3] mm[3] mx[3]
+    float *hpart = nullptr, *hwpart = nullptr, *hlpart = nullptr, *hcpart = nullptr;
+    float *pi = nullptr, *z = nullptr;
+    const oaz_sample* samples = nullptr;
+    oaz_sample* owned_samples = nullptr;
+    size_t n_samples = 0, owned_cap = 0;
+    int32_t* idx = nullptr;
+    int n_batches = 0, batch = 0;
+    size_t idx_cap = 0;
+    double* loss_acc = nullptr;
+
+    template <class T>
+    int alloc(T*& p, size_t count) {
+        void* q = nullptr;
+        HIP_TRY(hipMalloc(&q, count * sizeof(T) + 16));
+        HIP_TRY(hipMemset(q, 0, count * sizeof(T) + 16));
+        allocs.push_back(q);
+        p = (T*)q;
+        return 0;
+    }
+    ~oaz_trainer() {
+        if (owned_samples) (void)hipFree(owned_samples);
+        if (idx) (void)hipFree(idx);
+        for (void* q : allocs) (void)hipFree(q);
+        if (own) (void)hipStreamDestroy(own);
+    }
+};
+
+extern "C" void oaz_train_config_default(oaz_train_config* c) {
+    if (!c) return;
+    memset(c, 0, sizeof(*c));
+    c->blocks = 5;
+    c->max_batch = 512;
+    c->learning_rate = 5e-3;
+    c->momentum = 0.9;
+    c->weight_decay = 1e-4;
+    c->bn_momentum = 0.1;
+    c->bn_eps = 1e-5;
+    c->value_loss_broadcast = 1;
+}
+
+extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int device) {
+    if (!cfg || cfg->blocks < 0 || cfg->blocks > 16 || cfg->max_batch < 16 || cfg->max_batch % 16 ||
+        cfg->max_batch > (1 << 16)) {
+        oaz_set_err(OAZ_ERR_ARG, "trainer: blocks in [0,16], max_batch a multiple of 16 in [16, 65536]");
+        return nullptr;
+    }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+        oaz_set_err(OAZ_ERR_NO_DEVICE, "trainer: no HIP device %d", device);
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        oaz_set_err(OAZ_ERR_NO_DEVICE, "trainer: hipSetDevice(%d) failed", device);
+        return nullptr;
+    }
+    oaz_trainer* t = new oaz_trainer();
+    t->cfg = *cfg;
+    t->device = device;
+    t->nconv = 1 + 2 * cfg->blocks;
+    t->maxB = cfg->max_batch;
+    t->L = make_layout(cfg->blocks);
+    t->nparam = t->L.total;
+    const size_t R = (size_t)t->maxB * 25;
+    auto fail = [&]() -> oaz_trainer* { delete t; return nullptr; };
+    if (hipStreamCreateWithFlags(&t->own, hipStreamNonBlocking) != hipSuccess) {
+        oaz_set_err(OAZ_ERR_HIP, "trainer: stream");
+        return fail();
+    }
+    t->st = t->own;
+    if (t->alloc(t->P, t->nparam) || t->alloc(t->G, t->nparam) || t->alloc(t->MOM, t->nparam) ||
+        t->alloc(t->mask, t->nparam))
+        return fail();
+    for (int l = 0; l < t->nconv; ++l) {
+        const int chunks = l == 0 ? 2 : 4;
+        if (t->alloc(t->wf[l], (size_t)9 * chunks * 256)) return fail();
+        if (l > 0 && t->alloc(t->wd[l], (size_t)9 * chunks * 256)) return fail();
+        if (t->alloc(t->Z[l], R * kC) || t->alloc(t->A[l], R * kC) || t->alloc(t->M[l], R * kC) ||
+            t->alloc(t->mean[l], 64) || t->alloc(t->invstd[l], 64))
+            return fail();
+    }
+    const size_t nwg_conv = R / 16;
+    if (t->alloc(t->X0, R * kInPad) || t->alloc(t->DZ, R * kC) || t->alloc(t->bcoef, 3 * 64) ||
+        t->alloc(t->part, nwg_conv * 128) || t->alloc(t->bpart, (R + 63) / 64 * 64) ||
+        t->alloc(t->wpart, (size_t)9 * 25 * 64 * 64) || t->alloc(t->hz, R * 4) || t->alloc(t->g3, R * 4) ||
+        t->alloc(t->hstat, 16) || t->alloc(t->hpart, ((R + 255) / 256 + (size_t)t->maxB / kHS + 1) * 8) ||
+        t->alloc(t->hwpart, ((size_t)t->maxB / kHS + 1) * kHeadW) ||
+        t->alloc(t->hlpart, ((size_t)t->maxB / kHS + 1) * 2) ||
+        t->alloc(t->hcpart, ((R + 63) / 64) * (size_t)kHConvW) || t->alloc(t->pi, (size_t)t->maxB * 50) ||
+        t->alloc(t->z, (size_t)t->maxB) || t->alloc(t->loss_acc, 4))
+        return fail();
+    std::vector<uint8_t> mask(t->nparam, 1);
+    for (int l = 0; l < t->nconv; ++l)
+        for (int c = 0; c < 64; ++c) mask[t->L.brm[l] + c] = mask[t->L.brv[l] + c] = 0;
+    mask[t->L.h.vrm] = mask[t->L.h.vrv] = 0;
+    mask[t->L.h.prm] = mask[t->L.h.prm + 1] = mask[t->L.h.prv] = mask[t->L.h.prv + 1] = 0;
+    if (hipMemcpy(t->mask, mask.data(), t->nparam, hipMemcpyHostToDevice) != hipSuccess) {
+        oaz_set_err(OAZ_ERR_HIP, "trainer: mask upload");
+        return fail();
+    }
+    return t;
+}
+
+extern "C" void oaz_trainer_destroy(oaz_trainer* t) {
+    if (!t) return;
+    (void)hipSetDevice(t->device);
+    (void)hipDeviceSynchronize();
+    delete t;
+}
+
+extern "C" int oaz_trainer_set_stream(oaz_trainer* t, void* stream) {
+    if (!t) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
+    t->st = stream ? (hipStream_t)stream : t->own;
+    return 0;
+}
+
+static int repack(oaz_trainer* t) {
+    for (int l = 0; l < t->nconv; ++l) {
+        const int chunks = l == 0 ? 2 : 4, cin = l == 0 ? kIn : kC;
+        const int n = 9 * chunks * 256;
+        hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, t->st, t->P + t->L.cw[l], cin, chunks,
+                           t->wf[l], t->wd[l]);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+extern "C" int oaz_trainer_set_weights(oaz_trainer* t, const float* blob, size_t n) {
+    if (!t || !blob || n != t->nparam) return oaz_set_err(OAZ_ERR_ARG, "trainer: need %zu floats", t ? t->nparam : 0);
+    HIP_TRY(hipSetDevice(t->device));
+    HIP_TRY(hipMemcpyAsync(t->P, blob, n * sizeof(float), hipMemcpyHostToDevice, t->st));
+    HIP_TRY(hipMemsetAsync(t->MOM, 0, n * sizeof(float), t->st));
+    if (int rc = repack(t)) return rc;
+    HIP_TRY(hipStreamSynchronize(t->st));
+    return 0;
+}
+
+extern "C" int oaz_trainer_get_weights(oaz_trainer* t, float* blob, size_t n) {
+    if (!t || !blob || n != t->nparam) return oaz_set_err(OAZ_ERR_ARG, "trainer: need %zu floats", t ? t->nparam : 0);
+    HIP_TRY(hipSetDevice(t->device));
+    HIP_TRY(hipMemcpyAsync(blob, t->P, n * sizeof(float), hipMemcpyDeviceToHost, t->st));
+    HIP_TRY(hipStreamSynchronize(t->st));
+    return 0;
+}
+
+extern "C" int oaz_trainer_load_samples(oaz_trainer* t, const oaz_sample* s, size_t n) {
+    if (!t || (!s && n)) return oaz_set_err(OAZ_ERR_ARG, "trainer: null samples");
+    HIP_TRY(hipSetDevice(t->device));
+    if (n > t->owned_cap) {
+        HIP_TRY(hipStreamSynchronize(t->st));
+        if (t->owned_samples) HIP_TRY(hipFree(t->owned_samples));
+        t->owned_samples = nullptr;
+        t->owned_cap = 0;
+        HIP_TRY(hipMalloc(&t->owned_samples, n * sizeof(oaz_sample)));
+        t->owned_cap = n;
+    }
+    if (n) HIP_TRY(hipMemcpyAsync(t->owned_samples, s, n * sizeof(oaz_sample), hipMemcpyHostToDevice, t->st));
+    HIP_TRY(hipStreamSynchronize(t->st));
+    t->samples = t->owned_samples;
+    t->n_samples = n;
+    return 0;
+}
+
+extern "C" int oaz_trainer_bind_device_samples(oaz_trainer* t, const oaz_sample* s, size_t n) {
+    if (!t || (!s && n)) return oaz_set_err(OAZ_ERR_ARG, "trainer: null samples");
+    t->samples = s;
+    t->n_samples = n;
+    return 0;
+}
+
+extern "C" int oaz_trainer_set_batches(oaz_trainer* t, const int32_t* idx, int n_batches, int batch) {
+    if (!t || !idx || n_batches < 0 || batch < 16 || batch % 16 || batch > t->maxB)
+        return oaz_set_err(OAZ_ERR_ARG, "trainer: batch must be a multiple of 16 in [16, %d]", t ? t->maxB : 0);
+    const size_t n = (size_t)n_batches * batch;
+    for (size_t i = 0; i < n; ++i)
+        if (idx[i] < 0 || (size_t)idx[i] >= t->n_samples)
+            return oaz_set_err(OAZ_ERR_ARG, "trainer: index %d out of range (%zu samples)", idx[i], t->n_samples);
+    HIP_TRY(hipSetDevice(t->device));
+    if (n > t->idx_cap) {
+        HIP_TRY(hipStreamSynchronize(t->st));
+        if (t->idx) HIP_TRY(hipFree(t->idx));
+        t->idx = nullptr;
+        t->idx_cap = 0;
+        HIP_TRY(hipMalloc(&t->idx, n * sizeof(int32_t)));
+        t->idx_cap = n;
+    }
+    if (n) HIP_TRY(hipMemcpyAsync(t->idx, idx, n * sizeof(int32_t), hipMemcpyHostToDevice, t->st));
+    HIP_TRY(hipStreamSynchronize(t->st));
+    t->n_batches = n_batches;
+    t->batch = batch;
+    return 0;
+}
+
+static int backward(oaz_trainer* t, int bi) {
+    const int B = t->batch, R = B * 25, NB = t->cfg.blocks, nl = t->nconv;
+    const Layout& L = t->L;
+    const HeadOff& h = L.h;
+    hipStream_t st = t->st;
+    float* P = t->P;
+    float* G = t->G;
+    const float bn_mom = (float)t->cfg.bn_momentum, eps = (float)t->cfg.bn_eps;
+    const int nwg_conv = R / 16;
+    const dim3 conv_grid(B / 16, 25);
+    hipLaunchKernelGGL(k_gather, dim3((R + 255) / 256), dim3(256), 0, st, t->samples, t->idx + (size_t)bi * B, B,
+                       t->X0, t->pi, t->z);
+    // ---- forward
+    for (int l = 0; l < nl; ++l) {
+        ConvArgs a{};
+        a.in = l == 0 ? t->X0 : t->A[l - 1];
+        a.w = t->wf[l];
+        a.bias = P + L.cb[l];
+        a.out = t->Z[l];
+        a.part = t->part;
+        a.chunks = l == 0 ? 2 : 4;
+        a.B = B;
+        hipLaunchKernelGGL(k_conv<CONV_FWD>, conv_grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(256), 0, st, t->part, nwg_conv, 64, 0, 64, (double)R,
+                           P + L.brm[l], P + L.brv[l], bn_mom, eps, t->mean[l], t->invstd[l]);
+        const float* skip = (l >= 2 && l % 2 == 0) ? t->A[l - 2] : nullptr;  // block output adds the block input
+        const long long n = (long long)R * kC;
+        hipLaunchKernelGGL(k_bn_act, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, t->Z[l], t->mean[l],
+                           t->invstd[l], P + L.bg[l], P + L.bb[l], skip, t->A[l], n);
+    }
+    (void)NB;
+    // ---- heads
+    const float* AL = t->A[nl - 1];
+    const int nwg_hc = (R + 255) / 256;
+    hipLaunchKernelGGL(k_head_conv, dim3(nwg_hc), dim3(256), 0, st, AL, P, h, t->hz, t->hpart, R);
+    float* hmean = t->hstat;
+    float* hinv = t->hstat + 3;
+    float* hc1 = t->hstat + 6;
+    float* hmm = t->hstat + 9;
+    float* hmx = t->hstat + 12;
+    hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(256), 0, st, t->hpart, nwg_hc, 4, 0, 1, (double)R,
+                       P + h.vrm, P + h.vrv, bn_mom, eps, hmean, hinv);
+    hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(256), 0, st, t->hpart, nwg_hc, 4, 1, 2, (double)R,
+                       P + h.prm, P + h.prv, bn_mom, eps, hmean + 1, hinv + 1);
+    const int nwg_hs = (B + kHS - 1) / kHS;
+    float* hbpart = t->hpart + (size_t)nwg_hc * 8;
+    hipLaunchKernelGGL(k_head_sample, dim3(nwg_hs), dim3(kHS), 0, st, t->hz, hmean, hinv, P, h, t->pi, t->z, B,
+                       t->cfg.value_loss_broadcast, t->g3, hbpart, t->hwpart, t->hlpart);
+    hipLaunchKernelGGL(k_loss_acc, dim3(1), dim3(64), 0, st, t->hlpart, nwg_hs, t->loss_acc);
+    hipLaunchKernelGGL(k_colsum, dim3((kHeadVW + 255) / 256), dim3(256), 0, st, t->hwpart, nwg_hs, kHeadW, 0,
+                       kHeadVW, G + h.l1w);
+    hipLaunchKernelGGL(k_colsum, dim3((2550 + 255) / 256), dim3(256), 0, st, t->hwpart, nwg_hs, kHeadW, kHeadVW,
+                       2550, G + h.plw);
+    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(256), 0, st, hbpart, nwg_hs, 4, 0, 1, (double)R, P + h.vg,
+                       hinv, G + h.vg, G + h.vb, hc1, hmm, hmx);
+    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(256), 0, st, hbpart, nwg_hs, 4, 1, 2, (double)R, P + h.pg,
+                       hinv + 1, G + h.pg, G + h.pb, hc1 + 1, hmm + 1, hmx + 1);
+    const int nwg_rows = (R + 63) / 64;
+    hipLaunchKernelGGL(k_head_bwd_rows, dim3(nwg_rows), dim3(256), 0, st, AL, t->Z[nl - 1], t->mean[nl - 1],
+                       t->invstd[nl - 1], t->hz, t->g3, hmean, hinv, hc1, hmm, hmx, P, h, t->M[nl - 1], t->part,
+                       t->hcpart, R);
+    hipLaunchKernelGGL(k_colsum, dim3(1), dim3(256), 0, st, t->hcpart, nwg_rows, kHConvW, 0, 65, G + h.vcw);
+    hipLaunchKernelGGL(k_colsum, dim3(1), dim3(256), 0, st, t->hcpart, nwg_rows, kHConvW, 65, 130, G + h.pcw);
+    // ---- trunk backward; t->part holds the BN-backward partials of layer l (nwg, [2][64])
+    int nwg_part = nwg_rows;
+    for (int l = nl - 1; l >= 0; --l) {
+        float* c1 = t->bcoef;
+        float* mm = t->bcoef + 64;
+        float* mx = t->bcoef + 128;
+        hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(256), 0, st, t->part, nwg_part, 64, 0, 64, (double)R,
+                           P + L.bg[l], t->invstd[l], G + L.bg[l], G + L.bb[l], c1, mm, mx);
+        hipLaunchKernelGGL(k_bn_bwd_apply, dim3(nwg_rows), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
+                           t->invstd[l], c1, mm, mx, t->DZ, t->bpart, R);
+        const float* X = l == 0 ? t->X0 : t->A[l - 1];
+        if (l == 0)
+            hipLaunchKernelGGL(k_wgrad<2>, dim3(25, 9), dim3(256), 0, st, t->DZ, X, B, t->wpart);
+        else
+            hipLaunchKernelGGL(k_wgrad<4>, dim3(25, 9), dim3(256), 0, st, t->DZ, X, B, t->wpart);
+        const int cin = l == 0 ? kIn : kC;
+        const int nred = 9 * kC * cin;
+        hipLaunchKernelGGL(k_wgrad_reduce, dim3((nred + 255) / 256), dim3(256), 0, st, t->wpart,
+                           l == 0 ? kInPad : kC, cin, t->bpart, nwg_rows, G + L.cw[l], G + L.cb[l]);
+        if (l == 0) break;
+        ConvArgs a{};
+        a.in = t->DZ;
+        a.w = t->wd[l];
+        a.out = t->M[l - 1];
+        a.part = t->part;
+        a.act = t->A[l - 1];
+        a.zprev = t->Z[l - 1];
+        a.mean = t->mean[l - 1];
+        a.invstd = t->invstd[l - 1];
+        a.skip = (l % 2 == 1) ? t->M[l + 1] : nullptr;  // first conv of a block: add the block-output gradient
+        a.chunks = 4;
+        a.B = B;
+        hipLaunchKernelGGL(k_conv<CONV_DGRAD>, conv_grid, dim3(256), 0, st, a);
+        nwg_part = nwg_conv;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+extern "C" int oaz_trainer_backward(oaz_trainer* t, int b) {
+    if (!t) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
+    if (!t->samples || b < 0 || b >= t->n_batches) return oaz_set_err(OAZ_ERR_STATE, "trainer: batch %d not uploaded", b);
+    HIP_TRY(hipSetDevice(t->device));
+    return backward(t, b);
+}
+
+extern "C" int oaz_trainer_grads(oaz_trainer* t, float** dev, size_t* n) {
+    if (!t || !dev || !n) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
+    *dev = t->G;
+    *n = t->nparam;
+    return 0;
+}
+
+extern "C" int oaz_trainer_get_grads(oaz_trainer* t, float* host, size_t n) {
+    if (!t || !host || n != t->nparam) return oaz_set_err(OAZ_ERR_ARG, "trainer: need %zu floats", t ? t->nparam : 0);
+    HIP_TRY(hipSetDevice(t->device));
+    HIP_TRY(hipMemcpyAsync(host, t->G, n * sizeof(float), hipMemcpyDeviceToHost, t->st));
+    HIP_TRY(hipStreamSynchronize(t->st));
+    return 0;
+}
+
+static int apply(oaz_trainer* t, float scale) {
+    const long long n = (long long)t->nparam;
+    hipLaunchKernelGGL(k_sgd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, t->st, t->P, t->G, t->MOM, t->mask, n,
+                       (float)t->cfg.learning_rate, (float)t->cfg.momentum, (float)t->cfg.weight_decay, scale);
+    HIP_TRY(hipGetLastError());
+    return repack(t);
+}
+
+extern "C" int oaz_trainer_apply(oaz_trainer* t, float grad_scale) {
+    if (!t) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
+    HIP_TRY(hipSetDevice(t->device));
+    return apply(t, grad_scale);
+}
+
+extern "C" int oaz_trainer_train(oaz_trainer* t, int first, int count) {
+    if (!t) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
+    if (!t->samples || first < 0 || count < 0 || first + count > t->n_batches)
+        return oaz_set_err(OAZ_ERR_STATE, "trainer: batches [%d, %d) not uploaded", first, first + count);
+    HIP_TRY(hipSetDevice(t->device));
+    for (int b = first; b < first + count; ++b) {
+        if (int rc = backward(t, b)) return rc;
+        if (int rc = apply(t, 1.0f)) return rc;
+    }
+    return 0;
+}
+
+extern "C" int oaz_trainer_losses(oaz_trainer* t, double out[3]) {
+    if (!t || !out) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
+    HIP_TRY(hipSetDevice(t->device));
+    HIP_TRY(hipMemcpyAsync(out, t->loss_acc, 3 * sizeof(double), hipMemcpyDeviceToHost, t->st));
+    HIP_TRY(hipMemsetAsync(t->loss_acc, 0, 3 * sizeof(double), t->st));
+    HIP_TRY(hipStreamSynchronize(t->st));
+    return 0;
+}
+
+extern "C" int oaz_trainer_sync(oaz_trainer* t) {
+    if (!t) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
+    HIP_TRY(hipSetDevice(t->device));
+    HIP_TRY(hipStreamSynchronize(t->st));
+    return 0;
+}

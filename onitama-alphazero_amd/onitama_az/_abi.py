@@ -125,6 +125,20 @@ class oaz_kernel_times(C.Structure):
     ]
 
 
+class oaz_train_config(C.Structure):
+    _fields_ = [
+        ("blocks", C.c_int32),
+        ("max_batch", C.c_int32),
+        ("learning_rate", C.c_double),
+        ("momentum", C.c_double),
+        ("weight_decay", C.c_double),
+        ("bn_momentum", C.c_double),
+        ("bn_eps", C.c_double),
+        ("value_loss_broadcast", C.c_int32),
+        ("reserved", C.c_int32 * 7),
+    ]
+
+
 assert C.sizeof(oaz_state) == 24
 assert C.sizeof(oaz_move) == 4
 assert C.sizeof(oaz_node) == 32
@@ -176,6 +190,22 @@ _PROTOS = {
     "oaz_samples_fetch": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t, _P(C.c_size_t)]),
     "oaz_samples_export_device": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t, _P(C.c_size_t)]),
     "oaz_selfplay_run": (C.c_int, [_VOIDP, C.c_int, _VOIDP, C.c_size_t, _P(C.c_size_t), _P(oaz_selfplay_stats)]),
+    "oaz_train_config_default": (None, [_P(oaz_train_config)]),
+    "oaz_trainer_create": (_VOIDP, [_P(oaz_train_config), C.c_int]),
+    "oaz_trainer_destroy": (None, [_VOIDP]),
+    "oaz_trainer_set_stream": (C.c_int, [_VOIDP, _VOIDP]),
+    "oaz_trainer_set_weights": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
+    "oaz_trainer_get_weights": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
+    "oaz_trainer_load_samples": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
+    "oaz_trainer_bind_device_samples": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
+    "oaz_trainer_set_batches": (C.c_int, [_VOIDP, _VOIDP, C.c_int, C.c_int]),
+    "oaz_trainer_backward": (C.c_int, [_VOIDP, C.c_int]),
+    "oaz_trainer_grads": (C.c_int, [_VOIDP, _P(C.c_void_p), _P(C.c_size_t)]),
+    "oaz_trainer_get_grads": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
+    "oaz_trainer_apply": (C.c_int, [_VOIDP, C.c_float]),
+    "oaz_trainer_train": (C.c_int, [_VOIDP, C.c_int, C.c_int]),
+    "oaz_trainer_losses": (C.c_int, [_VOIDP, _P(C.c_double * 3)]),
+    "oaz_trainer_sync": (C.c_int, [_VOIDP]),
 }
 
 EXPORTED_SYMBOLS = tuple(_PROTOS)
