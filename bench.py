@@ -65,6 +65,10 @@ def parse():
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--mode", default="selfplay", choices=["selfplay", "train"],
+                    help="train: SGD steps of the training loop (SURVEY 8f #2), not the headline metric")
+    ap.add_argument("--train-blocks", type=int, default=5, help="train mode: residual blocks (bin/train.rs:60)")
+    ap.add_argument("--train-batch", type=int, default=512, help="train mode: global batch (train.rs:142)")
     return ap.parse_args()
 
 
@@ -120,6 +124,131 @@ def cpu_baseline(cfg, seconds, threads):
                       f"{plies} plies, {games} games finished"}
 
 
+TRAIN_METRIC = "training samples/sec (SGD steps of batch 512, forward(train) + alphaloss + backward + SGD)"
+
+
+def train_flop_per_sample(blocks):
+    """forward + input-gradient + weight-gradient dense FLOPs (3x forward, minus the first
+    layer's unneeded input gradient)."""
+    fwd = FLOP_PER_SIM[blocks] if blocks in FLOP_PER_SIM else 11_681_928 + (blocks - 3) * 3_686_400
+    return 3 * fwd - 2 * 25 * 9 * 21 * 64
+
+
+def train_cpu_baseline(blocks, batch, seconds, threads):
+    """The reference trains on the CPU through tch (train.rs:163 `Device::Cpu`): the same op graph
+    (oracle/train_ref.py) in fp32 ATen on `threads` host threads, batch 512."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
+    from train_ref import alphaloss, forward
+    from onitama_az.weights import named_from_blob, random_weights
+    torch.set_num_threads(threads)
+    named = {k: torch.tensor(v, requires_grad=not k.endswith(("running_mean", "running_var")))
+             for k, v in named_from_blob(random_weights(0, blocks), blocks).items()}
+    params = [t for k, t in named.items() if t.requires_grad]
+    opt = torch.optim.SGD(params, lr=5e-3, momentum=0.9, weight_decay=1e-4)
+    rng = np.random.default_rng(0)
+    x = torch.tensor((rng.random((batch, 21, 5, 5)) < 0.3).astype(np.float32))
+    pi = torch.softmax(torch.tensor(rng.normal(size=(batch, 2, 25)).astype(np.float32)).reshape(batch, 50), -1)
+    z = torch.tensor(rng.integers(-1, 2, batch).astype(np.float32))
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds or steps < 2:
+        opt.zero_grad()
+        p, v = forward(named, x, blocks, train=True)
+        lv, lp = alphaloss(v, p, pi.reshape(batch, 2, 25), z)
+        (lv + lp).backward()
+        opt.step()
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": steps * batch / dt, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} SGD steps of batch {batch} in {dt:.1f}s: fp32 ATen on {threads} host threads "
+                      f"(oracle/train_ref.py op graph = net.rs forward(train) + alphaloss + tch SGD), {blocks}-block"}
+
+
+def train_main(args, world, rank, local):
+    import numpy as np
+    from onitama_az import _abi
+    from onitama_az.game import initial_state_np
+    from onitama_az.trainer import Trainer, _DeviceArray, choose_batches
+    from onitama_az.weights import random_weights
+    blocks, B = args.train_blocks, args.train_batch
+    assert B % world == 0 and (B // world) % 16 == 0, "per-rank batch must be a multiple of 16"
+    shard = B // world
+    lib = _abi.load()
+    n_samples = 65536
+    rng = np.random.default_rng(rank)
+    deals = np.zeros((n_samples, 5), dtype=np.uint8)
+    for g in range(n_samples):  # seeded 5-of-16 deals, as the self-play engine deals them
+        import ctypes as C
+        d = (C.c_uint8 * 5)()
+        lib.oaz_deal_deck(C.c_uint64(20260101), C.c_uint64(g), d)
+        deals[g] = list(d)
+    samples = np.zeros(n_samples, dtype=_abi.SAMPLE_DTYPE)
+    samples["state"] = np.concatenate([initial_state_np(deals[g]) for g in range(n_samples)])
+    pi = rng.random((n_samples, 50)).astype(np.float32)
+    samples["pi"] = pi / pi.sum(1, keepdims=True)
+    samples["z"] = rng.integers(-1, 2, n_samples).astype(np.float32)
+    tr = Trainer(blocks=blocks, max_batch=shard, device=local)
+    tr.set_weights(random_weights(0, blocks))
+    tr.set_stream(torch.cuda.current_stream().cuda_stream)
+    tr.load_samples(samples)
+    nb = args.warmup + args.steps
+    idx = choose_batches(np.random.default_rng(1), n_samples, B, nb)[:, rank * shard:(rank + 1) * shard]
+    tr.set_batches(idx)
+    grads = None
+    if world > 1:
+        ptr, n = tr.grads_device()
+        grads = torch.as_tensor(_DeviceArray(ptr, n), device=f"cuda:{local}")
+
+    def step(b):
+        if world > 1:
+            tr.backward(b)
+            dist.all_reduce(grads)
+            tr.apply(1.0 / world)
+        else:
+            tr.train(b, 1)
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        tr.sync()
+        if world > 1:
+            dist.barrier()
+
+    for b in range(args.warmup):
+        step(b)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for b in range(args.warmup, nb):
+        step(b)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    T = float(tmax.item())
+    v, p, k = tr.losses()
+    if rank == 0:
+        fl = train_flop_per_sample(blocks) * shard
+        ms = 1e3 * T / args.steps
+        achieved = fl / (ms * 1e-3) / 1e12
+        out = {"metric": TRAIN_METRIC, "value": B * args.steps / T, "unit": "samples/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+               "data": "synthetic (seeded deals, random pi/z, random-init weights seed 0)",
+               "config": {"workload": f"train: {blocks}-block ResNet, global batch {B}, lr 5e-3, momentum 0.9, "
+                                      f"wd 1e-4", "parallelism": f"dp{world} (RCCL all-reduce of gradients)"},
+               "mean_losses": {"value": v / max(1, k), "policy": p / max(1, k)},
+               "roofline": {"bound": "mfma", "kernel": "whole SGD step (conv fwd/dgrad/wgrad on v_mfma_f32_16x16x4_f32)",
+                            "achieved": achieved, "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
+                            "frac": achieved / PEAK_TFLOPS["fp32"], "traffic": None,
+                            "flop_per_step_per_gpu": fl}}
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = train_cpu_baseline(blocks, B, args.cpu_seconds, args.cpu_threads or min(16, os.cpu_count() or 1))
+        print(json.dumps(out), flush=True)
+    tr.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,6 +257,8 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.mode == "train":
+        return train_main(args, world, rank, local)
     from onitama_az import _abi
     from onitama_az.engine import Engine
     from onitama_az.weights import random_weights

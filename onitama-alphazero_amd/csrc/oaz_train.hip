@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -59,12 +60,18 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // ---- gather: create_tensor_from_state (common.rs:26-80) for samples[idx[b]] ----------------------
+// threads [0, R): one input row (square, sample); [R, R + 50B): pi; [R + 50B, R + 51B): z
 __global__ void k_gather(const oaz_sample* samples, const int32_t* idx, int B, float* X0, float* pi, float* z) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= B * 25) return;
+    const int R = B * 25;
+    if (t >= R) {
+        const int u = t - R;
+        if (u < B * 50) pi[u] = samples[idx[u / 50]].pi[u % 50];
+        else if (u < B * 51) z[u - B * 50] = samples[idx[u - B * 50]].z;
+        return;
+    }
     const int b = t % B, sq = t / B;
-    const oaz_sample* s = samples + idx[b];
-    const oaz_state st = s->state;
+    const oaz_state st = samples[idx[b]].state;
     const int color = st.to_move & 1;
     const uint32_t bit = sq_bit(sq);
     float* row = X0 + (size_t)(sq * B + b) * kInPad;
@@ -81,10 +88,6 @@ __global__ void k_gather(const oaz_sample* samples, const int32_t* idx, int B, f
     v[20] = color == OAZ_BLUE ? 1.0f : 0.0f;
 #pragma unroll
     for (int c = 0; c < kInPad; c += 4) *reinterpret_cast<float4*>(row + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
-    if (sq == 0) {
-        for (int k = 0; k < 50; ++k) pi[b * 50 + k] = s->pi[k];
-        z[b] = s->z;
-    }
 }
 
 // ---- 3x3 conv (forward, and dgrad on flipped weights) ------------------------------------------
@@ -105,58 +108,114 @@ struct ConvArgs {
     int B;
 };
 
-template <int MODE>
+// Workgroup = 64 rows (4 sample tiles of 16, one per wave) of one square x all 64 output
+// channels. Per on-board tap the tap's packed weights (CH x 4 n-tiles x 64 lanes float4 = 16 KB
+// for 64 input channels) are staged once in LDS (double-buffered) and shared by the 4 waves;
+// each wave keeps 4 accumulators (one per 16-channel n-tile), so an A fragment feeds 4 MFMAs.
+template <int MODE, int CH, int RG>  // CH = input channels / 16; RG = 16-row groups per workgroup
 __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
-    const int sq = blockIdx.y, b0 = blockIdx.x * 16, B = a.B;
-    const int rs = 16 * a.chunks;
-    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int t = 0; t < 9; ++t) {
-        const int nb = nbr(sq, t);
-        if (nb < 0) continue;
-        const float* base = a.in + (size_t)(nb * B + b0 + i) * rs + 4 * kq;
-        const float4* wt = a.w + (size_t)t * a.chunks * 256 + wave * 64 + lane;
-        for (int g = 0; g < a.chunks; ++g) {
-            const float4 av = *reinterpret_cast<const float4*>(base + 16 * g);
-            const float4 bv = wt[g * 256];
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
+    constexpr int NPW = RG;  // n-tiles per wave: 4 waves = RG row groups x (4 / RG) channel splits
+    __shared__ float4 sw[2][CH * 256];
+    __shared__ float red[RG][2][64];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, kq = lane >> 4;
+    const int rg = wave % RG, n0 = (wave / RG) * NPW;
+    const int sq = blockIdx.y, B = a.B, b0 = blockIdx.x * 16 * RG + rg * 16;
+    const bool active = b0 < B;  // B is a multiple of 16
+    constexpr int rs = 16 * CH;
+    f32x4 acc[NPW];
+#pragma unroll
+    for (int n = 0; n < NPW; ++n) acc[n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    // Software pipeline over the on-board taps: the next tap's weights and A fragments are loaded
+    // into registers while the current tap's MFMAs run; weights go through a double-buffered LDS.
+    // Inactive waves (sample tile past B) load the first tile and discard their results, so the
+    // loads and MFMAs stay unconditional and the prefetch registers stay in VGPRs.
+    const int bl = active ? b0 : 0;
+    float4 wr[CH], av[CH], an[CH];
+    int t = 0;
+    while (nbr(sq, t) < 0) ++t;
+    {
+        const float4* wt = a.w + (size_t)t * CH * 256;
+#pragma unroll
+        for (int k = 0; k < CH; ++k) sw[0][k * 256 + tid] = wt[k * 256 + tid];
+        const float* base = a.in + (size_t)(nbr(sq, t) * B + bl + i) * rs + 4 * kq;
+#pragma unroll
+        for (int g = 0; g < CH; ++g) av[g] = *reinterpret_cast<const float4*>(base + 16 * g);
+    }
+    __syncthreads();
+    for (int cur = 0; t < 9; cur ^= 1) {
+        int tn = t + 1;
+        while (tn < 9 && nbr(sq, tn) < 0) ++tn;
+        const int tl = tn < 9 ? tn : t;  // after the last tap: a harmless reload
+        {
+            const float4* wt = a.w + (size_t)tl * CH * 256;
+#pragma unroll
+            for (int k = 0; k < CH; ++k) wr[k] = wt[k * 256 + tid];
+            const float* base = a.in + (size_t)(nbr(sq, tl) * B + bl + i) * rs + 4 * kq;
+#pragma unroll
+            for (int g = 0; g < CH; ++g) an[g] = *reinterpret_cast<const float4*>(base + 16 * g);
         }
+#pragma unroll
+        for (int g = 0; g < CH; ++g)
+#pragma unroll
+            for (int n = 0; n < NPW; ++n) {
+                const float4 bv = sw[cur][(g * 4 + n0 + n) * 64 + lane];
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].x, bv.x, acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].y, bv.y, acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].z, bv.z, acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].w, bv.w, acc[n], 0, 0, 0);
+            }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) sw[cur ^ 1][k * 256 + tid] = wr[k];
+#pragma unroll
+        for (int g = 0; g < CH; ++g) av[g] = an[g];
+        __syncthreads();
+        t = tn;
     }
     // C/D layout: reg r of lane l = (row 4*(l>>4) + r, col l&15)
-    const int co = wave * 16 + i;
-    float s1 = 0.0f, s2 = 0.0f;
-    if (MODE == CONV_FWD) {
-        const float bb = a.bias[co];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const size_t o = (size_t)(sq * B + b0 + kq * 4 + r) * kC + co;
-            const float v = acc[r] + bb;
-            a.out[o] = v;
-            s1 += v;
-            s2 += v * v;
+    for (int n = 0; n < NPW; ++n) {
+        const int co = (n0 + n) * 16 + i;
+        float s1 = 0.0f, s2 = 0.0f;
+        if (active) {
+            if (MODE == CONV_FWD) {
+                const float bb = a.bias[co];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const size_t o = (size_t)(sq * B + b0 + kq * 4 + r) * kC + co;
+                    const float v = acc[n][r] + bb;
+                    a.out[o] = v;
+                    s1 += v;
+                    s2 += v * v;
+                }
+            } else {
+                const float mu = a.mean[co], is = a.invstd[co];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const size_t o = (size_t)(sq * B + b0 + kq * 4 + r) * kC + co;
+                    float d = acc[n][r];
+                    if (a.skip) d += a.skip[o];
+                    const float m = a.act[o] > 0.0f ? d : 0.0f;
+                    a.out[o] = m;
+                    s1 += m;
+                    s2 += m * ((a.zprev[o] - mu) * is);
+                }
+            }
         }
-    } else {
-        const float mu = a.mean[co], is = a.invstd[co];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const size_t o = (size_t)(sq * B + b0 + kq * 4 + r) * kC + co;
-            float d = acc[r];
-            if (a.skip) d += a.skip[o];
-            const float m = a.act[o] > 0.0f ? d : 0.0f;
-            a.out[o] = m;
-            s1 += m;
-            s2 += m * ((a.zprev[o] - mu) * is);
+        s1 = wave_sum16(s1);
+        s2 = wave_sum16(s2);
+        if (kq == 0) {
+            red[rg][0][co] = s1;
+            red[rg][1][co] = s2;
         }
     }
-    s1 = wave_sum16(s1);
-    s2 = wave_sum16(s2);
-    if (kq == 0) {
+    __syncthreads();
+    if (tid < 128) {
+        const int k = tid >> 6, c = tid & 63;
         const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-        a.part[wg * 128 + co] = s1;
-        a.part[wg * 128 + 64 + co] = s2;
+        float v = 0.0f;
+#pragma unroll
+        for (int r = 0; r < RG; ++r) v += red[r][k][c];
+        a.part[wg * 128 + tid] = v;
     }
 }
 
@@ -164,22 +223,38 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
 // part [nwg][2][pstride] (sum, sumsq) columns coff..coff+C-1; torch batch_norm(training=True):
 // y = (x - mean) * invstd * gamma + beta, invstd = 1/sqrt(var_biased + eps);
 // running = (1 - m) * running + m * {mean, var_unbiased}.
-__global__ void k_bn_fwd_fin(const float* part, int nwg, int pstride, int coff, int C, double N,
+__global__ __launch_bounds__(1024) void k_bn_fwd_fin(const float* part, int nwg, int pstride, int coff, int C, double N,
                              float* rmean, float* rvar, float bn_mom, float eps, float* mean, float* invstd) {
-    __shared__ double sh[2][4][64];
+    __shared__ double sh[2][16][64];
     const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
     double s1 = 0.0, s2 = 0.0;
-    if (c < C)
-        for (int w = q; w < nwg; w += 4) {
-            s1 += part[(size_t)w * 2 * pstride + coff + c];
-            s2 += part[(size_t)w * 2 * pstride + pstride + coff + c];
+    if (c < C) {
+        double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
+        int w = q;
+        for (; w + 48 < nwg; w += 64) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                a1[u] += part[(size_t)(w + 16 * u) * 2 * pstride + coff + c];
+                a2[u] += part[(size_t)(w + 16 * u) * 2 * pstride + pstride + coff + c];
+            }
         }
+        for (; w < nwg; w += 16) {
+            a1[0] += part[(size_t)w * 2 * pstride + coff + c];
+            a2[0] += part[(size_t)w * 2 * pstride + pstride + coff + c];
+        }
+        s1 = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+        s2 = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+    }
     sh[0][q][c] = s1;
     sh[1][q][c] = s2;
     __syncthreads();
     if (q == 0 && c < C) {
-        s1 = sh[0][0][c] + sh[0][1][c] + sh[0][2][c] + sh[0][3][c];
-        s2 = sh[1][0][c] + sh[1][1][c] + sh[1][2][c] + sh[1][3][c];
+        s1 = 0.0;
+        s2 = 0.0;
+        for (int k = 0; k < 16; ++k) {
+            s1 += sh[0][k][c];
+            s2 += sh[1][k][c];
+        }
         const double mu = s1 / N;
         double var = s2 / N - mu * mu;
         if (var < 0.0) var = 0.0;
@@ -211,23 +286,39 @@ __global__ void k_bn_act(const float* Z, const float* mean, const float* invstd,
 }
 
 // ---- BN backward finalisation: dgamma = sum m*xhat, dbeta = sum m; dx coefficients -----------------
-__global__ void k_bn_bwd_fin(const float* part, int nwg, int pstride, int coff, int C, double N,
+__global__ __launch_bounds__(1024) void k_bn_bwd_fin(const float* part, int nwg, int pstride, int coff, int C, double N,
                              const float* gamma, const float* invstd, float* ggamma, float* gbeta,
                              float* c1, float* mm, float* mx) {
-    __shared__ double sh[2][4][64];
+    __shared__ double sh[2][16][64];
     const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
     double s1 = 0.0, s2 = 0.0;
-    if (c < C)
-        for (int w = q; w < nwg; w += 4) {
-            s1 += part[(size_t)w * 2 * pstride + coff + c];
-            s2 += part[(size_t)w * 2 * pstride + pstride + coff + c];
+    if (c < C) {
+        double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
+        int w = q;
+        for (; w + 48 < nwg; w += 64) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                a1[u] += part[(size_t)(w + 16 * u) * 2 * pstride + coff + c];
+                a2[u] += part[(size_t)(w + 16 * u) * 2 * pstride + pstride + coff + c];
+            }
         }
+        for (; w < nwg; w += 16) {
+            a1[0] += part[(size_t)w * 2 * pstride + coff + c];
+            a2[0] += part[(size_t)w * 2 * pstride + pstride + coff + c];
+        }
+        s1 = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+        s2 = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+    }
     sh[0][q][c] = s1;
     sh[1][q][c] = s2;
     __syncthreads();
     if (q == 0 && c < C) {
-        s1 = sh[0][0][c] + sh[0][1][c] + sh[0][2][c] + sh[0][3][c];
-        s2 = sh[1][0][c] + sh[1][1][c] + sh[1][2][c] + sh[1][3][c];
+        s1 = 0.0;
+        s2 = 0.0;
+        for (int k = 0; k < 16; ++k) {
+            s1 += sh[0][k][c];
+            s2 += sh[1][k][c];
+        }
         gbeta[c] = (float)s1;
         ggamma[c] = (float)s2;
         c1[c] = gamma[c] * invstd[c];
@@ -245,61 +336,121 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* M, const floa
     const int r0 = blockIdx.x * 64;
     const float mu = mean[c], is = invstd[c], k1 = c1[c], k2 = mm[c], k3 = mx[c];
     float s = 0.0f;
-    for (int r = r0 + q; r < min(r0 + 64, R); r += 4) {
-        const size_t o = (size_t)r * kC + c;
-        const float xh = (Z[o] - mu) * is;
-        const float d = k1 * (M[o] - k2 - xh * k3);
-        dZ[o] = d;
-        s += d;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int r = r0 + q + 4 * u;
+        if (r < R) {
+            const size_t o = (size_t)r * kC + c;
+            const float xh = (Z[o] - mu) * is;
+            const float d = k1 * (M[o] - k2 - xh * k3);
+            dZ[o] = d;
+            s += d;
+        }
     }
     sh[q][c] = s;
     __syncthreads();
     if (q == 0) part[(size_t)blockIdx.x * 64 + c] = sh[0][c] + sh[1][c] + sh[2][c] + sh[3][c];
 }
 
-// ---- weight gradient: per (tap, square) partial D[co][ci] = sum_b dZ[sq,b][co] * X[nbr,b][ci] ------
-template <int NCT>  // input channel tiles of 16 (4 for 64 channels, 2 for the padded 32)
+// ---- weight gradient: per (tap, square, row split z) partial D[co][ci] = sum_b dZ[sq,b][co] * X[nbr,b][ci]
+// v_mfma_f32_32x32x2_f32: lane l supplies A[m = l&31][k = l>>5] and B[k = l>>5][n = l&31], so one
+// k-pair = two rows, read as 128-B row segments. A wave owns the whole 64 x (32*NNT) tile (2 x NNT
+// accumulators); the 4 waves of a workgroup take interleaved row pairs and are summed in LDS.
+constexpr int kWSplit = 2;  // row splits per (tap, square)
+template <int NNT>  // input-channel tiles of 32 (2 for 64 channels, 1 for the padded 32)
 __global__ __launch_bounds__(256) void k_wgrad(const float* dZ, const float* X, int B, float* part) {
-    const int sq = blockIdx.x, t = blockIdx.y;
+    __shared__ float red[3][64 * 64];
+    const int sq = blockIdx.x, t = blockIdx.y, zs = blockIdx.z;
     const int nb = nbr(sq, t);
     if (nb < 0) return;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
-    const int xrs = NCT * 16;
-    f32x4 acc[NCT];
+    constexpr int xrs = 32 * NNT;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+    const int rows = B / kWSplit, r0 = zs * rows;
+    typedef float f32x16 __attribute__((ext_vector_type(16)));
+    f32x16 acc[2][NNT];
 #pragma unroll
-    for (int j = 0; j < NCT; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    const float* pa = dZ + (size_t)(sq * B + kq) * kC + wave * 16 + i;  // A[m = co][k = b]
-    const float* pb = X + (size_t)(nb * B + kq) * xrs + i;              // B[k = b][n = ci]
-    for (int b = 0; b < B; b += 4) {
-        const float av = pa[(size_t)b * kC];
+    for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int j = 0; j < NCT; ++j) {
-            const float bv = pb[(size_t)b * xrs + 16 * j];
-            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
+        for (int n = 0; n < NNT; ++n) acc[m][n] = f32x16{};
+    const float* pa = dZ + (size_t)(sq * B + r0 + h) * kC + c;
+    const float* pb = X + (size_t)(nb * B + r0 + h) * xrs + c;
+    float a[4][2], b[4][NNT], an[4][2], bn[4][NNT];
+    auto load = [&](int k, float (&aa)[4][2], float (&bb)[4][NNT]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int kk = k + 8 * u;
+            const bool ok = kk < rows;
+#pragma unroll
+            for (int m = 0; m < 2; ++m) aa[u][m] = ok ? pa[(size_t)kk * kC + 32 * m] : 0.0f;
+#pragma unroll
+            for (int n = 0; n < NNT; ++n) bb[u][n] = ok ? pb[(size_t)kk * xrs + 32 * n] : 0.0f;
+        }
+    };
+    load(2 * wave, a, b);
+    for (int k = 2 * wave; k < rows; k += 32) {  // 4 row pairs per iteration; next ones prefetched
+        if (k + 32 < rows) load(k + 32, an, bn);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int n = 0; n < NNT; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][m], b[u][n], acc[m][n], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int m = 0; m < 2; ++m) a[u][m] = an[u][m];
+#pragma unroll
+            for (int n = 0; n < NNT; ++n) b[u][n] = bn[u][n];
         }
     }
-    float* out = part + (size_t)(t * 25 + sq) * kC * xrs;
+    // D layout: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+    if (wave > 0) {
+        float* dst = red[wave - 1];
 #pragma unroll
-    for (int j = 0; j < NCT; ++j)
+        for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) out[(wave * 16 + kq * 4 + r) * xrs + 16 * j + i] = acc[j][r];
+            for (int n = 0; n < NNT; ++n)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    dst[row * xrs + 32 * n + c] = acc[m][n][r];
+                }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        float* out = part + ((size_t)(t * 25 + sq) * kWSplit + zs) * kC * xrs;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int n = 0; n < NNT; ++n)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int o = row * xrs + 32 * n + c;
+                    out[o] = acc[m][n][r] + red[0][o] + red[1][o] + red[2][o];
+                }
+    }
 }
 
-// grad_w[co][ci][tap] (canonical [co][cin][3][3]) = sum over on-board squares; grad_b = sum of dZ partials
-__global__ void k_wgrad_reduce(const float* part, int xrs, int cin, const float* bpart, int nbw,
-                               float* gw, float* gb) {
+// grad_w[co][ci][tap] (canonical [co][cin][3][3]) = sum over on-board squares and row splits.
+// Threads run ci-fastest so the partial reads coalesce.
+__global__ void k_wgrad_reduce(const float* part, int xrs, int cin, float* gw) {
     const int id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= 9 * kC * cin) return;
-    const int t = id % 9, ci = (id / 9) % cin, co = id / (9 * cin);
-    float s = 0.0f;
-    for (int sq = 0; sq < 25; ++sq)
-        if (nbr(sq, t) >= 0) s += part[((size_t)(t * 25 + sq) * kC + co) * xrs + ci];
-    gw[id] = s;
-    if (t == 0 && ci == 0) {
-        float sb = 0.0f;
-        for (int w = 0; w < nbw; ++w) sb += bpart[(size_t)w * 64 + co];
-        gb[co] = sb;
+    const int ci = id % cin, co = (id / cin) % kC, t = id / (cin * kC);
+    const float* p = part + ((size_t)t * 25 * kWSplit * kC + co) * xrs + ci;
+    float s[kWSplit] = {};
+#pragma unroll
+    for (int sq = 0; sq < 25; ++sq) {  // predicated, fully unrolled: all loads in flight
+        const bool ok = nbr(sq, t) >= 0;
+#pragma unroll
+        for (int zs = 0; zs < kWSplit; ++zs) s[zs] += ok ? p[(size_t)(sq * kWSplit + zs) * kC * xrs] : 0.0f;
     }
+    float tot = 0.0f;
+#pragma unroll
+    for (int zs = 0; zs < kWSplit; ++zs) tot += s[zs];
+    gw[((size_t)co * cin + ci) * 9 + t] = tot;
 }
 
 // ---- heads -------------------------------------------------------------------------------------
@@ -355,94 +506,129 @@ struct HeadStats {  // head BN batch statistics (channel 0 = value, 1..2 = polic
     float c1[3], mm[3], mx[3];
 };
 
-// One thread per sample: value MLP (25 -> 64 -> 1, tanh), policy linear (50 -> 50) + softmax,
-// alphaloss terms (net.rs:234-243) and their backward down to the head BN outputs.
+// Value MLP (25 -> 64 -> 1, tanh), policy linear (50 -> 50) + softmax, alphaloss terms
+// (net.rs:234-243) and their backward down to the head BN outputs. 16 lanes per sample (an
+// aligned 16-lane group: reductions are 4 xor-shuffles), 16 samples per workgroup.
 // Q16: with value_loss_broadcast the value loss is mean_{i,j} (z_j - v_i)^2 over [B,B].
-constexpr int kHS = 64;  // samples per workgroup
-__global__ __launch_bounds__(64) void k_head_sample(const float* hz, const float* hst_mean, const float* hst_inv,
-                                                    const float* P, HeadOff o, const float* pi, const float* z,
-                                                    int B, int broadcast, float* g3, float* part_bn,
-                                                    float* part_w, float* part_loss) {
-    __shared__ float lds[kHeadW + 254 * kHS];  // 82 KB (a workgroup may hold up to 160 KB)
-    float* W = lds;                        // kHeadW floats: l1w[64][25] l1b[64] l2w[64] l2b plw[50][50] plb[50]
-    float* hv = W + kHeadW;                // [25][kHS]
-    float* dh1 = hv + 25 * kHS;            // [64][kHS]
-    float* h1 = dh1 + 64 * kHS;            // [64][kHS]
-    float* hp = h1 + 64 * kHS;             // [50][kHS]
-    float* dl = hp + 50 * kHS;             // [50][kHS]
-    float* du = dl + 50 * kHS;             // [kHS]
-    const int lane = threadIdx.x;
-    for (int k = lane; k < kHeadVW; k += 64) W[k] = P[o.l1w + k];
-    for (int k = lane; k < 2550; k += 64) W[kHeadVW + k] = P[o.plw + k];
+constexpr int kHS = 16;  // samples per workgroup
+__device__ __forceinline__ float sum16(float v) {
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 8);
+    return v;
+}
+__device__ __forceinline__ float max16(float v) {
+    v = fmaxf(v, __shfl_xor(v, 1));
+    v = fmaxf(v, __shfl_xor(v, 2));
+    v = fmaxf(v, __shfl_xor(v, 4));
+    v = fmaxf(v, __shfl_xor(v, 8));
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_head_sample(const float* hz, const float* hst_mean, const float* hst_inv,
+                                                     const float* P, HeadOff o, const float* pi, const float* z,
+                                                     int B, int broadcast, float* g3, float* part_bn,
+                                                     float* part_w, float* part_loss) {
+    __shared__ float W[kHeadW];  // l1w[64][25] l1b[64] l2w[64] l2b | plw[50][50] plb[50]
+    __shared__ float hv[kHS][25], h1[kHS][64], dh1[kHS][64], hp[kHS][50], dl[kHS][50], du[kHS];
+    __shared__ float red[4][8];
+    const int tid = threadIdx.x, j = tid & 15, sl = tid >> 4, lane = tid & 63, wave = tid >> 6;
+    for (int k = tid; k < kHeadVW; k += 256) W[k] = P[o.l1w + k];
+    for (int k = tid; k < 2550; k += 256) W[kHeadVW + k] = P[o.plw + k];
+    float sz = 0.0f, sz2 = 0.0f;
+    if (broadcast) {  // batch sums of z (every workgroup; B floats)
+        for (int k = tid; k < B; k += 256) {
+            sz += z[k];
+            sz2 += z[k] * z[k];
+        }
+        sz = wave_sum(sz);
+        sz2 = wave_sum(sz2);
+        if (lane == 0) {
+            red[wave][0] = sz;
+            red[wave][1] = sz2;
+        }
+    }
     __syncthreads();
+    if (broadcast) {
+        sz = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        sz2 = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    }
     const float* l1w = W;
     const float* l1b = W + 1600;
     const float* l2w = W + 1664;
     const float l2b = W[1728];
     const float* plw = W + kHeadVW;
     const float* plb = plw + 2500;
-    // batch sums of z for the broadcast value loss
-    float sz = 0.0f, sz2 = 0.0f;
-    if (broadcast) {
-        for (int k = lane; k < B; k += 64) {
-            sz += z[k];
-            sz2 += z[k] * z[k];
-        }
-        sz = wave_sum(sz);
-        sz2 = wave_sum(sz2);
-    }
-    const int b = blockIdx.x * kHS + lane;
+    const int b = blockIdx.x * kHS + sl;
     const bool ok = b < B;
-    float bnp[3][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-    float lv = 0.0f, lp = 0.0f;
-    float xh_v[25];
-    if (ok) {
-        for (int sq = 0; sq < 25; ++sq) {
-            const float x = (hz[(size_t)(sq * B + b) * 4] - hst_mean[0]) * hst_inv[0];
-            xh_v[sq] = x;
-            const float y = x * P[o.vg] + P[o.vb];
-            hv[sq * kHS + lane] = y > 0.0f ? y : 0.0f;
-        }
-        float u = l2b;
-        for (int oo = 0; oo < 64; ++oo) {
-            float a = l1b[oo];
-            for (int sq = 0; sq < 25; ++sq) a += l1w[oo * 25 + sq] * hv[sq * kHS + lane];
-            a = a > 0.0f ? a : 0.0f;
-            h1[oo * kHS + lane] = a;
-            u += l2w[oo] * a;
-        }
-        const float v = tanhf(u);
-        for (int c = 0; c < 2; ++c)
-            for (int sq = 0; sq < 25; ++sq) {
-                const float x = (hz[(size_t)(sq * B + b) * 4 + 1 + c] - hst_mean[1 + c]) * hst_inv[1 + c];
-                const float y = x * P[o.pg + c] + P[o.pb + c];
-                hp[(c * 25 + sq) * kHS + lane] = y > 0.0f ? y : 0.0f;
-            }
-        float mxl = -INFINITY;
-        for (int j = 0; j < 50; ++j) {
-            float a = plb[j];
-            for (int k = 0; k < 50; ++k) a += plw[j * 50 + k] * hp[k * kHS + lane];
-            dl[j * kHS + lane] = a;  // logits for now
+    const float vm = hst_mean[0], vi = hst_inv[0], vg = P[o.vg], vb = P[o.vb];
+    for (int sq = j; sq < 25; sq += 16) {
+        float y = 0.0f;
+        if (ok) y = (hz[(size_t)(sq * B + b) * 4] - vm) * vi * vg + vb;
+        hv[sl][sq] = y > 0.0f ? y : 0.0f;
+    }
+    for (int k = j; k < 50; k += 16) {
+        const int c = k / 25, sq = k % 25;
+        float y = 0.0f;
+        if (ok) y = (hz[(size_t)(sq * B + b) * 4 + 1 + c] - hst_mean[1 + c]) * hst_inv[1 + c] * P[o.pg + c] + P[o.pb + c];
+        hp[sl][k] = y > 0.0f ? y : 0.0f;
+    }
+    __syncthreads();
+    // value MLP forward
+    float up = 0.0f;
+    for (int oo = j; oo < 64; oo += 16) {
+        float a = l1b[oo];
+        for (int sq = 0; sq < 25; ++sq) a += l1w[oo * 25 + sq] * hv[sl][sq];
+        a = a > 0.0f ? a : 0.0f;
+        h1[sl][oo] = a;
+        up += l2w[oo] * a;
+    }
+    const float v = tanhf(sum16(up) + l2b);
+    // policy linear + softmax
+    float lg[4];
+    float mxl = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int jj = j + 16 * q;
+        lg[q] = -INFINITY;
+        if (jj < 50) {
+            float a = plb[jj];
+            for (int k = 0; k < 50; ++k) a += plw[jj * 50 + k] * hp[sl][k];
+            lg[q] = a;
             mxl = fmaxf(mxl, a);
         }
-        float se = 0.0f;
-        for (int j = 0; j < 50; ++j) {
-            const float e = expf(dl[j * kHS + lane] - mxl);
-            dl[j * kHS + lane] = e;
-            se += e;
+    }
+    mxl = max16(mxl);
+    float se = 0.0f, spi = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int jj = j + 16 * q;
+        if (jj < 50) {
+            lg[q] = expf(lg[q] - mxl);
+            se += lg[q];
+            spi += ok ? pi[(size_t)b * 50 + jj] : 0.0f;
         }
-        const float inv25B = 1.0f / (25.0f * (float)B);
-        float spi = 0.0f;
-        for (int j = 0; j < 50; ++j) spi += pi[(size_t)b * 50 + j];
-        for (int j = 0; j < 50; ++j) {
-            const float p = dl[j * kHS + lane] / se;
-            const float t = pi[(size_t)b * 50 + j];
-            lp -= t * logf(p);
-            dl[j * kHS + lane] = (p * spi - t) * inv25B;
+    }
+    se = sum16(se);
+    spi = sum16(spi);
+    const float inv25B = 1.0f / (25.0f * (float)B);
+    float lp = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int jj = j + 16 * q;
+        if (jj < 50) {
+            const float p = lg[q] / se;
+            const float t = ok ? pi[(size_t)b * 50 + jj] : 0.0f;
+            if (t != 0.0f) lp -= t * logf(p);
+            dl[sl][jj] = ok ? (p * spi - t) * inv25B : 0.0f;
         }
-        lp *= inv25B;
-        const float fB = (float)B;
-        float dv;
+    }
+    lp = sum16(lp) * inv25B;
+    // value loss and d/dv
+    const float fB = (float)B;
+    float lv = 0.0f, dv = 0.0f;
+    if (ok) {
         if (broadcast) {
             lv = (sz2 - 2.0f * v * sz + fB * v * v) / (fB * fB);
             dv = 2.0f * (fB * v - sz) / (fB * fB);
@@ -451,88 +637,88 @@ __global__ __launch_bounds__(64) void k_head_sample(const float* hz, const float
             lv = d * d / fB;
             dv = 2.0f * d / fB;
         }
-        const float duv = dv * (1.0f - v * v);
-        du[lane] = duv;
-        for (int oo = 0; oo < 64; ++oo) dh1[oo * kHS + lane] = h1[oo * kHS + lane] > 0.0f ? duv * l2w[oo] : 0.0f;
-        for (int sq = 0; sq < 25; ++sq) {
+    }
+    const float duv = dv * (1.0f - v * v);
+    if (j == 0) du[sl] = duv;
+    for (int oo = j; oo < 64; oo += 16) dh1[sl][oo] = h1[sl][oo] > 0.0f ? duv * l2w[oo] : 0.0f;
+    __syncthreads();
+    // backward into the head BN outputs
+    float bnp[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // (sum g, sum g*xhat) x channel
+    if (ok) {
+        for (int sq = j; sq < 25; sq += 16) {
             float d = 0.0f;
-            for (int oo = 0; oo < 64; ++oo) d += l1w[oo * 25 + sq] * dh1[oo * kHS + lane];
-            const float g = hv[sq * kHS + lane] > 0.0f ? d : 0.0f;
-            g3[(size_t)(sq * B + b) * 4] = g;
-            bnp[0][0] += g;
-            bnp[0][1] += g * xh_v[sq];
+            for (int oo = 0; oo < 64; ++oo) d += l1w[oo * 25 + sq] * dh1[sl][oo];
+            const float g = hv[sl][sq] > 0.0f ? d : 0.0f;
+            const size_t r = (size_t)(sq * B + b);
+            g3[r * 4] = g;
+            bnp[0] += g;
+            bnp[1] += g * ((hz[r * 4] - vm) * vi);
         }
-        for (int k = 0; k < 50; ++k) {
+        for (int k = j; k < 50; k += 16) {
             float d = 0.0f;
-            for (int j = 0; j < 50; ++j) d += plw[j * 50 + k] * dl[j * kHS + lane];
-            const float g = hp[k * kHS + lane] > 0.0f ? d : 0.0f;
+            for (int jj = 0; jj < 50; ++jj) d += plw[jj * 50 + k] * dl[sl][jj];
+            const float g = hp[sl][k] > 0.0f ? d : 0.0f;
             const int c = k / 25, sq = k % 25;
             const size_t r = (size_t)(sq * B + b);
             g3[r * 4 + 1 + c] = g;
-            const float x = (hz[r * 4 + 1 + c] - hst_mean[1 + c]) * hst_inv[1 + c];
-            bnp[1 + c][0] += g;
-            bnp[1 + c][1] += g * x;
-        }
-    } else {
-        for (int sq = 0; sq < 25; ++sq) hv[sq * kHS + lane] = 0.0f;
-        for (int oo = 0; oo < 64; ++oo) {
-            h1[oo * kHS + lane] = 0.0f;
-            dh1[oo * kHS + lane] = 0.0f;
-        }
-        for (int j = 0; j < 50; ++j) {
-            hp[j * kHS + lane] = 0.0f;
-            dl[j * kHS + lane] = 0.0f;
-        }
-        du[lane] = 0.0f;
-    }
-    // per-workgroup partials: head BN backward sums, losses
-    for (int c = 0; c < 3; ++c) {
-        const float s1 = wave_sum(bnp[c][0]), s2 = wave_sum(bnp[c][1]);
-        if (lane == 0) {
-            part_bn[(size_t)blockIdx.x * 8 + c] = s1;
-            part_bn[(size_t)blockIdx.x * 8 + 4 + c] = s2;
+            bnp[2 + 2 * c] += g;
+            bnp[3 + 2 * c] += g * ((hz[r * 4 + 1 + c] - hst_mean[1 + c]) * hst_inv[1 + c]);
         }
     }
-    lv = wave_sum(lv);
-    lp = wave_sum(lp);
-    if (lane == 0) {
-        part_loss[blockIdx.x * 2] = lv;
-        part_loss[blockIdx.x * 2 + 1] = lp;
+    // workgroup partials: BN sums and losses (lv, lp are per sample: count them on lane j == 0)
+    float vals[8] = {bnp[0], bnp[2], bnp[4], bnp[1], bnp[3], bnp[5], j == 0 ? lv : 0.0f, j == 0 ? lp : 0.0f};
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float s = wave_sum(vals[k]);
+        if (lane == 0) red[wave][k] = s;
     }
     __syncthreads();
+    if (tid < 8) {
+        const float s = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+        if (tid < 3) part_bn[(size_t)blockIdx.x * 8 + tid] = s;            // sum g
+        else if (tid < 6) part_bn[(size_t)blockIdx.x * 8 + 4 + tid - 3] = s;  // sum g*xhat
+        else part_loss[blockIdx.x * 2 + tid - 6] = s;
+    }
     // weight-gradient partials over this workgroup's samples
     float* pw = part_w + (size_t)blockIdx.x * kHeadW;
-    for (int e = lane; e < kHeadW; e += 64) {
+    for (int e = tid; e < kHeadW; e += 256) {
         float s = 0.0f;
         if (e < 1600) {  // vh_linear1.weight [64][25]
             const int oo = e / 25, sq = e % 25;
-            for (int k = 0; k < kHS; ++k) s += dh1[oo * kHS + k] * hv[sq * kHS + k];
+            for (int k = 0; k < kHS; ++k) s += dh1[k][oo] * hv[k][sq];
         } else if (e < 1664) {  // vh_linear1.bias
-            const int oo = e - 1600;
-            for (int k = 0; k < kHS; ++k) s += dh1[oo * kHS + k];
+            for (int k = 0; k < kHS; ++k) s += dh1[k][e - 1600];
         } else if (e < 1728) {  // vh_linear2.weight [1][64]
-            const int oo = e - 1664;
-            for (int k = 0; k < kHS; ++k) s += du[k] * h1[oo * kHS + k];
+            for (int k = 0; k < kHS; ++k) s += du[k] * h1[k][e - 1664];
         } else if (e == 1728) {  // vh_linear2.bias
             for (int k = 0; k < kHS; ++k) s += du[k];
         } else if (e < kHeadVW + 2500) {  // ph_linear2.weight [50][50]
-            const int j = (e - kHeadVW) / 50, kk = (e - kHeadVW) % 50;
-            for (int k = 0; k < kHS; ++k) s += dl[j * kHS + k] * hp[kk * kHS + k];
+            const int jj = (e - kHeadVW) / 50, kk = (e - kHeadVW) % 50;
+            for (int k = 0; k < kHS; ++k) s += dl[k][jj] * hp[k][kk];
         } else {  // ph_linear2.bias
-            const int j = e - kHeadVW - 2500;
-            for (int k = 0; k < kHS; ++k) s += dl[j * kHS + k];
+            for (int k = 0; k < kHS; ++k) s += dl[k][e - kHeadVW - 2500];
         }
         pw[e] = s;
     }
 }
 
-// out[j] = sum_w part[w*pstride + src + j], j < width
-__global__ void k_colsum(const float* part, int nwg, int pstride, int src, int width, float* out) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= width) return;
+// out[j] = sum_w part[w*pstride + src + j], j < width (64 columns x 16 row groups per workgroup)
+__global__ __launch_bounds__(1024) void k_colsum(const float* part, int nwg, int pstride, int src, int width,
+                                                 float* out) {
+    __shared__ float sh[16][64];
+    const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + c;
     float s = 0.0f;
-    for (int w = 0; w < nwg; ++w) s += part[(size_t)w * pstride + src + j];
-    out[j] = s;
+    if (j < width)
+        for (int w = q; w < nwg; w += 16) s += part[(size_t)w * pstride + src + j];
+    sh[q][c] = s;
+    __syncthreads();
+    if (q == 0 && j < width) {
+        float t = 0.0f;
+        for (int k = 0; k < 16; ++k) t += sh[k][c];
+        out[j] = t;
+    }
 }
 
 // Loss accumulators (double) += this step's sums
@@ -605,14 +791,40 @@ __global__ __launch_bounds__(256) void k_head_bwd_rows(const float* A, const flo
 }
 
 // ---- optimiser + weight packing -------------------------------------------------------------------
+struct ConvTab {  // conv weight ranges of the blob and their packed copies (written by k_sgd)
+    int n;
+    int off[kMaxConv], cin[kMaxConv];
+    float* wf[kMaxConv];
+    float* wd[kMaxConv];
+};
+
+// SGD (torch semantics, dampening 0): d = g*scale + wd*p; buf = mom*buf + d; p -= lr*buf.
+// Conv weights are also scattered straight into the packed fwd / dgrad layouts of k_pack.
 __global__ void k_sgd(float* p, const float* g, float* buf, const uint8_t* mask, long long n, float lr,
-                      float mom, float wd, float scale) {
+                      float mom, float wd, float scale, ConvTab tab) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || !mask[i]) return;
     const float d = g[i] * scale + wd * p[i];
     const float bb = mom * buf[i] + d;
     buf[i] = bb;
-    p[i] = p[i] - lr * bb;
+    const float np = p[i] - lr * bb;
+    p[i] = np;
+    for (int l = 0; l < tab.n; ++l) {
+        const int cin = tab.cin[l];
+        const long long rel = i - tab.off[l];
+        if (rel < 0 || rel >= (long long)kC * cin * 9) continue;
+        const int t = (int)(rel % 9), ci = (int)((rel / 9) % cin), co = (int)(rel / (9 * cin));
+        const int chunks = cin == kC ? 4 : 2;
+        {
+            const int gg = ci >> 4, kq = (ci & 15) >> 2, j = ci & 3, nt = co >> 4, lane = (co & 15) + 16 * kq;
+            tab.wf[l][((((size_t)t * chunks + gg) * 4 + nt) * 64 + lane) * 4 + j] = np;
+        }
+        if (tab.wd[l]) {
+            const int gg = co >> 4, kq = (co & 15) >> 2, j = co & 3, nt = ci >> 4, lane = (ci & 15) + 16 * kq;
+            tab.wd[l][((((size_t)(8 - t) * 4 + gg) * 4 + nt) * 64 + lane) * 4 + j] = np;
+        }
+        break;
+    }
 }
 
 // Packed conv weights: float4 index ((t*chunks + g)*4 + nt)*64 + lane holds, for output channel
@@ -686,16 +898,19 @@ struct oaz_trainer {
     oaz_train_config cfg{};
     int device = 0;
     hipStream_t own = nullptr, st = nullptr;
+    hipStream_t st2 = nullptr;  // weight-gradient stream: wgrad(l) overlaps dgrad(l) on st
+    hipEvent_t ev_dz[2] = {}, ev_w[2] = {}, ev_done = nullptr;
     Layout L{};
     int nconv = 0, maxB = 0;
+    int conv_rg = 2;  // 16-row groups per conv workgroup (OAZ_CONV_RG=1|2|4 overrides; tuning knob)
     size_t nparam = 0;
     std::vector<void*> allocs;
     float *P = nullptr, *G = nullptr, *MOM = nullptr;
     uint8_t* mask = nullptr;
     float4 *wf[kMaxConv] = {}, *wd[kMaxConv] = {};
-    float *X0 = nullptr, *Z[kMaxConv] = {}, *A[kMaxConv] = {}, *M[kMaxConv] = {}, *DZ = nullptr;
+    float *X0 = nullptr, *Z[kMaxConv] = {}, *A[kMaxConv] = {}, *M[kMaxConv] = {}, *DZ[2] = {};
     float *mean[kMaxConv] = {}, *invstd[kMaxConv] = {}, *bcoef = nullptr;  // bcoef: c1, mm, mx [3][64]
-    float *part = nullptr, *bpart = nullptr, *wpart = nullptr;
+    float *part = nullptr, *bpart[2] = {}, *wpart = nullptr;
     float *hz = nullptr, *g3 = nullptr, *hstat = nullptr;  // hstat: mean[3] invstd[3] c1[3] mm[3] mx[3]
     float *hpart = nullptr, *hwpart = nullptr, *hlpart = nullptr, *hcpart = nullptr;
     float *pi = nullptr, *z = nullptr;
@@ -720,6 +935,12 @@ struct oaz_trainer {
         if (owned_samples) (void)hipFree(owned_samples);
         if (idx) (void)hipFree(idx);
         for (void* q : allocs) (void)hipFree(q);
+        for (int k = 0; k < 2; ++k) {
+            if (ev_dz[k]) (void)hipEventDestroy(ev_dz[k]);
+            if (ev_w[k]) (void)hipEventDestroy(ev_w[k]);
+        }
+        if (ev_done) (void)hipEventDestroy(ev_done);
+        if (st2) (void)hipStreamDestroy(st2);
         if (own) (void)hipStreamDestroy(own);
     }
 };
@@ -758,10 +979,19 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
     t->nconv = 1 + 2 * cfg->blocks;
     t->maxB = cfg->max_batch;
     t->L = make_layout(cfg->blocks);
+    if (const char* e = getenv("OAZ_CONV_RG")) {
+        const int v = atoi(e);
+        if (v == 1 || v == 2 || v == 4) t->conv_rg = v;
+    }
     t->nparam = t->L.total;
     const size_t R = (size_t)t->maxB * 25;
     auto fail = [&]() -> oaz_trainer* { delete t; return nullptr; };
-    if (hipStreamCreateWithFlags(&t->own, hipStreamNonBlocking) != hipSuccess) {
+    bool ev_ok = hipStreamCreateWithFlags(&t->st2, hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&t->ev_done, hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; k < 2 && ev_ok; ++k)
+        ev_ok = hipEventCreateWithFlags(&t->ev_dz[k], hipEventDisableTiming) == hipSuccess &&
+                hipEventCreateWithFlags(&t->ev_w[k], hipEventDisableTiming) == hipSuccess;
+    if (!ev_ok || hipStreamCreateWithFlags(&t->own, hipStreamNonBlocking) != hipSuccess) {
         oaz_set_err(OAZ_ERR_HIP, "trainer: stream");
         return fail();
     }
@@ -778,9 +1008,9 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
             return fail();
     }
     const size_t nwg_conv = R / 16;
-    if (t->alloc(t->X0, R * kInPad) || t->alloc(t->DZ, R * kC) || t->alloc(t->bcoef, 3 * 64) ||
-        t->alloc(t->part, nwg_conv * 128) || t->alloc(t->bpart, (R + 63) / 64 * 64) ||
-        t->alloc(t->wpart, (size_t)9 * 25 * 64 * 64) || t->alloc(t->hz, R * 4) || t->alloc(t->g3, R * 4) ||
+    if (t->alloc(t->X0, R * kInPad) || t->alloc(t->DZ[0], R * kC) || t->alloc(t->DZ[1], R * kC) || t->alloc(t->bcoef, 3 * 64) ||
+        t->alloc(t->part, nwg_conv * 128) || t->alloc(t->bpart[0], (R + 63) / 64 * 64) || t->alloc(t->bpart[1], (R + 63) / 64 * 64) ||
+        t->alloc(t->wpart, (size_t)9 * 25 * kWSplit * 64 * 64) || t->alloc(t->hz, R * 4) || t->alloc(t->g3, R * 4) ||
         t->alloc(t->hstat, 16) || t->alloc(t->hpart, ((R + 255) / 256 + (size_t)t->maxB / kHS + 1) * 8) ||
         t->alloc(t->hwpart, ((size_t)t->maxB / kHS + 1) * kHeadW) ||
         t->alloc(t->hlpart, ((size_t)t->maxB / kHS + 1) * 2) ||
@@ -889,6 +1119,17 @@ extern "C" int oaz_trainer_set_batches(oaz_trainer* t, const int32_t* idx, int n
     return 0;
 }
 
+template <int MODE>
+static void launch_conv(int ch, int rg, dim3 grid, hipStream_t st, const ConvArgs& a) {
+#define OAZ_CONV(CHV, RGV) hipLaunchKernelGGL((k_conv<MODE, CHV, RGV>), grid, dim3(256), 0, st, a)
+    if (ch == 2) {
+        if (rg == 1) OAZ_CONV(2, 1); else if (rg == 2) OAZ_CONV(2, 2); else OAZ_CONV(2, 4);
+    } else {
+        if (rg == 1) OAZ_CONV(4, 1); else if (rg == 2) OAZ_CONV(4, 2); else OAZ_CONV(4, 4);
+    }
+#undef OAZ_CONV
+}
+
 static int backward(oaz_trainer* t, int bi) {
     const int B = t->batch, R = B * 25, NB = t->cfg.blocks, nl = t->nconv;
     const Layout& L = t->L;
@@ -897,9 +1138,10 @@ static int backward(oaz_trainer* t, int bi) {
     float* P = t->P;
     float* G = t->G;
     const float bn_mom = (float)t->cfg.bn_momentum, eps = (float)t->cfg.bn_eps;
-    const int nwg_conv = R / 16;
-    const dim3 conv_grid(B / 16, 25);
-    hipLaunchKernelGGL(k_gather, dim3((R + 255) / 256), dim3(256), 0, st, t->samples, t->idx + (size_t)bi * B, B,
+    const int rg = t->conv_rg, rows_wg = 16 * rg;
+    const int nwg_conv = 25 * ((B + rows_wg - 1) / rows_wg);
+    const dim3 conv_grid((B + rows_wg - 1) / rows_wg, 25);
+    hipLaunchKernelGGL(k_gather, dim3((R + 51 * B + 255) / 256), dim3(256), 0, st, t->samples, t->idx + (size_t)bi * B, B,
                        t->X0, t->pi, t->z);
     // ---- forward
     for (int l = 0; l < nl; ++l) {
@@ -911,8 +1153,8 @@ static int backward(oaz_trainer* t, int bi) {
         a.part = t->part;
         a.chunks = l == 0 ? 2 : 4;
         a.B = B;
-        hipLaunchKernelGGL(k_conv<CONV_FWD>, conv_grid, dim3(256), 0, st, a);
-        hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(256), 0, st, t->part, nwg_conv, 64, 0, 64, (double)R,
+        launch_conv<CONV_FWD>(l == 0 ? 2 : 4, rg, conv_grid, st, a);
+        hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_conv, 64, 0, 64, (double)R,
                            P + L.brm[l], P + L.brv[l], bn_mom, eps, t->mean[l], t->invstd[l]);
         const float* skip = (l >= 2 && l % 2 == 0) ? t->A[l - 2] : nullptr;  // block output adds the block input
         const long long n = (long long)R * kC;
@@ -929,51 +1171,62 @@ static int backward(oaz_trainer* t, int bi) {
     float* hc1 = t->hstat + 6;
     float* hmm = t->hstat + 9;
     float* hmx = t->hstat + 12;
-    hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(256), 0, st, t->hpart, nwg_hc, 4, 0, 1, (double)R,
+    hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->hpart, nwg_hc, 4, 0, 1, (double)R,
                        P + h.vrm, P + h.vrv, bn_mom, eps, hmean, hinv);
-    hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(256), 0, st, t->hpart, nwg_hc, 4, 1, 2, (double)R,
+    hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->hpart, nwg_hc, 4, 1, 2, (double)R,
                        P + h.prm, P + h.prv, bn_mom, eps, hmean + 1, hinv + 1);
     const int nwg_hs = (B + kHS - 1) / kHS;
     float* hbpart = t->hpart + (size_t)nwg_hc * 8;
-    hipLaunchKernelGGL(k_head_sample, dim3(nwg_hs), dim3(kHS), 0, st, t->hz, hmean, hinv, P, h, t->pi, t->z, B,
+    hipLaunchKernelGGL(k_head_sample, dim3(nwg_hs), dim3(256), 0, st, t->hz, hmean, hinv, P, h, t->pi, t->z, B,
                        t->cfg.value_loss_broadcast, t->g3, hbpart, t->hwpart, t->hlpart);
     hipLaunchKernelGGL(k_loss_acc, dim3(1), dim3(64), 0, st, t->hlpart, nwg_hs, t->loss_acc);
-    hipLaunchKernelGGL(k_colsum, dim3((kHeadVW + 255) / 256), dim3(256), 0, st, t->hwpart, nwg_hs, kHeadW, 0,
+    hipLaunchKernelGGL(k_colsum, dim3((kHeadVW + 63) / 64), dim3(1024), 0, st, t->hwpart, nwg_hs, kHeadW, 0,
                        kHeadVW, G + h.l1w);
-    hipLaunchKernelGGL(k_colsum, dim3((2550 + 255) / 256), dim3(256), 0, st, t->hwpart, nwg_hs, kHeadW, kHeadVW,
+    hipLaunchKernelGGL(k_colsum, dim3((2550 + 63) / 64), dim3(1024), 0, st, t->hwpart, nwg_hs, kHeadW, kHeadVW,
                        2550, G + h.plw);
-    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(256), 0, st, hbpart, nwg_hs, 4, 0, 1, (double)R, P + h.vg,
+    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, hbpart, nwg_hs, 4, 0, 1, (double)R, P + h.vg,
                        hinv, G + h.vg, G + h.vb, hc1, hmm, hmx);
-    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(256), 0, st, hbpart, nwg_hs, 4, 1, 2, (double)R, P + h.pg,
+    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, hbpart, nwg_hs, 4, 1, 2, (double)R, P + h.pg,
                        hinv + 1, G + h.pg, G + h.pb, hc1 + 1, hmm + 1, hmx + 1);
     const int nwg_rows = (R + 63) / 64;
     hipLaunchKernelGGL(k_head_bwd_rows, dim3(nwg_rows), dim3(256), 0, st, AL, t->Z[nl - 1], t->mean[nl - 1],
                        t->invstd[nl - 1], t->hz, t->g3, hmean, hinv, hc1, hmm, hmx, P, h, t->M[nl - 1], t->part,
                        t->hcpart, R);
-    hipLaunchKernelGGL(k_colsum, dim3(1), dim3(256), 0, st, t->hcpart, nwg_rows, kHConvW, 0, 65, G + h.vcw);
-    hipLaunchKernelGGL(k_colsum, dim3(1), dim3(256), 0, st, t->hcpart, nwg_rows, kHConvW, 65, 130, G + h.pcw);
-    // ---- trunk backward; t->part holds the BN-backward partials of layer l (nwg, [2][64])
+    hipLaunchKernelGGL(k_colsum, dim3(2), dim3(1024), 0, st, t->hcpart, nwg_rows, kHConvW, 0, 65, G + h.vcw);
+    hipLaunchKernelGGL(k_colsum, dim3(3), dim3(1024), 0, st, t->hcpart, nwg_rows, kHConvW, 65, 130, G + h.pcw);
+    // ---- trunk backward; t->part holds the BN-backward partials of layer l (nwg, [2][64]).
+    // dZ of layer l feeds both dgrad(l) (on st, the critical path) and wgrad(l) (on st2); dZ and
+    // the bias partials are double-buffered so st never overwrites what st2 still reads.
     int nwg_part = nwg_rows;
+    bool used[2] = {false, false};
     for (int l = nl - 1; l >= 0; --l) {
+        const int k = l & 1;
         float* c1 = t->bcoef;
         float* mm = t->bcoef + 64;
         float* mx = t->bcoef + 128;
-        hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(256), 0, st, t->part, nwg_part, 64, 0, 64, (double)R,
+        float* dz = t->DZ[k];
+        hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_part, 64, 0, 64, (double)R,
                            P + L.bg[l], t->invstd[l], G + L.bg[l], G + L.bb[l], c1, mm, mx);
+        if (used[k]) HIP_TRY(hipStreamWaitEvent(st, t->ev_w[k], 0));
         hipLaunchKernelGGL(k_bn_bwd_apply, dim3(nwg_rows), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
-                           t->invstd[l], c1, mm, mx, t->DZ, t->bpart, R);
+                           t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
+        HIP_TRY(hipEventRecord(t->ev_dz[k], st));
+        HIP_TRY(hipStreamWaitEvent(t->st2, t->ev_dz[k], 0));
         const float* X = l == 0 ? t->X0 : t->A[l - 1];
         if (l == 0)
-            hipLaunchKernelGGL(k_wgrad<2>, dim3(25, 9), dim3(256), 0, st, t->DZ, X, B, t->wpart);
+            hipLaunchKernelGGL(k_wgrad<1>, dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
         else
-            hipLaunchKernelGGL(k_wgrad<4>, dim3(25, 9), dim3(256), 0, st, t->DZ, X, B, t->wpart);
+            hipLaunchKernelGGL(k_wgrad<2>, dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
         const int cin = l == 0 ? kIn : kC;
         const int nred = 9 * kC * cin;
-        hipLaunchKernelGGL(k_wgrad_reduce, dim3((nred + 255) / 256), dim3(256), 0, st, t->wpart,
-                           l == 0 ? kInPad : kC, cin, t->bpart, nwg_rows, G + L.cw[l], G + L.cb[l]);
+        hipLaunchKernelGGL(k_wgrad_reduce, dim3((nred + 255) / 256), dim3(256), 0, t->st2, t->wpart,
+                           l == 0 ? kInPad : kC, cin, G + L.cw[l]);
+        hipLaunchKernelGGL(k_colsum, dim3(1), dim3(1024), 0, t->st2, t->bpart[k], nwg_rows, 64, 0, 64, G + L.cb[l]);
+        HIP_TRY(hipEventRecord(t->ev_w[k], t->st2));
+        used[k] = true;
         if (l == 0) break;
         ConvArgs a{};
-        a.in = t->DZ;
+        a.in = dz;
         a.w = t->wd[l];
         a.out = t->M[l - 1];
         a.part = t->part;
@@ -984,9 +1237,11 @@ static int backward(oaz_trainer* t, int bi) {
         a.skip = (l % 2 == 1) ? t->M[l + 1] : nullptr;  // first conv of a block: add the block-output gradient
         a.chunks = 4;
         a.B = B;
-        hipLaunchKernelGGL(k_conv<CONV_DGRAD>, conv_grid, dim3(256), 0, st, a);
+        launch_conv<CONV_DGRAD>(4, rg, conv_grid, st, a);
         nwg_part = nwg_conv;
     }
+    HIP_TRY(hipEventRecord(t->ev_done, t->st2));
+    HIP_TRY(hipStreamWaitEvent(st, t->ev_done, 0));  // every gradient is in G before SGD / all-reduce
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -1015,10 +1270,18 @@ extern "C" int oaz_trainer_get_grads(oaz_trainer* t, float* host, size_t n) {
 
 static int apply(oaz_trainer* t, float scale) {
     const long long n = (long long)t->nparam;
+    ConvTab tab{};
+    tab.n = t->nconv;
+    for (int l = 0; l < t->nconv; ++l) {
+        tab.off[l] = (int)t->L.cw[l];
+        tab.cin[l] = l == 0 ? kIn : kC;
+        tab.wf[l] = reinterpret_cast<float*>(t->wf[l]);
+        tab.wd[l] = reinterpret_cast<float*>(t->wd[l]);
+    }
     hipLaunchKernelGGL(k_sgd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, t->st, t->P, t->G, t->MOM, t->mask, n,
-                       (float)t->cfg.learning_rate, (float)t->cfg.momentum, (float)t->cfg.weight_decay, scale);
+                       (float)t->cfg.learning_rate, (float)t->cfg.momentum, (float)t->cfg.weight_decay, scale, tab);
     HIP_TRY(hipGetLastError());
-    return repack(t);
+    return 0;
 }
 
 extern "C" int oaz_trainer_apply(oaz_trainer* t, float grad_scale) {
