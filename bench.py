@@ -65,9 +65,11 @@ def parse():
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--mode", default="selfplay", choices=["selfplay", "train"],
+    ap.add_argument("--mode", default="selfplay", choices=["selfplay", "train", "pure_mcts"],
                     help="train: SGD steps of the training loop (SURVEY 8f #2), not the headline metric")
     ap.add_argument("--train-blocks", type=int, default=5, help="train mode: residual blocks (bin/train.rs:60)")
+    ap.add_argument("--pm-games", type=int, default=262144, help="pure_mcts mode: searches per launch")
+    ap.add_argument("--pm-playouts", type=int, default=400, help="pure_mcts mode: playouts per search")
     ap.add_argument("--train-batch", type=int, default=512, help="train mode: global batch (train.rs:142)")
     return ap.parse_args()
 
@@ -249,6 +251,73 @@ def train_main(args, world, rank, local):
         dist.destroy_process_group()
 
 
+PM_METRIC = "pure-MCTS playouts/sec (random-rollout UCT agent, onitama-game ai/mcts)"
+
+
+def pure_mcts_main(args, world, rank, local):
+    """One step = one search (max_playouts random-rollout playouts) from each of pm_games seeded
+    deals (the arena opponent's config: min_node_visits 5, c 1.41, evaluator.rs:340-345)."""
+    import ctypes as C
+    import numpy as np
+    from onitama_az import _abi
+    from onitama_az.game import initial_state_np
+    from onitama_az.pure_mcts import pure_mcts_search
+    lib = _abi.load()
+    G, P = args.pm_games, args.pm_playouts
+    deals = []
+    for g in range(G):
+        d = (C.c_uint8 * 5)()
+        lib.oaz_deal_deck(C.c_uint64(20260101), C.c_uint64(rank * G + g), d)
+        deals.append(initial_state_np(list(d)))
+    roots = np.concatenate(deals)
+
+    def step(k):
+        return pure_mcts_search(roots, P, 5, 1.41, seed=20260101, game_id0=(k * world + rank) * G)
+
+    for k in range(args.warmup):
+        step(k)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    plies = 0
+    for k in range(args.steps):
+        r = step(args.warmup + k)
+        plies += r.stats.rollout_plies
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    T = float(tmax.item())
+    if rank == 0:
+        total = G * P * args.steps * world
+        out = {"metric": PM_METRIC, "value": total / T, "unit": "playouts/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": 1e3 * T / args.steps, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "int32/f32",
+               "data": "synthetic (seeded 5-of-16 deals, start positions)",
+               "config": {"workload": f"pure_mcts: {G} searches/GPU x {P} playouts, min_node_visits 5, c 1.41",
+                          "parallelism": f"searches sharded x{world}"},
+               "searches_per_s": G * args.steps * world / T,
+               "mean_rollout_plies": plies / max(1, G * P * args.steps)}
+        if not args.no_cpu_baseline and world == 1:
+            sys.path.insert(0, str(ROOT / "tests"))
+            import oracle_ffi as orc
+            from onitama_az.pure_mcts import default_config
+            cfg = default_config()
+            cfg.max_playouts, cfg.min_node_visits, cfg.exploration_c = P, 5, 1.41
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            t1 = time.perf_counter()
+            po, ns = orc.pure_mcts_bench(cfg, threads, args.cpu_seconds)
+            dt = time.perf_counter() - t1
+            out["cpu_baseline"] = {"value": po / dt, "unit": "playouts/s", "cores": threads, "kind": "port",
+                                   "sample": f"{ns} searches x {P} playouts in {dt:.1f}s on {threads} host threads "
+                                             f"(oracle C restatement of mcts_arena.rs)"}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -259,6 +328,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.mode == "train":
         return train_main(args, world, rank, local)
+    if args.mode == "pure_mcts":
+        return pure_mcts_main(args, world, rank, local)
     from onitama_az import _abi
     from onitama_az.engine import Engine
     from onitama_az.weights import random_weights

@@ -33,6 +33,7 @@
  *                          and Agent::generate_move for AlphaZeroMcts, alphazero_mcts/mod.rs:122-144)
  *   oaz_selfplay_*     <- self_play                           alphazero-training/src/train.rs:35-98
  *   oaz_load_weights   <- AlphaZeroMcts::from_model_file      alphazero-training/src/alphazero_mcts/mod.rs:89-105
+ *   oaz_pure_mcts_*    <- Mcts agent (random-rollout UCT)     onitama-game/src/ai/mcts/mcts_arena.rs:56-264, mod.rs:37-52
  *   oaz_trainer_*      <- the training loop body               alphazero-training/src/train.rs:264-313
  *                         (ConvResNet::forward(train=true) net.rs:215-232, alphaloss net.rs:234-243,
  *                          nn::Sgd{momentum 0.9} + set_weight_decay train.rs:181-186, opt.backward_step)
@@ -301,6 +302,45 @@ int oaz_trainer_train(oaz_trainer* t, int first, int count);
 /* Loss sums since the last call: out[0] value loss, out[1] policy loss, out[2] steps. */
 int oaz_trainer_losses(oaz_trainer* t, double out[3]);
 int oaz_trainer_sync(oaz_trainer* t);
+
+/* ---- pure MCTS agent --------------------------------
+ * The reference's `Mcts` agent: UCT (f32, winrate + c*sqrt(ln N / n)) over a tree expanded once a
+ * leaf has more than min_node_visits visits, random rollouts to the end of the game, +-1 backed up
+ * with a sign flip. One GPU thread runs one game's whole search. Rollout draws come from Philox
+ * (seed; game_id0 + g, playout, 0x9C7A0000, d/4); a rollout longer than rollout_cap plies scores 0. */
+typedef struct oaz_pure_mcts_config {
+    int32_t max_playouts;     /* 5000 (ai/mcts/mod.rs:25); the arena's opponent uses 400 (evaluator.rs:340-345) */
+    int32_t min_node_visits;  /* 5 */
+    float exploration_c;      /* sqrt(2) as f32 (the arena's opponent: 1.41) */
+    int32_t rollout_cap;      /* plies per rollout before it is scored as a draw (reference: none) */
+    uint64_t seed;
+    uint64_t game_id0;        /* RNG stream of root g = game_id0 + g */
+    int32_t reserved[4];
+} oaz_pure_mcts_config;
+
+typedef struct oaz_pure_node { /* MctsNode (mcts_arena.rs:330-352) */
+    uint32_t visits;
+    float reward;
+    float winrate;
+    uint32_t first;   /* first child (children are contiguous) */
+    uint32_t parent;  /* 0xFFFFFFFF for the root */
+    uint16_t mv;      /* from | to<<5 | slot<<10 | piece<<12 */
+    uint8_t nch;
+    uint8_t flags;    /* 1 expanded, 2 terminal */
+} oaz_pure_node;  /* 24 bytes */
+
+typedef struct oaz_pure_mcts_stats {
+    uint64_t playouts, expansions, rollout_plies, rollout_passes, rollouts_capped, max_nodes, tree_full;
+} oaz_pure_mcts_stats;
+
+void oaz_pure_mcts_config_default(oaz_pure_mcts_config* cfg);
+/* Nodes one search may allocate (the per-game capacity of tree_out). */
+size_t oaz_pure_mcts_tree_capacity(const oaz_pure_mcts_config* cfg);
+/* One search per root (colour = root.to_move). out_value = winrate of the chosen child. A root with
+ * no legal move returns the pass move (from = to = 25). tree_out (optional, G x tree_cap nodes)
+ * receives each game's tree. */
+int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pure_mcts_config* cfg, oaz_move* out_move,
+                         float* out_value, oaz_pure_mcts_stats* stats, oaz_pure_node* tree_out, size_t tree_cap);
 
 #ifdef __cplusplus
 }

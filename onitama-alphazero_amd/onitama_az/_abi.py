@@ -139,6 +139,23 @@ class oaz_train_config(C.Structure):
     ]
 
 
+class oaz_pure_mcts_config(C.Structure):
+    _fields_ = [
+        ("max_playouts", C.c_int32),
+        ("min_node_visits", C.c_int32),
+        ("exploration_c", C.c_float),
+        ("rollout_cap", C.c_int32),
+        ("seed", C.c_uint64),
+        ("game_id0", C.c_uint64),
+        ("reserved", C.c_int32 * 4),
+    ]
+
+
+class oaz_pure_mcts_stats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("playouts", "expansions", "rollout_plies", "rollout_passes",
+                                          "rollouts_capped", "max_nodes", "tree_full")]
+
+
 assert C.sizeof(oaz_state) == 24
 assert C.sizeof(oaz_move) == 4
 assert C.sizeof(oaz_node) == 32
@@ -153,6 +170,9 @@ NODE_DTYPE = np.dtype(
      ("flags", "u1"), ("pad", "<u4")]
 )
 SAMPLE_DTYPE = np.dtype([("state", STATE_DTYPE), ("pi", "<f4", 50), ("z", "<f4")])
+PURE_NODE_DTYPE = np.dtype([("visits", "<u4"), ("reward", "<f4"), ("winrate", "<f4"), ("first", "<u4"),
+                            ("parent", "<u4"), ("mv", "<u2"), ("nch", "u1"), ("flags", "u1")])
+assert PURE_NODE_DTYPE.itemsize == 24
 assert STATE_DTYPE.itemsize == 24 and NODE_DTYPE.itemsize == 32 and SAMPLE_DTYPE.itemsize == 228
 
 # C prototypes: name -> (restype, argtypes)
@@ -190,6 +210,10 @@ _PROTOS = {
     "oaz_samples_fetch": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t, _P(C.c_size_t)]),
     "oaz_samples_export_device": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t, _P(C.c_size_t)]),
     "oaz_selfplay_run": (C.c_int, [_VOIDP, C.c_int, _VOIDP, C.c_size_t, _P(C.c_size_t), _P(oaz_selfplay_stats)]),
+    "oaz_pure_mcts_config_default": (None, [_P(oaz_pure_mcts_config)]),
+    "oaz_pure_mcts_tree_capacity": (C.c_size_t, [_P(oaz_pure_mcts_config)]),
+    "oaz_pure_mcts_search": (C.c_int, [_VOIDP, C.c_int, _P(oaz_pure_mcts_config), _VOIDP, _VOIDP,
+                                       _P(oaz_pure_mcts_stats), _VOIDP, C.c_size_t]),
     "oaz_train_config_default": (None, [_P(oaz_train_config)]),
     "oaz_trainer_create": (_VOIDP, [_P(oaz_train_config), C.c_int]),
     "oaz_trainer_destroy": (None, [_VOIDP]),

@@ -90,9 +90,10 @@ class FightStatistics:  # evaluator.rs:37-110
 
 
 @dataclass
-class PitStatistics:  # evaluator.rs:112-118 (MCTS / alpha-beta opponents are out of scope)
+class PitStatistics:  # evaluator.rs:112-118 (the alpha-beta opponent is out of scope)
     self_fight: FightStatistics
     random_fight: Optional[FightStatistics] = None
+    mcts_fight: Optional[FightStatistics] = None
 
 
 @dataclass
@@ -223,7 +224,7 @@ def fight(config: EvaluatorConfig, agent: BatchedAgent, opponent: BatchedAgent, 
 
 class Evaluator:  # evaluator.rs:139-193
     def __init__(self, config: EvaluatorConfig, best: ConvResNet, new: ConvResNet,
-                 ratings: Sequence[Tuple[float, float]] = ((800.0, 800.0), (800.0, 800.0))):
+                 ratings: Sequence[Tuple[float, float]] = ((800.0, 800.0), (800.0, 800.0), (800.0, 800.0))):
         self.config, self.best, self.new, self.ratings = config, best, new, ratings
 
     def pit(self, sims: int = 400) -> Tuple[PitStatistics, bool]:
@@ -232,4 +233,9 @@ class Evaluator:  # evaluator.rs:139-193
                            *self.ratings[0])
         random_fight = fight(self.config, AlphaZeroAgent(cfg, self.new), RandomAgent(self.config.seed),
                              *self.ratings[1])
-        return PitStatistics(self_fight, random_fight), self_fight.winrate > self.config.winrate_percent
+        from .pure_mcts import Mcts  # evaluator.rs:314-353: Mcts{400 ms, min visits 5, c 1.41, 400 playouts}
+        mcts_fight = fight(self.config, AlphaZeroAgent(cfg, self.new),
+                           Mcts(search_time=0.4, min_node_visits=5, exploration_c=1.41, max_playouts=sims,
+                                seed=self.config.seed), *self.ratings[2])
+        return (PitStatistics(self_fight, random_fight, mcts_fight),
+                self_fight.winrate > self.config.winrate_percent)

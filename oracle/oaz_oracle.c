@@ -879,3 +879,220 @@ int64_t orc_selfplay_bench(const orc_selfplay_cfg* cfg, int threads, double seco
     if (plies_done) *plies_done = plies;
     return sims;
 }
+
+
+/* ---- pure MCTS (onitama-game/src/ai/mcts/mcts_arena.rs) ---------------------------------- */
+typedef struct {
+    uint64_t seed;
+    uint32_t game, playout, d, buf[4];
+} pm_rng;
+
+static uint32_t pm_next(pm_rng* r) {
+    if ((r->d & 3) == 0) {
+        const uint32_t ctr[4] = {r->game, r->playout, 0x9C7A0000u, r->d >> 2};
+        orc_philox(r->seed, ctr, r->buf);
+    }
+    return r->buf[r->d++ & 3];
+}
+
+static uint32_t pm_below(pm_rng* r, uint32_t n) { return (uint32_t)(((uint64_t)pm_next(r) * n) >> 32); }
+
+/* mcts_arena.rs:233-241 */
+static float pm_reward(int result, int color) {
+    if (result == OAZ_RED_WIN) return color == OAZ_RED ? 1.0f : -1.0f;
+    if (result == OAZ_BLUE_WIN) return color == OAZ_BLUE ? 1.0f : -1.0f;
+    return 0.0f;
+}
+
+static uint16_t pm_pack(const oaz_move* m) {
+    return (uint16_t)(m->from | (m->to << 5) | (m->slot << 10) | (m->piece << 12));
+}
+
+static void pm_unpack(uint16_t v, oaz_move* m) {
+    m->from = v & 31;
+    m->to = (v >> 5) & 31;
+    m->slot = (v >> 10) & 3;
+    m->piece = (v >> 12) & 1;
+}
+
+/* f32::total_cmp(a, b) > 0 */
+static int pm_total_ge(float a, float b) {
+    int32_t ia, ib;
+    memcpy(&ia, &a, 4);
+    memcpy(&ib, &b, 4);
+    ia ^= (int32_t)((uint32_t)(ia >> 31) >> 1);
+    ib ^= (int32_t)((uint32_t)(ib >> 31) >> 1);
+    return ia >= ib;
+}
+
+int orc_pure_mcts(const oaz_pure_mcts_config* cfg, uint64_t game_id, const oaz_state* root, oaz_move* out_move,
+                  float* out_value, oaz_pure_node* T, int cap, oaz_pure_mcts_stats* stats) {
+    if (cap < 1) return -1;
+    const int root_color = root->to_move & 1;
+    memset(&T[0], 0, sizeof(T[0]));
+    T[0].parent = 0xFFFFFFFFu;
+    int n_nodes = 1;
+    oaz_move moves[40];
+    for (int po = 0; po < cfg->max_playouts; ++po) {  /* search, mcts_arena.rs:56-62 */
+        oaz_state s = *root;
+        uint32_t idx = 0;
+        /* playout step 1 (:100-116): select while expanded and not terminal */
+        while ((T[idx].flags & 1) && !(T[idx].flags & 2) && T[idx].nch) {
+            const float lnN = logf((float)T[idx].visits);
+            uint32_t best = T[idx].first;
+            float bu = 0.0f;
+            for (uint32_t c = T[idx].first; c < T[idx].first + T[idx].nch; ++c) {
+                const float u = T[c].winrate + cfg->exploration_c * sqrtf(lnN / (float)T[c].visits); /* :141-143 */
+                if (c == T[idx].first || pm_total_ge(u, bu)) { /* max_by keeps the last maximum */
+                    bu = u;
+                    best = c;
+                }
+            }
+            oaz_move m;
+            pm_unpack(T[best].mv, &m);
+            const int res = orc_make_move(&s, &m, s.to_move & 1);
+            s.to_move ^= 1;
+            if (res == OAZ_RED_WIN || res == OAZ_BLUE_WIN) T[best].flags |= 2;
+            idx = best;
+        }
+        /* step 2 (:118-124): expand (:166-185) */
+        if (!(T[idx].flags & 3) && T[idx].visits > (uint32_t)cfg->min_node_visits) {
+            const int n = orc_movegen(&s, s.to_move & 1, moves);
+            if (n_nodes + n <= cap) {
+                T[idx].first = (uint32_t)n_nodes;
+                T[idx].nch = (uint8_t)n;
+                for (int k = 0; k < n; ++k) {
+                    oaz_pure_node* ch = &T[n_nodes + k];
+                    memset(ch, 0, sizeof(*ch));
+                    ch->parent = idx;
+                    ch->mv = pm_pack(&moves[k]);
+                }
+                n_nodes += n;
+                T[idx].flags |= 1;
+                if (stats) stats->expansions++;
+            } else if (stats) {
+                stats->tree_full++;
+            }
+        }
+        /* step 3 (:126-130, simulate :188-231): reward colour = the parent's colour */
+        const int reward_color = idx == 0 ? root_color : ((s.to_move & 1) ^ 1);
+        pm_rng rng = {cfg->seed, (uint32_t)game_id, (uint32_t)po, 0, {0, 0, 0, 0}};
+        int mr = orc_current_state(&s);
+        float r;
+        if (mr == OAZ_RED_WIN || mr == OAZ_BLUE_WIN) {
+            r = pm_reward(mr, reward_color);
+        } else {
+            int color = s.to_move & 1, plies = 0, capped = 0;
+            while (mr != OAZ_RED_WIN && mr != OAZ_BLUE_WIN) {
+                if (plies >= cfg->rollout_cap) {
+                    capped = 1;
+                    break;
+                }
+                const int n = orc_movegen(&s, color, moves);
+                if (n == 0) { /* pass with a random own card */
+                    const int slot = (color == OAZ_RED ? 0 : 2) + (int)pm_below(&rng, 2);
+                    const uint8_t t = s.cards[slot];
+                    s.cards[slot] = s.cards[4];
+                    s.cards[4] = t;
+                    color ^= 1;
+                    plies++;
+                    if (stats) stats->rollout_passes++;
+                    continue;
+                }
+                const oaz_move m = moves[pm_below(&rng, (uint32_t)n)];
+                mr = orc_make_move(&s, &m, color);
+                color ^= 1;
+                plies++;
+            }
+            if (stats) stats->rollout_plies += (uint64_t)plies;
+            if (capped) {
+                r = 0.0f;
+                if (stats) stats->rollouts_capped++;
+            } else {
+                r = pm_reward(mr, reward_color);
+            }
+        }
+        /* step 4 (:243-254) */
+        for (uint32_t v = idx;;) {
+            T[v].visits += 1;
+            T[v].reward += r;
+            T[v].winrate = T[v].reward / (float)T[v].visits;
+            if (v == 0) break;
+            v = T[v].parent;
+            r = -r;
+        }
+        if (stats) stats->playouts++;
+    }
+    if (stats && (uint64_t)n_nodes > stats->max_nodes) stats->max_nodes = (uint64_t)n_nodes;
+    if (T[0].nch == 0) {
+        out_move->from = 25;
+        out_move->to = 25;
+        out_move->piece = 0;
+        out_move->slot = (uint8_t)(root_color ? 2 : 0);
+        *out_value = 0.0f;
+    } else {
+        uint32_t best = T[0].first, bv = 0;
+        for (uint32_t c = T[0].first; c < T[0].first + T[0].nch; ++c)
+            if (T[c].visits >= bv) { /* max_by_key: last maximum */
+                bv = T[c].visits;
+                best = c;
+            }
+        pm_unpack(T[best].mv, out_move);
+        *out_value = T[best].winrate;
+    }
+    return n_nodes;
+}
+
+typedef struct {
+    const oaz_pure_mcts_config* cfg;
+    double seconds;
+    int tid;
+    int64_t playouts, searches;
+} pm_bench_arg;
+
+static void* pm_bench_worker(void* p) {
+    pm_bench_arg* a = (pm_bench_arg*)p;
+    const int cap = (int)(1 + 40 * (a->cfg->max_playouts / (a->cfg->min_node_visits + 1) + 1));
+    oaz_pure_node* T = (oaz_pure_node*)malloc(sizeof(oaz_pure_node) * (size_t)cap);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (uint64_t g = (uint64_t)a->tid << 32;; ++g) {
+        uint8_t deck[5];
+        orc_deal_deck(a->cfg->seed, g, deck);
+        oaz_state root;
+        orc_initial_state(deck, &root);
+        oaz_move mv;
+        float v;
+        oaz_pure_mcts_stats st;
+        memset(&st, 0, sizeof(st));
+        orc_pure_mcts(a->cfg, g, &root, &mv, &v, T, cap, &st);
+        a->playouts += (int64_t)st.playouts;
+        a->searches++;
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        if ((double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec) >= a->seconds) break;
+    }
+    free(T);
+    return NULL;
+}
+
+int64_t orc_pure_mcts_bench(const oaz_pure_mcts_config* cfg, int threads, double seconds, int64_t* searches) {
+    pthread_t th[256];
+    pm_bench_arg args[256];
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    for (int i = 0; i < threads; ++i) {
+        args[i].cfg = cfg;
+        args[i].seconds = seconds;
+        args[i].tid = i;
+        args[i].playouts = args[i].searches = 0;
+        pthread_create(&th[i], NULL, pm_bench_worker, &args[i]);
+    }
+    int64_t total = 0, ns = 0;
+    for (int i = 0; i < threads; ++i) {
+        pthread_join(th[i], NULL);
+        total += args[i].playouts;
+        ns += args[i].searches;
+    }
+    if (searches) *searches = ns;
+    return total;
+}

@@ -96,6 +96,14 @@ int orc_selfplay_game(const orc_selfplay_cfg* cfg, uint64_t game_id, oaz_sample*
 int64_t orc_selfplay_bench(const orc_selfplay_cfg* cfg, int threads, double seconds,
                            int64_t* games_done, int64_t* plies_done);
 
+/* Pure MCTS agent (onitama-game/src/ai/mcts/mcts_arena.rs): one search from `root`.
+ * Tree nodes use the ABI's oaz_pure_node layout so tests can compare them byte for byte.
+ * Rollout draws: Philox(seed; game_id, playout, 0x9C7A0000, d/4) word d%4, uniform int
+ * (u32 * n) >> 32 — the stream the GPU uses. Returns the node count or <0. */
+int orc_pure_mcts(const oaz_pure_mcts_config* cfg, uint64_t game_id, const oaz_state* root, oaz_move* out_move,
+                  float* out_value, oaz_pure_node* nodes, int cap, oaz_pure_mcts_stats* stats);
+int64_t orc_pure_mcts_bench(const oaz_pure_mcts_config* cfg, int threads, double seconds, int64_t* searches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -78,6 +78,9 @@ def load() -> C.CDLL:
         "orc_selfplay_game": (C.c_int, [P(orc_selfplay_cfg), C.c_uint64, V, C.c_int, P(C.c_int), P(C.c_int),
                                         P(_abi.oaz_search_stats)]),
         "orc_selfplay_bench": (C.c_int64, [P(orc_selfplay_cfg), C.c_int, C.c_double, P(C.c_int64), P(C.c_int64)]),
+        "orc_pure_mcts": (C.c_int, [P(_abi.oaz_pure_mcts_config), C.c_uint64, V, V, V, V, C.c_int,
+                                    P(_abi.oaz_pure_mcts_stats)]),
+        "orc_pure_mcts_bench": (C.c_int64, [P(_abi.oaz_pure_mcts_config), C.c_int, C.c_double, P(C.c_int64)]),
     }
     for name, (res, args) in protos.items():
         f = getattr(lib, name)
@@ -234,3 +237,22 @@ def selfplay_bench(search: orc_search_cfg, threads: int, seconds: float, max_pli
     games, plies = C.c_int64(0), C.c_int64(0)
     sims = load().orc_selfplay_bench(C.byref(cfg), threads, seconds, C.byref(games), C.byref(plies))
     return sims, games.value, plies.value
+
+
+def pure_mcts(cfg, game_id: int, root: np.ndarray, cap: int = 0):
+    """orc_pure_mcts: (move, value, tree nodes, stats)."""
+    root = np.ascontiguousarray(root.reshape(1), dtype=_abi.STATE_DTYPE)
+    cap = cap or int(_abi.load().oaz_pure_mcts_tree_capacity(C.byref(cfg)))
+    nodes = np.zeros(cap, dtype=_abi.PURE_NODE_DTYPE)
+    mv = np.zeros(1, dtype=_abi.MOVE_DTYPE)
+    val = C.c_float(0)
+    st = _abi.oaz_pure_mcts_stats()
+    n = load().orc_pure_mcts(C.byref(cfg), game_id, P_(root), P_(mv), C.byref(val), P_(nodes), cap, C.byref(st))
+    assert n > 0, n
+    return mv[0], val.value, nodes[:n], st
+
+
+def pure_mcts_bench(cfg, threads: int, seconds: float):
+    searches = C.c_int64(0)
+    playouts = load().orc_pure_mcts_bench(C.byref(cfg), threads, seconds, C.byref(searches))
+    return playouts, searches.value

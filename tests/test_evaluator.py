@@ -177,3 +177,4 @@ def test_evaluator_pit():
     pit, promote = ev.pit(sims=16)
     assert promote == (pit.self_fight.winrate > 0.55)
     assert pit.random_fight is not None and len(pit.random_fight.results) == 4
+    assert pit.mcts_fight is not None and len(pit.mcts_fight.results) == 4
