@@ -14,11 +14,15 @@ from .mcts import (AlphaZeroMcts, AlphaZeroMctsConfig, ConvResNet, ConvResNetCon
 from .selfplay import SelfPlayData, TrainConfig, self_play
 from .evaluator import (AlphaZeroAgent, EloRating, Evaluator, EvaluatorConfig, FightStatistics, PitStatistics,
                         RandomAgent, fight)
+from .pure_mcts import Mcts, pure_mcts_search
+from .trainer import Trainer, train_epochs
+from .train_loop import LoopConfig, Stats, train
 
 __all__ = [
     "_abi", "OazError", "load", "Engine", "SearchResult", "CARD_NAMES", "ORIGINAL_CARDS", "Card", "Deck",
     "DoneMove", "GameState", "Move", "MoveResult", "PieceKind", "PlayerColor", "State", "AlphaZeroMcts",
     "AlphaZeroMctsConfig", "ConvResNet", "ConvResNetConfig", "Options", "TrainingAlphaZeroMcts", "reward",
     "SelfPlayData", "TrainConfig", "self_play", "AlphaZeroAgent", "EloRating", "Evaluator", "EvaluatorConfig",
-    "FightStatistics", "PitStatistics", "RandomAgent", "fight",
+    "FightStatistics", "PitStatistics", "RandomAgent", "fight", "Mcts", "pure_mcts_search", "Trainer", "train_epochs",
+    "LoopConfig", "Stats", "train",
 ]

@@ -151,3 +151,29 @@ def test_train_epochs_reduce_loss(orc):
         hist = train_epochs(tr, samples, epochs=6, batch=128, seed=0)
     assert len(hist) == 6 and all(h.steps == 8 for h in hist)
     assert hist[-1].loss < hist[0].loss, [h.loss for h in hist]
+
+
+@pytest.mark.gpu
+def test_alphazero_loop_end_to_end(tmp_path):
+    """train.rs:158-412 in miniature: self-play -> SGD epochs -> pit -> checkpoints."""
+    import json
+    import os
+    from onitama_az.evaluator import EvaluatorConfig
+    from onitama_az.mcts import AlphaZeroMctsConfig, ConvResNetConfig
+    from onitama_az.train_loop import LoopConfig, train
+    from onitama_az.weights import blob_from_named, read_ot
+    cfg = LoopConfig(model_config=ConvResNetConfig(resnet_block_amnt=1),
+                     mcts_config=AlphaZeroMctsConfig(exploration_c=5.0, max_playouts=8, train=True),
+                     iterations=2, training_epochs=2, train_batch_size=32, self_play_game_amnt=16,
+                     save_checkpoint=2, evaluation_checkpoint=1, max_plies=40,
+                     evaluator_config=EvaluatorConfig(game_amnt=2, max_plies=20, seed=3))
+    st = train(cfg, folder=str(tmp_path), eval_sims=8)
+    assert st.iteration == [1, 2] and len(st.fight_statistics) == 2
+    assert all(g["positions_retrieved"] > 32 for g in st.games_played)
+    assert all(np.isfinite(st.loss))
+    files = os.listdir(tmp_path)
+    ckpt = [f for f in files if f.startswith("model_2_") and f.endswith(".ot")]
+    assert ckpt and "stats.json" in files
+    w = blob_from_named(read_ot(str(tmp_path / ckpt[0])), 1)
+    assert w.size == 240006 - 2 * 2 * (64 * 64 * 9 + 64 * 5)
+    json.load(open(tmp_path / "stats.json"))
