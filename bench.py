@@ -426,7 +426,7 @@ def main():
                                    "root_noise_stream2": kt.noise_ms / args.steps},
             "roofline": {"bound": "mfma",
                          "kernel": "k_nn_sq16<fp32> (fused ResNet, v_mfma_f32_16x16x4_f32)" if cfg["precision"] == "fp32"
-                         else "k_nn_sq16<bf16> (fused ResNet, v_mfma_f32_16x16x32_bf16)",
+                         else "k_nn_bf16g<2> (fused ResNet, 8 waves x 2 N-tiles, v_mfma_f32_16x16x32_bf16)",
                          "achieved": achieved, "peak": PEAK_TFLOPS[cfg["precision"]], "unit": "TFLOP/s",
                          "frac": achieved / PEAK_TFLOPS[cfg["precision"]],
                          "traffic": traffic["bytes_per_launch"] if traffic else None,

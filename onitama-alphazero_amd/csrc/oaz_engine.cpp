@@ -723,6 +723,10 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
     w.blob = e->weights;
     w.blocks = e->cfg.blocks;
     w.bf16 = e->cfg.precision == OAZ_BF16;
+    {
+        const char* v1 = getenv("OAZ_NN_BF16_V1");
+        w.bf16_v1 = v1 ? atoi(v1) : 0;  // 0: 8 waves x 2 N-tiles, 1: k_nn_sq16<bf16>, 2: 4 waves x 4 N-tiles
+    }
     return timed(e, 1, B, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, e->stream); });
 }
 

@@ -76,6 +76,7 @@ struct NNView {
     const float* blob;  // packed, BN-folded weights (DESIGN.md "NN weights layout")
     int32_t blocks;
     int32_t bf16;       // 1: bf16 MFMA inputs (fp32 accumulate)
+    int32_t bf16_v1;    // bf16 kernel variant (OAZ_NN_BF16_V1): 0 k_nn_bf16g<2>, 1 k_nn_sq16<bf16>, 2 k_nn_bf16g<4>
 };
 
 // rules

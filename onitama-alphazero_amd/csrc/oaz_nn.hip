@@ -353,13 +353,182 @@ __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __
     for (int s = wave; s < nn::kSB; s += nn::kWaves) heads<BF16>(act, scratch, s, p, lane, b0 + s, B, policy, value);
 }
 
+// ---- bf16, 4 waves x 4 N-tiles ------------------------------------------------------------------
+// Each wave owns all 64 output channels (4 N-tiles) of one square group, so every A fragment read
+// from LDS (one (square, tap) of 16 positions x 64 channels) feeds 8 MFMAs instead of 2: LDS
+// traffic per MFMA drops 4x, which is what bounds the 8-wave bf16 variant. Groups (corner, edges,
+// interior squares; on-board taps 40 / 40 / 46 / 43):
+namespace nn4 {
+constexpr int kTPW = 7;
+constexpr int lds_floats(int waves) { return nn::kSB * 25 * nn::kRSh / 2 + waves * nn::kScratch; }
+}
+__constant__ int8_t c_sq4[4][nn4::kTPW] = {{0, 1, 2, 3, 6, 7, 0}, {4, 9, 14, 19, 8, 13, 0},
+                                           {20, 5, 10, 15, 21, 11, 16}, {24, 22, 23, 12, 17, 18, 0}};
+__constant__ int8_t c_sq4_n[4] = {6, 6, 7, 6};
+
+// NPW = N-tiles per wave: 4 -> 4 waves (one per square group), 2 -> 8 waves (2 per group).
+template <int NPW>
+__global__ void __launch_bounds__(64 * 16 / NPW) k_nn_bf16g(const oaz_state* __restrict__ states, int B,
+                                                           const float* __restrict__ blob, int blocks,
+                                                           float* __restrict__ policy, float* __restrict__ value) {
+    constexpr int kWaves = 16 / NPW, kSplit = 4 / NPW;
+    constexpr int kImageFloats = nn::kSB * 25 * nn::kRSh / 2;
+    constexpr int T = nn4::kTPW;
+    __shared__ __attribute__((aligned(16))) float lds[nn4::lds_floats(kWaves)];
+    __bf16* act = reinterpret_cast<__bf16*>(lds);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int i = lane & 15, kq = lane >> 4;
+    const int grp = wave / kSplit, n0 = (wave % kSplit) * NPW;
+    const int ntiles = c_sq4_n[grp];
+    int sq[T];
+#pragma unroll
+    for (int j = 0; j < T; ++j) sq[j] = c_sq4[grp][j];
+    const int b0 = blockIdx.x * nn::kSB;
+    int* pinfo = reinterpret_cast<int*>(lds + kImageFloats);
+    f32x4 acc[T][NPW];
+
+    // first layer: 4 bitboards through the fp32 MFMA + the constant-plane table (see k_nn_sq16)
+    {
+        const int b = b0 + i < B ? b0 + i : b0;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
+        const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
+        if (tid < nn::kSB) {
+            const oaz_state st = states[b];
+            const int blue = st.to_move & 1;
+            const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
+            pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < T; ++j)
+#pragma unroll
+            for (int n = 0; n < NPW; ++n) acc[j][n] = f32x4{};
+        for (int t = 0; t < 9; ++t) {
+            float bw[NPW];
+#pragma unroll
+            for (int n = 0; n < NPW; ++n) bw[n] = blob[(t * 4 + n0 + n) * 64 + lane];
+#pragma unroll
+            for (int j = 0; j < T; ++j) {
+                const int nb = nbr_index(sq[j], t);
+                if (j < ntiles && nb < 25) {
+                    const float a = (float)((bb >> (31 - nb)) & 1u);
+#pragma unroll
+                    for (int n = 0; n < NPW; ++n) acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bw[n], acc[j][n], 0, 0, 0);
+                }
+            }
+        }
+        const float* bias = blob + nn::kL1B;
+        const float* table = bias + nn::kCh;
+#pragma unroll
+        for (int n = 0; n < NPW; ++n) {
+            const int co = (n0 + n) * 16 + i;
+            const float bbias = bias[co];
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+                if (j < ntiles)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int pos = kq * 4 + r;
+                        const int info = pinfo[pos];
+                        const float* ts = table + (size_t)sq[j] * 17 * nn::kCh + co;
+                        float v = acc[j][n][r] + bbias + ts[(info & 15) * nn::kCh] + ts[((info >> 4) & 15) * nn::kCh];
+                        if (info & 0x100) v += ts[16 * nn::kCh];
+                        act[(sq[j] * nn::kSB + pos) * nn::kRSh + co] = (__bf16)(v > 0.0f ? v : 0.0f);
+                    }
+        }
+        __syncthreads();
+    }
+
+    const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
+    // residual input kept as packed bf16 pairs (exact: the LDS image is bf16)
+    uint32_t skip[T][NPW][2];
+    const __bf16* abase = act + i * nn::kRSh + 8 * kq;
+    auto conv = [&](const bf16x8* W) {
+#pragma unroll
+        for (int j = 0; j < T; ++j)
+#pragma unroll
+            for (int n = 0; n < NPW; ++n) acc[j][n] = f32x4{};
+        for (int t = 0; t < 9; ++t) {
+            bf16x8 bw[2][NPW];
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int n = 0; n < NPW; ++n) bw[m][n] = W[((t * 2 + m) * 4 + n0 + n) * 64 + lane];
+#pragma unroll
+            for (int j = 0; j < T; ++j) {
+                const int nb = nbr_index(sq[j], t);
+                if (j < ntiles && nb < 25) {
+                    const __bf16* a = abase + nb * nn::kSB * nn::kRSh;
+                    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(a);
+                    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(a + 32);
+#pragma unroll
+                    for (int n = 0; n < NPW; ++n) {
+                        acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw[0][n], acc[j][n], 0, 0, 0);
+                        acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bw[1][n], acc[j][n], 0, 0, 0);
+                    }
+                }
+            }
+        }
+    };
+    auto epilogue = [&](const float* bias, bool with_skip) {
+#pragma unroll
+        for (int n = 0; n < NPW; ++n) {
+            const int co = (n0 + n) * 16 + i;
+            const float bb = bias[co];
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+                if (j < ntiles)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float v = acc[j][n][r] + bb;
+                        if (with_skip) {
+                            const uint32_t w = skip[j][n][r >> 1];
+                            v += __uint_as_float((r & 1) ? (w & 0xFFFF0000u) : (w << 16));
+                        }
+                        act[(sq[j] * nn::kSB + kq * 4 + r) * nn::kRSh + co] = (__bf16)(v > 0.0f ? v : 0.0f);
+                    }
+        }
+    };
+    for (int blk = 0; blk < blocks; ++blk) {
+#pragma unroll
+        for (int n = 0; n < NPW; ++n)
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+                if (j < ntiles)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const unsigned short* q = reinterpret_cast<const unsigned short*>(
+                            act + (sq[j] * nn::kSB + kq * 4 + 2 * h) * nn::kRSh + (n0 + n) * 16 + i);
+                        skip[j][n][h] = (uint32_t)q[0] | ((uint32_t)q[nn::kRSh] << 16);
+                    }
+        conv(reinterpret_cast<const bf16x8*>(p));  // small block 1: conv + BN + ReLU
+        p += nn::kW64h;
+        __syncthreads();
+        epilogue(p, false);
+        p += nn::kCh;
+        __syncthreads();
+        conv(reinterpret_cast<const bf16x8*>(p));  // small block 2: conv + BN, + skip, ReLU
+        p += nn::kW64h;
+        __syncthreads();
+        epilogue(p, true);
+        p += nn::kCh;
+        __syncthreads();
+    }
+    float* scratch = lds + kImageFloats + wave * nn::kScratch;
+    for (int s = wave; s < nn::kSB; s += kWaves) heads<true>(act, scratch, s, p, lane, b0 + s, B, policy, value);
+}
+
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy, float* value,
                              hipStream_t st) {
     if (B <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
-    if (w.bf16)
+    if (w.bf16 && w.bf16_v1 == 1)
         hipLaunchKernelGGL(k_nn_sq16<true>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
                            value);
+    else if (w.bf16 && w.bf16_v1 == 0)
+        hipLaunchKernelGGL(k_nn_bf16g<2>, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value);
+    else if (w.bf16)
+        hipLaunchKernelGGL(k_nn_bf16g<4>, dim3(grid), dim3(64 * 4), 0, st, s, B, w.blob, w.blocks, policy, value);
     else
         hipLaunchKernelGGL(k_nn_sq16<false>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
                            value);
