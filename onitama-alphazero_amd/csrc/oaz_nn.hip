@@ -153,6 +153,36 @@ __device__ __forceinline__ void conv64(f32x4 (&acc)[nn::kTPW], const float* act,
     }
 }
 
+// First layer, constant planes: the mover's two card planes and the blue-to-move plane are
+// constant over the board, so per square their contribution is sum_c onehot[pos][c] * T[sq][c][co]
+// with T the host table (folded weights summed over the on-board taps). That is a K = 17 (padded
+// to 20) GEMM per square: 5 v_mfma_f32_16x16x4_f32 whose A operand (0/1) is built from the
+// position's cards in registers and whose B operand is read from the table, all loads independent.
+__device__ __forceinline__ void conv_l1_const(f32x4 (&acc)[nn::kTPW], const float* table, int cinfo,
+                                              const int (&sq)[nn::kTPW], int lane, int nt, int ntiles) {
+    const int kq = lane >> 4, co = nt * 16 + (lane & 15);
+    const int c0 = cinfo & 15, c1 = (cinfo >> 4) & 15, blue = (cinfo >> 8) & 1;
+    float a[5];
+#pragma unroll
+    for (int st = 0; st < 5; ++st) {
+        const int k = 4 * st + kq;
+        a[st] = k < 16 ? ((k == c0 || k == c1) ? 1.0f : 0.0f) : (k == 16 ? (float)blue : 0.0f);
+    }
+#pragma unroll
+    for (int j = 0; j < nn::kTPW; ++j)
+        if (j < ntiles) {
+            const float* ts = table + (size_t)sq[j] * 17 * nn::kCh + co;
+            float b[5];
+#pragma unroll
+            for (int st = 0; st < 5; ++st) {
+                const int k = 4 * st + kq;
+                b[st] = k < 17 ? ts[k * nn::kCh] : 0.0f;
+            }
+#pragma unroll
+            for (int st = 0; st < 5; ++st) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], b[st], acc[j], 0, 0, 0);
+        }
+}
+
 // bf16: acc[j] += conv3x3 over 64 channels with v_mfma_f32_16x16x32_bf16. For K-half m, lane
 // l supplies A[row l&15][k = 8(l>>4) + e] = channel 32m + 8(l>>4) + e (natural order).
 __device__ __forceinline__ void conv64_bf16(f32x4 (&acc)[nn::kTPW], const __bf16* act, const bf16x8* W,
@@ -319,7 +349,8 @@ __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __
 #pragma unroll
         for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
         conv_l1(acc, bb, blob, sq, lane, nt, ntiles);
-        epilogue_l1<BF16>(acc, act, blob + nn::kL1B, blob + nn::kL1B + nn::kCh, pinfo, sq, lane, nt, ntiles);
+        conv_l1_const(acc, blob + nn::kL1B + nn::kCh, pinfo[lane & 15], sq, lane, nt, ntiles);
+        epilogue<BF16>(acc, act, blob + nn::kL1B, nullptr, sq, lane, nt, ntiles);
         __syncthreads();
     }
 
@@ -417,8 +448,31 @@ __global__ void __launch_bounds__(64 * 16 / NPW) k_nn_bf16g(const oaz_state* __r
                 }
             }
         }
+        {  // constant planes (cards, colour) as 5 MFMA k-steps per (square, N-tile), see conv_l1_const
+            const float* table = blob + nn::kL1B + nn::kCh;
+            const int cinfo = pinfo[i];
+            const int c0 = cinfo & 15, c1 = (cinfo >> 4) & 15, blue = (cinfo >> 8) & 1;
+            float a[5];
+#pragma unroll
+            for (int st = 0; st < 5; ++st) {
+                const int k = 4 * st + kq;
+                a[st] = k < 16 ? ((k == c0 || k == c1) ? 1.0f : 0.0f) : (k == 16 ? (float)blue : 0.0f);
+            }
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+                if (j < ntiles)
+#pragma unroll
+                    for (int n = 0; n < NPW; ++n) {
+                        const float* ts = table + (size_t)sq[j] * 17 * nn::kCh + (n0 + n) * 16 + i;
+#pragma unroll
+                        for (int st = 0; st < 5; ++st) {
+                            const int k = 4 * st + kq;
+                            const float b = k < 17 ? ts[k * nn::kCh] : 0.0f;
+                            acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], b, acc[j][n], 0, 0, 0);
+                        }
+                    }
+        }
         const float* bias = blob + nn::kL1B;
-        const float* table = bias + nn::kCh;
 #pragma unroll
         for (int n = 0; n < NPW; ++n) {
             const int co = (n0 + n) * 16 + i;
@@ -428,12 +482,8 @@ __global__ void __launch_bounds__(64 * 16 / NPW) k_nn_bf16g(const oaz_state* __r
                 if (j < ntiles)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int pos = kq * 4 + r;
-                        const int info = pinfo[pos];
-                        const float* ts = table + (size_t)sq[j] * 17 * nn::kCh + co;
-                        float v = acc[j][n][r] + bbias + ts[(info & 15) * nn::kCh] + ts[((info >> 4) & 15) * nn::kCh];
-                        if (info & 0x100) v += ts[16 * nn::kCh];
-                        act[(sq[j] * nn::kSB + pos) * nn::kRSh + co] = (__bf16)(v > 0.0f ? v : 0.0f);
+                        const float v = acc[j][n][r] + bbias;
+                        act[(sq[j] * nn::kSB + kq * 4 + r) * nn::kRSh + co] = (__bf16)(v > 0.0f ? v : 0.0f);
                     }
         }
         __syncthreads();
