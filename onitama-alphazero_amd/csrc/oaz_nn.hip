@@ -131,24 +131,45 @@ __device__ __forceinline__ void conv64(f32x4 (&acc)[nn::kTPW], const float* act,
     const int i = lane & 15, kq = lane >> 4;
     const float* base = act + i * nn::kRS + 4 * kq;
     for (int t = 0; t < 9; ++t) {
-        int off[nn::kTPW];  // wave-uniform: row offset of the neighbour square, -1 if off board
+        // Wave-uniform (scalar) neighbour offsets and on-board mask: the skip test becomes a scalar
+        // branch, and every A fragment of a k-group is requested before the first MFMA so the LDS
+        // latency hides behind the MFMAs of the earlier squares. Off-board squares load a harmless
+        // row (their own square) and skip their MFMAs.
+        int off[nn::kTPW];
+        uint32_t vm = 0;
 #pragma unroll
         for (int j = 0; j < nn::kTPW; ++j) {
             const int nb = nbr_index(sq[j], t);
-            off[j] = (j < ntiles && nb < 25) ? nb * nn::kSB * nn::kRS : -1;
+            const bool ok = j < ntiles && nb < 25;
+            off[j] = __builtin_amdgcn_readfirstlane((ok ? nb : sq[j]) * nn::kSB * nn::kRS);
+            vm |= (ok ? 1u : 0u) << j;
         }
+        vm = __builtin_amdgcn_readfirstlane(vm);
+        float4 b = W[((t * 4 + 0) * 4 + nt) * 64 + lane];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            const float4 b = W[((t * 4 + g) * 4 + nt) * 64 + lane];
+            const float4 bn = W[((t * 4 + (g < 3 ? g + 1 : g)) * 4 + nt) * 64 + lane];  // next k-group's B
+            constexpr int kH = (nn::kTPW + 1) / 2;  // two batches of A fragments (register budget)
 #pragma unroll
-            for (int j = 0; j < nn::kTPW; ++j)
-                if (off[j] >= 0) {
-                    const float4 a = *reinterpret_cast<const float4*>(base + off[j] + 16 * g);
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc[j], 0, 0, 0);
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc[j], 0, 0, 0);
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc[j], 0, 0, 0);
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc[j], 0, 0, 0);
+            for (int h = 0; h < 2; ++h) {
+                float4 a[kH];
+#pragma unroll
+                for (int q = 0; q < kH; ++q) {
+                    const int j = h * kH + q;
+                    if (j < nn::kTPW) a[q] = *reinterpret_cast<const float4*>(base + off[j] + 16 * g);
                 }
+#pragma unroll
+                for (int q = 0; q < kH; ++q) {
+                    const int j = h * kH + q;
+                    if (j < nn::kTPW && (vm & (1u << j))) {
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].x, b.x, acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].y, b.y, acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].z, b.z, acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].w, b.w, acc[j], 0, 0, 0);
+                    }
+                }
+            }
+            b = bn;
         }
     }
 }
