@@ -525,18 +525,38 @@ __global__ void __launch_bounds__(64 * 16 / NPW) k_nn_bf16g(const oaz_state* __r
             for (int m = 0; m < 2; ++m)
 #pragma unroll
                 for (int n = 0; n < NPW; ++n) bw[m][n] = W[((t * 2 + m) * 4 + n0 + n) * 64 + lane];
+            // scalar offsets / on-board mask; A fragments of a batch requested before its MFMAs
+            int off[T];
+            uint32_t vm = 0;
 #pragma unroll
             for (int j = 0; j < T; ++j) {
                 const int nb = nbr_index(sq[j], t);
-                if (j < ntiles && nb < 25) {
-                    const __bf16* a = abase + nb * nn::kSB * nn::kRSh;
-                    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(a);
-                    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(a + 32);
+                const bool ok = j < ntiles && nb < 25;
+                off[j] = __builtin_amdgcn_readfirstlane((ok ? nb : sq[j]) * nn::kSB * nn::kRSh);
+                vm |= (ok ? 1u : 0u) << j;
+            }
+            vm = __builtin_amdgcn_readfirstlane(vm);
+            constexpr int kH = (T + 1) / 2;
 #pragma unroll
-                    for (int n = 0; n < NPW; ++n) {
-                        acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw[0][n], acc[j][n], 0, 0, 0);
-                        acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bw[1][n], acc[j][n], 0, 0, 0);
+            for (int h = 0; h < 2; ++h) {
+                bf16x8 a0[kH], a1[kH];
+#pragma unroll
+                for (int q = 0; q < kH; ++q) {
+                    const int j = h * kH + q;
+                    if (j < T) {
+                        a0[q] = *reinterpret_cast<const bf16x8*>(abase + off[j]);
+                        a1[q] = *reinterpret_cast<const bf16x8*>(abase + off[j] + 32);
                     }
+                }
+#pragma unroll
+                for (int q = 0; q < kH; ++q) {
+                    const int j = h * kH + q;
+                    if (j < T && (vm & (1u << j)))
+#pragma unroll
+                        for (int n = 0; n < NPW; ++n) {
+                            acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[q], bw[0][n], acc[j][n], 0, 0, 0);
+                            acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[q], bw[1][n], acc[j][n], 0, 0, 0);
+                        }
                 }
             }
         }
