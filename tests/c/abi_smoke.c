@@ -1,0 +1,103 @@
+/* abi_smoke.c — the C ABI used from plain C, as a Rust/C host would bind it.
+ * Built by tests/test_c_abi.py with gcc against include/onitama_az.h and libonitama_az.so.
+ * Without a GPU it checks the host-side entry points and the loud no-device errors; with one it
+ * runs a batched search, a self-play game batch and the pure-MCTS agent. Prints "OK ..." lines. */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "onitama_az.h"
+
+#define CHECK(c)                                                                   \
+    do {                                                                           \
+        if (!(c)) {                                                                \
+            fprintf(stderr, "FAIL %s:%d %s (%s)\n", __FILE__, __LINE__, #c, oaz_last_error()); \
+            return 1;                                                              \
+        }                                                                          \
+    } while (0)
+
+int main(void) {
+    CHECK(oaz_abi_version() == OAZ_ABI_VERSION);
+    oaz_config cfg;
+    oaz_config_default(&cfg);
+    CHECK(cfg.blocks == 5 && cfg.sims == 400 && cfg.max_plies == 150);
+    CHECK(oaz_weight_count(3, 64, 21) == 240006);
+    uint32_t maps[2 * 16 * 25];
+    oaz_attack_maps(maps);
+    uint8_t deck[5] = {0, 1, 2, 3, 4};
+    oaz_state s;
+    oaz_initial_state(deck, &s);
+    CHECK(s.kings[0] == 0x200u && s.kings[1] == 0x20000000u && s.to_move == 1); /* Crab neutral: Blue starts */
+    printf("OK host\n");
+    int ndev = 0;
+    oaz_device_count(&ndev);
+    if (ndev == 0) {
+        CHECK(oaz_create(&cfg, 0) == NULL && strstr(oaz_last_error(), "device") != NULL);
+        CHECK(oaz_movegen(&s, 1, NULL, NULL, NULL) == OAZ_ERR_NO_DEVICE);
+        printf("OK no-device\n");
+        return 0;
+    }
+    /* rules */
+    oaz_move moves[40];
+    uint8_t count = 0;
+    CHECK(oaz_movegen(&s, 1, NULL, moves, &count) == 0 && count == 8); /* Frog + Rabbit from the start (oracle) */
+    /* one batched search per root (mirrors generate_move_tensor) */
+    cfg.blocks = 3;
+    cfg.sims = 64;
+    cfg.games = 4;
+    cfg.train_noise = 0;
+    oaz_engine* e = oaz_create(&cfg, 0);
+    CHECK(e != NULL);
+    size_t nw = oaz_weight_count(3, 64, 21);
+    float* w = (float*)malloc(nw * sizeof(float));
+    CHECK(oaz_random_weights(0, 3, w, nw) == 0 && oaz_load_weights(e, w, nw) == 0);
+    oaz_state roots[4];
+    for (int g = 0; g < 4; ++g) {
+        uint8_t d[5];
+        oaz_deal_deck(20260101ull, (uint64_t)g, d);
+        oaz_initial_state(d, &roots[g]);
+    }
+    oaz_move out[4];
+    float pi[4 * 50], rv[4];
+    oaz_search_stats st;
+    CHECK(oaz_search(e, roots, 4, out, pi, rv, &st) == 0 && st.sims == 4 * 64);
+    for (int g = 0; g < 4; ++g) {
+        float sum = 0;
+        for (int k = 0; k < 50; ++k) sum += pi[g * 50 + k];
+        CHECK(sum > 0.999f && sum < 1.001f && out[g].from < 25);
+    }
+    printf("OK search\n");
+    /* self-play */
+    oaz_sample* buf = (oaz_sample*)malloc(sizeof(oaz_sample) * 4 * 152);
+    size_t n = 0;
+    oaz_selfplay_stats sp;
+    CHECK(oaz_selfplay_run(e, 4, buf, 4 * 152, &n, &sp) == 0 && sp.games_finished + sp.games_cut == 4 && n > 0);
+    printf("OK selfplay %zu samples\n", n);
+    /* pure MCTS agent */
+    oaz_pure_mcts_config pc;
+    oaz_pure_mcts_config_default(&pc);
+    pc.max_playouts = 200;
+    oaz_move pm[4];
+    float pv[4];
+    oaz_pure_mcts_stats ps;
+    CHECK(oaz_pure_mcts_search(roots, 4, &pc, pm, pv, &ps, NULL, 0) == 0 && ps.playouts == 800);
+    printf("OK pure_mcts\n");
+    /* training step */
+    oaz_train_config tc;
+    oaz_train_config_default(&tc);
+    tc.blocks = 3;
+    tc.max_batch = 32;
+    oaz_trainer* t = oaz_trainer_create(&tc, 0);
+    CHECK(t != NULL && oaz_trainer_set_weights(t, w, nw) == 0 && oaz_trainer_load_samples(t, buf, n) == 0);
+    int32_t idx[32];
+    for (int i = 0; i < 32; ++i) idx[i] = (int32_t)(i % n);
+    double losses[3];
+    CHECK(oaz_trainer_set_batches(t, idx, 1, 32) == 0 && oaz_trainer_train(t, 0, 1) == 0);
+    CHECK(oaz_trainer_losses(t, losses) == 0 && losses[2] == 1.0 && losses[0] >= 0.0 && losses[1] > 0.0);
+    printf("OK train loss %.4f %.4f\n", losses[0], losses[1]);
+    oaz_trainer_destroy(t);
+    oaz_destroy(e);
+    free(buf);
+    free(w);
+    return 0;
+}
