@@ -390,7 +390,9 @@ struct oaz_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;       // root-noise producer, overlaps the NN kernel
+    hipStream_t stream3 = nullptr;       // second half of the games (tree kernels overlap the other half's NN)
     hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_consumed[2] = {nullptr, nullptr};
+    hipEvent_t ev_nn[2] = {nullptr, nullptr}, ev_join = nullptr;
     double* noise = nullptr;             // [2][kNoiseChunk][G][kNoiseStride]
     uint32_t G = 0, cap = 0, pathcap = 0, hcap = 0, out_cap = 0;
     // trees
@@ -531,6 +533,7 @@ static int timed(oaz_engine* e, int kind, uint32_t samples, F&& launch, hipStrea
     if (e->pending.size() > 4096) {  // resolve periodically to bound the pool
         HIP_TRY(hipStreamSynchronize(e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream2));
+        HIP_TRY(hipStreamSynchronize(e->stream3));
         for (auto& p : e->pending) {
             float ms = 0.f;
             (void)hipEventElapsedTime(&ms, p.a, p.b);
@@ -589,7 +592,11 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         return fail();
     }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_nn[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_nn[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess) {
         oaz_set_err(OAZ_ERR_HIP, "stream create failed");
         return fail();
     }
@@ -635,10 +642,13 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->stream2) (void)hipStreamSynchronize(e->stream2);
+    if (e->stream3) (void)hipStreamSynchronize(e->stream3);
     for (int i = 0; i < 2; ++i) {
         if (e->ev_ready[i]) (void)hipEventDestroy(e->ev_ready[i]);
         if (e->ev_consumed[i]) (void)hipEventDestroy(e->ev_consumed[i]);
+        if (e->ev_nn[i]) (void)hipEventDestroy(e->ev_nn[i]);
     }
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     for (auto& p : e->pending) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -651,6 +661,7 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     for (void* p : ptrs) dfree(p);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
+    if (e->stream3) (void)hipStreamDestroy(e->stream3);
     delete e;
 }
 
@@ -679,6 +690,7 @@ extern "C" int oaz_sync(oaz_engine* e) {
     if (!e) return oaz_set_err(OAZ_ERR_ARG, "sync: null");
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream2));
+    HIP_TRY(hipStreamSynchronize(e->stream3));
     return 0;
 }
 
@@ -691,6 +703,7 @@ extern "C" int oaz_set_timing(oaz_engine* e, int enable) {
 static int resolve_timing(oaz_engine* e) {
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream2));
+    HIP_TRY(hipStreamSynchronize(e->stream3));
     for (auto& p : e->pending) {
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b));
@@ -716,9 +729,11 @@ extern "C" int oaz_kernel_times_reset(oaz_engine* e) {
     return 0;
 }
 
-static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float* d_pol, float* d_val) {
+static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float* d_pol, float* d_val,
+                    hipStream_t st = nullptr) {
+    if (!st) st = e->stream;
     if (e->cfg.evaluator == OAZ_EVAL_HASH)
-        return timed(e, 1, B, [&] { return launch_hash_eval(d_states, (int)B, d_pol, d_val, e->stream); });
+        return timed(e, 1, B, [&] { return launch_hash_eval(d_states, (int)B, d_pol, d_val, st); }, st);
     NNView w;
     w.blob = e->weights;
     w.blocks = e->cfg.blocks;
@@ -727,7 +742,7 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
         const char* v1 = getenv("OAZ_NN_BF16_V1");
         w.bf16_v1 = v1 ? atoi(v1) : 0;  // 0: 8 waves x 2 N-tiles, 1: k_nn_sq16<bf16>, 2: 4 waves x 4 N-tiles
     }
-    return timed(e, 1, B, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, e->stream); });
+    return timed(e, 1, B, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, st); }, st);
 }
 
 extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* policy, float* value) {
@@ -746,6 +761,20 @@ extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* p
 // All cfg.sims simulations of one move for every game: select -> evaluate -> expand/backup,
 // in lock step. With root noise, k_root_noise fills chunk c+1 of the double-buffered noise
 // ring on stream2 while stream 1 runs chunk c (events order the two ring slots).
+// The trees of games [g0, g0 + n) as a view of their own (every per-game array offset).
+static TreeView slice_view(const TreeView& t, uint32_t g0, uint32_t n) {
+    TreeView v = t;
+    v.nodes = t.nodes + (size_t)g0 * t.cap;
+    v.n_nodes = t.n_nodes + g0;
+    v.path = t.path + (size_t)g0 * t.pathcap;
+    v.depth = t.depth + g0;
+    v.leaf = t.leaf + g0;
+    v.leaf_state = t.leaf_state + g0;
+    v.stats = t.stats + (size_t)g0 * GS_COUNT;
+    v.G = n;
+    return v;
+}
+
 static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, const uint8_t* active,
                     const uint64_t* gids, const uint32_t* plies) {
     const SearchParams prm = search_params(e);
@@ -769,24 +798,63 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
         HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[0], 0));
         if (int rc = produce(0)) return rc;
     }
+    // Optional (OAZ_SPLIT_HALVES=1): two halves of the games on two streams, the NN launches of the
+    // halves alternating and each half's select / expand-backup running beside the other half's NN.
+    // Measured no faster on MI355X (C3 11.88 vs 11.93 M sims/s; the tree kernels slow down 4x
+    // beside the NN), so one stream is the default.
+    const bool split = t.G >= 4096 && getenv("OAZ_SPLIT_HALVES") && getenv("OAZ_SPLIT_HALVES")[0] == '1';
+    const uint32_t GA = split ? (t.G / 2 + 63) / 64 * 64 : t.G;
+    hipStream_t sh[2] = {e->stream, e->stream3};
+    TreeView tv[2] = {t, t};
+    uint32_t g0[2] = {0, GA};
+    if (split) {
+        tv[0].G = GA;
+        tv[1] = slice_view(t, GA, t.G - GA);
+        HIP_TRY(hipEventRecord(e->ev_join, e->stream));  // stream3 starts after prior work
+        HIP_TRY(hipStreamWaitEvent(e->stream3, e->ev_join, 0));
+    }
+    const int nh = split ? 2 : 1;
+    bool nn_recorded[2] = {false, false};
     for (uint32_t c = 0; c < nchunks; ++c) {
         if (noise) {
             if (c + 1 < nchunks)
                 if (int rc = produce(c + 1)) return rc;
-            HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_ready[c & 1], 0));
+            for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(sh[h], e->ev_ready[c & 1], 0));
         }
         const uint32_t s0 = c * kNoiseChunk, s1 = s0 + kNoiseChunk < sims ? s0 + kNoiseChunk : sims;
         for (uint32_t s = s0; s < s1; ++s) {
-            const double* nz = noise ? e->noise + (c & 1) * slot_elems + (size_t)(s - s0) * t.G * kNoiseStride : nullptr;
-            if (int rc = timed(e, 0, t.G, [&] { return launch_select(t, roots, active, nz, prm, e->stream); }))
-                return rc;
-            if (int rc = evaluate(e, t.leaf_state, t.G, e->policy, e->value)) return rc;
-            if (int rc = timed(e, 2, t.G, [&] {
-                    return launch_expand_backup(t, roots, active, e->policy, e->value, e->stream);
-                }))
-                return rc;
+            for (int h = 0; h < nh; ++h) {
+                const TreeView& th = tv[h];
+                const size_t go = g0[h];
+                const double* nz = noise ? e->noise + (c & 1) * slot_elems + (size_t)(s - s0) * t.G * kNoiseStride +
+                                               go * kNoiseStride
+                                         : nullptr;
+                const uint8_t* act = active ? active + go : nullptr;  // null in search mode
+                if (int rc = timed(e, 0, th.G, [&] {
+                        return launch_select(th, roots + go, act, nz, prm, sh[h]);
+                    }, sh[h]))
+                    return rc;
+                if (split && nn_recorded[h ^ 1]) HIP_TRY(hipStreamWaitEvent(sh[h], e->ev_nn[h ^ 1], 0));
+                if (int rc = evaluate(e, th.leaf_state, th.G, e->policy + go * 50, e->value + go, sh[h])) return rc;
+                if (split) {
+                    HIP_TRY(hipEventRecord(e->ev_nn[h], sh[h]));
+                    nn_recorded[h] = true;
+                }
+                if (int rc = timed(e, 2, th.G, [&] {
+                        return launch_expand_backup(th, roots + go, act, e->policy + go * 50, e->value + go, sh[h]);
+                    }, sh[h]))
+                    return rc;
+            }
+        }
+        if (split) {  // both halves are done with this noise slot
+            HIP_TRY(hipEventRecord(e->ev_join, e->stream3));
+            HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));
         }
         if (noise) HIP_TRY(hipEventRecord(e->ev_consumed[c & 1], e->stream));
+    }
+    if (split) {
+        HIP_TRY(hipEventRecord(e->ev_join, e->stream3));
+        HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));
     }
     return 0;
 }
