@@ -54,6 +54,14 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 // argmax of (key, lane) keeping the LARGEST lane among equal keys (Iterator::max_by).
+// value of lane `lane` (wave-uniform index) as a wave-uniform double
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ int wave_argmax_last(int64_t key) {
     int idx = lane_id();
 #pragma unroll
@@ -330,20 +338,27 @@ __global__ void __launch_bounds__(kBlock) k_select(TreeView t, const oaz_state* 
             // sequential Iterator::max_by fold; each comparison re-evaluates both operands
             // with fresh noise (draw indices 2j and 2j+1 for comparison j)
             // draws precomputed by k_root_noise (same root, game id, ply and sim)
+            // Operand b of comparison j is child j with its own draw: every lane evaluates its
+            // own in parallel. Only operand a (the running best, with comparison j's fresh draw)
+            // is sequential; the fold runs on wave-uniform values read with v_readlane.
             double na = 0.0, nb = 0.0;
             if (l >= 1 && l < K) {
                 na = noise[(size_t)g * kNoiseStride + 2 * l];
                 nb = noise[(size_t)g * kNoiseStride + 2 * l + 1];
             }
             const double base = ch.P * (1.0 - prm.eps);
+            const double ubl = q + prm.c_puct * (base + nb * prm.eps) * sq;
             int acc = 0;
+            double qa = readlane_f64(q, 0), ba = readlane_f64(base, 0), sa = readlane_f64(sq, 0);
             for (int j = 1; j < K; ++j) {
-                const double qa = __shfl(q, acc), ba = __shfl(base, acc), sa = __shfl(sq, acc);
-                const double qb = __shfl(q, j), bb = __shfl(base, j), sb = __shfl(sq, j);
-                const double naj = __shfl(na, j), nbj = __shfl(nb, j);
-                const double ua = qa + prm.c_puct * (ba + naj * prm.eps) * sa;
-                const double ub = qb + prm.c_puct * (bb + nbj * prm.eps) * sb;
-                if (!(total_key(ua) > total_key(ub))) acc = j;
+                const double ua = qa + prm.c_puct * (ba + readlane_f64(na, j) * prm.eps) * sa;
+                const double ub = readlane_f64(ubl, j);
+                if (!(total_key(ua) > total_key(ub))) {
+                    acc = j;
+                    qa = readlane_f64(q, j);
+                    ba = readlane_f64(base, j);
+                    sa = readlane_f64(sq, j);
+                }
             }
             best = acc;
         } else {
