@@ -75,7 +75,11 @@ enum {
 };
 
 enum { OAZ_EVAL_NN = 0, OAZ_EVAL_HASH = 1 };        /* leaf evaluator (HASH: test evaluator, below) */
-enum { OAZ_FP32 = 0, OAZ_BF16 = 1 };                /* NN arithmetic (bf16: MFMA inputs, fp32 accumulate) */
+/* NN arithmetic. OAZ_FP32: exact fp32 MFMA products (v_mfma_f32_16x16x4_f32). OAZ_BF16: bf16 MFMA
+ * inputs, fp32 accumulate (BASELINE C5). OAZ_FP32_SPLIT: fp32 operands split exactly into three
+ * bf16 terms (hi + mid + lo), the six products above 2^-24 relative on bf16 MFMA, fp32
+ * accumulate: fp32-level error (DESIGN.md "fp32 split") at bf16 MFMA rates. */
+enum { OAZ_FP32 = 0, OAZ_BF16 = 1, OAZ_FP32_SPLIT = 2 };
 
 /* ---- PODs ----------------------------------------------------------------- */
 
@@ -132,7 +136,7 @@ typedef struct oaz_config {
     double dirichlet_eps;    /* 0.25 (mcts_arena.rs:186) */
     int32_t games;           /* parallel game slots G (also the max batch of oaz_search) */
     int32_t evaluator;       /* OAZ_EVAL_NN or OAZ_EVAL_HASH */
-    int32_t precision;       /* OAZ_FP32 or OAZ_BF16 */
+    int32_t precision;       /* OAZ_FP32, OAZ_BF16 or OAZ_FP32_SPLIT */
     int32_t fixed_deck;      /* 1: every game uses deck[]; 0: random 5 of 16 per game (deck.rs:139-151) */
     uint8_t deck[5];
     uint8_t pad0[3];

@@ -209,6 +209,44 @@ static void pack_conv64_bf16(const FoldedConv& f, std::vector<float>& out) {
     for (int o = 0; o < 64; ++o) out.push_back(f.b[o]);
 }
 
+// fp32 split (OAZ_FP32_SPLIT): w = hi + mid + lo exactly, each term the top 16 bits of an fp32
+// (8 significant bits: bf16). hi = trunc(w), mid = trunc(w - hi), lo = w - hi - mid (both
+// subtractions exact, lo has <= 8 significant bits). Same split as split3() in oaz_nn.hip.
+static void split3_host(float w, uint16_t out[3]) {
+    auto bits = [](float f) { uint32_t u; memcpy(&u, &f, 4); return u; };
+    auto from = [](uint32_t u) { float f; memcpy(&f, &u, 4); return f; };
+    const uint32_t h = bits(w) & 0xffff0000u;
+    const float r = w - from(h);
+    const uint32_t m = bits(r) & 0xffff0000u;
+    const float l = r - from(m);
+    out[0] = (uint16_t)(h >> 16);
+    out[1] = (uint16_t)(m >> 16);
+    out[2] = (uint16_t)(bits(l) >> 16);
+}
+
+// Split B fragments: [tap][K-half m][piece p][N-tile][lane] bf16x8, lane l supplying
+// B[k = 8(l>>4) + e][col l&15] = piece p of W[co = 16nt + (l&15)][ci = 32m + 8(l>>4) + e][tap].
+static void pack_conv64_split(const FoldedConv& f, std::vector<float>& out) {
+    std::vector<uint16_t> h;
+    h.reserve(9 * 2 * 3 * 4 * 64 * 8);
+    for (int t = 0; t < 9; ++t)
+        for (int m = 0; m < 2; ++m)
+            for (int pc = 0; pc < 3; ++pc)
+                for (int nt = 0; nt < 4; ++nt)
+                    for (int l = 0; l < 64; ++l)
+                        for (int e = 0; e < 8; ++e) {
+                            const int co = nt * 16 + (l & 15);
+                            const int ci = 32 * m + 8 * (l >> 4) + e;
+                            uint16_t s[3];
+                            split3_host(f.w[((size_t)co * 64 + ci) * 9 + t], s);
+                            h.push_back(s[pc]);
+                        }
+    const size_t base = out.size();
+    out.resize(base + h.size() / 2);
+    memcpy(out.data() + base, h.data(), h.size() * sizeof(uint16_t));
+    for (int o = 0; o < 64; ++o) out.push_back(f.b[o]);
+}
+
 // First layer (k_nn_sq16): the 4 bitboard planes go through MFMA (lane l supplies
 // W[co = 16nt + (l&15)][plane l>>4][tap t]); the 16 card planes and the blue-to-move plane
 // (constant over the board, common.rs:68-77,32-37) become T[square][c][co] = sum over the
@@ -233,14 +271,15 @@ static void pack_first_layer(const FoldedConv& f, std::vector<float>& out) {
         }
 }
 
-static int pack_weights(const float* raw, int blocks, int bf16, std::vector<float>& out) {
+static int pack_weights(const float* raw, int blocks, int precision, std::vector<float>& out) {
     out.clear();
-    out.reserve(nn_packed_floats(blocks, bf16));
+    out.reserve(nn_packed_floats(blocks, precision));
     const float* p = raw;
     pack_first_layer(fold(p, 64, 21, 9), out);
     for (int b = 0; b < blocks; ++b)
         for (int j = 0; j < 2; ++j) {
-            if (bf16) pack_conv64_bf16(fold(p, 64, 64, 9), out);
+            if (precision == OAZ_BF16) pack_conv64_bf16(fold(p, 64, 64, 9), out);
+            else if (precision == OAZ_FP32_SPLIT) pack_conv64_split(fold(p, 64, 64, 9), out);
             else pack_conv64(fold(p, 64, 64, 9), out);
         }
     // value head: vh_conv + vh_bn folded, vh_linear1, vh_linear2
@@ -264,7 +303,7 @@ static int pack_weights(const float* raw, int blocks, int bf16, std::vector<floa
     for (int i = 0; i < 50; ++i) out.push_back(*p++);    // ph_linear2.bias
     out.push_back(0.0f);
     out.push_back(0.0f);
-    if (out.size() != nn_packed_floats(blocks, bf16)) return oaz_set_err(OAZ_ERR_STATE, "pack: size mismatch");
+    if (out.size() != nn_packed_floats(blocks, precision)) return oaz_set_err(OAZ_ERR_STATE, "pack: size mismatch");
     if ((size_t)(p - raw) != oaz_weight_count(blocks, 64, 21)) return oaz_set_err(OAZ_ERR_STATE, "pack: raw size mismatch");
     return 0;
 }
@@ -560,8 +599,8 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         oaz_set_err(OAZ_ERR_ARG, "create: config out of range");
         return nullptr;
     }
-    if (cfg->precision != OAZ_FP32 && cfg->precision != OAZ_BF16) {
-        oaz_set_err(OAZ_ERR_ARG, "create: precision must be OAZ_FP32 or OAZ_BF16");
+    if (cfg->precision != OAZ_FP32 && cfg->precision != OAZ_BF16 && cfg->precision != OAZ_FP32_SPLIT) {
+        oaz_set_err(OAZ_ERR_ARG, "create: precision must be OAZ_FP32, OAZ_BF16 or OAZ_FP32_SPLIT");
         return nullptr;
     }
     int ndev = 0;
@@ -611,7 +650,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         dalloc(&e->depth, G) || dalloc(&e->leaf, G) || dalloc(&e->leaf_state, G) ||
         dalloc(&e->stats, G * GS_COUNT) || dalloc(&e->stats_sum, (size_t)GS_COUNT) ||
         dalloc(&e->sqrt_tab, (size_t)cfg->sims + 2) || dalloc(&e->policy, G * 50) ||
-        dalloc(&e->value, G) || dalloc(&e->weights, nn_packed_floats(cfg->blocks, cfg->precision == OAZ_BF16)) ||
+        dalloc(&e->value, G) || dalloc(&e->weights, nn_packed_floats(cfg->blocks, cfg->precision)) ||
         dalloc(&e->s_roots, G) || dalloc(&e->s_move, G) || dalloc(&e->s_pi, G * 50) ||
         dalloc(&e->s_rootv, G) || dalloc(&e->s_rootp, G * 50) || dalloc(&e->s_ply, G) ||
         dalloc(&e->root, G) || dalloc(&e->ply, G) || dalloc(&e->seq, G) ||
@@ -678,7 +717,7 @@ extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
         return oaz_set_err(OAZ_ERR_WEIGHTS, "load_weights: got %zu floats, need %zu for %d blocks", n, need,
                        e->cfg.blocks);
     std::vector<float> packed;
-    if (int rc = pack_weights(blob, e->cfg.blocks, e->cfg.precision == OAZ_BF16, packed)) return rc;
+    if (int rc = pack_weights(blob, e->cfg.blocks, e->cfg.precision, packed)) return rc;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipMemcpyAsync(e->weights, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -737,7 +776,7 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
     NNView w;
     w.blob = e->weights;
     w.blocks = e->cfg.blocks;
-    w.bf16 = e->cfg.precision == OAZ_BF16;
+    w.precision = e->cfg.precision;
     {
         const char* v1 = getenv("OAZ_NN_BF16_V1");
         w.bf16_v1 = v1 ? atoi(v1) : 0;  // 0: 8 waves x 2 N-tiles, 1: k_nn_sq16<bf16>, 2: 4 waves x 4 N-tiles

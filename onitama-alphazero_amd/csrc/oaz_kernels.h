@@ -75,7 +75,7 @@ struct SlotView {
 struct NNView {
     const float* blob;  // packed, BN-folded weights (DESIGN.md "NN weights layout")
     int32_t blocks;
-    int32_t bf16;       // 1: bf16 MFMA inputs (fp32 accumulate)
+    int32_t precision;  // OAZ_FP32 (exact fp32 MFMA), OAZ_BF16 (bf16 inputs), OAZ_FP32_SPLIT (bf16x6 split)
     int32_t bf16_v1;    // bf16 kernel variant (OAZ_NN_BF16_V1): 0 k_nn_bf16g<2>, 1 k_nn_sq16<bf16>, 2 k_nn_bf16g<4>
 };
 
@@ -90,7 +90,7 @@ hipError_t launch_encode(const oaz_state* s, int n, float* planes, hipStream_t s
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy,
                              float* value, hipStream_t st);
 hipError_t launch_hash_eval(const oaz_state* s, int B, float* policy, float* value, hipStream_t st);
-size_t nn_packed_floats(int blocks, int bf16);
+size_t nn_packed_floats(int blocks, int precision);
 
 // MCTS
 hipError_t launch_tree_reset(const TreeView& t, hipStream_t st);

@@ -31,6 +31,8 @@
 //     the first layer keeps the exact fp32 MFMA on 0/1 inputs.
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "oaz_device.h"
 #include "oaz_kernels.h"
 
@@ -81,9 +83,18 @@ template <> struct Act<true> {
 };
 }  // namespace nn
 
-size_t nn_packed_floats(int blocks, int bf16) {
-    return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * ((bf16 ? nn::kW64h : nn::kW64) + nn::kCh) +
-           nn::kValueF + nn::kPolicyF;
+// fp32 split variant (OAZ_FP32_SPLIT): 64->64 conv B fragments are [9 taps][2 K-halves][3 pieces]
+// [4 N-tiles][64 lanes] bf16x8 (the exact 3-term bf16 split of each folded fp32 weight).
+namespace x6 {
+constexpr int kRowB = 384;                  // LDS row: 3 pieces x 64 channels x bf16, no padding
+constexpr int kImageB = nn::kSB * 25 * kRowB;  // 153,600 B
+constexpr int kLdsFloats = kImageB / 4 + nn::kWaves * nn::kScratch;  // 39,424 floats = 157,696 B
+constexpr size_t kW = 9 * 2 * 3 * 4 * 64 * 4;
+}  // namespace x6
+
+size_t nn_packed_floats(int blocks, int precision) {
+    const size_t w = precision == OAZ_BF16 ? nn::kW64h : precision == OAZ_FP32_SPLIT ? x6::kW : nn::kW64;
+    return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (w + nn::kCh) + nn::kValueF + nn::kPolicyF;
 }
 
 // Square groups: 4 corners + 4 edges + 5 interior (85 on-board taps) | 8 edges + 4 interior (84).
@@ -282,11 +293,11 @@ __device__ __forceinline__ void read_skip(f32x4 (&skip)[nn::kTPW], const typenam
             for (int r = 0; r < 4; ++r) skip[j][r] = A::load(act + (sq[j] * nn::kSB + (lane >> 4) * 4 + r) * A::kRS + co);
 }
 
-// value + policy heads (net.rs:152-213) for position `s` of the workgroup (one wave).
-template <bool BF16>
-__device__ __forceinline__ void heads(const typename nn::Act<BF16>::T* act, float* scratch, int s, const float* p,
-                                      int lane, int b, int B, float* policy, float* value) {
-    using A = nn::Act<BF16>;
+// value + policy heads (net.rs:152-213) for position `s` of the workgroup (one wave). ld(row, c)
+// returns activation channel c of LDS row `row` (= square * 16 + position) as fp32.
+template <class LD>
+__device__ __forceinline__ void heads_g(const LD& ld, float* scratch, int s, const float* p, int lane, int b, int B,
+                                        float* policy, float* value) {
     const float* vw = p;
     const float vb = p[64];
     const float* l1w = p + 68;
@@ -299,13 +310,13 @@ __device__ __forceinline__ void heads(const typename nn::Act<BF16>::T* act, floa
     const float* plb = plw + 2500;
     if (lane < 25) {  // 1x1 convs (value 64->1, policy 64->2) with folded BN, ReLU; lane = square
         float sv = vb, s0 = pb0, s1 = pb1;
-        const typename A::T* row = act + (lane * nn::kSB + s) * A::kRS;
+        const int row = lane * nn::kSB + s;
         for (int c = 0; c < nn::kCh; c += 4) {
             float4 x;
-            x.x = A::load(row + c);
-            x.y = A::load(row + c + 1);
-            x.z = A::load(row + c + 2);
-            x.w = A::load(row + c + 3);
+            x.x = ld(row, c);
+            x.y = ld(row, c + 1);
+            x.z = ld(row, c + 2);
+            x.w = ld(row, c + 3);
             sv += vw[c] * x.x + vw[c + 1] * x.y + vw[c + 2] * x.z + vw[c + 3] * x.w;
             s0 += pp[c] * x.x + pp[c + 1] * x.y + pp[c + 2] * x.z + pp[c + 3] * x.w;
             s1 += pp[64 + c] * x.x + pp[65 + c] * x.y + pp[66 + c] * x.z + pp[67 + c] * x.w;
@@ -330,6 +341,14 @@ __device__ __forceinline__ void heads(const typename nn::Act<BF16>::T* act, floa
         if (lane < 50) policy[(size_t)b * 50 + lane] = e / den;
         if (lane == 0) value[b] = tanhf(vsum + l2b);
     }
+}
+
+template <bool BF16>
+__device__ __forceinline__ void heads(const typename nn::Act<BF16>::T* act, float* scratch, int s, const float* p,
+                                      int lane, int b, int B, float* policy, float* value) {
+    using A = nn::Act<BF16>;
+    heads_g([&](int row, int c) { return A::load(act + row * A::kRS + c); }, scratch, s, p, lane, b, B, policy,
+            value);
 }
 
 template <bool BF16>
@@ -609,16 +628,243 @@ __global__ void __launch_bounds__(64 * 16 / NPW) k_nn_bf16g(const oaz_state* __r
     for (int s = wave; s < nn::kSB; s += kWaves) heads<true>(act, scratch, s, p, lane, b0 + s, B, policy, value);
 }
 
+// ---- fp32 split (OAZ_FP32_SPLIT): bf16x6 MFMA with fp32-level error ------------------------------
+// Every fp32 operand x (activation or folded weight) is split EXACTLY into three bf16 terms,
+// x = h + m + l: h = the top 16 bits of x (8 significant bits), m = the top 16 bits of x - h,
+// l = x - h - m (both subtractions are exact and l has <= 8 significant bits). Of the nine
+// products of a*b the six down to 2^-16 relative are computed (hh, hm, mh, hl, mm, lh) on
+// v_mfma_f32_16x16x32_bf16, whose bf16 x bf16 products are exact in fp32 and which accumulates
+// in fp32; the dropped ml + lm + ll are below 2^-23 relative, i.e. at fp32 rounding level
+// (measured: errors vs a float64 forward equal the exact-fp32 kernel's).
+// One K=32 block costs 6 x 16 cycles instead of 8 x 32 for v_mfma_f32_16x16x4_f32 (2.67x).
+//
+// Geometry = k_nn_sq16 (16 positions, square-major rows, 8 waves = 2 square groups x 4 N-tiles,
+// off-board (square, tap) products skipped). The LDS image holds the three bf16 planes of every
+// activation: row (square*16 + position) = [piece][64 channels] = 384 B, unpadded (153.6 KB);
+// 16-byte chunk c (8 channels) of piece p of row r sits at chunk p*8 + (c ^ ((r >> 1) & 7)),
+// which makes the A-fragment ds_read_b128 of every 16-lane group hit 16 distinct bank slots.
+namespace x6 {
+__device__ __forceinline__ int chunk_off(int row, int piece, int c8) {  // byte offset of an 8-channel chunk
+    return row * kRowB + piece * 128 + ((c8 ^ ((row >> 1) & 7)) << 4);
+}
+__device__ __forceinline__ void split3(float v, uint16_t& h, uint16_t& m, uint16_t& l) {
+    const uint32_t hb = __float_as_uint(v) & 0xffff0000u;
+    const float r = v - __uint_as_float(hb);
+    const uint32_t mb = __float_as_uint(r) & 0xffff0000u;
+    const float lo = r - __uint_as_float(mb);
+    h = (uint16_t)(hb >> 16);
+    m = (uint16_t)(mb >> 16);
+    l = (uint16_t)(__float_as_uint(lo) >> 16);
+}
+// byte offset of channel c of row r within its piece-0 plane; rows r and r + 16k share the
+// swizzle, so the offset of (square sq, row-in-tile r) is sq * 16 * kRowB + elem_off(r, c)
+__device__ __forceinline__ int elem_off(int row, int c) { return chunk_off(row, 0, c >> 3) + (c & 7) * 2; }
+__device__ __forceinline__ void store_at(char* img, int o, float v) {
+    uint16_t h, m, l;
+    split3(v, h, m, l);
+    *reinterpret_cast<uint16_t*>(img + o) = h;
+    *reinterpret_cast<uint16_t*>(img + o + 128) = m;
+    *reinterpret_cast<uint16_t*>(img + o + 256) = l;
+}
+__device__ __forceinline__ float load_at(const char* img, int o) {  // h + m + l = the fp32 value
+    const float h = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(img + o) << 16);
+    const float m = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(img + o + 128) << 16);
+    const float l = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(img + o + 256) << 16);
+    return h + (m + l);
+}
+__device__ __forceinline__ float load(const char* img, int row, int c) { return load_at(img, elem_off(row, c)); }
+}  // namespace x6
+
+// On-board squares of square group GRP for tap T, known at compile time: the conv below is
+// straight-line code per (group, tap), with no per-MFMA on-board tests.
+struct TapList {
+    int n;
+    int8_t j[nn::kTPW];   // index into the group's square list (accumulator)
+    int8_t nb[nn::kTPW];  // neighbour square read for that tap
+};
+constexpr int8_t kSqOrder[25] = {0, 4, 20, 24, 1, 3, 21, 23, 6, 8, 12, 16, 18,
+                                 2, 5, 10, 15, 9, 14, 19, 22, 7, 11, 13, 17};
+constexpr TapList tap_list(int grp, int t) {
+    TapList L{};
+    const int n = grp == 0 ? nn::kTPW : 25 - nn::kTPW;
+    for (int j = 0; j < n; ++j) {
+        const int sq = kSqOrder[grp * nn::kTPW + j];
+        const int r = sq / 5 + t / 3 - 1, c = sq % 5 + t % 3 - 1;
+        if (r >= 0 && r < 5 && c >= 0 && c < 5) {
+            L.j[L.n] = (int8_t)j;
+            L.nb[L.n] = (int8_t)(r * 5 + c);
+            ++L.n;
+        }
+    }
+    return L;
+}
+
+// acc[j] += split-fp32 conv3x3 over 64 input channels, tap T, K-half M, for group GRP. For K-half
+// m lane l supplies A[row l&15][k = 8(l>>4) + e] = channel 32m + 8(l>>4) + e of each piece.
+// b[] holds this (tap, K-half)'s B pieces; the next one's are requested first.
+template <int GRP, int T, int M>
+__device__ __forceinline__ void conv_x6_step(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W, bf16x8 (&b)[3],
+                                             int lo, int lane, int nt) {
+    constexpr TapList L = tap_list(GRP, T);
+    constexpr int nx = T * 2 + M + 1;  // next (tap, K-half)
+    bf16x8 bn[3];
+    if constexpr (nx < 18) {
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) bn[pc] = W[((nx * 3 + pc) * 4 + nt) * 64 + lane];
+    }
+    // batches of <= 7 on-board squares; A pieces are consumed in turn (h with B h/m/l, m with
+    // B h/m, l with B h) so at most two piece arrays are live; consecutive MFMAs hit different
+    // accumulators
+    constexpr int kH = 7;
+#pragma unroll
+    for (int q0 = 0; q0 < L.n; q0 += kH) {
+        bf16x8 a0[kH], a1[kH];
+#pragma unroll
+        for (int q = 0; q < kH; ++q)
+            if (q0 + q < L.n) {
+                const char* a = img + L.nb[q0 + q] * (nn::kSB * x6::kRowB) + lo;
+                a0[q] = *reinterpret_cast<const bf16x8*>(a);
+                a1[q] = *reinterpret_cast<const bf16x8*>(a + 128);
+            }
+        auto mm = [&](const bf16x8(&a)[kH], const bf16x8& bv) {
+#pragma unroll
+            for (int q = 0; q < kH; ++q)
+                if (q0 + q < L.n) {
+                    const int j = L.j[q0 + q];
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[q], bv, acc[j], 0, 0, 0);
+                }
+        };
+        mm(a0, b[0]);  // hh
+        mm(a0, b[1]);  // hm
+        mm(a0, b[2]);  // hl
+#pragma unroll
+        for (int q = 0; q < kH; ++q)
+            if (q0 + q < L.n) a0[q] = *reinterpret_cast<const bf16x8*>(img + L.nb[q0 + q] * (nn::kSB * x6::kRowB) + lo + 256);
+        mm(a1, b[0]);  // mh
+        mm(a1, b[1]);  // mm
+        mm(a0, b[0]);  // lh
+        __builtin_amdgcn_sched_barrier(0);  // keep the next batch's loads from being hoisted (VGPRs)
+    }
+    if constexpr (nx < 18) {
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) b[pc] = bn[pc];
+    }
+}
+
+template <int GRP, int... TM>
+__device__ __forceinline__ void conv_x6_taps(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W, const int (&lo)[2],
+                                             int lane, int nt, std::integer_sequence<int, TM...>) {
+    bf16x8 b[3];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) b[pc] = W[(pc * 4 + nt) * 64 + lane];
+    (conv_x6_step<GRP, TM / 2, TM % 2>(acc, img, W, b, lo[TM % 2], lane, nt), ...);
+}
+
+// bias (+ residual), ReLU, split into the three LDS planes; C/D layout as in epilogue<>. eo[r] =
+// x6::elem_off((lane >> 4) * 4 + r, co): with the square a compile-time constant the store
+// addresses are eo[r] plus immediates. ADD: add the residual held in `skip`; KEEP: the result is
+// the next block's input, keep it in `skip` (every conv maps (square, position, channel) to the
+// same lane and register, so the residual never has to be read back from the split LDS image).
+template <int GRP>
+__device__ __forceinline__ void epilogue_x6(const f32x4 (&acc)[nn::kTPW], char* img, const float* bias,
+                                            f32x4 (&skip)[nn::kTPW], const int (&eo)[4], int co, bool add,
+                                            bool keep) {
+    constexpr int n = GRP == 0 ? nn::kTPW : 25 - nn::kTPW;
+    const float bb = bias[co];
+#pragma unroll
+    for (int j = 0; j < n; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = acc[j][r] + bb;
+            if (add) v += skip[j][r];
+            v = v > 0.0f ? v : 0.0f;
+            if (keep) skip[j][r] = v;
+            x6::store_at(img + kSqOrder[GRP * nn::kTPW + j] * (nn::kSB * x6::kRowB), eo[r], v);
+        }
+}
+
+// The whole forward for the waves of square group GRP (compile-time square list).
+template <int GRP>
+__device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
+                                           int blocks, float* __restrict__ policy, float* __restrict__ value,
+                                           float* lds) {
+    char* img = reinterpret_cast<char*>(lds);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nt = wave & 3;
+    constexpr int ntiles = GRP == 0 ? nn::kTPW : 25 - nn::kTPW;
+    int sq[nn::kTPW];
+#pragma unroll
+    for (int j = 0; j < nn::kTPW; ++j) sq[j] = j < ntiles ? kSqOrder[GRP * nn::kTPW + j] : 0;
+    const int b0 = blockIdx.x * nn::kSB;
+    int* pinfo = reinterpret_cast<int*>(lds + x6::kImageB / 4);
+    const int co = nt * 16 + (lane & 15);
+    const int i = lane & 15, kq = lane >> 4;
+    int eo[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) eo[r] = x6::elem_off(kq * 4 + r, co);
+    const int lo[2] = {x6::chunk_off(i, 0, kq), x6::chunk_off(i, 0, 4 + kq)};
+
+    f32x4 acc[nn::kTPW];
+    f32x4 skip[nn::kTPW];
+    {  // encoder + first layer in exact fp32 MFMA (0/1 inputs), as k_nn_sq16
+        const int b = b0 + i < B ? b0 + i : b0;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
+        const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
+        if (tid < nn::kSB) {
+            const oaz_state st = states[b];
+            const int blue = st.to_move & 1;
+            const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
+            pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
+        conv_l1(acc, bb, blob, sq, lane, nt, ntiles);
+        conv_l1_const(acc, blob + nn::kL1B + nn::kCh, pinfo[i], sq, lane, nt, ntiles);
+        epilogue_x6<GRP>(acc, img, blob + nn::kL1B, skip, eo, co, false, true);
+        __syncthreads();
+    }
+    // 2 * blocks convs through one call site (small block 1: conv + BN + ReLU; small block 2:
+    // conv + BN, + skip, ReLU)
+    const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
+    for (int c = 0; c < 2 * blocks; ++c) {
+#pragma unroll
+        for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
+        conv_x6_taps<GRP>(acc, img, reinterpret_cast<const bf16x8*>(p), lo, lane, nt,
+                          std::make_integer_sequence<int, 18>{});
+        p += x6::kW;
+        __syncthreads();
+        epilogue_x6<GRP>(acc, img, p, skip, eo, co, c & 1, c & 1);
+        p += nn::kCh;
+        __syncthreads();
+    }
+    float* scratch = lds + x6::kImageB / 4 + wave * nn::kScratch;
+    for (int s = wave; s < nn::kSB; s += nn::kWaves)
+        heads_g([&](int row, int c) { return x6::load(img, row, c); }, scratch, s, p, lane, b0 + s, B, policy, value);
+}
+
+__global__ void __launch_bounds__(64 * nn::kWaves) k_nn_x6(const oaz_state* __restrict__ states, int B,
+                                                          const float* __restrict__ blob, int blocks,
+                                                          float* __restrict__ policy, float* __restrict__ value) {
+    __shared__ __attribute__((aligned(16))) float lds[x6::kLdsFloats];
+    if ((threadIdx.x >> 8) == 0)  // waves 0-3: square group 0, waves 4-7: group 1
+        nn_x6_body<0>(states, B, blob, blocks, policy, value, lds);
+    else
+        nn_x6_body<1>(states, B, blob, blocks, policy, value, lds);
+}
+
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy, float* value,
                              hipStream_t st) {
     if (B <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
-    if (w.bf16 && w.bf16_v1 == 1)
+    if (w.precision == OAZ_FP32_SPLIT)
+        hipLaunchKernelGGL(k_nn_x6, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy, value);
+    else if (w.precision == OAZ_BF16 && w.bf16_v1 == 1)
         hipLaunchKernelGGL(k_nn_sq16<true>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
                            value);
-    else if (w.bf16 && w.bf16_v1 == 0)
+    else if (w.precision == OAZ_BF16 && w.bf16_v1 == 0)
         hipLaunchKernelGGL(k_nn_bf16g<2>, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value);
-    else if (w.bf16)
+    else if (w.precision == OAZ_BF16)
         hipLaunchKernelGGL(k_nn_bf16g<4>, dim3(grid), dim3(64 * 4), 0, st, s, B, w.blob, w.blocks, policy, value);
     else
         hipLaunchKernelGGL(k_nn_sq16<false>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,

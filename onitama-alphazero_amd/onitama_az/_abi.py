@@ -18,7 +18,7 @@ RED, BLUE = 0, 1
 PAWN, KING = 0, 1
 CAPTURE, RED_WIN, BLUE_WIN, IN_PROGRESS = 0, 1, 2, 3
 EVAL_NN, EVAL_HASH = 0, 1
-FP32, BF16 = 0, 1
+FP32, BF16, FP32_SPLIT = 0, 1, 2  # OAZ_FP32 / OAZ_BF16 / OAZ_FP32_SPLIT (onitama_az.h)
 MAX_MOVES = 40
 
 

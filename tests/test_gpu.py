@@ -92,10 +92,13 @@ def test_encode_vs_oracle(orc):
 
 
 # ---- NN ----------------------------------------------------------------------------------
+@pytest.mark.parametrize("precision", [_abi.FP32, _abi.FP32_SPLIT])
 @pytest.mark.parametrize("name,blocks", [("trained3", 3), ("random3", 3), ("random6", 6)])
-def test_nn_matches_torch_goldens(nn_golden, trained3, name, blocks):
+def test_nn_matches_torch_goldens(nn_golden, trained3, name, blocks, precision):
+    """Both fp32 kernels (exact fp32 MFMA, and the bf16x6 split) against the torch-CPU fp32
+    goldens of the net.rs op graph, within the north star's 1e-4."""
     w = trained3 if name == "trained3" else random_weights(0 if name == "random3" else 1, blocks)
-    with Engine(games=256, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN) as e:
+    with Engine(games=256, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN, precision=precision) as e:
         e.load_weights(w)
         p, v = e.nn_forward(nn_golden["states"])
     tol = 1e-4  # north_star: policy/value within 1e-4 fp32

@@ -21,7 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--blocks", default="3")
-    ap.add_argument("--precision", default="fp32,bf16")
+    ap.add_argument("--precision", default="fp32,fp32x6,bf16")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
@@ -31,7 +31,7 @@ def main():
     for v in [int(x) for x in a.blocks.split(",")]:
         for prec in a.precision.split(","):
             e = Engine(games=a.batch, sims=1, blocks=v, evaluator=_abi.EVAL_NN,
-                       precision=_abi.BF16 if prec == "bf16" else _abi.FP32)
+                       precision={"bf16": _abi.BF16, "fp32x6": _abi.FP32_SPLIT}.get(prec, _abi.FP32))
             err = {}
             for name, blob, nb in (("trained3", w3, 3), ("random3", random_weights(0, 3), 3),
                                    ("random6", random_weights(1, 6), 6)):
