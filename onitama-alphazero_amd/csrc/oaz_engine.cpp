@@ -287,7 +287,9 @@ static int pack_weights(const float* raw, int blocks, int precision, std::vector
     for (int c = 0; c < 64; ++c) out.push_back(vc.w[c]);
     out.push_back(vc.b[0]);
     for (int i = 0; i < 3; ++i) out.push_back(0.0f);
-    for (int i = 0; i < 64 * 25; ++i) out.push_back(*p++);  // vh_linear1.weight [64][25]
+    for (int q = 0; q < 25; ++q)  // vh_linear1.weight [64][25], stored transposed [25][64] (coalesced per lane)
+        for (int o = 0; o < 64; ++o) out.push_back(p[o * 25 + q]);
+    p += 64 * 25;
     for (int i = 0; i < 64; ++i) out.push_back(*p++);       // vh_linear1.bias
     for (int i = 0; i < 64; ++i) out.push_back(*p++);       // vh_linear2.weight [1][64]
     out.push_back(*p++);                                    // vh_linear2.bias
@@ -299,7 +301,9 @@ static int pack_weights(const float* raw, int blocks, int precision, std::vector
     out.push_back(pc.b[1]);
     out.push_back(0.0f);
     out.push_back(0.0f);
-    for (int i = 0; i < 2500; ++i) out.push_back(*p++);  // ph_linear2.weight [50][50]
+    for (int f = 0; f < 50; ++f)  // ph_linear2.weight [50 out][50 in], stored transposed [in][out]
+        for (int o = 0; o < 50; ++o) out.push_back(p[o * 50 + f]);
+    p += 2500;
     for (int i = 0; i < 50; ++i) out.push_back(*p++);    // ph_linear2.bias
     out.push_back(0.0f);
     out.push_back(0.0f);
@@ -780,6 +784,8 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
     {
         const char* v1 = getenv("OAZ_NN_BF16_V1");
         w.bf16_v1 = v1 ? atoi(v1) : 0;  // 0: 8 waves x 2 N-tiles, 1: k_nn_sq16<bf16>, 2: 4 waves x 4 N-tiles
+        const char* xv = getenv("OAZ_NN_X6_V");
+        w.x6_variant = xv ? atoi(xv) : 0;
     }
     return timed(e, 1, B, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, st); }, st);
 }

@@ -52,8 +52,8 @@ constexpr int kLdsFloats = kSB * 25 * kRS + kWaves * kScratch;  // 29824 floats 
 // Packed blob (floats), built by pack_weights() in oaz_engine.cpp:
 //   [L1 B: 9 taps x 4 N-tiles x 64 lanes][L1 bias 64][L1 table: 25 squares x 17 x 64]
 //   blocks x 2 x [W: 9 taps x 4 groups x 4 N-tiles x 64 lanes x 4][bias 64]
-//   value head:  wv[64] bv pad[3] l1w[64*25] l1b[64] l2w[64] l2b pad[3]
-//   policy head: wp[2*64] bp[2] pad[2] plw[50*50] plb[50] pad[2]
+//   value head:  wv[64] bv pad[3] l1w[25][64] (transposed) l1b[64] l2w[64] l2b pad[3]
+//   policy head: wp[2*64] bp[2] pad[2] plw[50 in][50 out] (transposed) plb[50] pad[2]
 constexpr size_t kL1B = 9 * 4 * 64;
 constexpr size_t kL1Table = 25 * 17 * kCh;
 constexpr size_t kW64 = 9 * 4 * 4 * 64 * 4;
@@ -326,13 +326,13 @@ __device__ __forceinline__ void heads_g(const LD& ld, float* scratch, int s, con
         scratch[57 + lane] = s1 > 0.0f ? s1 : 0.0f;
     }
     float hj = l1b[lane];
-    for (int q = 0; q < 25; ++q) hj += l1w[lane * 25 + q] * scratch[q];
+    for (int q = 0; q < 25; ++q) hj += l1w[q * 64 + lane] * scratch[q];  // l1w stored [25][64]
     hj = hj > 0.0f ? hj : 0.0f;
     const float vsum = wave_sum_f(l2w[lane] * hj);
     float lg = -INFINITY;
     if (lane < 50) {
         lg = plb[lane];
-        for (int f = 0; f < 50; ++f) lg += plw[lane * 50 + f] * scratch[32 + f];
+        for (int f = 0; f < 50; ++f) lg += plw[f * 50 + lane] * scratch[32 + f];  // plw stored [in][out]
     }
     const float mx = wave_max_f(lg);
     const float e = lane < 50 ? expf(lg - mx) : 0.0f;
@@ -699,10 +699,25 @@ constexpr TapList tap_list(int grp, int t) {
     return L;
 }
 
+// Kernel variant knobs (A/B-tested, DESIGN.md perf log): KH = on-board squares per A batch; SB = a
+// scheduling barrier after each batch (bounds VGPR live ranges); EPI = epilogue store form (0:
+// ds_write_b16 per piece, 1: lane pairs exchange one value and store bf16 pairs as ds_write_b32).
+// PIPE: 1 = the conv is one software-pipelined sequence of balanced batches over all (tap, K-half)
+// steps (conv_x6_pipe), 0 = per-step batches of KH (conv_x6_step).
+// DBG (timing experiments only, wrong results): 1 = conv epilogue stores skipped.
+template <int KH_, bool SB_, int EPI_, int PIPE_ = 0, int DBG_ = 0>
+struct X6Cfg {
+    static constexpr int KH = KH_;
+    static constexpr bool SB = SB_;
+    static constexpr int EPI = EPI_;
+    static constexpr int PIPE = PIPE_;
+    static constexpr int DBG = DBG_;
+};
+
 // acc[j] += split-fp32 conv3x3 over 64 input channels, tap T, K-half M, for group GRP. For K-half
 // m lane l supplies A[row l&15][k = 8(l>>4) + e] = channel 32m + 8(l>>4) + e of each piece.
 // b[] holds this (tap, K-half)'s B pieces; the next one's are requested first.
-template <int GRP, int T, int M>
+template <class C, int GRP, int T, int M>
 __device__ __forceinline__ void conv_x6_step(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W, bf16x8 (&b)[3],
                                              int lo, int lane, int nt) {
     constexpr TapList L = tap_list(GRP, T);
@@ -712,10 +727,10 @@ __device__ __forceinline__ void conv_x6_step(f32x4 (&acc)[nn::kTPW], const char*
 #pragma unroll
         for (int pc = 0; pc < 3; ++pc) bn[pc] = W[((nx * 3 + pc) * 4 + nt) * 64 + lane];
     }
-    // batches of <= 7 on-board squares; A pieces are consumed in turn (h with B h/m/l, m with
+    // batches of <= KH on-board squares; A pieces are consumed in turn (h with B h/m/l, m with
     // B h/m, l with B h) so at most two piece arrays are live; consecutive MFMAs hit different
     // accumulators
-    constexpr int kH = 7;
+    constexpr int kH = C::KH;
 #pragma unroll
     for (int q0 = 0; q0 < L.n; q0 += kH) {
         bf16x8 a0[kH], a1[kH];
@@ -743,7 +758,7 @@ __device__ __forceinline__ void conv_x6_step(f32x4 (&acc)[nn::kTPW], const char*
         mm(a1, b[0]);  // mh
         mm(a1, b[1]);  // mm
         mm(a0, b[0]);  // lh
-        __builtin_amdgcn_sched_barrier(0);  // keep the next batch's loads from being hoisted (VGPRs)
+        if constexpr (C::SB) __builtin_amdgcn_sched_barrier(0);  // keep the next batch's loads from being hoisted
     }
     if constexpr (nx < 18) {
 #pragma unroll
@@ -751,13 +766,128 @@ __device__ __forceinline__ void conv_x6_step(f32x4 (&acc)[nn::kTPW], const char*
     }
 }
 
-template <int GRP, int... TM>
+template <class C, int GRP, int... TM>
 __device__ __forceinline__ void conv_x6_taps(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W, const int (&lo)[2],
                                              int lane, int nt, std::integer_sequence<int, TM...>) {
     bf16x8 b[3];
 #pragma unroll
     for (int pc = 0; pc < 3; ++pc) b[pc] = W[(pc * 4 + nt) * 64 + lane];
-    (conv_x6_step<GRP, TM / 2, TM % 2>(acc, img, W, b, lo[TM % 2], lane, nt), ...);
+    (conv_x6_step<C, GRP, TM / 2, TM % 2>(acc, img, W, b, lo[TM % 2], lane, nt), ...);
+}
+
+// ---- pipelined conv (PIPE = 1) ----
+// The 18 (tap, K-half) steps of a group are cut into batches of near-equal size (<= KH squares;
+// a step of n on-board squares gives ceil(n / KH) batches), and each batch runs
+//   [X = m pieces, loaded by the previous batch]  load Y = h pieces
+//   m*Bh, m*Bm                                    load X = l pieces
+//   h*Bh, h*Bm, h*Bl                              load Y = next batch's m pieces
+//   l*Bh
+// so every A load has >= KH MFMAs of cover and only two piece arrays are live.
+struct X6Batch {
+    int t, m, n;
+    int8_t j[8], nb[8];
+};
+struct X6Plan {
+    int nbat;
+    X6Batch b[64];
+};
+constexpr X6Plan x6_plan(int grp, int kh) {
+    X6Plan P{};
+    for (int s = 0; s < 18; ++s) {
+        const TapList L = tap_list(grp, s / 2);
+        const int nb = (L.n + kh - 1) / kh;
+        int q = 0;
+        for (int k = 0; k < nb; ++k) {
+            const int n = (L.n - q) / (nb - k);  // near-equal split, larger batches last
+            X6Batch B{};
+            B.t = s / 2;
+            B.m = s % 2;
+            B.n = n;
+            for (int i = 0; i < n; ++i) {
+                B.j[i] = L.j[q + i];
+                B.nb[i] = L.nb[q + i];
+            }
+            q += n;
+            P.b[P.nbat++] = B;
+        }
+    }
+    return P;
+}
+
+template <int GRP, int KH>
+struct X6PlanOf {
+    static constexpr X6Plan P = x6_plan(GRP, KH);
+};
+
+template <int N>
+__device__ __forceinline__ void x6_load(bf16x8 (&a)[N], const char* img, const X6Batch& B, int lo, int piece) {
+#pragma unroll
+    for (int q = 0; q < N; ++q)
+        if (q < B.n) a[q] = *reinterpret_cast<const bf16x8*>(img + B.nb[q] * (nn::kSB * x6::kRowB) + lo + piece * 128);
+}
+
+template <int N>
+__device__ __forceinline__ void x6_mfma(f32x4 (&acc)[nn::kTPW], const bf16x8 (&a)[N], const bf16x8& bv, const X6Batch& B) {
+#pragma unroll
+    for (int q = 0; q < N; ++q)
+        if (q < B.n) acc[B.j[q]] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[q], bv, acc[B.j[q]], 0, 0, 0);
+}
+
+// batch K of the plan. X holds its m pieces on entry and the next batch's m pieces on exit
+// (swapped by the caller through the X/Y roles alternating with K's parity).
+template <class C, int GRP, int K>
+__device__ __forceinline__ void conv_x6_batch(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W,
+                                              bf16x8 (&b)[3], bf16x8 (&bn)[3], bf16x8 (&X)[C::KH],
+                                              bf16x8 (&Y)[C::KH], const int (&lo)[2], int lane, int nt) {
+    constexpr const X6Plan& P = X6PlanOf<GRP, C::KH>::P;
+    constexpr X6Batch B = P.b[K];
+    constexpr bool first_of_step = K == 0 || P.b[K - 1].t * 2 + P.b[K - 1].m != B.t * 2 + B.m;
+    constexpr int step = B.t * 2 + B.m;
+    if constexpr (first_of_step && K > 0) {
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) b[pc] = bn[pc];
+    }
+    if constexpr (first_of_step && step + 1 < 18) {  // prefetch the next step's B pieces
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) bn[pc] = W[(((step + 1) * 3 + pc) * 4 + nt) * 64 + lane];
+    }
+    x6_load(Y, img, B, lo[B.m], 0);  // h
+    x6_mfma(acc, X, b[0], B);        // mh
+    x6_mfma(acc, X, b[1], B);        // mm
+    x6_load(X, img, B, lo[B.m], 2);  // l
+    x6_mfma(acc, Y, b[0], B);        // hh
+    x6_mfma(acc, Y, b[1], B);        // hm
+    x6_mfma(acc, Y, b[2], B);        // hl
+    if constexpr (K + 1 < P.nbat) {
+        constexpr X6Batch Bn = P.b[K + 1];
+        x6_load(Y, img, Bn, lo[Bn.m], 1);  // next batch's m
+    }
+    x6_mfma(acc, X, b[0], B);  // lh
+    if constexpr (C::SB) __builtin_amdgcn_sched_barrier(0);
+}
+
+template <class C, int GRP, int... K>
+__device__ __forceinline__ void conv_x6_pipe(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W,
+                                             const int (&lo)[2], int lane, int nt, std::integer_sequence<int, K...>) {
+    constexpr const X6Plan& P = X6PlanOf<GRP, C::KH>::P;
+    bf16x8 b[3], bn[3], X[C::KH], Y[C::KH];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) b[pc] = W[(pc * 4 + nt) * 64 + lane];
+    x6_load(X, img, P.b[0], lo[P.b[0].m], 1);
+    // even batches: m pieces in X; odd batches: in Y (the roles swap after every batch)
+    ((K % 2 == 0 ? conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, lo, lane, nt)
+                 : conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, Y, X, lo, lane, nt)),
+     ...);
+}
+
+template <class C, int GRP>
+__device__ __forceinline__ void conv_x6(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W, const int (&lo)[2],
+                                        int lane, int nt) {
+    if constexpr (C::PIPE)
+        conv_x6_pipe<C, GRP>(acc, img, W, lo, lane, nt,
+                             std::make_integer_sequence<int, X6PlanOf<GRP, C::KH>::P.nbat>{});
+    else
+        conv_x6_taps<C, GRP>(acc, img, W, lo, lane, nt, std::make_integer_sequence<int, 18>{});
 }
 
 // bias (+ residual), ReLU, split into the three LDS planes; C/D layout as in epilogue<>. eo[r] =
@@ -765,26 +895,51 @@ __device__ __forceinline__ void conv_x6_taps(f32x4 (&acc)[nn::kTPW], const char*
 // addresses are eo[r] plus immediates. ADD: add the residual held in `skip`; KEEP: the result is
 // the next block's input, keep it in `skip` (every conv maps (square, position, channel) to the
 // same lane and register, so the residual never has to be read back from the split LDS image).
-template <int GRP>
+template <class C, int GRP>
 __device__ __forceinline__ void epilogue_x6(const f32x4 (&acc)[nn::kTPW], char* img, const float* bias,
                                             f32x4 (&skip)[nn::kTPW], const int (&eo)[4], int co, bool add,
                                             bool keep) {
     constexpr int n = GRP == 0 ? nn::kTPW : 25 - nn::kTPW;
     const float bb = bias[co];
+    const bool odd = co & 1;
 #pragma unroll
-    for (int j = 0; j < n; ++j)
+    for (int j = 0; j < n; ++j) {
+        char* sqimg = img + kSqOrder[GRP * nn::kTPW + j] * (nn::kSB * x6::kRowB);
+        float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            float v = acc[j][r] + bb;
-            if (add) v += skip[j][r];
-            v = v > 0.0f ? v : 0.0f;
-            if (keep) skip[j][r] = v;
-            x6::store_at(img + kSqOrder[GRP * nn::kTPW + j] * (nn::kSB * x6::kRowB), eo[r], v);
+            v[r] = acc[j][r] + bb;
+            if (add) v[r] += skip[j][r];
+            v[r] = v[r] > 0.0f ? v[r] : 0.0f;
+            if (keep) skip[j][r] = v[r];
         }
+        if constexpr (C::EPI == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x6::store_at(sqimg, eo[r], v[r]);
+        } else {
+            // lanes co (even) and co^1 hold the same rows: the even lane stores rows 0 and 2, the
+            // odd lane rows 1 and 3, each as (even channel, odd channel) bf16 pairs per piece;
+            // eo[k] = elem_off(row of store k, co & ~1)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const float mine = odd ? v[2 * k + 1] : v[2 * k];  // the row this lane stores
+                const float give = odd ? v[2 * k] : v[2 * k + 1];  // the row the partner stores
+                const float got = __shfl_xor(give, 1);
+                const float lo = odd ? got : mine, hi = odd ? mine : got;
+                uint16_t lh, lm, ll, hh, hm, hl;
+                x6::split3(lo, lh, lm, ll);
+                x6::split3(hi, hh, hm, hl);
+                uint32_t* d = reinterpret_cast<uint32_t*>(sqimg + eo[k]);
+                d[0] = (uint32_t)lh | ((uint32_t)hh << 16);
+                d[32] = (uint32_t)lm | ((uint32_t)hm << 16);
+                d[64] = (uint32_t)ll | ((uint32_t)hl << 16);
+            }
+        }
+    }
 }
 
 // The whole forward for the waves of square group GRP (compile-time square list).
-template <int GRP>
+template <class C, int GRP>
 __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
                                            int blocks, float* __restrict__ policy, float* __restrict__ value,
                                            float* lds) {
@@ -800,8 +955,13 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
     const int co = nt * 16 + (lane & 15);
     const int i = lane & 15, kq = lane >> 4;
     int eo[4];
+    if constexpr (C::EPI == 0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) eo[r] = x6::elem_off(kq * 4 + r, co);
+        for (int r = 0; r < 4; ++r) eo[r] = x6::elem_off(kq * 4 + r, co);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) eo[k] = eo[k + 2] = x6::elem_off(kq * 4 + 2 * k + (co & 1), co & ~1);
+    }
     const int lo[2] = {x6::chunk_off(i, 0, kq), x6::chunk_off(i, 0, 4 + kq)};
 
     f32x4 acc[nn::kTPW];
@@ -821,7 +981,7 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
         for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
         conv_l1(acc, bb, blob, sq, lane, nt, ntiles);
         conv_l1_const(acc, blob + nn::kL1B + nn::kCh, pinfo[i], sq, lane, nt, ntiles);
-        epilogue_x6<GRP>(acc, img, blob + nn::kL1B, skip, eo, co, false, true);
+        epilogue_x6<C, GRP>(acc, img, blob + nn::kL1B, skip, eo, co, false, true);
         __syncthreads();
     }
     // 2 * blocks convs through one call site (small block 1: conv + BN + ReLU; small block 2:
@@ -830,11 +990,10 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
     for (int c = 0; c < 2 * blocks; ++c) {
 #pragma unroll
         for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
-        conv_x6_taps<GRP>(acc, img, reinterpret_cast<const bf16x8*>(p), lo, lane, nt,
-                          std::make_integer_sequence<int, 18>{});
+        conv_x6<C, GRP>(acc, img, reinterpret_cast<const bf16x8*>(p), lo, lane, nt);
         p += x6::kW;
         __syncthreads();
-        epilogue_x6<GRP>(acc, img, p, skip, eo, co, c & 1, c & 1);
+        if (C::DBG != 1 || B == -12345) epilogue_x6<C, GRP>(acc, img, p, skip, eo, co, c & 1, c & 1);
         p += nn::kCh;
         __syncthreads();
     }
@@ -843,22 +1002,33 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
         heads_g([&](int row, int c) { return x6::load(img, row, c); }, scratch, s, p, lane, b0 + s, B, policy, value);
 }
 
+template <class C>
 __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_x6(const oaz_state* __restrict__ states, int B,
                                                           const float* __restrict__ blob, int blocks,
                                                           float* __restrict__ policy, float* __restrict__ value) {
     __shared__ __attribute__((aligned(16))) float lds[x6::kLdsFloats];
     if ((threadIdx.x >> 8) == 0)  // waves 0-3: square group 0, waves 4-7: group 1
-        nn_x6_body<0>(states, B, blob, blocks, policy, value, lds);
+        nn_x6_body<C, 0>(states, B, blob, blocks, policy, value, lds);
     else
-        nn_x6_body<1>(states, B, blob, blocks, policy, value, lds);
+        nn_x6_body<C, 1>(states, B, blob, blocks, policy, value, lds);
 }
 
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy, float* value,
                              hipStream_t st) {
     if (B <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
-    if (w.precision == OAZ_FP32_SPLIT)
-        hipLaunchKernelGGL(k_nn_x6, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy, value);
+    if (w.precision == OAZ_FP32_SPLIT) {
+        // default: pipelined balanced batches of <= 7 squares, paired b32 epilogue stores
+        // (DESIGN.md perf log); OAZ_NN_X6_V selects the A/B alternatives
+        auto k = k_nn_x6<X6Cfg<7, true, 1, 1>>;
+        switch (w.x6_variant) {
+            case 1: k = k_nn_x6<X6Cfg<7, true, 0, 0>>; break;     // per-step batches, b16 stores
+            case 2: k = k_nn_x6<X6Cfg<5, true, 1, 1>>; break;     // batches of <= 5
+            case 9: k = k_nn_x6<X6Cfg<7, true, 1, 1, 1>>; break;  // timing only: epilogue stores skipped
+            default: break;
+        }
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy, value);
+    }
     else if (w.precision == OAZ_BF16 && w.bf16_v1 == 1)
         hipLaunchKernelGGL(k_nn_sq16<true>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
                            value);

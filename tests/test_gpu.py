@@ -316,7 +316,7 @@ def test_selfplay_matches_oracle_games(orc, fixed, max_plies):
     assert np.array_equal(_sorted_rows(got), _sorted_rows(ref))
 
 
-@pytest.mark.parametrize("precision,blocks", [(_abi.FP32, 3), (_abi.BF16, 6)])
+@pytest.mark.parametrize("precision,blocks", [(_abi.FP32, 3), (_abi.FP32_SPLIT, 3), (_abi.BF16, 6)])
 def test_selfplay_nn_continuous_batching_runs(precision, blocks):
     with Engine(games=256, sims=16, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_NN, blocks=blocks, max_plies=150,
                 precision=precision, fixed_deck=0) as e:

@@ -24,12 +24,15 @@ def main():
     ap.add_argument("--precision", default="fp32,fp32x6,bf16")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--x6-variants", default="0", help="OAZ_NN_X6_V values to compare for fp32x6")
     a = ap.parse_args()
     g = np.load(ROOT / "tests/golden/nn_golden.npz")
     w3 = np.load(ROOT / "tests/golden/weights_3block_trained.npy")
     engines = {}
     for v in [int(x) for x in a.blocks.split(",")]:
-        for prec in a.precision.split(","):
+        for prec, var in [(p, x) for p in a.precision.split(",")
+                          for x in (a.x6_variants.split(",") if p == "fp32x6" else ["0"])]:
+            os.environ["OAZ_NN_X6_V"] = var
             e = Engine(games=a.batch, sims=1, blocks=v, evaluator=_abi.EVAL_NN,
                        precision={"bf16": _abi.BF16, "fp32x6": _abi.FP32_SPLIT}.get(prec, _abi.FP32))
             err = {}
@@ -42,11 +45,12 @@ def main():
                 err[name] = {"policy": float(np.abs(p - g[f"policy_{name}"]).max()),
                              "value": float(np.abs(val - g[f"value_{name}"]).max())}
             e.load_weights(random_weights(0, v))
-            engines[f"{v}-{prec}"] = (e, err, v)
+            engines[f"{v}-{prec}" + (f"-v{var}" if prec == "fp32x6" else "")] = (e, err, v, var)
     states = np.concatenate([g["states"]] * (a.batch // len(g["states"]) + 1))[: a.batch]
     res = {v: [] for v in engines}
     for _ in range(a.rounds):
-        for v, (e, _, _) in engines.items():
+        for v, (e, _, _, var) in engines.items():
+            os.environ["OAZ_NN_X6_V"] = var
             e.nn_forward(states[:1024])
             e.kernel_times_reset()
             e.set_timing(True)
