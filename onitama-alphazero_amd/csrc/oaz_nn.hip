@@ -675,20 +675,25 @@ __device__ __forceinline__ float load_at(const char* img, int o) {  // h + m + l
 __device__ __forceinline__ float load(const char* img, int row, int c) { return load_at(img, elem_off(row, c)); }
 }  // namespace x6
 
-// On-board squares of square group GRP for tap T, known at compile time: the conv below is
-// straight-line code per (group, tap), with no per-MFMA on-board tests.
-struct TapList {
-    int n;
-    int8_t j[nn::kTPW];   // index into the group's square list (accumulator)
-    int8_t nb[nn::kTPW];  // neighbour square read for that tap
-};
+// Square groups (compile-time): GRP 0 / 1 are the two halves of the 8-wave kernel (waves 0-3 /
+// 4-7; 4 corners + 4 edges + 5 interior | 8 edges + 4 interior = 85 / 84 on-board taps), GRP 2 is
+// the whole board (4-wave kernel: one wave per SIMD, all 25 squares of one N-tile).
 constexpr int8_t kSqOrder[25] = {0, 4, 20, 24, 1, 3, 21, 23, 6, 8, 12, 16, 18,
                                  2, 5, 10, 15, 9, 14, 19, 22, 7, 11, 13, 17};
+constexpr int grp_n(int grp) { return grp == 0 ? nn::kTPW : grp == 1 ? 25 - nn::kTPW : 25; }
+constexpr int grp_sq(int grp, int j) { return grp == 2 ? j : kSqOrder[grp * nn::kTPW + j]; }
+
+// On-board squares of group GRP for tap T: the conv is straight-line code per (group, tap), with no
+// per-MFMA on-board tests.
+struct TapList {
+    int n;
+    int8_t j[25];   // index into the group's square list (accumulator)
+    int8_t nb[25];  // neighbour square read for that tap
+};
 constexpr TapList tap_list(int grp, int t) {
     TapList L{};
-    const int n = grp == 0 ? nn::kTPW : 25 - nn::kTPW;
-    for (int j = 0; j < n; ++j) {
-        const int sq = kSqOrder[grp * nn::kTPW + j];
+    for (int j = 0; j < grp_n(grp); ++j) {
+        const int sq = grp_sq(grp, j);
         const int r = sq / 5 + t / 3 - 1, c = sq % 5 + t % 3 - 1;
         if (r >= 0 && r < 5 && c >= 0 && c < 5) {
             L.j[L.n] = (int8_t)j;
@@ -699,97 +704,14 @@ constexpr TapList tap_list(int grp, int t) {
     return L;
 }
 
-// Kernel variant knobs (A/B-tested, DESIGN.md perf log): KH = on-board squares per A batch; SB = a
-// scheduling barrier after each batch (bounds VGPR live ranges); EPI = epilogue store form (0:
-// ds_write_b16 per piece, 1: lane pairs exchange one value and store bf16 pairs as ds_write_b32).
-// PIPE: 1 = the conv is one software-pipelined sequence of balanced batches over all (tap, K-half)
-// steps (conv_x6_pipe), 0 = per-step batches of KH (conv_x6_step).
-// DBG (timing experiments only, wrong results): 1 = conv epilogue stores skipped.
-template <int KH_, bool SB_, int EPI_, int PIPE_ = 0, int DBG_ = 0>
-struct X6Cfg {
-    static constexpr int KH = KH_;
-    static constexpr bool SB = SB_;
-    static constexpr int EPI = EPI_;
-    static constexpr int PIPE = PIPE_;
-    static constexpr int DBG = DBG_;
-};
-
-// acc[j] += split-fp32 conv3x3 over 64 input channels, tap T, K-half M, for group GRP. For K-half
-// m lane l supplies A[row l&15][k = 8(l>>4) + e] = channel 32m + 8(l>>4) + e of each piece.
-// b[] holds this (tap, K-half)'s B pieces; the next one's are requested first.
-template <class C, int GRP, int T, int M>
-__device__ __forceinline__ void conv_x6_step(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W, bf16x8 (&b)[3],
-                                             int lo, int lane, int nt) {
-    constexpr TapList L = tap_list(GRP, T);
-    constexpr int nx = T * 2 + M + 1;  // next (tap, K-half)
-    bf16x8 bn[3];
-    if constexpr (nx < 18) {
-#pragma unroll
-        for (int pc = 0; pc < 3; ++pc) bn[pc] = W[((nx * 3 + pc) * 4 + nt) * 64 + lane];
-    }
-    // batches of <= KH on-board squares; A pieces are consumed in turn (h with B h/m/l, m with
-    // B h/m, l with B h) so at most two piece arrays are live; consecutive MFMAs hit different
-    // accumulators
-    constexpr int kH = C::KH;
-#pragma unroll
-    for (int q0 = 0; q0 < L.n; q0 += kH) {
-        bf16x8 a0[kH], a1[kH];
-#pragma unroll
-        for (int q = 0; q < kH; ++q)
-            if (q0 + q < L.n) {
-                const char* a = img + L.nb[q0 + q] * (nn::kSB * x6::kRowB) + lo;
-                a0[q] = *reinterpret_cast<const bf16x8*>(a);
-                a1[q] = *reinterpret_cast<const bf16x8*>(a + 128);
-            }
-        auto mm = [&](const bf16x8(&a)[kH], const bf16x8& bv) {
-#pragma unroll
-            for (int q = 0; q < kH; ++q)
-                if (q0 + q < L.n) {
-                    const int j = L.j[q0 + q];
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[q], bv, acc[j], 0, 0, 0);
-                }
-        };
-        mm(a0, b[0]);  // hh
-        mm(a0, b[1]);  // hm
-        mm(a0, b[2]);  // hl
-#pragma unroll
-        for (int q = 0; q < kH; ++q)
-            if (q0 + q < L.n) a0[q] = *reinterpret_cast<const bf16x8*>(img + L.nb[q0 + q] * (nn::kSB * x6::kRowB) + lo + 256);
-        mm(a1, b[0]);  // mh
-        mm(a1, b[1]);  // mm
-        mm(a0, b[0]);  // lh
-        if constexpr (C::SB) __builtin_amdgcn_sched_barrier(0);  // keep the next batch's loads from being hoisted
-    }
-    if constexpr (nx < 18) {
-#pragma unroll
-        for (int pc = 0; pc < 3; ++pc) b[pc] = bn[pc];
-    }
-}
-
-template <class C, int GRP, int... TM>
-__device__ __forceinline__ void conv_x6_taps(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W, const int (&lo)[2],
-                                             int lane, int nt, std::integer_sequence<int, TM...>) {
-    bf16x8 b[3];
-#pragma unroll
-    for (int pc = 0; pc < 3; ++pc) b[pc] = W[(pc * 4 + nt) * 64 + lane];
-    (conv_x6_step<C, GRP, TM / 2, TM % 2>(acc, img, W, b, lo[TM % 2], lane, nt), ...);
-}
-
-// ---- pipelined conv (PIPE = 1) ----
-// The 18 (tap, K-half) steps of a group are cut into batches of near-equal size (<= KH squares;
-// a step of n on-board squares gives ceil(n / KH) batches), and each batch runs
-//   [X = m pieces, loaded by the previous batch]  load Y = h pieces
-//   m*Bh, m*Bm                                    load X = l pieces
-//   h*Bh, h*Bm, h*Bl                              load Y = next batch's m pieces
-//   l*Bh
-// so every A load has >= KH MFMAs of cover and only two piece arrays are live.
+// Batch plan: the 18 (tap, K-half) steps cut into near-equal batches of <= KH on-board squares.
 struct X6Batch {
     int t, m, n;
-    int8_t j[8], nb[8];
+    int8_t j[16], nb[16];
 };
 struct X6Plan {
     int nbat;
-    X6Batch b[64];
+    X6Batch b[96];
 };
 constexpr X6Plan x6_plan(int grp, int kh) {
     X6Plan P{};
@@ -813,36 +735,53 @@ constexpr X6Plan x6_plan(int grp, int kh) {
     }
     return P;
 }
-
 template <int GRP, int KH>
 struct X6PlanOf {
     static constexpr X6Plan P = x6_plan(GRP, KH);
 };
 
-template <int N>
-__device__ __forceinline__ void x6_load(bf16x8 (&a)[N], const char* img, const X6Batch& B, int lo, int piece) {
+// Kernel configuration. WAVES 8: two waves per SIMD (square groups 0/1 x 4 N-tiles, <= 256 VGPRs);
+// WAVES 4: one wave per SIMD owning one N-tile of all 25 squares (up to 512 VGPRs). KH: squares per
+// batch. PIPE 1: two A-piece buffers (the m pieces of batch k+1 load during batch k's last
+// products); PIPE 2: three buffers (m, h, l each loaded one batch ahead). DBG 2 (timing only,
+// wrong results): per-wave s_memtime phase sums over the first policy rows (tools/nn_phases.py).
+template <int WAVES_, int KH_, int PIPE_, int DBG_ = 0>
+struct X6Cfg {
+    static constexpr int WAVES = WAVES_;
+    static constexpr int NS = WAVES_ == 8 ? nn::kTPW : 25;  // accumulator tiles per wave
+    static constexpr int KH = KH_;
+    static constexpr int PIPE = PIPE_;
+    static constexpr int DBG = DBG_;
+};
+
+// A-fragment loads / MFMAs of batch K (compile-time: the LDS address is one of six per-lane bases
+// ab[m][seg] = lo[m] + seg * 64 KiB plus an immediate offset < 64 KiB)
+template <int GRP, int KH, int K, int N>
+__device__ __forceinline__ void x6_load(bf16x8 (&a)[N], const char* img, const int (&ab)[2][3], int piece) {
+    constexpr X6Batch B = X6PlanOf<GRP, KH>::P.b[K];
 #pragma unroll
     for (int q = 0; q < N; ++q)
-        if (q < B.n) a[q] = *reinterpret_cast<const bf16x8*>(img + B.nb[q] * (nn::kSB * x6::kRowB) + lo + piece * 128);
+        if (q < B.n) {
+            const int off = B.nb[q] * (nn::kSB * x6::kRowB) + piece * 128;  // folds to a constant
+            a[q] = *reinterpret_cast<const bf16x8*>(img + ab[B.m][off >> 16] + (off & 0xffff));
+        }
 }
 
-template <int N>
-__device__ __forceinline__ void x6_mfma(f32x4 (&acc)[nn::kTPW], const bf16x8 (&a)[N], const bf16x8& bv, const X6Batch& B) {
+template <int GRP, int KH, int K, int NS, int N>
+__device__ __forceinline__ void x6_mfma(f32x4 (&acc)[NS], const bf16x8 (&a)[N], const bf16x8& bv) {
+    constexpr X6Batch B = X6PlanOf<GRP, KH>::P.b[K];
 #pragma unroll
     for (int q = 0; q < N; ++q)
         if (q < B.n) acc[B.j[q]] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[q], bv, acc[B.j[q]], 0, 0, 0);
 }
 
-// batch K of the plan. X holds its m pieces on entry and the next batch's m pieces on exit
-// (swapped by the caller through the X/Y roles alternating with K's parity).
+// B pieces of (tap, K-half) step S for N-tile nt: [step][piece][N-tile][lane] bf16x8
 template <class C, int GRP, int K>
-__device__ __forceinline__ void conv_x6_batch(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W,
-                                              bf16x8 (&b)[3], bf16x8 (&bn)[3], bf16x8 (&X)[C::KH],
-                                              bf16x8 (&Y)[C::KH], const int (&lo)[2], int lane, int nt) {
+__device__ __forceinline__ void x6_step_b(const bf16x8* W, bf16x8 (&b)[3], bf16x8 (&bn)[3], int lane, int nt) {
     constexpr const X6Plan& P = X6PlanOf<GRP, C::KH>::P;
     constexpr X6Batch B = P.b[K];
-    constexpr bool first_of_step = K == 0 || P.b[K - 1].t * 2 + P.b[K - 1].m != B.t * 2 + B.m;
     constexpr int step = B.t * 2 + B.m;
+    constexpr bool first_of_step = K == 0 || P.b[K - 1].t * 2 + P.b[K - 1].m != step;
     if constexpr (first_of_step && K > 0) {
 #pragma unroll
         for (int pc = 0; pc < 3; ++pc) b[pc] = bn[pc];
@@ -851,122 +790,199 @@ __device__ __forceinline__ void conv_x6_batch(f32x4 (&acc)[nn::kTPW], const char
 #pragma unroll
         for (int pc = 0; pc < 3; ++pc) bn[pc] = W[(((step + 1) * 3 + pc) * 4 + nt) * 64 + lane];
     }
-    x6_load(Y, img, B, lo[B.m], 0);  // h
-    x6_mfma(acc, X, b[0], B);        // mh
-    x6_mfma(acc, X, b[1], B);        // mm
-    x6_load(X, img, B, lo[B.m], 2);  // l
-    x6_mfma(acc, Y, b[0], B);        // hh
-    x6_mfma(acc, Y, b[1], B);        // hm
-    x6_mfma(acc, Y, b[2], B);        // hl
-    if constexpr (K + 1 < P.nbat) {
-        constexpr X6Batch Bn = P.b[K + 1];
-        x6_load(Y, img, Bn, lo[Bn.m], 1);  // next batch's m
-    }
-    x6_mfma(acc, X, b[0], B);  // lh
-    if constexpr (C::SB) __builtin_amdgcn_sched_barrier(0);
+}
+
+// PIPE 1, batch K (X holds its m pieces on entry and the next batch's on exit; X/Y swap roles
+// with K's parity):
+//   load Y = h | m*Bh, m*Bm | load X = l | h*Bh, h*Bm, h*Bl | load Y = next m | l*Bh
+template <class C, int GRP, int K>
+__device__ __forceinline__ void conv_x6_batch(f32x4 (&acc)[C::NS], const char* img, const bf16x8* W,
+                                              bf16x8 (&b)[3], bf16x8 (&bn)[3], bf16x8 (&X)[C::KH],
+                                              bf16x8 (&Y)[C::KH], const int (&ab)[2][3], int lane, int nt) {
+    constexpr int KH = C::KH, NS = C::NS;
+    x6_step_b<C, GRP, K>(W, b, bn, lane, nt);
+    x6_load<GRP, KH, K>(Y, img, ab, 0);
+    x6_mfma<GRP, KH, K, NS>(acc, X, b[0]);  // mh
+    x6_mfma<GRP, KH, K, NS>(acc, X, b[1]);  // mm
+    x6_load<GRP, KH, K>(X, img, ab, 2);
+    x6_mfma<GRP, KH, K, NS>(acc, Y, b[0]);  // hh
+    x6_mfma<GRP, KH, K, NS>(acc, Y, b[1]);  // hm
+    x6_mfma<GRP, KH, K, NS>(acc, Y, b[2]);  // hl
+    if constexpr (K + 1 < X6PlanOf<GRP, KH>::P.nbat) x6_load<GRP, KH, K + 1>(Y, img, ab, 1);
+    x6_mfma<GRP, KH, K, NS>(acc, X, b[0]);  // lh
+    __builtin_amdgcn_sched_barrier(0);      // bound the live ranges: no loads hoisted across batches
+}
+
+// PIPE 2, batch K: three buffers, each piece loaded one batch ahead of its use
+//   load BL = l | m*Bh, m*Bm | load BM = next m | h*Bh, h*Bm, h*Bl | load BH = next h | l*Bh
+template <class C, int GRP, int K>
+__device__ __forceinline__ void conv_x6_batch3(f32x4 (&acc)[C::NS], const char* img, const bf16x8* W,
+                                               bf16x8 (&b)[3], bf16x8 (&bn)[3], bf16x8 (&BM)[C::KH],
+                                               bf16x8 (&BH)[C::KH], bf16x8 (&BL)[C::KH], const int (&ab)[2][3],
+                                               int lane, int nt) {
+    constexpr int KH = C::KH, NS = C::NS;
+    constexpr bool more = K + 1 < X6PlanOf<GRP, KH>::P.nbat;
+    x6_step_b<C, GRP, K>(W, b, bn, lane, nt);
+    x6_load<GRP, KH, K>(BL, img, ab, 2);
+    x6_mfma<GRP, KH, K, NS>(acc, BM, b[0]);  // mh
+    x6_mfma<GRP, KH, K, NS>(acc, BM, b[1]);  // mm
+    if constexpr (more) x6_load<GRP, KH, K + 1>(BM, img, ab, 1);
+    x6_mfma<GRP, KH, K, NS>(acc, BH, b[0]);  // hh
+    x6_mfma<GRP, KH, K, NS>(acc, BH, b[1]);  // hm
+    x6_mfma<GRP, KH, K, NS>(acc, BH, b[2]);  // hl
+    if constexpr (more) x6_load<GRP, KH, K + 1>(BH, img, ab, 0);
+    x6_mfma<GRP, KH, K, NS>(acc, BL, b[0]);  // lh
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 template <class C, int GRP, int... K>
-__device__ __forceinline__ void conv_x6_pipe(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W,
-                                             const int (&lo)[2], int lane, int nt, std::integer_sequence<int, K...>) {
-    constexpr const X6Plan& P = X6PlanOf<GRP, C::KH>::P;
-    bf16x8 b[3], bn[3], X[C::KH], Y[C::KH];
+__device__ __forceinline__ void conv_x6_run(f32x4 (&acc)[C::NS], const char* img, const bf16x8* W, const int (&lo)[2],
+                                            int lane, int nt, std::integer_sequence<int, K...>) {
+    int ab[2][3];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int sg = 0; sg < 3; ++sg) ab[m][sg] = lo[m] + sg * 65536;
+    bf16x8 b[3], bn[3];
 #pragma unroll
     for (int pc = 0; pc < 3; ++pc) b[pc] = W[(pc * 4 + nt) * 64 + lane];
-    x6_load(X, img, P.b[0], lo[P.b[0].m], 1);
-    // even batches: m pieces in X; odd batches: in Y (the roles swap after every batch)
-    ((K % 2 == 0 ? conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, lo, lane, nt)
-                 : conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, Y, X, lo, lane, nt)),
-     ...);
+    if constexpr (C::PIPE == 2) {
+        bf16x8 BM[C::KH], BH[C::KH], BL[C::KH];
+        x6_load<GRP, C::KH, 0>(BM, img, ab, 1);
+        x6_load<GRP, C::KH, 0>(BH, img, ab, 0);
+        (conv_x6_batch3<C, GRP, K>(acc, img, W, b, bn, BM, BH, BL, ab, lane, nt), ...);
+    } else {
+        bf16x8 X[C::KH], Y[C::KH];
+        x6_load<GRP, C::KH, 0>(X, img, ab, 1);
+        ((K % 2 == 0 ? conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab, lane, nt)
+                     : conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, Y, X, ab, lane, nt)),
+         ...);
+    }
 }
 
+// bias (+ residual), ReLU, split into the three LDS planes; C/D layout as in epilogue<>. Lanes co
+// (even) and co^1 hold the same rows: the even lane stores rows 0 and 2, the odd lane rows 1 and
+// 3, each as (even channel, odd channel) bf16 pairs per piece; eo[k] = elem_off(row of store k,
+// co & ~1). ADD: add the residual held in `skip`; KEEP: the result is the next block's input, keep
+// it in `skip` (every conv maps (square, position, channel) to the same lane and register, so the
+// residual is never read back from the split LDS image).
 template <class C, int GRP>
-__device__ __forceinline__ void conv_x6(f32x4 (&acc)[nn::kTPW], const char* img, const bf16x8* W, const int (&lo)[2],
-                                        int lane, int nt) {
-    if constexpr (C::PIPE)
-        conv_x6_pipe<C, GRP>(acc, img, W, lo, lane, nt,
-                             std::make_integer_sequence<int, X6PlanOf<GRP, C::KH>::P.nbat>{});
-    else
-        conv_x6_taps<C, GRP>(acc, img, W, lo, lane, nt, std::make_integer_sequence<int, 18>{});
-}
-
-// bias (+ residual), ReLU, split into the three LDS planes; C/D layout as in epilogue<>. eo[r] =
-// x6::elem_off((lane >> 4) * 4 + r, co): with the square a compile-time constant the store
-// addresses are eo[r] plus immediates. ADD: add the residual held in `skip`; KEEP: the result is
-// the next block's input, keep it in `skip` (every conv maps (square, position, channel) to the
-// same lane and register, so the residual never has to be read back from the split LDS image).
-template <class C, int GRP>
-__device__ __forceinline__ void epilogue_x6(const f32x4 (&acc)[nn::kTPW], char* img, const float* bias,
-                                            f32x4 (&skip)[nn::kTPW], const int (&eo)[4], int co, bool add,
-                                            bool keep) {
-    constexpr int n = GRP == 0 ? nn::kTPW : 25 - nn::kTPW;
+__device__ __forceinline__ void epilogue_x6(const f32x4 (&acc)[C::NS], char* img, const float* bias,
+                                            f32x4 (&skip)[C::NS], const int (&eo)[2], int co, bool add, bool keep) {
     const float bb = bias[co];
     const bool odd = co & 1;
+    const float addf = add ? 1.0f : 0.0f;  // fma(skip, addf, v) = v + skip or v, exactly
 #pragma unroll
-    for (int j = 0; j < n; ++j) {
-        char* sqimg = img + kSqOrder[GRP * nn::kTPW + j] * (nn::kSB * x6::kRowB);
+    for (int j = 0; j < grp_n(GRP); ++j) {
+        char* sqimg = img + grp_sq(GRP, j) * (nn::kSB * x6::kRowB);
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            v[r] = acc[j][r] + bb;
-            if (add) v[r] += skip[j][r];
+            v[r] = __builtin_fmaf(skip[j][r], addf, acc[j][r] + bb);
             v[r] = v[r] > 0.0f ? v[r] : 0.0f;
             if (keep) skip[j][r] = v[r];
         }
-        if constexpr (C::EPI == 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) x6::store_at(sqimg, eo[r], v[r]);
-        } else {
-            // lanes co (even) and co^1 hold the same rows: the even lane stores rows 0 and 2, the
-            // odd lane rows 1 and 3, each as (even channel, odd channel) bf16 pairs per piece;
-            // eo[k] = elem_off(row of store k, co & ~1)
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const float mine = odd ? v[2 * k + 1] : v[2 * k];  // the row this lane stores
-                const float give = odd ? v[2 * k] : v[2 * k + 1];  // the row the partner stores
-                const float got = __shfl_xor(give, 1);
-                const float lo = odd ? got : mine, hi = odd ? mine : got;
-                uint16_t lh, lm, ll, hh, hm, hl;
-                x6::split3(lo, lh, lm, ll);
-                x6::split3(hi, hh, hm, hl);
-                uint32_t* d = reinterpret_cast<uint32_t*>(sqimg + eo[k]);
-                d[0] = (uint32_t)lh | ((uint32_t)hh << 16);
-                d[32] = (uint32_t)lm | ((uint32_t)hm << 16);
-                d[64] = (uint32_t)ll | ((uint32_t)hl << 16);
-            }
+        for (int k = 0; k < 2; ++k) {
+            // 2x2 transpose of (rows 2k, 2k+1) x (channels co&~1, co|1) between the lane pair:
+            // one DPP swap (quad_perm [1,0,3,2]); then per piece one v_perm_b32 packs the two
+            // bf16 (high halves) in channel order, its selector depending on the lane's parity
+            const float keep_ = odd ? v[2 * k + 1] : v[2 * k];  // stays in this lane
+            const float send = odd ? v[2 * k] : v[2 * k + 1];   // goes to the partner
+            const float got = __int_as_float(
+                __builtin_amdgcn_update_dpp(0, __float_as_int(send), 0xB1, 0xF, 0xF, false));
+            const uint32_t sel = odd ? 0x03020706u : 0x07060302u;
+            const uint32_t ka = __float_as_uint(keep_), ga = __float_as_uint(got);
+            const float kr = keep_ - __uint_as_float(ka & 0xffff0000u), gr = got - __uint_as_float(ga & 0xffff0000u);
+            const uint32_t kb = __float_as_uint(kr), gb = __float_as_uint(gr);
+            const float kl = kr - __uint_as_float(kb & 0xffff0000u), gl = gr - __uint_as_float(gb & 0xffff0000u);
+            uint32_t* d = reinterpret_cast<uint32_t*>(sqimg + eo[k]);
+            d[0] = __builtin_amdgcn_perm(ga, ka, sel);
+            d[32] = __builtin_amdgcn_perm(gb, kb, sel);
+            d[64] = __builtin_amdgcn_perm(__float_as_uint(gl), __float_as_uint(kl), sel);
         }
     }
 }
 
-// The whole forward for the waves of square group GRP (compile-time square list).
+// First layer (exact fp32 MFMA on 0/1 inputs, as k_nn_sq16): 4 bitboards x on-board taps, then the
+// constant planes (the mover's two cards, blue-to-move) as 5 k-steps against the per-square table.
+template <class C, int GRP>
+__device__ __forceinline__ void first_layer_x6(f32x4 (&acc)[C::NS], uint32_t bb, const float* W, const float* table,
+                                               int cinfo, int lane, int nt) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        const float b = W[(t * 4 + nt) * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < grp_n(GRP); ++j) {
+            const int sq = grp_sq(GRP, j);
+            const int r = sq / 5 + t / 3 - 1, c = sq % 5 + t % 3 - 1;
+            if (r >= 0 && r < 5 && c >= 0 && c < 5) {
+                const float a = (float)((bb >> (31 - (r * 5 + c))) & 1u);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+            }
+        }
+    }
+    const int kq = lane >> 4, co = nt * 16 + (lane & 15);
+    const int c0 = cinfo & 15, c1 = (cinfo >> 4) & 15, blue = (cinfo >> 8) & 1;
+    float a[5];
+#pragma unroll
+    for (int st = 0; st < 5; ++st) {
+        const int k = 4 * st + kq;
+        a[st] = k < 16 ? ((k == c0 || k == c1) ? 1.0f : 0.0f) : (k == 16 ? (float)blue : 0.0f);
+    }
+    constexpr int kBatch = 5;  // squares whose table entries are requested together
+#pragma unroll
+    for (int j0 = 0; j0 < grp_n(GRP); j0 += kBatch) {
+        float b[kBatch][5];
+#pragma unroll
+        for (int q = 0; q < kBatch; ++q)
+            if (j0 + q < grp_n(GRP)) {
+                const float* ts = table + (size_t)grp_sq(GRP, j0 + q) * 17 * nn::kCh + co;
+#pragma unroll
+                for (int st = 0; st < 5; ++st) {
+                    const int k = 4 * st + kq;
+                    b[q][st] = k < 17 ? ts[k * nn::kCh] : 0.0f;
+                }
+            }
+#pragma unroll
+        for (int st = 0; st < 5; ++st)
+#pragma unroll
+            for (int q = 0; q < kBatch; ++q)
+                if (j0 + q < grp_n(GRP))
+                    acc[j0 + q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], b[q][st], acc[j0 + q], 0, 0, 0);
+    }
+}
+
+// The whole forward for the waves of square group GRP.
 template <class C, int GRP>
 __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
                                            int blocks, float* __restrict__ policy, float* __restrict__ value,
                                            float* lds) {
+    constexpr int NS = C::NS;
     char* img = reinterpret_cast<char*>(lds);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nt = wave & 3;
-    constexpr int ntiles = GRP == 0 ? nn::kTPW : 25 - nn::kTPW;
-    int sq[nn::kTPW];
-#pragma unroll
-    for (int j = 0; j < nn::kTPW; ++j) sq[j] = j < ntiles ? kSqOrder[GRP * nn::kTPW + j] : 0;
     const int b0 = blockIdx.x * nn::kSB;
     int* pinfo = reinterpret_cast<int*>(lds + x6::kImageB / 4);
     const int co = nt * 16 + (lane & 15);
     const int i = lane & 15, kq = lane >> 4;
-    int eo[4];
-    if constexpr (C::EPI == 0) {
+    int eo[2];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) eo[r] = x6::elem_off(kq * 4 + r, co);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) eo[k] = eo[k + 2] = x6::elem_off(kq * 4 + 2 * k + (co & 1), co & ~1);
-    }
+    for (int k = 0; k < 2; ++k) eo[k] = x6::elem_off(kq * 4 + 2 * k + (co & 1), co & ~1);
     const int lo[2] = {x6::chunk_off(i, 0, kq), x6::chunk_off(i, 0, 4 + kq)};
 
-    f32x4 acc[nn::kTPW];
-    f32x4 skip[nn::kTPW];
-    {  // encoder + first layer in exact fp32 MFMA (0/1 inputs), as k_nn_sq16
+    f32x4 acc[NS];
+    f32x4 skip[NS];
+    uint64_t ph[6] = {0, 0, 0, 0, 0, 0};  // DBG 2: first layer, conv, barrier 1, epilogue, barrier 2, heads
+    uint64_t tm = C::DBG == 2 ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int k) {
+        if constexpr (C::DBG == 2) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            ph[k] += t - tm;
+            tm = t;
+        }
+    };
+    {  // encoder + first layer
         const int b = b0 + i < B ? b0 + i : b0;
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
         const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
@@ -978,36 +994,48 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
-        conv_l1(acc, bb, blob, sq, lane, nt, ntiles);
-        conv_l1_const(acc, blob + nn::kL1B + nn::kCh, pinfo[i], sq, lane, nt, ntiles);
+        for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};  // skip: finite for the fma in epilogue_x6
+        first_layer_x6<C, GRP>(acc, bb, blob, blob + nn::kL1B + nn::kCh, pinfo[i], lane, nt);
         epilogue_x6<C, GRP>(acc, img, blob + nn::kL1B, skip, eo, co, false, true);
         __syncthreads();
     }
     // 2 * blocks convs through one call site (small block 1: conv + BN + ReLU; small block 2:
     // conv + BN, + skip, ReLU)
+    stamp(0);
     const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
     for (int c = 0; c < 2 * blocks; ++c) {
 #pragma unroll
-        for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
-        conv_x6<C, GRP>(acc, img, reinterpret_cast<const bf16x8*>(p), lo, lane, nt);
+        for (int j = 0; j < NS; ++j) acc[j] = f32x4{};
+        conv_x6_run<C, GRP>(acc, img, reinterpret_cast<const bf16x8*>(p), lo, lane, nt,
+                            std::make_integer_sequence<int, X6PlanOf<GRP, C::KH>::P.nbat>{});
+        stamp(1);
         p += x6::kW;
         __syncthreads();
-        if (C::DBG != 1 || B == -12345) epilogue_x6<C, GRP>(acc, img, p, skip, eo, co, c & 1, c & 1);
+        stamp(2);
+        epilogue_x6<C, GRP>(acc, img, p, skip, eo, co, c & 1, c & 1);
+        stamp(3);
         p += nn::kCh;
         __syncthreads();
+        stamp(4);
     }
     float* scratch = lds + x6::kImageB / 4 + wave * nn::kScratch;
-    for (int s = wave; s < nn::kSB; s += nn::kWaves)
+    for (int s = wave; s < nn::kSB; s += C::WAVES)
         heads_g([&](int row, int c) { return x6::load(img, row, c); }, scratch, s, p, lane, b0 + s, B, policy, value);
+    if constexpr (C::DBG == 2) {
+        stamp(5);
+        __syncthreads();
+        if (lane < 6 && b0 + nn::kSB <= B) policy[(size_t)b0 * 50 + wave * 6 + lane] = (float)ph[lane];
+    }
 }
 
 template <class C>
-__global__ void __launch_bounds__(64 * nn::kWaves) k_nn_x6(const oaz_state* __restrict__ states, int B,
-                                                          const float* __restrict__ blob, int blocks,
-                                                          float* __restrict__ policy, float* __restrict__ value) {
+__global__ void __launch_bounds__(64 * C::WAVES) k_nn_x6(const oaz_state* __restrict__ states, int B,
+                                                        const float* __restrict__ blob, int blocks,
+                                                        float* __restrict__ policy, float* __restrict__ value) {
     __shared__ __attribute__((aligned(16))) float lds[x6::kLdsFloats];
-    if ((threadIdx.x >> 8) == 0)  // waves 0-3: square group 0, waves 4-7: group 1
+    if constexpr (C::WAVES == 4)
+        nn_x6_body<C, 2>(states, B, blob, blocks, policy, value, lds);
+    else if ((threadIdx.x >> 8) == 0)  // waves 0-3: square group 0, waves 4-7: group 1
         nn_x6_body<C, 0>(states, B, blob, blocks, policy, value, lds);
     else
         nn_x6_body<C, 1>(states, B, blob, blocks, policy, value, lds);
@@ -1018,16 +1046,21 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
     if (B <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
     if (w.precision == OAZ_FP32_SPLIT) {
-        // default: pipelined balanced batches of <= 7 squares, paired b32 epilogue stores
-        // (DESIGN.md perf log); OAZ_NN_X6_V selects the A/B alternatives
-        auto k = k_nn_x6<X6Cfg<7, true, 1, 1>>;
+        // default: 8 waves, pipelined batches of <= 7 squares (DESIGN.md perf log); OAZ_NN_X6_V
+        // selects the A/B alternatives
+        auto k = k_nn_x6<X6Cfg<8, 7, 1>>;
+        int waves = 8;
         switch (w.x6_variant) {
-            case 1: k = k_nn_x6<X6Cfg<7, true, 0, 0>>; break;     // per-step batches, b16 stores
-            case 2: k = k_nn_x6<X6Cfg<5, true, 1, 1>>; break;     // batches of <= 5
-            case 9: k = k_nn_x6<X6Cfg<7, true, 1, 1, 1>>; break;  // timing only: epilogue stores skipped
+            case 1: k = k_nn_x6<X6Cfg<4, 8, 1>>; waves = 4; break;
+            case 2: k = k_nn_x6<X6Cfg<4, 8, 2>>; waves = 4; break;
+            case 3: k = k_nn_x6<X6Cfg<4, 10, 2>>; waves = 4; break;
+            case 4: k = k_nn_x6<X6Cfg<4, 13, 2>>; waves = 4; break;
+            case 10: k = k_nn_x6<X6Cfg<8, 7, 1, 2>>; break;             // timing only: phase stamps
+            case 11: k = k_nn_x6<X6Cfg<4, 8, 2, 2>>; waves = 4; break;  // timing only: phase stamps
+            case 12: k = k_nn_x6<X6Cfg<4, 8, 1, 2>>; waves = 4; break;  // timing only: phase stamps
             default: break;
         }
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy, value);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value);
     }
     else if (w.precision == OAZ_BF16 && w.bf16_v1 == 1)
         hipLaunchKernelGGL(k_nn_sq16<true>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,

@@ -1,0 +1,31 @@
+"""Per-wave phase breakdown of k_nn_x6 (timing build OAZ_NN_X6_V=10: s_memtime sums per phase,
+written over each workgroup's first policy rows). Output: mean cycles per wave per phase."""
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "onitama-alphazero_amd"))
+os.environ["OAZ_NN_X6_V"] = os.environ.get("OAZ_NN_X6_V", "10")
+from onitama_az import _abi  # noqa: E402
+from onitama_az.engine import Engine  # noqa: E402
+from onitama_az.weights import random_weights  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+blocks = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+g = np.load(ROOT / "tests/golden/nn_golden.npz")
+states = np.concatenate([g["states"]] * (B // len(g["states"]) + 1))[:B]
+with Engine(games=B, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT) as e:
+    e.load_weights(random_weights(0, blocks))
+    e.nn_forward(states)
+    p, _ = e.nn_forward(states)
+flat = p.reshape(B // 16, 800)[:, :48].reshape(-1, 8, 6).astype(np.float64)
+names = ["first_layer", "conv", "barrier1", "epilogue", "barrier2", "heads"]
+mean = flat.mean(axis=0)  # [wave][phase]
+out = {"per_wave_mean_cycles": {f"w{w}": dict(zip(names, mean[w].round(0).tolist())) for w in range(8)},
+       "all_waves": dict(zip(names, mean.mean(0).round(0).tolist())),
+       "per_conv": {k: float(v) / (2 * blocks) for k, v in zip(names, mean.mean(0)) if k in ("conv", "barrier1", "epilogue", "barrier2")}}
+print(json.dumps(out, indent=1))
