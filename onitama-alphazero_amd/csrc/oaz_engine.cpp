@@ -307,6 +307,25 @@ static int pack_weights(const float* raw, int blocks, int precision, std::vector
     for (int i = 0; i < 50; ++i) out.push_back(*p++);    // ph_linear2.bias
     out.push_back(0.0f);
     out.push_back(0.0f);
+    if (precision == OAZ_FP32_SPLIT) {
+        // k_nn_x6 head 1x1 convs on MFMA: split B pieces [K-half m][piece][lane] bf16x8, lane l
+        // supplying B[k = 8(l>>4) + e][col n = l&15] for channel 32m + 8(l>>4) + e, columns
+        // n = 0 value conv, 1 / 2 policy conv planes, 3..15 zero
+        std::vector<uint16_t> h;
+        for (int m = 0; m < 2; ++m)
+            for (int pcs = 0; pcs < 3; ++pcs)
+                for (int l = 0; l < 64; ++l)
+                    for (int e = 0; e < 8; ++e) {
+                        const int c = 32 * m + 8 * (l >> 4) + e, n = l & 15;
+                        const float w = n == 0 ? vc.w[c] : n <= 2 ? pc.w[(n - 1) * 64 + c] : 0.0f;
+                        uint16_t sp[3];
+                        split3_host(w, sp);
+                        h.push_back(sp[pcs]);
+                    }
+        const size_t base = out.size();
+        out.resize(base + h.size() / 2);
+        memcpy(out.data() + base, h.data(), h.size() * sizeof(uint16_t));
+    }
     if (out.size() != nn_packed_floats(blocks, precision)) return oaz_set_err(OAZ_ERR_STATE, "pack: size mismatch");
     if ((size_t)(p - raw) != oaz_weight_count(blocks, 64, 21)) return oaz_set_err(OAZ_ERR_STATE, "pack: raw size mismatch");
     return 0;

@@ -90,11 +90,13 @@ constexpr int kRowB = 384;                  // LDS row: 3 pieces x 64 channels x
 constexpr int kImageB = nn::kSB * 25 * kRowB;  // 153,600 B
 constexpr int kLdsFloats = kImageB / 4 + nn::kWaves * nn::kScratch;  // 39,424 floats = 157,696 B
 constexpr size_t kW = 9 * 2 * 3 * 4 * 64 * 4;
+constexpr size_t kHeadB = 2 * 3 * 64 * 4;  // head 1x1 convs: [K-half][piece][lane] bf16x8 (after the heads)
 }  // namespace x6
 
 size_t nn_packed_floats(int blocks, int precision) {
     const size_t w = precision == OAZ_BF16 ? nn::kW64h : precision == OAZ_FP32_SPLIT ? x6::kW : nn::kW64;
-    return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (w + nn::kCh) + nn::kValueF + nn::kPolicyF;
+    return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (w + nn::kCh) + nn::kValueF + nn::kPolicyF +
+           (precision == OAZ_FP32_SPLIT ? x6::kHeadB : 0);
 }
 
 // Square groups: 4 corners + 4 edges + 5 interior (85 on-board taps) | 8 edges + 4 interior (84).
@@ -333,6 +335,36 @@ __device__ __forceinline__ void heads_g(const LD& ld, float* scratch, int s, con
     if (lane < 50) {
         lg = plb[lane];
         for (int f = 0; f < 50; ++f) lg += plw[f * 50 + lane] * scratch[32 + f];  // plw stored [in][out]
+    }
+    const float mx = wave_max_f(lg);
+    const float e = lane < 50 ? expf(lg - mx) : 0.0f;
+    const float den = wave_sum_f(e);
+    if (b < B) {
+        if (lane < 50) policy[(size_t)b * 50 + lane] = e / den;
+        if (lane == 0) value[b] = tanhf(vsum + l2b);
+    }
+}
+
+// The heads after the 1x1 convs, for position `s` (one wave): feat[0..24] = value features,
+// feat[25..74] = policy features in flatten(1,-1) order (already bias + ReLU). Same arithmetic as
+// heads_g's second half.
+__device__ __forceinline__ void heads_mlp(const float* feat, const float* p, int lane, int b, int B, float* policy,
+                                          float* value) {
+    const float* l1w = p + 68;
+    const float* l1b = l1w + 64 * 25;
+    const float* l2w = l1b + 64;
+    const float l2b = l2w[64];
+    const float* pp = p + nn::kValueF;
+    const float* plw = pp + 132;
+    const float* plb = plw + 2500;
+    float hj = l1b[lane];
+    for (int q = 0; q < 25; ++q) hj += l1w[q * 64 + lane] * feat[q];
+    hj = hj > 0.0f ? hj : 0.0f;
+    const float vsum = wave_sum_f(l2w[lane] * hj);
+    float lg = -INFINITY;
+    if (lane < 50) {
+        lg = plb[lane];
+        for (int f = 0; f < 50; ++f) lg += plw[f * 50 + lane] * feat[25 + f];
     }
     const float mx = wave_max_f(lg);
     const float e = lane < 50 ? expf(lg - mx) : 0.0f;
@@ -906,23 +938,44 @@ __device__ __forceinline__ void epilogue_x6(const f32x4 (&acc)[C::NS], char* img
 
 // First layer (exact fp32 MFMA on 0/1 inputs, as k_nn_sq16): 4 bitboards x on-board taps, then the
 // constant planes (the mover's two cards, blue-to-move) as 5 k-steps against the per-square table.
-template <class C, int GRP>
-__device__ __forceinline__ void first_layer_x6(f32x4 (&acc)[C::NS], uint32_t bb, const float* W, const float* table,
-                                               int cinfo, int lane, int nt) {
+// Its weights do not depend on the positions, so they are requested (first_layer_x6_fetch) before
+// the positions are read, and their latency overlaps the state load.
+template <int GRP>
+struct L1Regs {
+    float w[9];                 // bitboard weights per tap (lane: plane kq, channel co)
+    float t[grp_n(GRP)][5];     // table rows T[sq][4 st + kq][co]
+};
+template <int GRP>
+__device__ __forceinline__ void first_layer_x6_fetch(L1Regs<GRP>& R, const float* W, const float* table, int lane,
+                                                     int nt) {
+    const int kq = lane >> 4, co = nt * 16 + (lane & 15);
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-        const float b = W[(t * 4 + nt) * 64 + lane];
+    for (int t = 0; t < 9; ++t) R.w[t] = W[(t * 4 + nt) * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < grp_n(GRP); ++j) {
+        const float* ts = table + (size_t)grp_sq(GRP, j) * 17 * nn::kCh + co;
+#pragma unroll
+        for (int st = 0; st < 5; ++st) {
+            const int k = 4 * st + kq;
+            R.t[j][st] = k < 17 ? ts[k * nn::kCh] : 0.0f;
+        }
+    }
+}
+template <class C, int GRP>
+__device__ __forceinline__ void first_layer_x6(f32x4 (&acc)[C::NS], const L1Regs<GRP>& R, uint32_t bb, int cinfo,
+                                               int lane) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
 #pragma unroll
         for (int j = 0; j < grp_n(GRP); ++j) {
             const int sq = grp_sq(GRP, j);
             const int r = sq / 5 + t / 3 - 1, c = sq % 5 + t % 3 - 1;
             if (r >= 0 && r < 5 && c >= 0 && c < 5) {
                 const float a = (float)((bb >> (31 - (r * 5 + c))) & 1u);
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, R.w[t], acc[j], 0, 0, 0);
             }
         }
-    }
-    const int kq = lane >> 4, co = nt * 16 + (lane & 15);
+    const int kq = lane >> 4;
     const int c0 = cinfo & 15, c1 = (cinfo >> 4) & 15, blue = (cinfo >> 8) & 1;
     float a[5];
 #pragma unroll
@@ -930,27 +983,11 @@ __device__ __forceinline__ void first_layer_x6(f32x4 (&acc)[C::NS], uint32_t bb,
         const int k = 4 * st + kq;
         a[st] = k < 16 ? ((k == c0 || k == c1) ? 1.0f : 0.0f) : (k == 16 ? (float)blue : 0.0f);
     }
-    constexpr int kBatch = 5;  // squares whose table entries are requested together
 #pragma unroll
-    for (int j0 = 0; j0 < grp_n(GRP); j0 += kBatch) {
-        float b[kBatch][5];
+    for (int st = 0; st < 5; ++st)
 #pragma unroll
-        for (int q = 0; q < kBatch; ++q)
-            if (j0 + q < grp_n(GRP)) {
-                const float* ts = table + (size_t)grp_sq(GRP, j0 + q) * 17 * nn::kCh + co;
-#pragma unroll
-                for (int st = 0; st < 5; ++st) {
-                    const int k = 4 * st + kq;
-                    b[q][st] = k < 17 ? ts[k * nn::kCh] : 0.0f;
-                }
-            }
-#pragma unroll
-        for (int st = 0; st < 5; ++st)
-#pragma unroll
-            for (int q = 0; q < kBatch; ++q)
-                if (j0 + q < grp_n(GRP))
-                    acc[j0 + q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], b[q][st], acc[j0 + q], 0, 0, 0);
-    }
+        for (int j = 0; j < grp_n(GRP); ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], R.t[j][st], acc[j], 0, 0, 0);
 }
 
 // The whole forward for the waves of square group GRP.
@@ -983,6 +1020,8 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
         }
     };
     {  // encoder + first layer
+        L1Regs<GRP> l1;
+        first_layer_x6_fetch<GRP>(l1, blob, blob + nn::kL1B + nn::kCh, lane, nt);
         const int b = b0 + i < B ? b0 + i : b0;
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
         const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
@@ -995,7 +1034,7 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};  // skip: finite for the fma in epilogue_x6
-        first_layer_x6<C, GRP>(acc, bb, blob, blob + nn::kL1B + nn::kCh, pinfo[i], lane, nt);
+        first_layer_x6<C, GRP>(acc, l1, bb, pinfo[i], lane);
         epilogue_x6<C, GRP>(acc, img, blob + nn::kL1B, skip, eo, co, false, true);
         __syncthreads();
     }
@@ -1018,9 +1057,54 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
         __syncthreads();
         stamp(4);
     }
-    float* scratch = lds + x6::kImageB / 4 + wave * nn::kScratch;
-    for (int s = wave; s < nn::kSB; s += C::WAVES)
-        heads_g([&](int row, int c) { return x6::load(img, row, c); }, scratch, s, p, lane, b0 + s, B, policy, value);
+    // heads: the value / policy 1x1 convs as split-fp32 MFMAs on the LDS image (one 16x16 tile
+    // per square: rows = positions, columns 0 / 1 / 2 = value, policy planes 0 / 1), then the MLPs
+    // per position on the VALU from a feature table in LDS
+    {
+        const bf16x8* HB = reinterpret_cast<const bf16x8*>(p + nn::kValueF + nn::kPolicyF);
+        bf16x8 hb[2][3];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) hb[m][pc] = HB[(m * 3 + pc) * 64 + lane];
+        constexpr int kSqPerWave = (25 + C::WAVES - 1) / C::WAVES;
+        f32x4 hacc[kSqPerWave];
+#pragma unroll
+        for (int q = 0; q < kSqPerWave; ++q) {
+            hacc[q] = f32x4{};
+            const int sq = wave + q * C::WAVES;
+            if (sq < 25) {
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const char* a = img + sq * (nn::kSB * x6::kRowB) + lo[m];
+                    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a);
+                    const bf16x8 am = *reinterpret_cast<const bf16x8*>(a + 128);
+                    const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + 256);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, hb[m][0], hacc[q], 0, 0, 0);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, hb[m][1], hacc[q], 0, 0, 0);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[m][0], hacc[q], 0, 0, 0);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[m][1], hacc[q], 0, 0, 0);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[m][2], hacc[q], 0, 0, 0);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hb[m][0], hacc[q], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();  // the image is no longer read: its first 4.8 KB become the feature table
+        float* feat = reinterpret_cast<float*>(img);  // [16 positions][80]
+        const float hbias = i == 0 ? p[64] : i == 1 ? p[nn::kValueF + 128] : p[nn::kValueF + 129];
+#pragma unroll
+        for (int q = 0; q < kSqPerWave; ++q) {
+            const int sq = wave + q * C::WAVES;
+            if (sq < 25 && i < 3)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v = hacc[q][r] + hbias;
+                    feat[(kq * 4 + r) * 80 + i * 25 + sq] = v > 0.0f ? v : 0.0f;
+                }
+        }
+        __syncthreads();
+        for (int s = wave; s < nn::kSB; s += C::WAVES) heads_mlp(feat + s * 80, p, lane, b0 + s, B, policy, value);
+    }
     if constexpr (C::DBG == 2) {
         stamp(5);
         __syncthreads();
