@@ -807,9 +807,25 @@ __device__ __forceinline__ void x6_mfma(f32x4 (&acc)[NS], const bf16x8 (&a)[N], 
         if (q < B.n) acc[B.j[q]] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[q], bv, acc[B.j[q]], 0, 0, 0);
 }
 
-// B pieces of (tap, K-half) step S for N-tile nt: [step][piece][N-tile][lane] bf16x8
+// B pieces of (tap, K-half) step S for N-tile nt: [step][piece][N-tile][lane] bf16x8, read with
+// buffer loads (descriptor + one per-lane VGPR offset + a constant SGPR offset: no 64-bit vector
+// address arithmetic per load)
+struct X6W {
+    __amdgpu_buffer_rsrc_t r;
+    int voff;  // (nt * 64 + lane) * 16
+};
+__device__ __forceinline__ X6W x6_w(const float* p, int lane, int nt) {
+    X6W w;
+    w.r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(x6::kW * 4), 0x00020000);
+    w.voff = (nt * 64 + lane) * 16;
+    return w;
+}
+__device__ __forceinline__ bf16x8 x6_ldb(const X6W& w, int entry) {  // entry = (step * 3 + piece) * 4
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w.r, w.voff, entry * 64 * 16, 0));
+}
+
 template <class C, int GRP, int K>
-__device__ __forceinline__ void x6_step_b(const bf16x8* W, bf16x8 (&b)[3], bf16x8 (&bn)[3], int lane, int nt) {
+__device__ __forceinline__ void x6_step_b(const X6W& W, bf16x8 (&b)[3], bf16x8 (&bn)[3]) {
     constexpr const X6Plan& P = X6PlanOf<GRP, C::KH>::P;
     constexpr X6Batch B = P.b[K];
     constexpr int step = B.t * 2 + B.m;
@@ -820,7 +836,7 @@ __device__ __forceinline__ void x6_step_b(const bf16x8* W, bf16x8 (&b)[3], bf16x
     }
     if constexpr (first_of_step && step + 1 < 18) {  // prefetch the next step's B pieces
 #pragma unroll
-        for (int pc = 0; pc < 3; ++pc) bn[pc] = W[(((step + 1) * 3 + pc) * 4 + nt) * 64 + lane];
+        for (int pc = 0; pc < 3; ++pc) bn[pc] = x6_ldb(W, ((step + 1) * 3 + pc) * 4);
     }
 }
 
@@ -828,11 +844,11 @@ __device__ __forceinline__ void x6_step_b(const bf16x8* W, bf16x8 (&b)[3], bf16x
 // with K's parity):
 //   load Y = h | m*Bh, m*Bm | load X = l | h*Bh, h*Bm, h*Bl | load Y = next m | l*Bh
 template <class C, int GRP, int K>
-__device__ __forceinline__ void conv_x6_batch(f32x4 (&acc)[C::NS], const char* img, const bf16x8* W,
+__device__ __forceinline__ void conv_x6_batch(f32x4 (&acc)[C::NS], const char* img, const X6W& W,
                                               bf16x8 (&b)[3], bf16x8 (&bn)[3], bf16x8 (&X)[C::KH],
-                                              bf16x8 (&Y)[C::KH], const int (&ab)[2][3], int lane, int nt) {
+                                              bf16x8 (&Y)[C::KH], const int (&ab)[2][3]) {
     constexpr int KH = C::KH, NS = C::NS;
-    x6_step_b<C, GRP, K>(W, b, bn, lane, nt);
+    x6_step_b<C, GRP, K>(W, b, bn);
     x6_load<GRP, KH, K>(Y, img, ab, 0);
     x6_mfma<GRP, KH, K, NS>(acc, X, b[0]);  // mh
     x6_mfma<GRP, KH, K, NS>(acc, X, b[1]);  // mm
@@ -848,13 +864,12 @@ __device__ __forceinline__ void conv_x6_batch(f32x4 (&acc)[C::NS], const char* i
 // PIPE 2, batch K: three buffers, each piece loaded one batch ahead of its use
 //   load BL = l | m*Bh, m*Bm | load BM = next m | h*Bh, h*Bm, h*Bl | load BH = next h | l*Bh
 template <class C, int GRP, int K>
-__device__ __forceinline__ void conv_x6_batch3(f32x4 (&acc)[C::NS], const char* img, const bf16x8* W,
+__device__ __forceinline__ void conv_x6_batch3(f32x4 (&acc)[C::NS], const char* img, const X6W& W,
                                                bf16x8 (&b)[3], bf16x8 (&bn)[3], bf16x8 (&BM)[C::KH],
-                                               bf16x8 (&BH)[C::KH], bf16x8 (&BL)[C::KH], const int (&ab)[2][3],
-                                               int lane, int nt) {
+                                               bf16x8 (&BH)[C::KH], bf16x8 (&BL)[C::KH], const int (&ab)[2][3]) {
     constexpr int KH = C::KH, NS = C::NS;
     constexpr bool more = K + 1 < X6PlanOf<GRP, KH>::P.nbat;
-    x6_step_b<C, GRP, K>(W, b, bn, lane, nt);
+    x6_step_b<C, GRP, K>(W, b, bn);
     x6_load<GRP, KH, K>(BL, img, ab, 2);
     x6_mfma<GRP, KH, K, NS>(acc, BM, b[0]);  // mh
     x6_mfma<GRP, KH, K, NS>(acc, BM, b[1]);  // mm
@@ -868,8 +883,8 @@ __device__ __forceinline__ void conv_x6_batch3(f32x4 (&acc)[C::NS], const char* 
 }
 
 template <class C, int GRP, int... K>
-__device__ __forceinline__ void conv_x6_run(f32x4 (&acc)[C::NS], const char* img, const bf16x8* W, const int (&lo)[2],
-                                            int lane, int nt, std::integer_sequence<int, K...>) {
+__device__ __forceinline__ void conv_x6_run(f32x4 (&acc)[C::NS], const char* img, const X6W& W, const int (&lo)[2],
+                                            std::integer_sequence<int, K...>) {
     int ab[2][3];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -877,17 +892,17 @@ __device__ __forceinline__ void conv_x6_run(f32x4 (&acc)[C::NS], const char* img
         for (int sg = 0; sg < 3; ++sg) ab[m][sg] = lo[m] + sg * 65536;
     bf16x8 b[3], bn[3];
 #pragma unroll
-    for (int pc = 0; pc < 3; ++pc) b[pc] = W[(pc * 4 + nt) * 64 + lane];
+    for (int pc = 0; pc < 3; ++pc) b[pc] = x6_ldb(W, pc * 4);
     if constexpr (C::PIPE == 2) {
         bf16x8 BM[C::KH], BH[C::KH], BL[C::KH];
         x6_load<GRP, C::KH, 0>(BM, img, ab, 1);
         x6_load<GRP, C::KH, 0>(BH, img, ab, 0);
-        (conv_x6_batch3<C, GRP, K>(acc, img, W, b, bn, BM, BH, BL, ab, lane, nt), ...);
+        (conv_x6_batch3<C, GRP, K>(acc, img, W, b, bn, BM, BH, BL, ab), ...);
     } else {
         bf16x8 X[C::KH], Y[C::KH];
         x6_load<GRP, C::KH, 0>(X, img, ab, 1);
-        ((K % 2 == 0 ? conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab, lane, nt)
-                     : conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, Y, X, ab, lane, nt)),
+        ((K % 2 == 0 ? conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab)
+                     : conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, Y, X, ab)),
          ...);
     }
 }
@@ -899,14 +914,15 @@ __device__ __forceinline__ void conv_x6_run(f32x4 (&acc)[C::NS], const char* img
 // it in `skip` (every conv maps (square, position, channel) to the same lane and register, so the
 // residual is never read back from the split LDS image).
 template <class C, int GRP>
-__device__ __forceinline__ void epilogue_x6(const f32x4 (&acc)[C::NS], char* img, const float* bias,
-                                            f32x4 (&skip)[C::NS], const int (&eo)[2], int co, bool add, bool keep) {
+__device__ __forceinline__ void epilogue_x6_pack(const f32x4 (&acc)[C::NS], uint32_t (&pk)[C::NS][2][3],
+                                                 const float* bias, f32x4 (&skip)[C::NS], int co, bool add,
+                                                 bool keep) {
     const float bb = bias[co];
     const bool odd = co & 1;
     const float addf = add ? 1.0f : 0.0f;  // fma(skip, addf, v) = v + skip or v, exactly
+    const uint32_t sel = odd ? 0x03020706u : 0x07060302u;
 #pragma unroll
     for (int j = 0; j < grp_n(GRP); ++j) {
-        char* sqimg = img + grp_sq(GRP, j) * (nn::kSB * x6::kRowB);
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -923,17 +939,42 @@ __device__ __forceinline__ void epilogue_x6(const f32x4 (&acc)[C::NS], char* img
             const float send = odd ? v[2 * k] : v[2 * k + 1];   // goes to the partner
             const float got = __int_as_float(
                 __builtin_amdgcn_update_dpp(0, __float_as_int(send), 0xB1, 0xF, 0xF, false));
-            const uint32_t sel = odd ? 0x03020706u : 0x07060302u;
             const uint32_t ka = __float_as_uint(keep_), ga = __float_as_uint(got);
             const float kr = keep_ - __uint_as_float(ka & 0xffff0000u), gr = got - __uint_as_float(ga & 0xffff0000u);
             const uint32_t kb = __float_as_uint(kr), gb = __float_as_uint(gr);
             const float kl = kr - __uint_as_float(kb & 0xffff0000u), gl = gr - __uint_as_float(gb & 0xffff0000u);
-            uint32_t* d = reinterpret_cast<uint32_t*>(sqimg + eo[k]);
-            d[0] = __builtin_amdgcn_perm(ga, ka, sel);
-            d[32] = __builtin_amdgcn_perm(gb, kb, sel);
-            d[64] = __builtin_amdgcn_perm(__float_as_uint(gl), __float_as_uint(kl), sel);
+            pk[j][k][0] = __builtin_amdgcn_perm(ga, ka, sel);
+            pk[j][k][1] = __builtin_amdgcn_perm(gb, kb, sel);
+            pk[j][k][2] = __builtin_amdgcn_perm(__float_as_uint(gl), __float_as_uint(kl), sel);
         }
     }
+}
+template <class C, int GRP>
+__device__ __forceinline__ void epilogue_x6_store(const uint32_t (&pk)[C::NS][2][3], char* img, const int (&eo)[2]) {
+#pragma unroll
+    for (int j = 0; j < grp_n(GRP); ++j)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            uint32_t* d = reinterpret_cast<uint32_t*>(img + grp_sq(GRP, j) * (nn::kSB * x6::kRowB) + eo[k]);
+            d[0] = pk[j][k][0];
+            d[32] = pk[j][k][1];
+            d[64] = pk[j][k][2];
+        }
+}
+// bias (+ residual), ReLU, split into the three LDS planes; C/D layout as in epilogue<>. Lanes co
+// (even) and co^1 hold the same rows: the even lane stores rows 0 and 2, the odd lane rows 1 and
+// 3, each as (even channel, odd channel) bf16 pairs per piece; eo[k] = elem_off(row of store k,
+// co & ~1). ADD: add the residual held in `skip`; KEEP: the result is the next block's input, keep
+// it in `skip` (every conv maps (square, position, channel) to the same lane and register, so the
+// residual is never read back from the split LDS image). The VALU part (_pack) runs before the
+// barrier that ends the conv's reads, so a wave that finishes its MFMAs early packs while its SIMD
+// partner still computes; only the stores (_store) wait for the barrier.
+template <class C, int GRP>
+__device__ __forceinline__ void epilogue_x6(const f32x4 (&acc)[C::NS], char* img, const float* bias,
+                                            f32x4 (&skip)[C::NS], const int (&eo)[2], int co, bool add, bool keep) {
+    uint32_t pk[C::NS][2][3];
+    epilogue_x6_pack<C, GRP>(acc, pk, bias, skip, co, add, keep);
+    epilogue_x6_store<C, GRP>(pk, img, eo);
 }
 
 // First layer (exact fp32 MFMA on 0/1 inputs, as k_nn_sq16): 4 bitboards x on-board taps, then the
@@ -942,28 +983,32 @@ __device__ __forceinline__ void epilogue_x6(const f32x4 (&acc)[C::NS], char* img
 // the positions are read, and their latency overlaps the state load.
 template <int GRP>
 struct L1Regs {
-    float w[9];                 // bitboard weights per tap (lane: plane kq, channel co)
-    float t[grp_n(GRP)][5];     // table rows T[sq][4 st + kq][co]
+    float w[9];  // bitboard weights per tap (lane: plane kq, channel co)
 };
 template <int GRP>
-__device__ __forceinline__ void first_layer_x6_fetch(L1Regs<GRP>& R, const float* W, const float* table, int lane,
-                                                     int nt) {
-    const int kq = lane >> 4, co = nt * 16 + (lane & 15);
+__device__ __forceinline__ void first_layer_x6_fetch(L1Regs<GRP>& R, const float* W, int lane, int nt) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) R.w[t] = W[(t * 4 + nt) * 64 + lane];
-#pragma unroll
-    for (int j = 0; j < grp_n(GRP); ++j) {
-        const float* ts = table + (size_t)grp_sq(GRP, j) * 17 * nn::kCh + co;
-#pragma unroll
-        for (int st = 0; st < 5; ++st) {
-            const int k = 4 * st + kq;
-            R.t[j][st] = k < 17 ? ts[k * nn::kCh] : 0.0f;
-        }
-    }
 }
 template <class C, int GRP>
-__device__ __forceinline__ void first_layer_x6(f32x4 (&acc)[C::NS], const L1Regs<GRP>& R, uint32_t bb, int cinfo,
-                                               int lane) {
+__device__ __forceinline__ void first_layer_x6(f32x4 (&acc)[C::NS], const L1Regs<GRP>& R, const float* table,
+                                               uint32_t bb, int cinfo, int lane, int nt) {
+    const int kq = lane >> 4, co = nt * 16 + (lane & 15);
+    constexpr int kBatch = 5;  // squares whose table rows are requested together
+    float tb[kBatch][5];
+    auto fetch = [&](int j0) {
+#pragma unroll
+        for (int q = 0; q < kBatch; ++q)
+            if (j0 + q < grp_n(GRP)) {
+                const float* ts = table + (size_t)grp_sq(GRP, j0 + q) * 17 * nn::kCh + co;
+#pragma unroll
+                for (int st = 0; st < 5; ++st) {
+                    const int k = 4 * st + kq;
+                    tb[q][st] = k < 17 ? ts[k * nn::kCh] : 0.0f;
+                }
+            }
+    };
+    fetch(0);
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -975,7 +1020,6 @@ __device__ __forceinline__ void first_layer_x6(f32x4 (&acc)[C::NS], const L1Regs
                 acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, R.w[t], acc[j], 0, 0, 0);
             }
         }
-    const int kq = lane >> 4;
     const int c0 = cinfo & 15, c1 = (cinfo >> 4) & 15, blue = (cinfo >> 8) & 1;
     float a[5];
 #pragma unroll
@@ -984,10 +1028,15 @@ __device__ __forceinline__ void first_layer_x6(f32x4 (&acc)[C::NS], const L1Regs
         a[st] = k < 16 ? ((k == c0 || k == c1) ? 1.0f : 0.0f) : (k == 16 ? (float)blue : 0.0f);
     }
 #pragma unroll
-    for (int st = 0; st < 5; ++st)
+    for (int j0 = 0; j0 < grp_n(GRP); j0 += kBatch) {
 #pragma unroll
-        for (int j = 0; j < grp_n(GRP); ++j)
-            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], R.t[j][st], acc[j], 0, 0, 0);
+        for (int st = 0; st < 5; ++st)
+#pragma unroll
+            for (int q = 0; q < kBatch; ++q)
+                if (j0 + q < grp_n(GRP))
+                    acc[j0 + q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], tb[q][st], acc[j0 + q], 0, 0, 0);
+        if (j0 + kBatch < grp_n(GRP)) fetch(j0 + kBatch);
+    }
 }
 
 // The whole forward for the waves of square group GRP.
@@ -1021,7 +1070,7 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
     };
     {  // encoder + first layer
         L1Regs<GRP> l1;
-        first_layer_x6_fetch<GRP>(l1, blob, blob + nn::kL1B + nn::kCh, lane, nt);
+        first_layer_x6_fetch<GRP>(l1, blob, lane, nt);
         const int b = b0 + i < B ? b0 + i : b0;
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
         const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
@@ -1034,7 +1083,7 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};  // skip: finite for the fma in epilogue_x6
-        first_layer_x6<C, GRP>(acc, l1, bb, pinfo[i], lane);
+        first_layer_x6<C, GRP>(acc, l1, blob + nn::kL1B + nn::kCh, bb, pinfo[i], lane, nt);
         epilogue_x6<C, GRP>(acc, img, blob + nn::kL1B, skip, eo, co, false, true);
         __syncthreads();
     }
@@ -1045,13 +1094,16 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
     for (int c = 0; c < 2 * blocks; ++c) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = f32x4{};
-        conv_x6_run<C, GRP>(acc, img, reinterpret_cast<const bf16x8*>(p), lo, lane, nt,
+        conv_x6_run<C, GRP>(acc, img, x6_w(p, lane, nt), lo,
                             std::make_integer_sequence<int, X6PlanOf<GRP, C::KH>::P.nbat>{});
         stamp(1);
         p += x6::kW;
+        uint32_t pk[NS][2][3];
+        epilogue_x6_pack<C, GRP>(acc, pk, p, skip, co, c & 1, c & 1);
+        stamp(3);
         __syncthreads();
         stamp(2);
-        epilogue_x6<C, GRP>(acc, img, p, skip, eo, co, c & 1, c & 1);
+        epilogue_x6_store<C, GRP>(pk, img, eo);
         stamp(3);
         p += nn::kCh;
         __syncthreads();
@@ -1130,18 +1182,19 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
     if (B <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
     if (w.precision == OAZ_FP32_SPLIT) {
-        // default: 8 waves, pipelined batches of <= 7 squares (DESIGN.md perf log); OAZ_NN_X6_V
+        // default: 8 waves, pipelined batches of <= 5 squares (DESIGN.md perf log); OAZ_NN_X6_V
         // selects the A/B alternatives
-        auto k = k_nn_x6<X6Cfg<8, 7, 1>>;
+        auto k = k_nn_x6<X6Cfg<8, 5, 1>>;
         int waves = 8;
         switch (w.x6_variant) {
             case 1: k = k_nn_x6<X6Cfg<4, 8, 1>>; waves = 4; break;
             case 2: k = k_nn_x6<X6Cfg<4, 8, 2>>; waves = 4; break;
             case 3: k = k_nn_x6<X6Cfg<4, 10, 2>>; waves = 4; break;
             case 4: k = k_nn_x6<X6Cfg<4, 13, 2>>; waves = 4; break;
-            case 10: k = k_nn_x6<X6Cfg<8, 7, 1, 2>>; break;             // timing only: phase stamps
+            case 10: k = k_nn_x6<X6Cfg<8, 5, 1, 2>>; break;             // timing only: phase stamps
             case 11: k = k_nn_x6<X6Cfg<4, 8, 2, 2>>; waves = 4; break;  // timing only: phase stamps
             case 12: k = k_nn_x6<X6Cfg<4, 8, 1, 2>>; waves = 4; break;  // timing only: phase stamps
+            case 5: k = k_nn_x6<X6Cfg<8, 7, 1>>; break;
             default: break;
         }
         hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value);
