@@ -712,8 +712,19 @@ __device__ __forceinline__ float load(const char* img, int row, int c) { return 
 // the whole board (4-wave kernel: one wave per SIMD, all 25 squares of one N-tile).
 constexpr int8_t kSqOrder[25] = {0, 4, 20, 24, 1, 3, 21, 23, 6, 8, 12, 16, 18,
                                  2, 5, 10, 15, 9, 14, 19, 22, 7, 11, 13, 17};
-constexpr int grp_n(int grp) { return grp == 0 ? nn::kTPW : grp == 1 ? 25 - nn::kTPW : 25; }
-constexpr int grp_sq(int grp, int j) { return grp == 2 ? j : kSqOrder[grp * nn::kTPW + j]; }
+// GRP 3 / 4: an uneven split for the two waves of a SIMD (interior + corners + 2 edges = 109
+// on-board taps | the other 10 edges = 60): the older wave wins MFMA arbitration and runs ahead,
+// the younger fills its gaps, so equal halves leave the younger finishing alone.
+constexpr int8_t kSqOrderU[25] = {6, 7, 8, 11, 12, 13, 16, 17, 18, 0, 4, 20, 24, 2, 22,
+                                  1, 3, 5, 10, 9, 14, 15, 19, 21, 23};
+// GRP 5 / 6: 16 / 9 squares (115 / 54 taps), same order with one more edge in the first group.
+constexpr int grp_n(int grp) {
+    return grp == 0 ? nn::kTPW : grp == 1 ? 25 - nn::kTPW : grp == 3 ? 15 : grp == 4 ? 10 : grp == 5 ? 16 : grp == 6 ? 9 : 25;
+}
+constexpr int grp_sq(int grp, int j) {
+    return grp == 2 ? j : grp >= 5 ? kSqOrderU[(grp - 5) * 16 + j] : grp >= 3 ? kSqOrderU[(grp - 3) * 15 + j]
+                                                                            : kSqOrder[grp * nn::kTPW + j];
+}
 
 // On-board squares of group GRP for tap T: the conv is straight-line code per (group, tap), with no
 // per-MFMA on-board tests.
@@ -777,10 +788,13 @@ struct X6PlanOf {
 // batch. PIPE 1: two A-piece buffers (the m pieces of batch k+1 load during batch k's last
 // products); PIPE 2: three buffers (m, h, l each loaded one batch ahead). DBG 2 (timing only,
 // wrong results): per-wave s_memtime phase sums over the first policy rows (tools/nn_phases.py).
-template <int WAVES_, int KH_, int PIPE_, int DBG_ = 0>
+// UNEVEN (8 waves): square groups 3 / 4 (15 / 10 squares) instead of 0 / 1, the bigger group at
+// s_setprio 1.
+template <int WAVES_, int KH_, int PIPE_, int DBG_ = 0, int UNEVEN_ = 0>
 struct X6Cfg {
     static constexpr int WAVES = WAVES_;
-    static constexpr int NS = WAVES_ == 8 ? nn::kTPW : 25;  // accumulator tiles per wave
+    static constexpr int UNEVEN = UNEVEN_;
+    static constexpr int NS = WAVES_ == 8 ? (UNEVEN_ == 2 ? 16 : UNEVEN_ ? 15 : nn::kTPW) : 25;  // tiles per wave
     static constexpr int KH = KH_;
     static constexpr int PIPE = PIPE_;
     static constexpr int DBG = DBG_;
@@ -1169,9 +1183,17 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_x6(const oaz_state* __rest
                                                         const float* __restrict__ blob, int blocks,
                                                         float* __restrict__ policy, float* __restrict__ value) {
     __shared__ __attribute__((aligned(16))) float lds[x6::kLdsFloats];
-    if constexpr (C::WAVES == 4)
+    if constexpr (C::WAVES == 4) {
         nn_x6_body<C, 2>(states, B, blob, blocks, policy, value, lds);
-    else if ((threadIdx.x >> 8) == 0)  // waves 0-3: square group 0, waves 4-7: group 1
+    } else if constexpr (C::UNEVEN) {
+        constexpr int g0 = C::UNEVEN == 2 ? 5 : 3;
+        if ((threadIdx.x >> 8) == 0) {
+            __builtin_amdgcn_s_setprio(1);
+            nn_x6_body<C, g0>(states, B, blob, blocks, policy, value, lds);
+        } else {
+            nn_x6_body<C, g0 + 1>(states, B, blob, blocks, policy, value, lds);
+        }
+    } else if ((threadIdx.x >> 8) == 0)  // waves 0-3: square group 0, waves 4-7: group 1
         nn_x6_body<C, 0>(states, B, blob, blocks, policy, value, lds);
     else
         nn_x6_body<C, 1>(states, B, blob, blocks, policy, value, lds);
@@ -1182,19 +1204,19 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
     if (B <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
     if (w.precision == OAZ_FP32_SPLIT) {
-        // default: 8 waves, pipelined batches of <= 5 squares (DESIGN.md perf log); OAZ_NN_X6_V
-        // selects the A/B alternatives
-        auto k = k_nn_x6<X6Cfg<8, 5, 1>>;
+        // default: 8 waves, uneven 15 / 10 square split, pipelined batches of <= 4 squares
+        // (DESIGN.md perf log); OAZ_NN_X6_V selects the A/B alternatives
+        auto k = k_nn_x6<X6Cfg<8, 4, 1, 0, 1>>;
         int waves = 8;
         switch (w.x6_variant) {
-            case 1: k = k_nn_x6<X6Cfg<4, 8, 1>>; waves = 4; break;
-            case 2: k = k_nn_x6<X6Cfg<4, 8, 2>>; waves = 4; break;
-            case 3: k = k_nn_x6<X6Cfg<4, 10, 2>>; waves = 4; break;
-            case 4: k = k_nn_x6<X6Cfg<4, 13, 2>>; waves = 4; break;
+            case 1: k = k_nn_x6<X6Cfg<4, 8, 1>>; waves = 4; break;  // one 512-VGPR wave per SIMD
+            case 2: k = k_nn_x6<X6Cfg<4, 8, 2>>; waves = 4; break;  // + three piece buffers
             case 10: k = k_nn_x6<X6Cfg<8, 5, 1, 2>>; break;             // timing only: phase stamps
-            case 11: k = k_nn_x6<X6Cfg<4, 8, 2, 2>>; waves = 4; break;  // timing only: phase stamps
-            case 12: k = k_nn_x6<X6Cfg<4, 8, 1, 2>>; waves = 4; break;  // timing only: phase stamps
             case 5: k = k_nn_x6<X6Cfg<8, 7, 1>>; break;
+            case 6: k = k_nn_x6<X6Cfg<8, 5, 1, 0, 1>>; break;
+            case 7: k = k_nn_x6<X6Cfg<8, 5, 1>>; break;  // even 13 / 12 split
+            case 9: k = k_nn_x6<X6Cfg<8, 3, 1, 0, 1>>; break;
+            case 13: k = k_nn_x6<X6Cfg<8, 4, 1, 2, 1>>; break;  // timing only: phase stamps
             default: break;
         }
         hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value);
