@@ -74,6 +74,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
+    ap.add_argument("--no-noise", action="store_true", help=argparse.SUPPRESS)  # experiments only: not C3
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--mode", default="selfplay", choices=["selfplay", "train", "pure_mcts"],
                     help="train: SGD steps of the training loop (SURVEY 8f #2), not the headline metric")
@@ -356,7 +357,8 @@ def main():
     traffic = None
     if not args.pmc_child and not args.no_pmc and world == 1:
         traffic = pmc_traffic(args, cfg)  # child processes; this process has not touched the GPU yet
-    eng = Engine(device=local, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0, train_noise=1,
+    eng = Engine(device=local, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0,
+                 train_noise=0 if args.no_noise else 1,
                  max_plies=150, evaluator=_abi.EVAL_NN,
                  precision={"bf16": _abi.BF16, "fp32_split": _abi.FP32_SPLIT}.get(cfg["precision"], _abi.FP32),
                  fixed_deck=cfg["fixed_deck"],

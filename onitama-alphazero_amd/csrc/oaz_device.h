@@ -162,6 +162,74 @@ OAZ_HD double u01(uint32_t a, uint32_t b) {
     return ((double)m + 0.5) * (1.0 / 9007199254740992.0);
 }
 
+// ---- Dirichlet root noise (mcts_arena.rs:186-203) ------------------------------------------
+// The reference draws a fresh Dirichlet(alpha; K) vector for every PUCT evaluation at the root
+// and uses component child.idx-1: marginally Beta(alpha, (K-1) alpha) = X / (X + Y) with
+// X ~ Gamma(alpha), Y ~ Gamma((K-1) alpha) (rand_distr 0.4.3: Marsaglia-Tsang, u^(1/shape) boost
+// for shape < 1). The noise parity with the reference is distributional (its thread_rng is
+// unseedable), so the draws are made in f32 and in the log domain: log X = log G(1+a) + log(U)/a,
+// eta = 1 / (1 + exp(log Y - log X)), which never underflows (u^(1/0.03) would, in f32). log and
+// exp are the polynomials below (only +, -, *, / and bit operations, no fma contraction): the
+// device and the C oracle compute bit-identical draws.
+OAZ_HD float nz_u(uint32_t x) {  // uniform in (0,1): (2k + 1) 2^-24, k = x >> 9 (exact in f32)
+    return (float)(((x >> 9) << 1) | 1u) * (1.0f / 16777216.0f);
+}
+OAZ_HD float nz_log(float x) {  // natural log for normal x > 0 (|rel err| < 2e-7)
+    uint32_t b = __builtin_bit_cast(uint32_t, x);
+    int e = (int)((b >> 23) & 0xFF) - 127;
+    b = (b & 0x007FFFFFu) | 0x3F800000u;  // mantissa m in [1, 2)
+    float m = __builtin_bit_cast(float, b);
+    if (m > 1.41421356f) {
+        m = m * 0.5f;
+        e += 1;
+    }
+    const float t = (m - 1.0f) / (m + 1.0f), t2 = t * t;
+    const float p = t * (2.0f + t2 * (0.666666667f + t2 * (0.4f + t2 * (0.285714286f + t2 * 0.222222222f))));
+    return (float)e * 0.693147182f + p;
+}
+OAZ_HD float nz_exp(float x) {  // e^x (|rel err| < 3e-7); 0 below -87, +inf above 88
+    if (x < -87.0f) return 0.0f;
+    if (x > 88.0f) return __builtin_bit_cast(float, 0x7F800000u);
+    const float k = (float)(int)(x * 1.44269504f + (x >= 0.0f ? 0.5f : -0.5f));
+    const float r = (x - k * 0.693145752f) - k * 1.42860677e-6f;  // ln2 split hi + lo
+    const float q = 1.0f + r * (1.0f + r * (0.5f + r * (0.166666667f + r * (0.0416666667f + r * (0.00833333333f +
+                                                                                        r * 0.00138888889f)))));
+    return q * __builtin_bit_cast(float, (uint32_t)((int)k + 127) << 23);
+}
+// log of a Gamma(shape >= 1) variate: Marsaglia-Tsang; attempt t uses Philox block
+// (game lo, game hi, c2, idx << 12 | which << 11 | t): a polar-method normal from words 0, 1
+// (attempts whose pair falls outside the unit disc are rejected too) and the acceptance uniform
+// from word 2.
+OAZ_HD float nz_log_gamma_large(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx, uint32_t which,
+                                float shape) {
+    const float d = shape - 0.333333333f;
+    const float c = 1.0f / __builtin_sqrtf(9.0f * d);
+    for (uint32_t t = 0; t < 1000u; ++t) {
+        const u32x4 r = philox(seed, (uint32_t)game, (uint32_t)(game >> 32), c2, (idx << 12) | (which << 11) | t);
+        const float v1 = 2.0f * nz_u(r.x) - 1.0f, v2 = 2.0f * nz_u(r.y) - 1.0f;
+        const float s = v1 * v1 + v2 * v2;
+        if (s >= 1.0f || s == 0.0f) continue;
+        const float x = v1 * __builtin_sqrtf(-2.0f * nz_log(s) / s);
+        const float vc = 1.0f + c * x;
+        if (vc <= 0.0f) continue;
+        const float lv = 3.0f * nz_log(vc), v = vc * vc * vc;
+        const float u = nz_u(r.z), x2 = x * x;
+        if (u < 1.0f - 0.0331f * (x2 * x2) || nz_log(u) < 0.5f * x2 + d * (1.0f - v + lv)) return nz_log(d) + lv;
+    }
+    return nz_log(d);
+}
+OAZ_HD float nz_log_gamma(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx, uint32_t which, float shape) {
+    if (shape >= 1.0f) return nz_log_gamma_large(seed, game, c2, idx, which, shape);
+    const u32x4 r = philox(seed, (uint32_t)game, (uint32_t)(game >> 32), c2, (idx << 12) | (which << 11) | 2047u);
+    return nz_log_gamma_large(seed, game, c2, idx, which, 1.0f + shape) + nz_log(nz_u(r.x)) / shape;
+}
+// draw idx (2j + {0: running best, 1: child j}) of comparison j; c2 = ply << 16 | sim
+OAZ_HD float root_noise(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx, float alpha, int K) {
+    const float lx = nz_log_gamma(seed, game, c2, idx, 0, alpha);
+    const float ly = nz_log_gamma(seed, game, c2, idx, 1, alpha * (float)(K - 1));
+    return 1.0f / (1.0f + nz_exp(ly - lx));
+}
+
 // Deck::default (deck.rs:139-151): random 5 of the 16 cards; Fisher-Yates driven by
 // Philox(seed; game_id, 0xDEA1, q).
 OAZ_HD void deal_deck(uint64_t seed, uint64_t game_id, uint8_t out[5]) {

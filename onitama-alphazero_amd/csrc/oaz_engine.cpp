@@ -131,6 +131,11 @@ extern "C" void oaz_initial_state(const uint8_t deck[5], oaz_state* out) {
     initial_state(deck, *out);
 }
 
+extern "C" float oaz_root_noise(uint64_t seed, uint64_t game_id, uint32_t ply, uint32_t sim, uint32_t draw,
+                                double alpha, int nchild) {
+    return root_noise(seed, game_id, (ply << 16) | (sim & 0xFFFFu), draw, (float)alpha, nchild);
+}
+
 extern "C" void oaz_hash_eval(const oaz_state* s, float policy[50], float* value) {
     const uint64_t h = hash_state(*s);
     for (int i = 0; i < 50; ++i) policy[i] = hash_policy(h, i);
@@ -455,7 +460,7 @@ struct oaz_engine {
     hipStream_t stream3 = nullptr;       // second half of the games (tree kernels overlap the other half's NN)
     hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_consumed[2] = {nullptr, nullptr};
     hipEvent_t ev_nn[2] = {nullptr, nullptr}, ev_join = nullptr;
-    double* noise = nullptr;             // [2][kNoiseChunk][G][kNoiseStride]
+    float* noise = nullptr;              // [2][kNoiseChunk][G][kNoiseStride]
     uint32_t G = 0, cap = 0, pathcap = 0, hcap = 0, out_cap = 0;
     // trees
     oaz_node* nodes = nullptr;
@@ -849,7 +854,7 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
     auto produce = [&](uint32_t c) -> int {
         if (c >= 2) HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[c & 1], 0));
         const uint32_t s0 = c * kNoiseChunk, n = sims - s0 < kNoiseChunk ? sims - s0 : kNoiseChunk;
-        double* buf = e->noise + (c & 1) * slot_elems;
+        float* buf = e->noise + (c & 1) * slot_elems;
         if (int rc = timed(e, 4, t.G * n, [&] {
                 return launch_root_noise(roots, active, gids, plies, prm, t.G, s0, n, buf, e->stream2);
             }, e->stream2))
@@ -890,7 +895,7 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
             for (int h = 0; h < nh; ++h) {
                 const TreeView& th = tv[h];
                 const size_t go = g0[h];
-                const double* nz = noise ? e->noise + (c & 1) * slot_elems + (size_t)(s - s0) * t.G * kNoiseStride +
+                const float* nz = noise ? e->noise + (c & 1) * slot_elems + (size_t)(s - s0) * t.G * kNoiseStride +
                                                go * kNoiseStride
                                          : nullptr;
                 const uint8_t* act = active ? active + go : nullptr;  // null in search mode

@@ -97,10 +97,10 @@ size_t nn_packed_floats(int blocks, int precision);
 hipError_t launch_tree_reset(const TreeView& t, hipStream_t st);
 constexpr int kNoiseStride = 2 * OAZ_MAX_MOVES;  // doubles per (sim, game) in the noise buffer
 hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
-                         const double* noise /* [G][kNoiseStride] or null */, SearchParams p, hipStream_t st);
+                         const float* noise /* [G][kNoiseStride] or null */, SearchParams p, hipStream_t st);
 hipError_t launch_root_noise(const oaz_state* roots, const uint8_t* active, const uint64_t* game_id,
                              const uint32_t* ply, SearchParams p, uint32_t G, uint32_t sim0, uint32_t nsims,
-                             double* out /* [nsims][G][kNoiseStride] */, hipStream_t st);
+                             float* out /* [nsims][G][kNoiseStride] */, hipStream_t st);
 hipError_t launch_expand_backup(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                                 const float* policy, const float* value, hipStream_t st);
 hipError_t launch_search_finalize(const TreeView& t, const oaz_state* roots, oaz_move* out_move,

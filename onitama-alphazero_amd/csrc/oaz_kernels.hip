@@ -195,45 +195,7 @@ __global__ void k_hash_eval(const oaz_state* states, int n, float* policy, float
     value[i] = hash_value(h);
 }
 
-// ---- Dirichlet root noise ----------------------------------------------------------------
-// mcts_arena.rs:186-203 samples a fresh Dirichlet(alpha; K) vector for EVERY PUCT
-// evaluation at the root and reads component child.idx-1: marginally Beta(alpha, (K-1)alpha),
-// drawn as X/(X+Y) from gamma variates (rand_distr 0.4.3 Gamma: Marsaglia-Tsang with the
-// u^(1/shape) boost for shape < 1). Counter layout = oracle/oaz_oracle.c gamma_ctr.
-__device__ double gamma_large_dev(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx,
-                                  uint32_t which, double shape) {
-    const double d = shape - 1.0 / 3.0;
-    const double c = 1.0 / sqrt(9.0 * d);
-    for (uint32_t t = 0; t < 1000; ++t) {
-        const uint32_t c3 = (idx << 12) | (which << 11);
-        const u32x4 r = philox(seed, (uint32_t)game, (uint32_t)(game >> 32), c2, c3 | t);
-        const u32x4 r2 = philox(seed, (uint32_t)game, (uint32_t)(game >> 32), c2, c3 | (t | 1024u));
-        const double u1 = u01(r.x, r.y), u2 = u01(r.z, r.w);
-        const double x = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-        const double vc = 1.0 + c * x;
-        if (vc <= 0.0) continue;
-        const double v = vc * vc * vc;
-        const double u = u01(r2.x, r2.y);
-        const double x2 = x * x;
-        if (u < 1.0 - 0.0331 * x2 * x2 || log(u) < 0.5 * x2 + d * (1.0 - v + log(v))) return d * v;
-    }
-    return d;
-}
-__device__ double gamma_dev(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx,
-                            uint32_t which, double shape) {
-    if (shape >= 1.0) return gamma_large_dev(seed, game, c2, idx, which, shape);
-    const u32x4 r = philox(seed, (uint32_t)game, (uint32_t)(game >> 32), c2,
-                           (idx << 12) | (which << 11) | 2047u);
-    return gamma_large_dev(seed, game, c2, idx, which, 1.0 + shape) * pow(u01(r.x, r.y), 1.0 / shape);
-}
-__device__ double beta_noise_dev(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx,
-                                 double alpha, int K) {
-    const double x = gamma_dev(seed, game, c2, idx, 0, alpha);
-    const double y = gamma_dev(seed, game, c2, idx, 1, alpha * (double)(K - 1));
-    const double s = x + y;
-    return s > 0.0 ? x / s : 0.0;
-}
-
+// ---- Dirichlet root noise: root_noise() in oaz_device.h ------------------------------------
 // Dirichlet draws of nsims consecutive simulations for every root: out[(k*G + g)*80 + 2j + {0,1}]
 // holds the noise for comparison j (operand a, operand b) of simulation sim0+k. They depend only
 // on (root position, game id, ply, sim), so they are produced off the critical path (second
@@ -243,7 +205,7 @@ __global__ void __launch_bounds__(kBlock) k_root_noise(const oaz_state* __restri
                                                        const uint8_t* __restrict__ active,
                                                        const uint64_t* __restrict__ game_ids,
                                                        const uint32_t* __restrict__ plies, SearchParams prm,
-                                                       uint32_t G, uint32_t sim0, uint32_t nsims, double* out) {
+                                                       uint32_t G, uint32_t sim0, uint32_t nsims, float* out) {
     const uint32_t g = wave_game();
     if (g >= G) return;
     if (active && active[g] != 1) return;
@@ -259,7 +221,7 @@ __global__ void __launch_bounds__(kBlock) k_root_noise(const oaz_state* __restri
         const int k = idx / per_sim, r = idx - k * per_sim;
         const uint32_t d = 2u + (uint32_t)r;  // draw index 2j + which, j = 1 + r/2
         const uint32_t c2 = (ply << 16) | ((sim0 + k) & 0xFFFFu);
-        out[((size_t)k * G + g) * kNoiseStride + d] = beta_noise_dev(prm.seed, gid, c2, d, prm.alpha, K);
+        out[((size_t)k * G + g) * kNoiseStride + d] = root_noise(prm.seed, gid, c2, d, (float)prm.alpha, K);
     }
 }
 
@@ -302,7 +264,7 @@ __global__ void __launch_bounds__(kBlock) k_tree_reset(TreeView t) {
 // not terminal; replay each chosen move; mark children whose move wins as terminal.
 __global__ void __launch_bounds__(kBlock) k_select(TreeView t, const oaz_state* __restrict__ roots,
                                                    const uint8_t* __restrict__ active,
-                                                   const double* __restrict__ noise,
+                                                   const float* __restrict__ noise,
                                                    SearchParams prm) {
     const uint32_t g = wave_game();
     if (g >= t.G) return;
@@ -343,8 +305,8 @@ __global__ void __launch_bounds__(kBlock) k_select(TreeView t, const oaz_state* 
             // is sequential; the fold runs on wave-uniform values read with v_readlane.
             double na = 0.0, nb = 0.0;
             if (l >= 1 && l < K) {
-                na = noise[(size_t)g * kNoiseStride + 2 * l];
-                nb = noise[(size_t)g * kNoiseStride + 2 * l + 1];
+                na = (double)noise[(size_t)g * kNoiseStride + 2 * l];
+                nb = (double)noise[(size_t)g * kNoiseStride + 2 * l + 1];
             }
             const double base = ch.P * (1.0 - prm.eps);
             const double ubl = q + prm.c_puct * (base + nb * prm.eps) * sq;
@@ -685,13 +647,13 @@ hipError_t launch_tree_reset(const TreeView& t, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
-                         const double* noise, SearchParams p, hipStream_t st) {
+                         const float* noise, SearchParams p, hipStream_t st) {
     hipLaunchKernelGGL(k_select, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, roots, active, noise, p);
     return hipGetLastError();
 }
 hipError_t launch_root_noise(const oaz_state* roots, const uint8_t* active, const uint64_t* game_id,
                              const uint32_t* ply, SearchParams p, uint32_t G, uint32_t sim0, uint32_t nsims,
-                             double* out, hipStream_t st) {
+                             float* out, hipStream_t st) {
     hipLaunchKernelGGL(k_root_noise, dim3(wave_grid(G)), dim3(kBlock), 0, st, roots, active, game_id, ply, p, G,
                        sim0, nsims, out);
     return hipGetLastError();

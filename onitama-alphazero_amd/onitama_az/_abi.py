@@ -189,6 +189,7 @@ _PROTOS = {
     "oaz_deal_deck": (None, [C.c_uint64, C.c_uint64, _VOIDP]),
     "oaz_initial_state": (None, [_VOIDP, _VOIDP]),
     "oaz_hash_eval": (None, [_VOIDP, _VOIDP, _VOIDP]),
+    "oaz_root_noise": (C.c_float, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double, C.c_int]),
     "oaz_movegen": (C.c_int, [_VOIDP, C.c_int, _VOIDP, _VOIDP, _VOIDP]),
     "oaz_step": (C.c_int, [_VOIDP, _VOIDP, C.c_int, _VOIDP]),
     "oaz_current_state": (C.c_int, [_VOIDP, C.c_int, _VOIDP]),

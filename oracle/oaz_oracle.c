@@ -489,12 +489,44 @@ static inline int64_t tkey(double x) {
 
 /* --- Dirichlet root noise (mcts_arena.rs:186-203). Each PUCT evaluation at the root draws
  * a fresh Dirichlet(alpha; K) vector and uses component child.idx-1, i.e. a
- * Beta(alpha, (K-1)alpha) variate; drawn here as X/(X+Y) from two gamma variates
- * (rand_distr 0.4.3 Gamma: Marsaglia-Tsang, small-shape boost u^(1/shape)). */
+ * Beta(alpha, (K-1)alpha) variate X/(X+Y) from two gamma variates (rand_distr 0.4.3 Gamma:
+ * Marsaglia-Tsang, small-shape boost u^(1/shape)). The reference's thread_rng is unseedable, so
+ * noise parity is distributional; this restates the engine's f32 log-domain formulation
+ * (oaz_device.h root_noise) op for op so that the engine's draws can be checked bit for bit:
+ * log X = log G(1+a) + log(U)/a, eta = 1/(1 + exp(log Y - log X)), with polynomial log/exp
+ * (+, -, *, /, sqrt and bit operations only; built with -ffp-contract=off). */
 typedef struct {
     uint64_t seed, game;
     uint32_t c2;
 } noise_key;
+
+static float f_from_u(uint32_t b) { float f; memcpy(&f, &b, 4); return f; }
+static uint32_t u_from_f(float f) { uint32_t b; memcpy(&b, &f, 4); return b; }
+
+static float nz_u(uint32_t x) { return (float)(((x >> 9) << 1) | 1u) * (1.0f / 16777216.0f); }
+
+static float nz_log(float x) {
+    uint32_t b = u_from_f(x);
+    int e = (int)((b >> 23) & 0xFF) - 127;
+    float m = f_from_u((b & 0x007FFFFFu) | 0x3F800000u);
+    if (m > 1.41421356f) {
+        m = m * 0.5f;
+        e += 1;
+    }
+    const float t = (m - 1.0f) / (m + 1.0f), t2 = t * t;
+    const float p = t * (2.0f + t2 * (0.666666667f + t2 * (0.4f + t2 * (0.285714286f + t2 * 0.222222222f))));
+    return (float)e * 0.693147182f + p;
+}
+
+static float nz_exp(float x) {
+    if (x < -87.0f) return 0.0f;
+    if (x > 88.0f) return f_from_u(0x7F800000u);
+    const float k = (float)(int)(x * 1.44269504f + (x >= 0.0f ? 0.5f : -0.5f));
+    const float r = (x - k * 0.693145752f) - k * 1.42860677e-6f;
+    const float q = 1.0f + r * (1.0f + r * (0.5f + r * (0.166666667f + r * (0.0416666667f + r * (0.00833333333f +
+                                                                                        r * 0.00138888889f)))));
+    return q * f_from_u((uint32_t)((int)k + 127) << 23);
+}
 
 static void gamma_ctr(const noise_key* k, uint32_t idx, uint32_t which, uint32_t t, uint32_t out[4]) {
     uint32_t ctr[4] = {(uint32_t)k->game, (uint32_t)(k->game >> 32), k->c2,
@@ -502,38 +534,43 @@ static void gamma_ctr(const noise_key* k, uint32_t idx, uint32_t which, uint32_t
     orc_philox(k->seed, ctr, out);
 }
 
-static double gamma_large(const noise_key* k, uint32_t idx, uint32_t which, double shape) {
-    const double d = shape - 1.0 / 3.0;
-    const double c = 1.0 / sqrt(9.0 * d);
-    for (uint32_t t = 0; t < 1000; t++) {
-        uint32_t r[4], r2[4];
+/* log of a Gamma(shape >= 1) variate: Marsaglia-Tsang with a polar-method normal (words 0, 1)
+ * and the acceptance uniform (word 2) of attempt t's Philox block */
+static float log_gamma_large(const noise_key* k, uint32_t idx, uint32_t which, float shape) {
+    const float d = shape - 0.333333333f;
+    const float c = 1.0f / sqrtf(9.0f * d);
+    for (uint32_t t = 0; t < 1000u; t++) {
+        uint32_t r[4];
         gamma_ctr(k, idx, which, t, r);
-        gamma_ctr(k, idx, which, t | 1024u, r2);
-        const double u1 = u01_open(r[0], r[1]), u2 = u01_open(r[2], r[3]);
-        const double x = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-        const double vc = 1.0 + c * x;
-        if (vc <= 0.0) continue;
-        const double v = vc * vc * vc;
-        const double u = u01_open(r2[0], r2[1]);
-        const double x2 = x * x;
-        if (u < 1.0 - 0.0331 * x2 * x2 || log(u) < 0.5 * x2 + d * (1.0 - v + log(v))) return d * v;
+        const float v1 = 2.0f * nz_u(r[0]) - 1.0f, v2 = 2.0f * nz_u(r[1]) - 1.0f;
+        const float s = v1 * v1 + v2 * v2;
+        if (s >= 1.0f || s == 0.0f) continue;
+        const float x = v1 * sqrtf(-2.0f * nz_log(s) / s);
+        const float vc = 1.0f + c * x;
+        if (vc <= 0.0f) continue;
+        const float lv = 3.0f * nz_log(vc), v = vc * vc * vc;
+        const float u = nz_u(r[2]), x2 = x * x;
+        if (u < 1.0f - 0.0331f * (x2 * x2) || nz_log(u) < 0.5f * x2 + d * (1.0f - v + lv)) return nz_log(d) + lv;
     }
-    return d;
+    return nz_log(d);
 }
 
-static double gamma_draw(const noise_key* k, uint32_t idx, uint32_t which, double shape) {
-    if (shape >= 1.0) return gamma_large(k, idx, which, shape);
+static float log_gamma(const noise_key* k, uint32_t idx, uint32_t which, float shape) {
+    if (shape >= 1.0f) return log_gamma_large(k, idx, which, shape);
     uint32_t r[4];
     gamma_ctr(k, idx, which, 2047u, r);
-    const double u = u01_open(r[0], r[1]);
-    return gamma_large(k, idx, which, 1.0 + shape) * pow(u, 1.0 / shape);
+    return log_gamma_large(k, idx, which, 1.0f + shape) + nz_log(nz_u(r[0])) / shape;
 }
 
 static double beta_noise(const noise_key* k, uint32_t idx, double alpha, int nchild) {
-    const double x = gamma_draw(k, idx, 0, alpha);
-    const double y = gamma_draw(k, idx, 1, alpha * (double)(nchild - 1));
-    const double s = x + y;
-    return s > 0.0 ? x / s : 0.0;
+    const float lx = log_gamma(k, idx, 0, (float)alpha);
+    const float ly = log_gamma(k, idx, 1, (float)alpha * (float)(nchild - 1));
+    return (double)(1.0f / (1.0f + nz_exp(ly - lx)));
+}
+
+double orc_root_noise(uint64_t seed, uint64_t game_id, uint32_t c2, uint32_t draw, double alpha, int nchild) {
+    const noise_key k = {seed, game_id, c2};
+    return beta_noise(&k, draw, alpha, nchild);
 }
 
 typedef struct {

@@ -49,6 +49,8 @@ void orc_encode(const oaz_state* s, int color, float planes[21 * 25]);
 void orc_philox(uint64_t key, const uint32_t ctr[4], uint32_t out[4]);
 void orc_deal_deck(uint64_t seed, uint64_t game_id, uint8_t out[5]);
 void orc_hash_eval(const oaz_state* s, float policy[50], float* value);
+/* root-noise draw (see oaz_oracle.c beta_noise): c2 = ply << 16 | sim */
+double orc_root_noise(uint64_t seed, uint64_t game_id, uint32_t c2, uint32_t draw, double alpha, int nchild);
 
 /* NN: raw (un-folded) weights in canonical order, fp32 */
 size_t orc_weight_count(int blocks);

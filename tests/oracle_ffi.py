@@ -72,6 +72,7 @@ def load() -> C.CDLL:
         "orc_philox": (None, [C.c_uint64, V, V]),
         "orc_deal_deck": (None, [C.c_uint64, C.c_uint64, V]),
         "orc_hash_eval": (None, [V, V, V]),
+        "orc_root_noise": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_double, C.c_int]),
         "orc_weight_count": (C.c_size_t, [C.c_int]),
         "orc_nn_forward": (C.c_int, [V, C.c_int, V, C.c_int, V, V]),
         "orc_search": (C.c_int, [P(orc_search_cfg), V, V, V, V, C.c_int, P(C.c_int), P(_abi.oaz_search_stats)]),

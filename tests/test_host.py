@@ -128,3 +128,24 @@ def test_display_kat(kats):  # state.rs:397-417 (State::display is host-side for
     from onitama_az.game import ORIGINAL_CARDS, Deck, State
     st = State.with_deck(Deck([ORIGINAL_CARDS[i] for i in range(5)]))
     assert st.display() == kats["display"]["expected"]
+
+
+def test_root_noise_host_matches_oracle_and_distribution():
+    """The engine's root-noise draw (f32 log-domain Beta(alpha, (K-1) alpha), the marginal of the
+    reference's per-comparison Dirichlet sample, mcts_arena.rs:186-203) equals the oracle's
+    restatement bit for bit, and its sample mean is 1/K (Beta(a, b) mean a / (a + b))."""
+    import oracle_ffi as orc
+    lib = _abi.load()
+    olib = orc.load()
+    rng = np.random.default_rng(5)
+    for _ in range(2000):
+        seed, gid = int(rng.integers(0, 2**63)), int(rng.integers(0, 2**40))
+        ply, sim, draw, K = int(rng.integers(0, 152)), int(rng.integers(0, 800)), int(rng.integers(2, 80)), int(rng.integers(2, 41))
+        a = lib.oaz_root_noise(seed, gid, ply, sim, draw, 0.03, K)
+        b = olib.orc_root_noise(seed, gid, (ply << 16) | sim, draw, 0.03, K)
+        assert np.float32(a) == np.float32(b)
+        assert 0.0 <= a <= 1.0
+    for K in (2, 12, 40):
+        xs = np.array([lib.oaz_root_noise(7, g, 0, s, 3, 0.03, K) for g in range(40) for s in range(100)])
+        se = np.sqrt((1.0 / K) * (1 - 1.0 / K) / (0.03 * K + 1) / len(xs))  # Beta variance
+        assert abs(xs.mean() - 1.0 / K) < 5 * se, (K, xs.mean())
