@@ -334,9 +334,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # OAZ_BENCH_REHEARSE=1: every rank on GPU 0 with gloo collectives (exercises the multi-rank path
+    # of this script on a one-GPU box; its timings mean nothing)
+    rehearse = os.environ.get("OAZ_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.mode == "train":
         return train_main(args, world, rank, local)
     if args.mode == "pure_mcts":
@@ -400,8 +408,9 @@ def main():
     expansions = st1.search.expansions - st0.search.expansions
     depth = (st1.search.depth_sum - st0.search.depth_sum) / max(1, sims)
     branching = (st1.search.children - st0.search.children) / max(1, expansions)
-    tot = torch.tensor([float(sims), float(games_done), float(plies), float(expansions)], dtype=torch.float64, device="cuda")
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    cdev = "cpu" if rehearse else "cuda"
+    tot = torch.tensor([float(sims), float(games_done), float(plies), float(expansions)], dtype=torch.float64, device=cdev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -412,10 +421,10 @@ def main():
     if not args.no_allgather:  # C4: RCCL all-gather of (s, pi, z) after the timed region
         from onitama_az.dist import allgather_samples
         t1 = time.perf_counter()
-        got = allgather_samples(eng, world, torch.device("cuda", local))
+        got = allgather_samples(eng, world, torch.device("cuda", local), host=rehearse)
         torch.cuda.synchronize()
         allgather = {"samples_total": int(got), "bytes_per_sample": 228, "seconds": time.perf_counter() - t1,
-                     "backend": "nccl(RCCL)" if world > 1 else "local"}
+                     "backend": ("gloo (rehearsal)" if rehearse else "nccl(RCCL)") if world > 1 else "local"}
 
     if rank == 0:
         nn_avg_ms = kt.nn_ms / max(1, kt.nn_n)

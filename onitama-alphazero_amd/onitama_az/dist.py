@@ -37,14 +37,18 @@ def allgather_sample_bytes(local: torch.Tensor, world: int) -> torch.Tensor:
     return torch.cat(parts)
 
 
-def allgather_samples(eng, world: int, device: torch.device) -> int:
+def allgather_samples(eng, world: int, device: torch.device, host: bool = False) -> int:
     """Move this rank's buffered samples device-to-device into a tensor and all-gather them over
-    RCCL (xGMI on one node). Returns the number of samples every rank now holds."""
+    RCCL (xGMI on one node). Returns the number of samples every rank now holds. host=True
+    gathers a host copy instead (gloo)."""
     st = eng.selfplay_stats()
     n = int(st.samples_ready)
     local = torch.empty(max(n, 0) * SAMPLE_BYTES, dtype=torch.uint8, device=device)
     if n:
         got = eng.samples_export_device(local.data_ptr(), local.numel())
         local = local[: got * SAMPLE_BYTES]
+    if host:
+        torch.cuda.synchronize()
+        local = local.cpu()
     allg = allgather_sample_bytes(local, world)
     return allg.numel() // SAMPLE_BYTES
