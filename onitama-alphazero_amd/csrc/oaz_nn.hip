@@ -673,11 +673,15 @@ __global__ void __launch_bounds__(64 * 16 / NPW) k_nn_bf16g(const oaz_state* __r
 // Geometry = k_nn_sq16 (16 positions, square-major rows, 8 waves = 2 square groups x 4 N-tiles,
 // off-board (square, tap) products skipped). The LDS image holds the three bf16 planes of every
 // activation: row (square*16 + position) = [piece][64 channels] = 384 B, unpadded (153.6 KB);
-// 16-byte chunk c (8 channels) of piece p of row r sits at chunk p*8 + (c ^ ((r >> 1) & 7)),
-// which makes the A-fragment ds_read_b128 of every 16-lane group hit 16 distinct bank slots.
+// 16-byte chunk c (8 channels) of piece p of row r sits at chunk p*8 + (c ^ key(r)) (chunk_off):
+// conflict-free A-fragment reads and epilogue stores.
 namespace x6 {
-__device__ __forceinline__ int chunk_off(int row, int piece, int c8) {  // byte offset of an 8-channel chunk
-    return row * kRowB + piece * 128 + ((c8 ^ ((row >> 1) & 7)) << 4);
+// byte offset of an 8-channel chunk. Swizzle key ((row >> 1) ^ 4 (row & 1)) & 7: every 16-lane group of
+// the A-fragment ds_read_b128s hits 16 distinct bank slots, and every 32-lane half of the
+// epilogue's paired ds_write_b32s (rows 2k, 2k+1, 2k+4, 2k+5 x 16 channels) 32 distinct banks
+// (with key (row >> 1) & 7 rows 2k and 2k+1 collided: a 2-way conflict on every store).
+__device__ __forceinline__ int chunk_off(int row, int piece, int c8) {
+    return row * kRowB + piece * 128 + ((c8 ^ (((row >> 1) ^ ((row & 1) << 2)) & 7)) << 4);
 }
 __device__ __forceinline__ void split3(float v, uint16_t& h, uint16_t& m, uint16_t& l) {
     const uint32_t hb = __float_as_uint(v) & 0xffff0000u;
