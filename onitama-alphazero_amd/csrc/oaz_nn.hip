@@ -345,11 +345,13 @@ __device__ __forceinline__ void heads_g(const LD& ld, float* scratch, int s, con
     }
 }
 
-// The heads after the 1x1 convs, for position `s` (one wave): feat[0..24] = value features,
-// feat[25..74] = policy features in flatten(1,-1) order (already bias + ReLU). Same arithmetic as
-// heads_g's second half.
-__device__ __forceinline__ void heads_mlp(const float* feat, const float* p, int lane, int b, int B, float* policy,
-                                          float* value) {
+// The heads after the 1x1 convs for NP positions of one wave: feat[q] = the q-th position's
+// features, [0..24] value, [25..74] policy in flatten(1,-1) order (already bias + ReLU). Same
+// arithmetic per position as heads_g's second half; the weights are read once for all NP
+// positions and the NP dot products are independent chains.
+template <int NP>
+__device__ __forceinline__ void heads_mlp(const float* const (&feat)[NP], const int (&bs)[NP], const float* p, int lane,
+                                          int B, float* policy, float* value) {
     const float* l1w = p + 68;
     const float* l1b = l1w + 64 * 25;
     const float* l2w = l1b + 64;
@@ -357,21 +359,35 @@ __device__ __forceinline__ void heads_mlp(const float* feat, const float* p, int
     const float* pp = p + nn::kValueF;
     const float* plw = pp + 132;
     const float* plb = plw + 2500;
-    float hj = l1b[lane];
-    for (int q = 0; q < 25; ++q) hj += l1w[q * 64 + lane] * feat[q];
-    hj = hj > 0.0f ? hj : 0.0f;
-    const float vsum = wave_sum_f(l2w[lane] * hj);
-    float lg = -INFINITY;
-    if (lane < 50) {
-        lg = plb[lane];
-        for (int f = 0; f < 50; ++f) lg += plw[f * 50 + lane] * feat[25 + f];
+    float hj[NP], lg[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) hj[q] = l1b[lane];
+    for (int k = 0; k < 25; ++k) {
+        const float w = l1w[k * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) hj[q] += w * feat[q][k];
     }
-    const float mx = wave_max_f(lg);
-    const float e = lane < 50 ? expf(lg - mx) : 0.0f;
-    const float den = wave_sum_f(e);
-    if (b < B) {
-        if (lane < 50) policy[(size_t)b * 50 + lane] = e / den;
-        if (lane == 0) value[b] = tanhf(vsum + l2b);
+    const bool pl = lane < 50;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) lg[q] = pl ? plb[lane] : -INFINITY;
+    if (pl)
+        for (int f = 0; f < 50; ++f) {
+            const float w = plw[f * 50 + lane];
+#pragma unroll
+            for (int q = 0; q < NP; ++q) lg[q] += w * feat[q][25 + f];
+        }
+    const float w2 = l2w[lane];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+        const float h = hj[q] > 0.0f ? hj[q] : 0.0f;
+        const float vsum = wave_sum_f(w2 * h);
+        const float mx = wave_max_f(lg[q]);
+        const float e = pl ? expf(lg[q] - mx) : 0.0f;
+        const float den = wave_sum_f(e);
+        if (bs[q] < B) {
+            if (pl) policy[(size_t)bs[q] * 50 + lane] = e / den;
+            if (lane == 0) value[bs[q]] = tanhf(vsum + l2b);
+        }
     }
 }
 
@@ -1173,7 +1189,15 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
                 }
         }
         __syncthreads();
-        for (int s = wave; s < nn::kSB; s += C::WAVES) heads_mlp(feat + s * 80, p, lane, b0 + s, B, policy, value);
+        constexpr int NP = nn::kSB / C::WAVES;  // positions per wave
+        const float* fq[NP];
+        int bq[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            fq[q] = feat + (wave + q * C::WAVES) * 80;
+            bq[q] = b0 + wave + q * C::WAVES;
+        }
+        heads_mlp<NP>(fq, bq, p, lane, B, policy, value);
     }
     if constexpr (C::DBG == 2) {
         stamp(5);
