@@ -50,9 +50,14 @@ PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: F32 matrix
 # fp32 split kernel (OAZ_FP32_SPLIT): every fp32 MAC is six bf16 MFMA products, so its MFMA ceiling
 # in fp32 FLOP/s is the bf16 dense peak / 6
 PEAK_TFLOPS["fp32_split"] = PEAK_TFLOPS["bf16"] / 6.0
+# fp16 split kernel (OAZ_FP32_SPLIT16): three fp16 MFMA products per fp32 MAC (fp16 and bf16 MFMA
+# share one rate on gfx950), so its ceiling is the dense fp16 peak / 3
+PEAK_TFLOPS["fp32_split16"] = PEAK_TFLOPS["bf16"] / 3.0
 NN_KERNEL = {"fp32": "k_nn_sq16<fp32> (fused ResNet, exact fp32 v_mfma_f32_16x16x4_f32)",
              "fp32_split": "k_nn_x6 (fused ResNet, fp32 operands split exactly into 3 bf16 terms, 6 products on "
                            "v_mfma_f32_16x16x32_bf16, fp32 accumulate)",
+             "fp32_split16": "k_nn_h3 (fused ResNet, fp32 operands split into hi+lo fp16 terms, 3 products on "
+                             "v_mfma_f32_16x16x32_f16, fp32 accumulate)",
              "bf16": "k_nn_bf16g<2> (fused ResNet, 8 waves x 2 N-tiles, v_mfma_f32_16x16x32_bf16)"}
 METRIC = "MCTS node-expansions/sec/GPU @400 sims; self-play games/sec at 1/2/4/8 GPU"
 
@@ -67,8 +72,9 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--games", type=int, default=0, help="override games per GPU")
     ap.add_argument("--sims", type=int, default=0, help="override sims per move")
-    ap.add_argument("--fp32-kernel", default="split", choices=["split", "exact"],
-                    help="fp32 NN kernel: split (bf16x6, fp32-level error) or exact (fp32 MFMA products)")
+    ap.add_argument("--fp32-kernel", default="split", choices=["split", "split16", "exact"],
+                    help="fp32 NN kernel: split (bf16x6), split16 (fp16x3; both fp32-level error) or exact "
+                         "(fp32 MFMA products)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="cpu_baseline sample length")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -354,8 +360,8 @@ def main():
     from onitama_az.weights import random_weights
 
     cfg = dict(CONFIGS[args.config])
-    if cfg["precision"] == "fp32" and args.fp32_kernel == "split":
-        cfg["precision"] = "fp32_split"
+    if cfg["precision"] == "fp32" and args.fp32_kernel in ("split", "split16"):
+        cfg["precision"] = {"split": "fp32_split", "split16": "fp32_split16"}[args.fp32_kernel]
     if args.games:
         cfg["games"] = args.games
     if args.sims:
@@ -368,7 +374,8 @@ def main():
     eng = Engine(device=local, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0,
                  train_noise=0 if args.no_noise else 1,
                  max_plies=150, evaluator=_abi.EVAL_NN,
-                 precision={"bf16": _abi.BF16, "fp32_split": _abi.FP32_SPLIT}.get(cfg["precision"], _abi.FP32),
+                 precision={"bf16": _abi.BF16, "fp32_split": _abi.FP32_SPLIT,
+                            "fp32_split16": _abi.FP32_SPLIT16}.get(cfg["precision"], _abi.FP32),
                  fixed_deck=cfg["fixed_deck"],
                  deck=[0, 1, 2, 3, 4], seed=20260101, rank=rank, world=world,
                  sample_capacity=cfg["games"] * 24, stagger=0 if args.pmc_child else stagger)
@@ -442,6 +449,10 @@ def main():
                               "fp32_split": "fp32 operands split exactly into hi+mid+lo bf16 terms, the 6 products "
                                             "above 2^-24 relative on bf16 MFMA, fp32 accumulate (error vs float64 = "
                                             "the exact-fp32 kernel's; tests/test_gpu.py 1e-4 parity)",
+                              "fp32_split16": "fp32 operands split into hi = fp16(x) and lo = fp16(x - hi) (weights "
+                                              "pre-scaled per output channel by a power of two), the 3 products "
+                                              "hi*hi, hi*lo, lo*hi on fp16 MFMA, fp32 accumulate (within 1e-5 of the "
+                                              "fp32 goldens, tests/test_gpu.py; range-checked: OAZ_ERR_RANGE)",
                               "bf16": "bf16 MFMA inputs, fp32 accumulate"}[cfg["precision"]],
             "data": "synthetic (random-init weights seed 0, seeded deals)",
             "config": {"workload": f"{args.config}: {cfg['games']} self-play games/GPU x {cfg['sims']} sims/move, "
@@ -463,7 +474,8 @@ def main():
                          "achieved_nonzero": achieved_nz, "frac_nonzero": achieved_nz / PEAK_TFLOPS[cfg["precision"]],
                          "algorithmic_bytes_per_launch": alg_bytes, "traffic_detail": traffic,
                          "peak_note": {"fp32": "F32 MFMA dense peak", "bf16": "BF16 dense MFMA peak",
-                                       "fp32_split": "BF16 dense MFMA peak / 6 products per fp32 MAC"}[cfg["precision"]],
+                                       "fp32_split": "BF16 dense MFMA peak / 6 products per fp32 MAC",
+                                       "fp32_split16": "FP16 dense MFMA peak / 3 products per fp32 MAC"}[cfg["precision"]],
                          "frac_of_fp32_mfma_peak": achieved / PEAK_TFLOPS["fp32"]},
             "allgather": allgather,
         }

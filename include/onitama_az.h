@@ -71,15 +71,22 @@ enum {
     OAZ_ERR_HIP = -3,
     OAZ_ERR_CAPACITY = -4,
     OAZ_ERR_STATE = -5,
-    OAZ_ERR_WEIGHTS = -6
+    OAZ_ERR_WEIGHTS = -6,
+    OAZ_ERR_RANGE = -7      /* OAZ_FP32_SPLIT16: an activation left the fp16 range (|x| >= 65504) */
 };
 
 enum { OAZ_EVAL_NN = 0, OAZ_EVAL_HASH = 1 };        /* leaf evaluator (HASH: test evaluator, below) */
 /* NN arithmetic. OAZ_FP32: exact fp32 MFMA products (v_mfma_f32_16x16x4_f32). OAZ_BF16: bf16 MFMA
  * inputs, fp32 accumulate (BASELINE C5). OAZ_FP32_SPLIT: fp32 operands split exactly into three
  * bf16 terms (hi + mid + lo), the six products above 2^-24 relative on bf16 MFMA, fp32
- * accumulate: fp32-level error (DESIGN.md "fp32 split") at bf16 MFMA rates. */
-enum { OAZ_FP32 = 0, OAZ_BF16 = 1, OAZ_FP32_SPLIT = 2 };
+ * accumulate: fp32-level error (DESIGN.md "fp32 split") at bf16 MFMA rates. OAZ_FP32_SPLIT16: fp32
+ * operands split into two fp16 terms (hi = fp16(x), lo = fp16(x - hi): 22 significant bits), the
+ * three products hi*hi, hi*lo, lo*hi on fp16 MFMA, fp32 accumulate; conv weights are pre-scaled per
+ * output channel by a power of two (exact). Errors vs a float64 forward are at the fp32 level
+ * (DESIGN.md "fp16 split") at half the MFMA work of OAZ_FP32_SPLIT. Activations must stay below
+ * 65504 in magnitude: an engine that saw one beyond returns OAZ_ERR_RANGE from its next
+ * synchronising call (nn_forward, search, selfplay stats / samples), never a silent result. */
+enum { OAZ_FP32 = 0, OAZ_BF16 = 1, OAZ_FP32_SPLIT = 2, OAZ_FP32_SPLIT16 = 3 };
 
 /* ---- PODs ----------------------------------------------------------------- */
 
@@ -136,7 +143,7 @@ typedef struct oaz_config {
     double dirichlet_eps;    /* 0.25 (mcts_arena.rs:186) */
     int32_t games;           /* parallel game slots G (also the max batch of oaz_search) */
     int32_t evaluator;       /* OAZ_EVAL_NN or OAZ_EVAL_HASH */
-    int32_t precision;       /* OAZ_FP32, OAZ_BF16 or OAZ_FP32_SPLIT */
+    int32_t precision;       /* OAZ_FP32, OAZ_BF16, OAZ_FP32_SPLIT or OAZ_FP32_SPLIT16 */
     int32_t fixed_deck;      /* 1: every game uses deck[]; 0: random 5 of 16 per game (deck.rs:139-151) */
     uint8_t deck[5];
     uint8_t pad0[3];

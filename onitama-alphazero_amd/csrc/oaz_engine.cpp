@@ -252,6 +252,55 @@ static void pack_conv64_split(const FoldedConv& f, std::vector<float>& out) {
     for (int o = 0; o < 64; ++o) out.push_back(f.b[o]);
 }
 
+// fp16 split (OAZ_FP32_SPLIT16): hi = fp16(x) (round to nearest even), lo = fp16(x - hi); the same
+// split as epilogue_h3_pack in oaz_nn.hip. Weights are first scaled by s = 2^k per output channel
+// (max |w s| in [1, 2)); 1/s is stored for the epilogue.
+static void split16_host(float x, uint16_t out[2]) {
+    const _Float16 h = (_Float16)x;
+    const _Float16 l = (_Float16)(x - (float)h);
+    memcpy(&out[0], &h, 2);
+    memcpy(&out[1], &l, 2);
+}
+static float pow2_scale(const float* w, size_t n, size_t stride, float* inv) {
+    float mx = 0.0f;
+    for (size_t k = 0; k < n; ++k) mx = fmaxf(mx, fabsf(w[k * stride]));
+    if (!(mx > 0.0f) || !std::isfinite(mx)) {
+        *inv = 1.0f;
+        return 1.0f;
+    }
+    int e = 0;
+    (void)frexpf(mx, &e);  // mx = f 2^e, f in [0.5, 1)
+    *inv = ldexpf(1.0f, e - 1);
+    return ldexpf(1.0f, 1 - e);
+}
+
+// Split16 B fragments: [tap][K-half m][piece p][N-tile][lane] f16x8, lane l supplying
+// B[k = 8(l>>4) + e][col l&15] = piece p of s_co W[co = 16nt + (l&15)][ci = 32m + 8(l>>4) + e][tap];
+// then bias[64], 1/s[64].
+static void pack_conv64_split16(const FoldedConv& f, std::vector<float>& out) {
+    float sc[64], inv[64];
+    for (int co = 0; co < 64; ++co) sc[co] = pow2_scale(&f.w[(size_t)co * 64 * 9], 64 * 9, 1, &inv[co]);
+    std::vector<uint16_t> h;
+    h.reserve(9 * 2 * 2 * 4 * 64 * 8);
+    for (int t = 0; t < 9; ++t)
+        for (int m = 0; m < 2; ++m)
+            for (int pc = 0; pc < 2; ++pc)
+                for (int nt = 0; nt < 4; ++nt)
+                    for (int l = 0; l < 64; ++l)
+                        for (int e = 0; e < 8; ++e) {
+                            const int co = nt * 16 + (l & 15);
+                            const int ci = 32 * m + 8 * (l >> 4) + e;
+                            uint16_t s2[2];
+                            split16_host(f.w[((size_t)co * 64 + ci) * 9 + t] * sc[co], s2);  // exact scaling
+                            h.push_back(s2[pc]);
+                        }
+    const size_t base = out.size();
+    out.resize(base + h.size() / 2);
+    memcpy(out.data() + base, h.data(), h.size() * sizeof(uint16_t));
+    for (int o = 0; o < 64; ++o) out.push_back(f.b[o]);
+    for (int o = 0; o < 64; ++o) out.push_back(inv[o]);
+}
+
 // First layer (k_nn_sq16): the 4 bitboard planes go through MFMA (lane l supplies
 // W[co = 16nt + (l&15)][plane l>>4][tap t]); the 16 card planes and the blue-to-move plane
 // (constant over the board, common.rs:68-77,32-37) become T[square][c][co] = sum over the
@@ -285,6 +334,7 @@ static int pack_weights(const float* raw, int blocks, int precision, std::vector
         for (int j = 0; j < 2; ++j) {
             if (precision == OAZ_BF16) pack_conv64_bf16(fold(p, 64, 64, 9), out);
             else if (precision == OAZ_FP32_SPLIT) pack_conv64_split(fold(p, 64, 64, 9), out);
+            else if (precision == OAZ_FP32_SPLIT16) pack_conv64_split16(fold(p, 64, 64, 9), out);
             else pack_conv64(fold(p, 64, 64, 9), out);
         }
     // value head: vh_conv + vh_bn folded, vh_linear1, vh_linear2
@@ -330,6 +380,29 @@ static int pack_weights(const float* raw, int blocks, int precision, std::vector
         const size_t base = out.size();
         out.resize(base + h.size() / 2);
         memcpy(out.data() + base, h.data(), h.size() * sizeof(uint16_t));
+    }
+    if (precision == OAZ_FP32_SPLIT16) {
+        // k_nn_h3 head 1x1 convs: [K-half m][piece][lane] f16x8 of the column-scaled weights
+        // (column n = 0 value conv, 1 / 2 policy conv planes, 3..15 zero), then 1/s per column (+pad)
+        float sc[3], inv[4] = {1.0f, 1.0f, 1.0f, 0.0f};
+        sc[0] = pow2_scale(vc.w.data(), 64, 1, &inv[0]);
+        sc[1] = pow2_scale(pc.w.data(), 64, 1, &inv[1]);
+        sc[2] = pow2_scale(pc.w.data() + 64, 64, 1, &inv[2]);
+        std::vector<uint16_t> h;
+        for (int m = 0; m < 2; ++m)
+            for (int pcs = 0; pcs < 2; ++pcs)
+                for (int l = 0; l < 64; ++l)
+                    for (int e = 0; e < 8; ++e) {
+                        const int c = 32 * m + 8 * (l >> 4) + e, n = l & 15;
+                        const float w = n == 0 ? vc.w[c] * sc[0] : n <= 2 ? pc.w[(n - 1) * 64 + c] * sc[n] : 0.0f;
+                        uint16_t sp[2];
+                        split16_host(w, sp);
+                        h.push_back(sp[pcs]);
+                    }
+        const size_t base = out.size();
+        out.resize(base + h.size() / 2);
+        memcpy(out.data() + base, h.data(), h.size() * sizeof(uint16_t));
+        for (int k = 0; k < 4; ++k) out.push_back(inv[k]);
     }
     if (out.size() != nn_packed_floats(blocks, precision)) return oaz_set_err(OAZ_ERR_STATE, "pack: size mismatch");
     if ((size_t)(p - raw) != oaz_weight_count(blocks, 64, 21)) return oaz_set_err(OAZ_ERR_STATE, "pack: raw size mismatch");
@@ -472,6 +545,7 @@ struct oaz_engine {
     float *policy = nullptr, *value = nullptr;
     float* weights = nullptr;
     bool have_weights = false;
+    uint32_t* range_flag = nullptr;      // OAZ_FP32_SPLIT16: an activation reached the fp16 range limit
     // search mode
     oaz_state* s_roots = nullptr;
     oaz_move* s_move = nullptr;
@@ -627,8 +701,9 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         oaz_set_err(OAZ_ERR_ARG, "create: config out of range");
         return nullptr;
     }
-    if (cfg->precision != OAZ_FP32 && cfg->precision != OAZ_BF16 && cfg->precision != OAZ_FP32_SPLIT) {
-        oaz_set_err(OAZ_ERR_ARG, "create: precision must be OAZ_FP32, OAZ_BF16 or OAZ_FP32_SPLIT");
+    if (cfg->precision != OAZ_FP32 && cfg->precision != OAZ_BF16 && cfg->precision != OAZ_FP32_SPLIT &&
+        cfg->precision != OAZ_FP32_SPLIT16) {
+        oaz_set_err(OAZ_ERR_ARG, "create: precision must be OAZ_FP32, OAZ_BF16, OAZ_FP32_SPLIT or OAZ_FP32_SPLIT16");
         return nullptr;
     }
     int ndev = 0;
@@ -683,7 +758,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         dalloc(&e->s_rootv, G) || dalloc(&e->s_rootp, G * 50) || dalloc(&e->s_ply, G) ||
         dalloc(&e->root, G) || dalloc(&e->ply, G) || dalloc(&e->seq, G) ||
         dalloc(&e->game_id, G) || dalloc(&e->active, G) || dalloc(&e->hist, G * e->hcap) ||
-        dalloc(&e->out, (size_t)e->out_cap) || dalloc(&e->out_count, (size_t)1) ||
+        dalloc(&e->out, (size_t)e->out_cap) || dalloc(&e->out_count, (size_t)1) || dalloc(&e->range_flag, (size_t)1) ||
         (cfg->train_noise && dalloc(&e->noise, 2 * kNoiseChunk * G * kNoiseStride)))
         return fail();
     // sqrt((double)n) from the host libm (IEEE correctly rounded), so device PUCT = oracle PUCT
@@ -692,6 +767,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
     if (hipMemcpy(e->sqrt_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(e->stats, 0, G * GS_COUNT * sizeof(uint64_t)) != hipSuccess ||
         hipMemset(e->out_count, 0, sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(e->range_flag, 0, sizeof(uint32_t)) != hipSuccess ||
         hipMemset(e->active, 0, G) != hipSuccess) {
         oaz_set_err(OAZ_ERR_HIP, "create: init copies failed");
         return fail();
@@ -724,7 +800,7 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     void* ptrs[] = {e->nodes, e->n_nodes, e->path, e->depth, e->leaf, e->leaf_state, e->stats,
                     e->stats_sum, e->sqrt_tab, e->policy, e->value, e->weights, e->s_roots,
                     e->s_move, e->s_pi, e->s_rootv, e->s_rootp, e->s_ply, e->root, e->ply,
-                    e->seq, e->game_id, e->active, e->hist, e->out, e->out_count, e->noise};
+                    e->seq, e->game_id, e->active, e->hist, e->out, e->out_count, e->noise, e->range_flag};
     for (void* p : ptrs) dfree(p);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
@@ -748,6 +824,7 @@ extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
     if (int rc = pack_weights(blob, e->cfg.blocks, e->cfg.precision, packed)) return rc;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipMemcpyAsync(e->weights, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemsetAsync(e->range_flag, 0, sizeof(uint32_t), e->stream));  // new weights: a fresh range check
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->have_weights = true;
     return 0;
@@ -811,7 +888,23 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
         const char* xv = getenv("OAZ_NN_X6_V");
         w.x6_variant = xv ? atoi(xv) : 0;
     }
+    w.range_flag = e->range_flag;
     return timed(e, 1, B, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, st); }, st);
+}
+
+// OAZ_FP32_SPLIT16: did any NN launch so far see an activation beyond the fp16 range? Called after
+// the engine's stream has been synchronised; the flag stays set (every later call fails too) until
+// new weights are loaded.
+static int check_range(oaz_engine* e) {
+    if (e->cfg.precision != OAZ_FP32_SPLIT16 || e->cfg.evaluator != OAZ_EVAL_NN) return 0;
+    uint32_t f = 0;
+    HIP_TRY(hipMemcpyAsync(&f, e->range_flag, sizeof(f), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (f)
+        return oaz_set_err(OAZ_ERR_RANGE,
+                           "NN activation reached the fp16 range (|x| >= 65504) under OAZ_FP32_SPLIT16; "
+                           "results since the last weight load are invalid: use OAZ_FP32_SPLIT or OAZ_FP32");
+    return 0;
 }
 
 extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* policy, float* value) {
@@ -824,7 +917,7 @@ extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* p
     if (policy) HIP_TRY(hipMemcpyAsync(policy, e->s_rootp, (size_t)B * 50 * 4, hipMemcpyDeviceToHost, e->stream));
     if (value) HIP_TRY(hipMemcpyAsync(value, e->s_rootv, (size_t)B * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    return 0;
+    return check_range(e);
 }
 
 // All cfg.sims simulations of one move for every game: select -> evaluate -> expand/backup,
@@ -970,6 +1063,7 @@ extern "C" int oaz_search(oaz_engine* e, const oaz_state* roots, int G, oaz_move
     if (out_move) HIP_TRY(hipMemcpyAsync(out_move, e->s_move, (size_t)G * sizeof(oaz_move), hipMemcpyDeviceToHost, e->stream));
     if (out_pi) HIP_TRY(hipMemcpyAsync(out_pi, e->s_pi, (size_t)G * 50 * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    if (int rc = check_range(e)) return rc;
     if (stats) {
         uint64_t s[GS_COUNT];
         if (int rc = reduce_stats(e, (uint32_t)G, s)) return rc;
@@ -1027,6 +1121,7 @@ extern "C" int oaz_selfplay_stats_get(oaz_engine* e, oaz_selfplay_stats* o) {
     HIP_TRY(hipSetDevice(e->device));
     uint64_t s[GS_COUNT];
     if (int rc = reduce_stats(e, e->G, s)) return rc;
+    if (int rc = check_range(e)) return rc;
     unsigned long long cnt = 0;
     HIP_TRY(hipMemcpy(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost));
     memset(o, 0, sizeof(*o));
@@ -1048,6 +1143,7 @@ static int samples_copy(oaz_engine* e, void* dst, size_t cap, size_t* n_out, hip
     unsigned long long cnt = 0;
     HIP_TRY(hipMemcpyAsync(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    if (int rc = check_range(e)) return rc;
     const unsigned long long avail = (cnt < e->out_cap ? cnt : e->out_cap);
     const size_t ready = avail > e->out_read ? (size_t)(avail - e->out_read) : 0;
     const size_t n = ready < cap ? ready : cap;

@@ -75,9 +75,11 @@ struct SlotView {
 struct NNView {
     const float* blob;  // packed, BN-folded weights (DESIGN.md "NN weights layout")
     int32_t blocks;
-    int32_t precision;  // OAZ_FP32 (exact fp32 MFMA), OAZ_BF16 (bf16 inputs), OAZ_FP32_SPLIT (bf16x6 split)
+    int32_t precision;  // OAZ_FP32 (exact fp32 MFMA), OAZ_BF16 (bf16 inputs), OAZ_FP32_SPLIT (bf16x6 split),
+                        // OAZ_FP32_SPLIT16 (fp16x3 split)
     int32_t x6_variant; // fp32-split kernel variant (OAZ_NN_X6_V, A/B testing)
     int32_t bf16_v1;    // bf16 kernel variant (OAZ_NN_BF16_V1): 0 k_nn_bf16g<2>, 1 k_nn_sq16<bf16>, 2 k_nn_bf16g<4>
+    uint32_t* range_flag;  // OAZ_FP32_SPLIT16: set to 1 when an activation reached the fp16 range limit
 };
 
 // rules

@@ -93,7 +93,22 @@ constexpr size_t kW = 9 * 2 * 3 * 4 * 64 * 4;
 constexpr size_t kHeadB = 2 * 3 * 64 * 4;  // head 1x1 convs: [K-half][piece][lane] bf16x8 (after the heads)
 }  // namespace x6
 
+// fp16 split variant (OAZ_FP32_SPLIT16): 64->64 conv B fragments are [9 taps][2 K-halves][2 pieces]
+// [4 N-tiles][64 lanes] f16x8 of the per-output-channel scaled weights, then bias[64] and the
+// inverse scales[64]; the head 1x1 convs [K-half][piece][lane] f16x8 + 4 inverse column scales.
+namespace h3 {
+constexpr int kRowB = 128;                     // LDS row of one piece plane: 64 channels x f16
+constexpr int kPlaneB = nn::kSB * 25 * kRowB;  // 51,200 B per piece plane
+constexpr int kImageB = 2 * kPlaneB;           // 102,400 B
+constexpr int kLdsFloats = kImageB / 4 + nn::kWaves * nn::kScratch;  // 26,624 floats = 106,496 B
+constexpr size_t kW = 9 * 2 * 2 * 4 * 64 * 4;
+constexpr size_t kHeadB = 2 * 2 * 64 * 4 + 4;
+}  // namespace h3
+
 size_t nn_packed_floats(int blocks, int precision) {
+    if (precision == OAZ_FP32_SPLIT16)
+        return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) + nn::kValueF +
+               nn::kPolicyF + h3::kHeadB;
     const size_t w = precision == OAZ_BF16 ? nn::kW64h : precision == OAZ_FP32_SPLIT ? x6::kW : nn::kW64;
     return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (w + nn::kCh) + nn::kValueF + nn::kPolicyF +
            (precision == OAZ_FP32_SPLIT ? x6::kHeadB : 0);
@@ -1227,11 +1242,344 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_x6(const oaz_state* __rest
         nn_x6_body<C, 1>(states, B, blob, blocks, policy, value, lds);
 }
 
+// ---- fp32 split over fp16 (OAZ_FP32_SPLIT16): three f16 MFMA products per fp32 MAC -----------------
+// Every fp32 operand x is split into two fp16 terms, hi = fp16(x) (round to nearest even) and
+// lo = fp16(x - hi) (x - hi is exact in fp32): hi + lo carries 22 significant bits. Of the four
+// products the three down to 2^-22 relative are computed (hi*hi, hi*lo, lo*hi) on
+// v_mfma_f32_16x16x32_f16 (fp16 x fp16 products are exact in fp32, fp32 accumulation); lo*lo is
+// below 2^-22 relative. One K=32 block costs 3 x 16 cycles (half of k_nn_x6's six products).
+// fp16's exponent range is the price: conv weights are scaled per output channel by a power of two
+// s (max |w s| in [1, 2), exact) and the epilogue multiplies by 1/s (exact); activations below 2^-14
+// fall into fp16 subnormals (absolute error <= 2^-25 per term, below the fp32 rounding of the dot
+// products); an activation >= 65504 would overflow, so every lane tracks the largest value it
+// splits and raises range_flag (the engine reports OAZ_ERR_RANGE, never a silent result).
+// Geometry, batch plans and pipelining as k_nn_x6. The LDS image holds two piece planes
+// [piece][row][64 channels] (row = square*16 + position, 128 B); the 16-byte chunk c of row r sits
+// at c ^ key(r), an XOR-linear key on the row bits found by exhaustive search
+// (tools/h3_swizzle.py): conflict-free A-fragment ds_read_b128s and epilogue ds_write_b32s.
+namespace h3 {
+__device__ __forceinline__ int key(int r) {
+    return ((r & 1) << 1) ^ ((r >> 1) & 1) ^ (((r >> 2) & 1) << 2) ^ (((r >> 3) & 1) << 1);
+}
+__device__ __forceinline__ int chunk_off(int row, int c8) { return row * kRowB + ((c8 ^ key(row)) << 4); }
+__device__ __forceinline__ int elem_off(int row, int c) { return chunk_off(row, c >> 3) + (c & 7) * 2; }
+}  // namespace h3
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// A-fragment loads / MFMAs of batch K; the LDS address is one of four per-lane bases
+// ab[m][seg] = lo[m] + seg * 64 KiB plus an immediate offset < 64 KiB (piece 1 = + kPlaneB)
+template <int GRP, int KH, int K, int N>
+__device__ __forceinline__ void h3_load(f16x8 (&a)[N], const char* img, const int (&ab)[2][2], int piece) {
+    constexpr X6Batch B = X6PlanOf<GRP, KH>::P.b[K];
+#pragma unroll
+    for (int q = 0; q < N; ++q)
+        if (q < B.n) {
+            const int off = B.nb[q] * (nn::kSB * h3::kRowB) + piece * h3::kPlaneB;  // folds to a constant
+            a[q] = *reinterpret_cast<const f16x8*>(img + ab[B.m][off >> 16] + (off & 0xffff));
+        }
+}
+
+template <int GRP, int KH, int K, int NS, int N>
+__device__ __forceinline__ void h3_mfma(f32x4 (&acc)[NS], const f16x8 (&a)[N], const f16x8& bv) {
+    constexpr X6Batch B = X6PlanOf<GRP, KH>::P.b[K];
+#pragma unroll
+    for (int q = 0; q < N; ++q)
+        if (q < B.n) acc[B.j[q]] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[q], bv, acc[B.j[q]], 0, 0, 0);
+}
+
+// B pieces of (tap, K-half) step S for N-tile nt: [step][piece][N-tile][lane] f16x8, buffer loads
+__device__ __forceinline__ X6W h3_w(const float* p, int lane, int nt) {
+    X6W w;
+    w.r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(h3::kW * 4), 0x00020000);
+    w.voff = (nt * 64 + lane) * 16;
+    return w;
+}
+__device__ __forceinline__ f16x8 h3_ldb(const X6W& w, int entry) {  // entry = (step * 2 + piece) * 4
+    return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(w.r, w.voff, entry * 64 * 16, 0));
+}
+
+template <class C, int GRP, int K>
+__device__ __forceinline__ void h3_step_b(const X6W& W, f16x8 (&b)[2], f16x8 (&bn)[2]) {
+    constexpr const X6Plan& P = X6PlanOf<GRP, C::KH>::P;
+    constexpr X6Batch B = P.b[K];
+    constexpr int step = B.t * 2 + B.m;
+    constexpr bool first_of_step = K == 0 || P.b[K - 1].t * 2 + P.b[K - 1].m != step;
+    if constexpr (first_of_step && K > 0) {
+        b[0] = bn[0];
+        b[1] = bn[1];
+    }
+    if constexpr (first_of_step && step + 1 < 18) {  // prefetch the next step's B pieces
+        bn[0] = h3_ldb(W, ((step + 1) * 2 + 0) * 4);
+        bn[1] = h3_ldb(W, ((step + 1) * 2 + 1) * 4);
+    }
+}
+
+// PIPE 1, batch K (X holds its lo pieces on entry and the next batch's on exit):
+//   load Y = hi | lo*Bhi | load X = next lo | hi*Bhi, hi*Blo
+template <class C, int GRP, int K>
+__device__ __forceinline__ void conv_h3_batch(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
+                                              f16x8 (&bn)[2], f16x8 (&X)[C::KH], f16x8 (&Y)[C::KH],
+                                              const int (&ab)[2][2]) {
+    constexpr int KH = C::KH, NS = C::NS;
+    h3_step_b<C, GRP, K>(W, b, bn);
+    h3_load<GRP, KH, K>(Y, img, ab, 0);
+    h3_mfma<GRP, KH, K, NS>(acc, X, b[0]);  // lo*hi
+    if constexpr (K + 1 < X6PlanOf<GRP, KH>::P.nbat) h3_load<GRP, KH, K + 1>(X, img, ab, 1);
+    h3_mfma<GRP, KH, K, NS>(acc, Y, b[0]);  // hi*hi
+    h3_mfma<GRP, KH, K, NS>(acc, Y, b[1]);  // hi*lo
+    __builtin_amdgcn_sched_barrier(0);      // bound the live ranges: no loads hoisted across batches
+}
+
+// PIPE 2, batch K: both pieces of batch K+1 load during batch K (four buffers, roles swap with K's
+// parity):  lo*Bhi | load next lo | hi*Bhi | load next hi | hi*Blo
+template <class C, int GRP, int K>
+__device__ __forceinline__ void conv_h3_batch2(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
+                                               f16x8 (&bn)[2], f16x8 (&L)[C::KH], f16x8 (&H)[C::KH],
+                                               f16x8 (&Ln)[C::KH], f16x8 (&Hn)[C::KH], const int (&ab)[2][2]) {
+    constexpr int KH = C::KH, NS = C::NS;
+    constexpr bool more = K + 1 < X6PlanOf<GRP, KH>::P.nbat;
+    h3_step_b<C, GRP, K>(W, b, bn);
+    h3_mfma<GRP, KH, K, NS>(acc, L, b[0]);  // lo*hi
+    if constexpr (more) h3_load<GRP, KH, K + 1>(Ln, img, ab, 1);
+    h3_mfma<GRP, KH, K, NS>(acc, H, b[0]);  // hi*hi
+    if constexpr (more) h3_load<GRP, KH, K + 1>(Hn, img, ab, 0);
+    h3_mfma<GRP, KH, K, NS>(acc, H, b[1]);  // hi*lo
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <class C, int GRP, int... K>
+__device__ __forceinline__ void conv_h3_run(f32x4 (&acc)[C::NS], const char* img, const X6W& W, const int (&lo)[2],
+                                            std::integer_sequence<int, K...>) {
+    int ab[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int sg = 0; sg < 2; ++sg) ab[m][sg] = lo[m] + sg * 65536;
+    f16x8 b[2], bn[2];
+    b[0] = h3_ldb(W, 0);
+    b[1] = h3_ldb(W, 4);
+    if constexpr (C::PIPE == 2) {
+        f16x8 L[C::KH], H[C::KH], L2[C::KH], H2[C::KH];
+        h3_load<GRP, C::KH, 0>(L, img, ab, 1);
+        h3_load<GRP, C::KH, 0>(H, img, ab, 0);
+        ((K % 2 == 0 ? conv_h3_batch2<C, GRP, K>(acc, img, W, b, bn, L, H, L2, H2, ab)
+                     : conv_h3_batch2<C, GRP, K>(acc, img, W, b, bn, L2, H2, L, H, ab)),
+         ...);
+    } else {
+        f16x8 X[C::KH], Y[C::KH];
+        h3_load<GRP, C::KH, 0>(X, img, ab, 1);
+        (conv_h3_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab), ...);
+    }
+}
+
+// acc * (1/s) + bias (+ residual), ReLU, split into the two LDS planes; lane pairing, DPP exchange
+// and ADD / KEEP as epilogue_x6_pack. vmax: the largest activation this lane has split.
+template <class C, int GRP>
+__device__ __forceinline__ void epilogue_h3_pack(const f32x4 (&acc)[C::NS], uint32_t (&pk)[C::NS][2][2], float bb,
+                                                 float sc, f32x4 (&skip)[C::NS], int co, bool add, bool keep,
+                                                 float& vmax) {
+    const bool odd = co & 1;
+    const float addf = add ? 1.0f : 0.0f;  // fma(skip, addf, v) = v + skip or v, exactly
+#pragma unroll
+    for (int j = 0; j < grp_n(GRP); ++j) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            v[r] = __builtin_fmaf(skip[j][r], addf, __builtin_fmaf(acc[j][r], sc, bb));
+            v[r] = v[r] > 0.0f ? v[r] : 0.0f;
+            if (keep) skip[j][r] = v[r];
+        }
+        vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const float keep_ = odd ? v[2 * k + 1] : v[2 * k];  // stays in this lane
+            const float send = odd ? v[2 * k] : v[2 * k + 1];   // goes to the partner
+            const float got = __int_as_float(
+                __builtin_amdgcn_update_dpp(0, __float_as_int(send), 0xB1, 0xF, 0xF, false));
+            const float e0 = odd ? got : keep_, e1 = odd ? keep_ : got;  // (even, odd) channel
+            const _Float16 h0 = (_Float16)e0, h1 = (_Float16)e1;
+            const _Float16 l0 = (_Float16)(e0 - (float)h0), l1 = (_Float16)(e1 - (float)h1);
+            pk[j][k][0] = __builtin_bit_cast(uint32_t, f16x2{h0, h1});
+            pk[j][k][1] = __builtin_bit_cast(uint32_t, f16x2{l0, l1});
+        }
+    }
+}
+template <class C, int GRP>
+__device__ __forceinline__ void epilogue_h3_store(const uint32_t (&pk)[C::NS][2][2], char* img, const int (&eo)[2]) {
+#pragma unroll
+    for (int j = 0; j < grp_n(GRP); ++j)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            char* d = img + grp_sq(GRP, j) * (nn::kSB * h3::kRowB) + eo[k];
+            *reinterpret_cast<uint32_t*>(d) = pk[j][k][0];
+            *reinterpret_cast<uint32_t*>(d + h3::kPlaneB) = pk[j][k][1];
+        }
+}
+
+// The whole forward for the waves of square group GRP.
+template <class C, int GRP>
+__device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
+                                           int blocks, float* __restrict__ policy, float* __restrict__ value,
+                                           uint32_t* __restrict__ range_flag, float* lds) {
+    constexpr int NS = C::NS;
+    char* img = reinterpret_cast<char*>(lds);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nt = wave & 3;
+    const int b0 = blockIdx.x * nn::kSB;
+    int* pinfo = reinterpret_cast<int*>(lds + h3::kImageB / 4);
+    const int co = nt * 16 + (lane & 15);
+    const int i = lane & 15, kq = lane >> 4;
+    int eo[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) eo[k] = h3::elem_off(kq * 4 + 2 * k + (co & 1), co & ~1);
+    const int lo[2] = {h3::chunk_off(i, kq), h3::chunk_off(i, 4 + kq)};
+
+    f32x4 acc[NS];
+    f32x4 skip[NS];
+    float vmax = 0.0f;
+    {  // encoder + first layer (exact fp32 MFMA on the 0/1 inputs, as k_nn_x6)
+        L1Regs<GRP> l1;
+        first_layer_x6_fetch<GRP>(l1, blob, lane, nt);
+        const int b = b0 + i < B ? b0 + i : b0;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
+        const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
+        if (tid < nn::kSB) {
+            const oaz_state st = states[b];
+            const int blue = st.to_move & 1;
+            const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
+            pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
+        }
+        const float bias1 = blob[nn::kL1B + co];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};  // skip: finite for the fma in the epilogue
+        first_layer_x6<C, GRP>(acc, l1, blob + nn::kL1B + nn::kCh, bb, pinfo[i], lane, nt);
+        uint32_t pk[NS][2][2];
+        epilogue_h3_pack<C, GRP>(acc, pk, bias1, 1.0f, skip, co, false, true, vmax);
+        epilogue_h3_store<C, GRP>(pk, img, eo);
+        __syncthreads();
+    }
+    // 2 * blocks convs through one call site (small block 1: conv + BN + ReLU; small block 2:
+    // conv + BN, + skip, ReLU)
+    const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
+    for (int c = 0; c < 2 * blocks; ++c) {
+        const float bb = p[h3::kW + co], sc = p[h3::kW + nn::kCh + co];  // in flight during the conv
+#pragma unroll
+        for (int j = 0; j < NS; ++j) acc[j] = f32x4{};
+        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt), lo,
+                            std::make_integer_sequence<int, X6PlanOf<GRP, C::KH>::P.nbat>{});
+        p += h3::kW + 2 * nn::kCh;
+        uint32_t pk[NS][2][2];
+        epilogue_h3_pack<C, GRP>(acc, pk, bb, sc, skip, co, c & 1, c & 1, vmax);
+        __syncthreads();
+        epilogue_h3_store<C, GRP>(pk, img, eo);
+        __syncthreads();
+    }
+    // heads: the value / policy 1x1 convs as split MFMAs on the LDS image (one 16x16 tile per
+    // square: rows = positions, columns 0 / 1 / 2 = value, policy planes 0 / 1, each scaled by a
+    // power of two), then the MLPs per position on the VALU from a feature table in LDS
+    {
+        const float* hp = p + nn::kValueF + nn::kPolicyF;
+        const f16x8* HB = reinterpret_cast<const f16x8*>(hp);
+        f16x8 hb[2][2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int pc = 0; pc < 2; ++pc) hb[m][pc] = HB[(m * 2 + pc) * 64 + lane];
+        const float hs = hp[2 * 2 * 64 * 4 + (i < 3 ? i : 0)];
+        constexpr int kSqPerWave = (25 + C::WAVES - 1) / C::WAVES;
+        f32x4 hacc[kSqPerWave];
+#pragma unroll
+        for (int q = 0; q < kSqPerWave; ++q) {
+            hacc[q] = f32x4{};
+            const int sq = wave + q * C::WAVES;
+            if (sq < 25) {
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const char* a = img + sq * (nn::kSB * h3::kRowB) + lo[m];
+                    const f16x8 ah = *reinterpret_cast<const f16x8*>(a);
+                    const f16x8 al = *reinterpret_cast<const f16x8*>(a + h3::kPlaneB);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, hb[m][0], hacc[q], 0, 0, 0);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][0], hacc[q], 0, 0, 0);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][1], hacc[q], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();  // the image is no longer read: its first 4.8 KB become the feature table
+        float* feat = reinterpret_cast<float*>(img);  // [16 positions][80]
+        const float hbias = i == 0 ? p[64] : i == 1 ? p[nn::kValueF + 128] : p[nn::kValueF + 129];
+#pragma unroll
+        for (int q = 0; q < kSqPerWave; ++q) {
+            const int sq = wave + q * C::WAVES;
+            if (sq < 25 && i < 3)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v = __builtin_fmaf(hacc[q][r], hs, hbias);
+                    feat[(kq * 4 + r) * 80 + i * 25 + sq] = v > 0.0f ? v : 0.0f;
+                }
+        }
+        __syncthreads();
+        constexpr int NP = nn::kSB / C::WAVES;  // positions per wave
+        const float* fq[NP];
+        int bq[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            fq[q] = feat + (wave + q * C::WAVES) * 80;
+            bq[q] = b0 + wave + q * C::WAVES;
+        }
+        heads_mlp<NP>(fq, bq, p, lane, B, policy, value);
+    }
+    if (vmax >= 65504.0f) atomicOr(range_flag, 1u);  // an fp16 hi term overflowed (or would have)
+}
+
+template <class C>
+__global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __restrict__ states, int B,
+                                                        const float* __restrict__ blob, int blocks,
+                                                        float* __restrict__ policy, float* __restrict__ value,
+                                                        uint32_t* __restrict__ range_flag) {
+    __shared__ __attribute__((aligned(16))) float lds[h3::kLdsFloats];
+    if constexpr (C::WAVES == 4) {
+        nn_h3_body<C, 2>(states, B, blob, blocks, policy, value, range_flag, lds);
+    } else if constexpr (C::UNEVEN) {
+        constexpr int g0 = C::UNEVEN == 2 ? 5 : 3;
+        if ((threadIdx.x >> 8) == 0) {
+            __builtin_amdgcn_s_setprio(1);
+            nn_h3_body<C, g0>(states, B, blob, blocks, policy, value, range_flag, lds);
+        } else {
+            nn_h3_body<C, g0 + 1>(states, B, blob, blocks, policy, value, range_flag, lds);
+        }
+    } else if ((threadIdx.x >> 8) == 0)  // waves 0-3: square group 0, waves 4-7: group 1
+        nn_h3_body<C, 0>(states, B, blob, blocks, policy, value, range_flag, lds);
+    else
+        nn_h3_body<C, 1>(states, B, blob, blocks, policy, value, range_flag, lds);
+}
+
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy, float* value,
                              hipStream_t st) {
     if (B <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
-    if (w.precision == OAZ_FP32_SPLIT) {
+    if (w.precision == OAZ_FP32_SPLIT16) {
+        if (!w.range_flag) return hipErrorInvalidValue;
+        // default: 8 waves, uneven 15 / 10 square split, batches of <= 4 squares; OAZ_NN_X6_V
+        // selects the A/B alternatives
+        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1>>;
+        int waves = 8;
+        switch (w.x6_variant) {
+            case 1: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 1>>; break;  // both pieces one batch ahead
+            case 2: k = k_nn_h3<X6Cfg<8, 6, 1, 0, 1>>; break;
+            case 3: k = k_nn_h3<X6Cfg<8, 6, 2, 0, 1>>; break;
+            case 4: k = k_nn_h3<X6Cfg<8, 5, 1, 0, 1>>; break;
+            case 5: k = k_nn_h3<X6Cfg<8, 4, 1>>; break;  // even 13 / 12 split
+            case 6: k = k_nn_h3<X6Cfg<8, 8, 1, 0, 1>>; break;
+            case 7: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 2>>; break;  // 16 / 9 split
+            case 8: k = k_nn_h3<X6Cfg<4, 8, 1>>; waves = 4; break;  // one 512-VGPR wave per SIMD
+            default: break;
+        }
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value,
+                           w.range_flag);
+    } else if (w.precision == OAZ_FP32_SPLIT) {
         // default: 8 waves, uneven 15 / 10 square split, pipelined batches of <= 4 squares
         // (DESIGN.md perf log); OAZ_NN_X6_V selects the A/B alternatives
         auto k = k_nn_x6<X6Cfg<8, 4, 1, 0, 1>>;

@@ -18,7 +18,8 @@ RED, BLUE = 0, 1
 PAWN, KING = 0, 1
 CAPTURE, RED_WIN, BLUE_WIN, IN_PROGRESS = 0, 1, 2, 3
 EVAL_NN, EVAL_HASH = 0, 1
-FP32, BF16, FP32_SPLIT = 0, 1, 2  # OAZ_FP32 / OAZ_BF16 / OAZ_FP32_SPLIT (onitama_az.h)
+FP32, BF16, FP32_SPLIT, FP32_SPLIT16 = 0, 1, 2, 3  # OAZ_FP32 / OAZ_BF16 / OAZ_FP32_SPLIT / OAZ_FP32_SPLIT16
+ERR_RANGE = -7  # OAZ_ERR_RANGE (onitama_az.h)
 MAX_MOVES = 40
 
 

@@ -92,11 +92,11 @@ def test_encode_vs_oracle(orc):
 
 
 # ---- NN ----------------------------------------------------------------------------------
-@pytest.mark.parametrize("precision", [_abi.FP32, _abi.FP32_SPLIT])
+@pytest.mark.parametrize("precision", [_abi.FP32, _abi.FP32_SPLIT, _abi.FP32_SPLIT16])
 @pytest.mark.parametrize("name,blocks", [("trained3", 3), ("random3", 3), ("random6", 6)])
 def test_nn_matches_torch_goldens(nn_golden, trained3, name, blocks, precision):
-    """Both fp32 kernels (exact fp32 MFMA, and the bf16x6 split) against the torch-CPU fp32
-    goldens of the net.rs op graph, within the north star's 1e-4."""
+    """The three fp32 kernels (exact fp32 MFMA, the bf16x6 split, the fp16x3 split) against the
+    torch-CPU fp32 goldens of the net.rs op graph, within the north star's 1e-4."""
     w = trained3 if name == "trained3" else random_weights(0 if name == "random3" else 1, blocks)
     with Engine(games=256, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN, precision=precision) as e:
         e.load_weights(w)
@@ -105,6 +105,45 @@ def test_nn_matches_torch_goldens(nn_golden, trained3, name, blocks, precision):
     assert np.abs(p - nn_golden[f"policy_{name}"]).max() < tol
     assert np.abs(v - nn_golden[f"value_{name}"]).max() < tol
     assert np.allclose(p.reshape(-1, 50).sum(1), 1.0, atol=1e-5)
+
+
+@pytest.mark.parametrize("name,blocks", [("trained3", 3), ("random3", 3), ("random6", 6)])
+def test_nn_split16_error_at_fp32_level(nn_golden, trained3, name, blocks):
+    """OAZ_FP32_SPLIT16 (hi/lo fp16 terms, three products) is an fp32 path, not a reduced-precision
+    one: its distance to the torch fp32 goldens stays within 1e-5 (10x inside the north star's 1e-4;
+    a single bf16 or fp16 product per MAC, or a two-term bf16 split, lands at 1e-4 - 1e-2) and within
+    4x of the exact-fp32 MFMA kernel's own distance (+1e-6 for ties at the fp32 rounding level)."""
+    w = trained3 if name == "trained3" else random_weights(0 if name == "random3" else 1, blocks)
+    err = {}
+    for prec in (_abi.FP32, _abi.FP32_SPLIT16):
+        with Engine(games=256, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN, precision=prec) as e:
+            e.load_weights(w)
+            p, v = e.nn_forward(nn_golden["states"])
+        err[prec] = max(np.abs(p - nn_golden[f"policy_{name}"]).max(), np.abs(v - nn_golden[f"value_{name}"]).max())
+    assert err[_abi.FP32_SPLIT16] < 1e-5, err
+    assert err[_abi.FP32_SPLIT16] <= 4 * err[_abi.FP32] + 1e-6, err
+
+
+def test_nn_split16_range_guard(nn_golden, trained3):
+    """An activation beyond the fp16 range fails loudly (OAZ_ERR_RANGE) instead of returning
+    garbage, and a later load of sane weights clears the condition."""
+    from onitama_az.weights import blob_from_named, named_from_blob
+    named = {k: v.copy() for k, v in named_from_blob(trained3.copy(), 3).items()}
+    named["bn1|bias"][:] = 1.0e5  # first-layer activations ~1e5 > 65504
+    bad = blob_from_named(named, 3)
+    states = nn_golden["states"][:32]
+    with Engine(games=64, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT16) as e:
+        e.load_weights(bad)
+        with pytest.raises(_abi.OazError, match="fp16 range"):
+            e.nn_forward(states)
+        e.load_weights(trained3)
+        p, _ = e.nn_forward(states)
+    assert np.abs(p - nn_golden["policy_trained3"][:32]).max() < 1e-5
+    # the exact kernels have no such limit: same weights, finite softmax
+    with Engine(games=64, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT) as e:
+        e.load_weights(bad)
+        p, v = e.nn_forward(states)
+    assert np.isfinite(p).all() and np.isfinite(v).all()
 
 
 @pytest.mark.parametrize("name,blocks", [("trained3", 3), ("random3", 3), ("random6", 6)])
@@ -120,9 +159,10 @@ def test_nn_bf16_mode_close_to_fp32_goldens(nn_golden, trained3, name, blocks):
     assert np.allclose(p.reshape(-1, 50).sum(1), 1.0, atol=1e-5)
 
 
-def test_nn_batch_position_invariance(orc):
+@pytest.mark.parametrize("precision", [_abi.FP32, _abi.FP32_SPLIT16])
+def test_nn_batch_position_invariance(orc, precision):
     pos = random_positions(orc, 64, seed=404)
-    with Engine(games=1024, sims=1, blocks=3) as e:
+    with Engine(games=1024, sims=1, blocks=3, precision=precision) as e:
         p1, v1 = e.nn_forward(pos)
         big = np.concatenate([pos[::-1], pos, pos[:7]])
         p2, v2 = e.nn_forward(big)
@@ -155,14 +195,16 @@ def test_search_hash_trees_bitexact(orc, sims, c_puct):
     assert r.stats.sims == sims * len(roots)
 
 
-def test_search_nn_trees_bitexact_with_gpu_evaluator(orc):
+@pytest.mark.parametrize("precision", [_abi.FP32, _abi.FP32_SPLIT16])
+def test_search_nn_trees_bitexact_with_gpu_evaluator(orc, precision):
     """Real network: the oracle's search is fed the GPU network's outputs (batch-1 calls of
     the same kernel), so both searches see identical evaluations and must agree exactly."""
     roots = random_positions(orc, 4, seed=606)
     w = random_weights(3, 3)
     sims = 48
-    with Engine(games=len(roots), sims=sims, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_NN, blocks=3) as e, \
-            Engine(games=4, sims=1, blocks=3) as ev:
+    with Engine(games=len(roots), sims=sims, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_NN, blocks=3,
+                precision=precision) as e, \
+            Engine(games=4, sims=1, blocks=3, precision=precision) as ev:
         e.load_weights(w)
         ev.load_weights(w)
         r = e.search(roots)
@@ -316,7 +358,8 @@ def test_selfplay_matches_oracle_games(orc, fixed, max_plies):
     assert np.array_equal(_sorted_rows(got), _sorted_rows(ref))
 
 
-@pytest.mark.parametrize("precision,blocks", [(_abi.FP32, 3), (_abi.FP32_SPLIT, 3), (_abi.BF16, 6)])
+@pytest.mark.parametrize("precision,blocks", [(_abi.FP32, 3), (_abi.FP32_SPLIT, 3), (_abi.FP32_SPLIT16, 3),
+                                              (_abi.BF16, 6)])
 def test_selfplay_nn_continuous_batching_runs(precision, blocks):
     with Engine(games=256, sims=16, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_NN, blocks=blocks, max_plies=150,
                 precision=precision, fixed_deck=0) as e:

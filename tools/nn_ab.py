@@ -24,17 +24,18 @@ def main():
     ap.add_argument("--precision", default="fp32,fp32x6,bf16")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--x6-variants", default="0", help="OAZ_NN_X6_V values to compare for fp32x6")
+    ap.add_argument("--x6-variants", default="0", help="OAZ_NN_X6_V values to compare for fp32x6 / fp32h3")
     a = ap.parse_args()
     g = np.load(ROOT / "tests/golden/nn_golden.npz")
     w3 = np.load(ROOT / "tests/golden/weights_3block_trained.npy")
     engines = {}
     for v in [int(x) for x in a.blocks.split(",")]:
         for prec, var in [(p, x) for p in a.precision.split(",")
-                          for x in (a.x6_variants.split(",") if p == "fp32x6" else ["0"])]:
+                          for x in (a.x6_variants.split(",") if p in ("fp32x6", "fp32h3") else ["0"])]:
             os.environ["OAZ_NN_X6_V"] = var
             e = Engine(games=a.batch, sims=1, blocks=v, evaluator=_abi.EVAL_NN,
-                       precision={"bf16": _abi.BF16, "fp32x6": _abi.FP32_SPLIT}.get(prec, _abi.FP32))
+                       precision={"bf16": _abi.BF16, "fp32x6": _abi.FP32_SPLIT,
+                                  "fp32h3": _abi.FP32_SPLIT16}.get(prec, _abi.FP32))
             err = {}
             for name, blob, nb in (("trained3", w3, 3), ("random3", random_weights(0, 3), 3),
                                    ("random6", random_weights(1, 6), 6)):
@@ -45,7 +46,7 @@ def main():
                 err[name] = {"policy": float(np.abs(p - g[f"policy_{name}"]).max()),
                              "value": float(np.abs(val - g[f"value_{name}"]).max())}
             e.load_weights(random_weights(0, v))
-            engines[f"{v}-{prec}" + (f"-v{var}" if prec == "fp32x6" else "")] = (e, err, v, var)
+            engines[f"{v}-{prec}" + (f"-v{var}" if prec in ("fp32x6", "fp32h3") else "")] = (e, err, v, var)
     states = np.concatenate([g["states"]] * (a.batch // len(g["states"]) + 1))[: a.batch]
     res = {v: [] for v in engines}
     for _ in range(a.rounds):
