@@ -33,7 +33,7 @@ CONFIGS = {
     # BASELINE.json configs[1]: 4096 parallel games, 100 sims/move, 3-block fp32, 1 GPU
     "c2": dict(games=4096, sims=100, blocks=3, fixed_deck=1, precision="fp32"),
     # configs[2]: 65536 parallel games, 400 sims/move, 1 GPU (the metric's "@400 sims"); fp32 NN
-    # arithmetic (north star: policy/value within 1e-4 fp32) on the split kernel by default
+    # arithmetic (north star: policy/value within 1e-4 fp32) on the fp16x3 split kernel by default
     "c3": dict(games=65536, sims=400, blocks=3, fixed_deck=1, precision="fp32"),
     # configs[4] (per GPU): 16-card random deals, 800 sims, 6-block, bf16 MFMA inputs / fp32 accumulate
     "c5": dict(games=65536, sims=800, blocks=6, fixed_deck=0, precision="bf16"),
@@ -72,7 +72,7 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--games", type=int, default=0, help="override games per GPU")
     ap.add_argument("--sims", type=int, default=0, help="override sims per move")
-    ap.add_argument("--fp32-kernel", default="split", choices=["split", "split16", "exact"],
+    ap.add_argument("--fp32-kernel", default="split16", choices=["split", "split16", "exact"],
                     help="fp32 NN kernel: split (bf16x6), split16 (fp16x3; both fp32-level error) or exact "
                          "(fp32 MFMA products)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="cpu_baseline sample length")

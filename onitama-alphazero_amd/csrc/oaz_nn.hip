@@ -1439,6 +1439,15 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
     f32x4 acc[NS];
     f32x4 skip[NS];
     float vmax = 0.0f;
+    uint64_t ph[6] = {0, 0, 0, 0, 0, 0};  // DBG 2: first layer, conv, barrier 1, epilogue, barrier 2, heads
+    uint64_t tm = C::DBG == 2 ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int k) {
+        if constexpr (C::DBG == 2) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            ph[k] += t - tm;
+            tm = t;
+        }
+    };
     {  // encoder + first layer (exact fp32 MFMA on the 0/1 inputs, as k_nn_x6)
         L1Regs<GRP> l1;
         first_layer_x6_fetch<GRP>(l1, blob, lane, nt);
@@ -1463,6 +1472,7 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
     }
     // 2 * blocks convs through one call site (small block 1: conv + BN + ReLU; small block 2:
     // conv + BN, + skip, ReLU)
+    stamp(0);
     const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
     for (int c = 0; c < 2 * blocks; ++c) {
         const float bb = p[h3::kW + co], sc = p[h3::kW + nn::kCh + co];  // in flight during the conv
@@ -1470,12 +1480,17 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
         for (int j = 0; j < NS; ++j) acc[j] = f32x4{};
         conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt), lo,
                             std::make_integer_sequence<int, X6PlanOf<GRP, C::KH>::P.nbat>{});
+        stamp(1);
         p += h3::kW + 2 * nn::kCh;
         uint32_t pk[NS][2][2];
         epilogue_h3_pack<C, GRP>(acc, pk, bb, sc, skip, co, c & 1, c & 1, vmax);
+        stamp(3);
         __syncthreads();
+        stamp(2);
         epilogue_h3_store<C, GRP>(pk, img, eo);
+        stamp(3);
         __syncthreads();
+        stamp(4);
     }
     // heads: the value / policy 1x1 convs as split MFMAs on the LDS image (one 16x16 tile per
     // square: rows = positions, columns 0 / 1 / 2 = value, policy planes 0 / 1, each scaled by a
@@ -1532,6 +1547,11 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
         heads_mlp<NP>(fq, bq, p, lane, B, policy, value);
     }
     if (vmax >= 65504.0f) atomicOr(range_flag, 1u);  // an fp16 hi term overflowed (or would have)
+    if constexpr (C::DBG == 2) {
+        stamp(5);
+        __syncthreads();
+        if (lane < 6 && b0 + nn::kSB <= B) policy[(size_t)b0 * 50 + wave * 6 + lane] = (float)ph[lane];
+    }
 }
 
 template <class C>
@@ -1575,6 +1595,7 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             case 6: k = k_nn_h3<X6Cfg<8, 8, 1, 0, 1>>; break;
             case 7: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 2>>; break;  // 16 / 9 split
             case 8: k = k_nn_h3<X6Cfg<4, 8, 1>>; waves = 4; break;  // one 512-VGPR wave per SIMD
+            case 10: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1>>; break;     // timing only: phase stamps
             default: break;
         }
         hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value,

@@ -1,5 +1,6 @@
-"""Per-wave phase breakdown of k_nn_x6 (timing build OAZ_NN_X6_V=10: s_memtime sums per phase,
-written over each workgroup's first policy rows). Output: mean cycles per wave per phase."""
+"""Per-wave phase breakdown of k_nn_x6 / k_nn_h3 (timing build OAZ_NN_X6_V=10: s_memtime sums per
+phase, written over each workgroup's first policy rows). Output: mean cycles per wave per phase.
+Usage: python tools/nn_phases.py [B] [blocks] [x6|h3]"""
 import json
 import os
 import sys
@@ -18,7 +19,8 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 blocks = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 g = np.load(ROOT / "tests/golden/nn_golden.npz")
 states = np.concatenate([g["states"]] * (B // len(g["states"]) + 1))[:B]
-with Engine(games=B, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT) as e:
+prec = _abi.FP32_SPLIT16 if (sys.argv[3] if len(sys.argv) > 3 else "x6") == "h3" else _abi.FP32_SPLIT
+with Engine(games=B, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN, precision=prec) as e:
     e.load_weights(random_weights(0, blocks))
     e.nn_forward(states)
     p, _ = e.nn_forward(states)
