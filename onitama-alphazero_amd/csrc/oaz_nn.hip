@@ -406,6 +406,156 @@ __device__ __forceinline__ void heads_mlp(const float* const (&feat)[NP], const 
     }
 }
 
+// Wave reductions on DPP within each 16-lane row (quad swaps, half-row and row mirrors) and four
+// v_readlane for the rows: a few cycles per step instead of a ds_bpermute round trip per step.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_mov<0x141>(v);  // row_half_mirror
+    v += dpp_mov<0x140>(v);  // row_mirror: every lane holds its row's sum
+    return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+    v = fmaxf(v, dpp_mov<0xB1>(v));
+    v = fmaxf(v, dpp_mov<0x4E>(v));
+    v = fmaxf(v, dpp_mov<0x141>(v));
+    v = fmaxf(v, dpp_mov<0x140>(v));
+    return fmaxf(fmaxf(readlane_f(v, 0), readlane_f(v, 16)), fmaxf(readlane_f(v, 32), readlane_f(v, 48)));
+}
+
+// heads_mlp with the MLP weights requested up front (HeadRegs, issued before the head 1x1 convs, so
+// their latency hides behind those MFMAs and barriers) and the features read as float4s; the same
+// arithmetic in the same order as heads_mlp.
+struct HeadRegs {
+    float w1[25], wp[50], b1, bp, w2, b2;
+};
+__device__ __forceinline__ void heads_fetch(HeadRegs& R, const float* p, int lane) {
+    const float* l1w = p + 68;
+    const float* l1b = l1w + 64 * 25;
+    const float* l2w = l1b + 64;
+    const float* pp = p + nn::kValueF;
+    const float* plw = pp + 132;
+    const float* plb = plw + 2500;
+    const int pl = lane < 50 ? lane : 0;  // lanes >= 50 carry no logit (masked below)
+#pragma unroll
+    for (int k = 0; k < 25; ++k) R.w1[k] = l1w[k * 64 + lane];
+#pragma unroll
+    for (int f = 0; f < 50; ++f) R.wp[f] = plw[f * 50 + pl];
+    R.b1 = l1b[lane];
+    R.bp = plb[pl];
+    R.w2 = l2w[lane];
+    R.b2 = l2w[64];
+}
+template <int NP>
+__device__ __forceinline__ void heads_mlp_r(const HeadRegs& R, const float* const (&feat)[NP], const int (&bs)[NP],
+                                            int lane, int B, float* policy, float* value) {
+    const bool pl = lane < 50;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+        float f[76];
+#pragma unroll
+        for (int k = 0; k < 19; ++k) {  // features 0..75 (75: pad, unused)
+            const float4 v = *reinterpret_cast<const float4*>(feat[q] + 4 * k);
+            f[4 * k] = v.x;
+            f[4 * k + 1] = v.y;
+            f[4 * k + 2] = v.z;
+            f[4 * k + 3] = v.w;
+        }
+        float hj = R.b1, lg = pl ? R.bp : -INFINITY;
+#pragma unroll
+        for (int k = 0; k < 25; ++k) hj += R.w1[k] * f[k];
+        if (pl) {
+#pragma unroll
+            for (int k = 0; k < 50; ++k) lg += R.wp[k] * f[25 + k];
+        }
+        const float h = hj > 0.0f ? hj : 0.0f;
+        const float vsum = wave_sum_dpp(R.w2 * h);
+        const float mx = wave_max_dpp(lg);
+        const float e = pl ? expf(lg - mx) : 0.0f;
+        const float den = wave_sum_dpp(e);
+        if (bs[q] < B) {
+            if (pl) policy[(size_t)bs[q] * 50 + lane] = e / den;
+            if (lane == 0) value[bs[q]] = tanhf(vsum + R.b2);
+        }
+    }
+}
+
+// Heads MLPs as exact-fp32 MFMAs over the workgroup's 16 positions (8 waves): waves 0-3 the value
+// hidden layer (K = 25 features, 16 units each), waves 4-7 the policy logits (K = 50, 16 logits
+// each; logits 50..63 and K padding have zero weights). Each wave fetches only its B fragments
+// (20 KB per workgroup instead of every wave reading all 16 KB of MLP weights). The results go to
+// an LDS table [16][128] (64 hidden | 64 logits); then every wave finishes 2 positions with the
+// lane = unit / logit: ReLU, the 64-term value dot + tanh, the 50-way softmax (DPP reductions).
+struct HeadMM {
+    float w[13];
+    float b1, w2, bp, b2;
+};
+__device__ __forceinline__ void heads_mm_fetch(HeadMM& R, const float* p, int wave, int lane) {
+    const float* l1w = p + 68;
+    const float* l1b = l1w + 64 * 25;
+    const float* l2w = l1b + 64;
+    const float* plw = p + nn::kValueF + 132;
+    const float* plb = plw + 2500;
+    const int n = (wave & 3) * 16 + (lane & 15), kq = lane >> 4;
+#pragma unroll
+    for (int kk = 0; kk < 13; ++kk) {
+        const int k = 4 * kk + kq;
+        if (wave < 4)
+            R.w[kk] = (kk < 7 && k < 25) ? l1w[k * 64 + n] : 0.0f;
+        else
+            R.w[kk] = (k < 50 && n < 50) ? plw[k * 50 + n] : 0.0f;
+    }
+    R.b1 = l1b[lane];
+    R.w2 = l2w[lane];
+    R.bp = plb[lane < 50 ? lane : 0];
+    R.b2 = l2w[64];
+}
+__device__ __forceinline__ void heads_mm(const HeadMM& R, const float* feat, float* tab, int wave, int lane, int b0,
+                                         int B, float* policy, float* value) {
+    const int p = lane & 15, kq = lane >> 4;
+    f32x4 acc = {};
+    if (wave < 4) {
+#pragma unroll
+        for (int kk = 0; kk < 7; ++kk)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(feat[p * 80 + 4 * kk + kq], R.w[kk], acc, 0, 0, 0);
+    } else {
+#pragma unroll
+        for (int kk = 0; kk < 13; ++kk) {
+            const int f = 4 * kk + kq;
+            const float a = f < 50 ? feat[p * 80 + 25 + f] : 0.0f;  // (the table's pad is not initialised)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, R.w[kk], acc, 0, 0, 0);
+        }
+    }
+    // C/D: column = unit (lane & 15) of this wave's 16, rows = positions 4 * kq + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tab[(4 * kq + r) * 128 + wave * 16 + p] = acc[r];
+    __syncthreads();
+    const bool pl = lane < 50;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int pos = wave + 8 * q;
+        const float hj = tab[pos * 128 + lane] + R.b1;
+        const float lg = pl ? tab[pos * 128 + 64 + lane] + R.bp : -INFINITY;
+        const float h = hj > 0.0f ? hj : 0.0f;
+        const float vsum = wave_sum_dpp(R.w2 * h);
+        const float mx = wave_max_dpp(lg);
+        const float e = pl ? expf(lg - mx) : 0.0f;
+        const float den = wave_sum_dpp(e);
+        const int b = b0 + pos;
+        if (b < B) {
+            if (pl) policy[(size_t)b * 50 + lane] = e / den;
+            if (lane == 0) value[b] = tanhf(vsum + R.b2);
+        }
+    }
+}
+
 template <bool BF16>
 __device__ __forceinline__ void heads(const typename nn::Act<BF16>::T* act, float* scratch, int s, const float* p,
                                       int lane, int b, int B, float* policy, float* value) {
@@ -818,6 +968,75 @@ struct X6PlanOf {
     static constexpr X6Plan P = x6_plan(GRP, KH);
 };
 
+// k_nn_h3 plan: the group's squares in NPH phases (consecutive slices of the square list), each
+// phase a full pass over the 18 (tap, K-half) steps cut into batches of <= KH squares. A batch
+// also carries the squares of the previous phase whose epilogue (pack) it runs between its MFMAs,
+// so only the last phase's packs remain after the conv. first: the batch starts a step run (its
+// B pieces were prefetched); nstep: the step of the next run (its B pieces are prefetched now).
+struct H3Batch {
+    int t, m, n, first, nstep, ne;
+    int8_t j[16], nb[16], e[16];
+};
+struct H3Plan {
+    int nbat, tail;  // tail: first square index packed after the conv
+    H3Batch b[160];
+};
+constexpr H3Plan h3_plan(int grp, int kh, int nph) {
+    H3Plan P{};
+    const int n = grp_n(grp);
+    for (int ph = 0; ph < nph; ++ph) {
+        const int lo = ph * n / nph, hi = (ph + 1) * n / nph;
+        const int b0 = P.nbat;
+        for (int s = 0; s < 18; ++s) {
+            const TapList L0 = tap_list(grp, s / 2);
+            TapList L{};
+            for (int q = 0; q < L0.n; ++q)
+                if (L0.j[q] >= lo && L0.j[q] < hi) {
+                    L.j[L.n] = L0.j[q];
+                    L.nb[L.n] = L0.nb[q];
+                    ++L.n;
+                }
+            const int nb = (L.n + kh - 1) / kh;
+            int q = 0;
+            for (int k = 0; k < nb; ++k) {
+                const int m = (L.n - q) / (nb - k);
+                H3Batch B{};
+                B.t = s / 2;
+                B.m = s % 2;
+                B.n = m;
+                B.first = k == 0;
+                B.nstep = -1;
+                for (int i = 0; i < m; ++i) {
+                    B.j[i] = L.j[q + i];
+                    B.nb[i] = L.nb[q + i];
+                }
+                q += m;
+                P.b[P.nbat++] = B;
+            }
+        }
+        if (ph > 0) {  // spread the previous phase's packs over this phase's batches
+            const int plo = (ph - 1) * n / nph, cnt = lo - plo, nbt = P.nbat - b0;
+            for (int i = 0; i < cnt; ++i) {
+                H3Batch& B = P.b[b0 + (i * nbt) / cnt];
+                B.e[B.ne++] = (int8_t)(plo + i);
+            }
+        }
+        P.tail = lo;
+    }
+    int next = -1;
+    for (int k = P.nbat - 1; k >= 0; --k) {
+        if (P.b[k].first) {
+            P.b[k].nstep = next;
+            next = P.b[k].t * 2 + P.b[k].m;
+        }
+    }
+    return P;
+}
+template <int GRP, int KH, int NPH>
+struct H3PlanOf {
+    static constexpr H3Plan P = h3_plan(GRP, KH, NPH);
+};
+
 // Kernel configuration. WAVES 8: two waves per SIMD (square groups 0/1 x 4 N-tiles, <= 256 VGPRs);
 // WAVES 4: one wave per SIMD owning one N-tile of all 25 squares (up to 512 VGPRs). KH: squares per
 // batch. PIPE 1: two A-piece buffers (the m pieces of batch k+1 load during batch k's last
@@ -825,8 +1044,11 @@ struct X6PlanOf {
 // wrong results): per-wave s_memtime phase sums over the first policy rows (tools/nn_phases.py).
 // UNEVEN (8 waves): square groups 3 / 4 (15 / 10 squares) instead of 0 / 1, the bigger group at
 // s_setprio 1.
-template <int WAVES_, int KH_, int PIPE_, int DBG_ = 0, int UNEVEN_ = 0>
+template <int WAVES_, int KH_, int PIPE_, int DBG_ = 0, int UNEVEN_ = 0, int TR_ = 0, int PH_ = 1, int HV_ = 0>
 struct X6Cfg {
+    static constexpr int HV = HV_;  // h3 heads: 0 MLPs on MFMA (8 waves), 1 per-position VALU MLPs
+    static constexpr int TR = TR_;
+    static constexpr int PH = PH_;  // h3 + TR: square phases of the second (younger) group
     static constexpr int WAVES = WAVES_;
     static constexpr int UNEVEN = UNEVEN_;
     static constexpr int NS = WAVES_ == 8 ? (UNEVEN_ == 2 ? 16 : UNEVEN_ ? 15 : nn::kTPW) : 25;  // tiles per wave
@@ -1066,7 +1288,8 @@ __device__ __forceinline__ void first_layer_x6(f32x4 (&acc)[C::NS], const L1Regs
             const int r = sq / 5 + t / 3 - 1, c = sq % 5 + t % 3 - 1;
             if (r >= 0 && r < 5 && c >= 0 && c < 5) {
                 const float a = (float)((bb >> (31 - (r * 5 + c))) & 1u);
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, R.w[t], acc[j], 0, 0, 0);
+                acc[j] = C::TR ? __builtin_amdgcn_mfma_f32_16x16x4f32(R.w[t], a, acc[j], 0, 0, 0)
+                               : __builtin_amdgcn_mfma_f32_16x16x4f32(a, R.w[t], acc[j], 0, 0, 0);
             }
         }
     const int c0 = cinfo & 15, c1 = (cinfo >> 4) & 15, blue = (cinfo >> 8) & 1;
@@ -1083,7 +1306,9 @@ __device__ __forceinline__ void first_layer_x6(f32x4 (&acc)[C::NS], const L1Regs
 #pragma unroll
             for (int q = 0; q < kBatch; ++q)
                 if (j0 + q < grp_n(GRP))
-                    acc[j0 + q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], tb[q][st], acc[j0 + q], 0, 0, 0);
+                    acc[j0 + q] = C::TR
+                                      ? __builtin_amdgcn_mfma_f32_16x16x4f32(tb[q][st], a[st], acc[j0 + q], 0, 0, 0)
+                                      : __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], tb[q][st], acc[j0 + q], 0, 0, 0);
         if (j0 + kBatch < grp_n(GRP)) fetch(j0 + kBatch);
     }
 }
@@ -1268,11 +1493,19 @@ __device__ __forceinline__ int elem_off(int row, int c) { return chunk_off(row, 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
+// Phases of group GRP's squares (C::PH for the second group of the TR kernel, else 1).
+template <class C, int GRP>
+constexpr int h3_nph() {
+    return (C::TR && (GRP == 1 || GRP == 4 || GRP == 6)) ? C::PH : 1;
+}
+template <class C, int GRP>
+using H3P = H3PlanOf<GRP, C::KH, h3_nph<C, GRP>()>;
+
 // A-fragment loads / MFMAs of batch K; the LDS address is one of four per-lane bases
 // ab[m][seg] = lo[m] + seg * 64 KiB plus an immediate offset < 64 KiB (piece 1 = + kPlaneB)
-template <int GRP, int KH, int K, int N>
+template <class C, int GRP, int K, int N>
 __device__ __forceinline__ void h3_load(f16x8 (&a)[N], const char* img, const int (&ab)[2][2], int piece) {
-    constexpr X6Batch B = X6PlanOf<GRP, KH>::P.b[K];
+    constexpr H3Batch B = H3P<C, GRP>::P.b[K];
 #pragma unroll
     for (int q = 0; q < N; ++q)
         if (q < B.n) {
@@ -1281,12 +1514,24 @@ __device__ __forceinline__ void h3_load(f16x8 (&a)[N], const char* img, const in
         }
 }
 
-template <int GRP, int KH, int K, int NS, int N>
-__device__ __forceinline__ void h3_mfma(f32x4 (&acc)[NS], const f16x8 (&a)[N], const f16x8& bv) {
-    constexpr X6Batch B = X6PlanOf<GRP, KH>::P.b[K];
+// TR: the operands swapped (weights as A, positions as B), so the C/D tile is transposed: lane =
+// (position lane & 15, channels 4 * (lane >> 4) + r of the N-tile) -- the A/B fragment layouts of
+// 16x16x32 are symmetric, so the same registers serve either order.
+template <class C, int GRP, int K, int N>
+__device__ __forceinline__ void h3_mfma(f32x4 (&acc)[C::NS], const f16x8 (&a)[N], const f16x8& bv) {
+    constexpr H3Batch B = H3P<C, GRP>::P.b[K];
 #pragma unroll
     for (int q = 0; q < N; ++q)
-        if (q < B.n) acc[B.j[q]] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[q], bv, acc[B.j[q]], 0, 0, 0);
+        if (q < B.n)
+            acc[B.j[q]] = C::TR ? __builtin_amdgcn_mfma_f32_16x16x32_f16(bv, a[q], acc[B.j[q]], 0, 0, 0)
+                                : __builtin_amdgcn_mfma_f32_16x16x32_f16(a[q], bv, acc[B.j[q]], 0, 0, 0);
+}
+
+// the packs of earlier-phase squares that batch K runs (compile-time list)
+template <class C, int GRP, int K, class E, int... I>
+__device__ __forceinline__ void h3_epi(E& epi, std::integer_sequence<int, I...>) {
+    constexpr H3Batch B = H3P<C, GRP>::P.b[K];
+    ((I < B.ne ? epi(std::integral_constant<int, B.e[I < B.ne ? I : 0]>{}) : void()), ...);
 }
 
 // B pieces of (tap, K-half) step S for N-tile nt: [step][piece][N-tile][lane] f16x8, buffer loads
@@ -1302,75 +1547,74 @@ __device__ __forceinline__ f16x8 h3_ldb(const X6W& w, int entry) {  // entry = (
 
 template <class C, int GRP, int K>
 __device__ __forceinline__ void h3_step_b(const X6W& W, f16x8 (&b)[2], f16x8 (&bn)[2]) {
-    constexpr const X6Plan& P = X6PlanOf<GRP, C::KH>::P;
-    constexpr X6Batch B = P.b[K];
-    constexpr int step = B.t * 2 + B.m;
-    constexpr bool first_of_step = K == 0 || P.b[K - 1].t * 2 + P.b[K - 1].m != step;
-    if constexpr (first_of_step && K > 0) {
+    constexpr H3Batch B = H3P<C, GRP>::P.b[K];
+    if constexpr (B.first && K > 0) {
         b[0] = bn[0];
         b[1] = bn[1];
     }
-    if constexpr (first_of_step && step + 1 < 18) {  // prefetch the next step's B pieces
-        bn[0] = h3_ldb(W, ((step + 1) * 2 + 0) * 4);
-        bn[1] = h3_ldb(W, ((step + 1) * 2 + 1) * 4);
+    if constexpr (B.first && B.nstep >= 0) {  // prefetch the next step run's B pieces
+        bn[0] = h3_ldb(W, (B.nstep * 2 + 0) * 4);
+        bn[1] = h3_ldb(W, (B.nstep * 2 + 1) * 4);
     }
 }
 
 // PIPE 1, batch K (X holds its lo pieces on entry and the next batch's on exit):
-//   load Y = hi | lo*Bhi | load X = next lo | hi*Bhi, hi*Blo
-template <class C, int GRP, int K>
+//   load Y = hi | lo*Bhi | load X = next lo | hi*Bhi, hi*Blo | earlier-phase packs
+template <class C, int GRP, int K, class E>
 __device__ __forceinline__ void conv_h3_batch(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
                                               f16x8 (&bn)[2], f16x8 (&X)[C::KH], f16x8 (&Y)[C::KH],
-                                              const int (&ab)[2][2]) {
-    constexpr int KH = C::KH, NS = C::NS;
+                                              const int (&ab)[2][2], E& epi) {
     h3_step_b<C, GRP, K>(W, b, bn);
-    h3_load<GRP, KH, K>(Y, img, ab, 0);
-    h3_mfma<GRP, KH, K, NS>(acc, X, b[0]);  // lo*hi
-    if constexpr (K + 1 < X6PlanOf<GRP, KH>::P.nbat) h3_load<GRP, KH, K + 1>(X, img, ab, 1);
-    h3_mfma<GRP, KH, K, NS>(acc, Y, b[0]);  // hi*hi
-    h3_mfma<GRP, KH, K, NS>(acc, Y, b[1]);  // hi*lo
-    __builtin_amdgcn_sched_barrier(0);      // bound the live ranges: no loads hoisted across batches
+    h3_load<C, GRP, K>(Y, img, ab, 0);
+    h3_mfma<C, GRP, K>(acc, X, b[0]);  // lo*hi
+    if constexpr (K + 1 < H3P<C, GRP>::P.nbat) h3_load<C, GRP, K + 1>(X, img, ab, 1);
+    h3_mfma<C, GRP, K>(acc, Y, b[0]);  // hi*hi
+    h3_mfma<C, GRP, K>(acc, Y, b[1]);  // hi*lo
+    h3_epi<C, GRP, K>(epi, std::make_integer_sequence<int, 16>{});
+    __builtin_amdgcn_sched_barrier(0);  // bound the live ranges: no loads hoisted across batches
 }
 
 // PIPE 2, batch K: both pieces of batch K+1 load during batch K (four buffers, roles swap with K's
 // parity):  lo*Bhi | load next lo | hi*Bhi | load next hi | hi*Blo
-template <class C, int GRP, int K>
+template <class C, int GRP, int K, class E>
 __device__ __forceinline__ void conv_h3_batch2(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
                                                f16x8 (&bn)[2], f16x8 (&L)[C::KH], f16x8 (&H)[C::KH],
-                                               f16x8 (&Ln)[C::KH], f16x8 (&Hn)[C::KH], const int (&ab)[2][2]) {
-    constexpr int KH = C::KH, NS = C::NS;
-    constexpr bool more = K + 1 < X6PlanOf<GRP, KH>::P.nbat;
+                                               f16x8 (&Ln)[C::KH], f16x8 (&Hn)[C::KH], const int (&ab)[2][2],
+                                               E& epi) {
+    constexpr bool more = K + 1 < H3P<C, GRP>::P.nbat;
     h3_step_b<C, GRP, K>(W, b, bn);
-    h3_mfma<GRP, KH, K, NS>(acc, L, b[0]);  // lo*hi
-    if constexpr (more) h3_load<GRP, KH, K + 1>(Ln, img, ab, 1);
-    h3_mfma<GRP, KH, K, NS>(acc, H, b[0]);  // hi*hi
-    if constexpr (more) h3_load<GRP, KH, K + 1>(Hn, img, ab, 0);
-    h3_mfma<GRP, KH, K, NS>(acc, H, b[1]);  // hi*lo
+    h3_mfma<C, GRP, K>(acc, L, b[0]);  // lo*hi
+    if constexpr (more) h3_load<C, GRP, K + 1>(Ln, img, ab, 1);
+    h3_mfma<C, GRP, K>(acc, H, b[0]);  // hi*hi
+    if constexpr (more) h3_load<C, GRP, K + 1>(Hn, img, ab, 0);
+    h3_mfma<C, GRP, K>(acc, H, b[1]);  // hi*lo
+    h3_epi<C, GRP, K>(epi, std::make_integer_sequence<int, 16>{});
     __builtin_amdgcn_sched_barrier(0);
 }
 
-template <class C, int GRP, int... K>
+template <class C, int GRP, class E, int... K>
 __device__ __forceinline__ void conv_h3_run(f32x4 (&acc)[C::NS], const char* img, const X6W& W, const int (&lo)[2],
-                                            std::integer_sequence<int, K...>) {
+                                            E& epi, std::integer_sequence<int, K...>) {
     int ab[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int sg = 0; sg < 2; ++sg) ab[m][sg] = lo[m] + sg * 65536;
+    constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
     f16x8 b[2], bn[2];
-    b[0] = h3_ldb(W, 0);
-    b[1] = h3_ldb(W, 4);
+    b[0] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 0) * 4);
+    b[1] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 1) * 4);
     if constexpr (C::PIPE == 2) {
         f16x8 L[C::KH], H[C::KH], L2[C::KH], H2[C::KH];
-        h3_load<GRP, C::KH, 0>(L, img, ab, 1);
-        h3_load<GRP, C::KH, 0>(H, img, ab, 0);
-        ((K % 2 == 0 ? conv_h3_batch2<C, GRP, K>(acc, img, W, b, bn, L, H, L2, H2, ab)
-                     : conv_h3_batch2<C, GRP, K>(acc, img, W, b, bn, L2, H2, L, H, ab)),
+        h3_load<C, GRP, 0>(L, img, ab, 1);
+        h3_load<C, GRP, 0>(H, img, ab, 0);
+        ((K % 2 == 0 ? conv_h3_batch2<C, GRP, K>(acc, img, W, b, bn, L, H, L2, H2, ab, epi)
+                     : conv_h3_batch2<C, GRP, K>(acc, img, W, b, bn, L2, H2, L, H, ab, epi)),
          ...);
     } else {
         f16x8 X[C::KH], Y[C::KH];
-        h3_load<GRP, C::KH, 0>(X, img, ab, 1);
-        (conv_h3_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab), ...);
+        h3_load<C, GRP, 0>(X, img, ab, 1);
+        (conv_h3_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab, epi), ...);
     }
 }
 
@@ -1418,6 +1662,70 @@ __device__ __forceinline__ void epilogue_h3_store(const uint32_t (&pk)[C::NS][2]
         }
 }
 
+// TR epilogue: the lane holds 4 consecutive channels (4 * kq + r of the N-tile) of one position,
+// so no lane exchange is needed: bias / scale per register, the pair splits are packed
+// conversions (v_cvt_pk_f16_f32, RNE), lo = fp16(fma(hi, -1, v)) (x - hi is exact in fp32, one
+// rounding: v_fma_mix), and each piece is one 8-byte store per square.
+// lo = fp16(v - hi) for a pair: v_fma_mix{lo,hi}_f16 computes -hi * 1 + v from the f16 half of
+// the packed hi word, with one rounding to f16 (v - hi is exact in fp32, so this equals the
+// cvt(sub) sequence bit for bit).
+__device__ __forceinline__ uint32_t h3_lo_pair(uint32_t hi, float v0, float v1) {
+    uint32_t d;
+    asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+        : "=&v"(d)
+        : "v"(hi), "v"(v0), "v"(v1));
+    return d;
+}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// FIRST (the first layer): no residual, keep the result. Convs: res = the block's second conv (add
+// the residual, keep the result for the next block). (A compile-time parity branch instead of the
+// selects makes the allocator spill.)
+// vmax: the largest hi bit pattern (v >= 0 after ReLU, so the u16 order is the value order; an
+// overflowed hi is +inf = 0x7C00).
+template <bool FIRST>
+__device__ __forceinline__ void h3t_pack_one(const f32x4& acc, uint32_t (&pk)[2][2], const f32x4& bb, const f32x4& sc,
+                                             f32x4& skip, bool res, uint32_t& hmax) {
+    const f32x2 rf = {res ? 1.0f : 0.0f, res ? 1.0f : 0.0f};  // fma(skip, rf, v) = v + skip or v, exactly
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const f32x2 a2 = {acc[2 * k], acc[2 * k + 1]}, s2 = {sc[2 * k], sc[2 * k + 1]};
+        const f32x2 b2 = {bb[2 * k], bb[2 * k + 1]};
+        f32x2 v = __builtin_elementwise_fma(a2, s2, b2);
+        if constexpr (!FIRST) v = __builtin_elementwise_fma(f32x2{skip[2 * k], skip[2 * k + 1]}, rf, v);
+        v[0] = v[0] > 0.0f ? v[0] : 0.0f;
+        v[1] = v[1] > 0.0f ? v[1] : 0.0f;
+        if (FIRST || res) {
+            skip[2 * k] = v[0];
+            skip[2 * k + 1] = v[1];
+        }
+        uint32_t hi;  // (RNE; one packed conversion)
+        asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(hi) : "v"(v[0]), "v"(v[1]));
+        hmax = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, hmax),
+                                                                      __builtin_bit_cast(u16x2, hi)));
+        pk[0][k] = hi;
+        pk[1][k] = h3_lo_pair(hi, v[0], v[1]);
+    }
+}
+template <class C, int GRP, bool FIRST>
+__device__ __forceinline__ void epilogue_h3t_pack(const f32x4 (&acc)[C::NS], uint32_t (&pk)[C::NS][2][2],
+                                                  const f32x4& bb, const f32x4& sc, f32x4 (&skip)[C::NS], bool res,
+                                                  uint32_t& hmax, int from = 0) {
+#pragma unroll
+    for (int j = 0; j < grp_n(GRP); ++j)
+        if (j >= from) h3t_pack_one<FIRST>(acc[j], pk[j], bb, sc, skip[j], res, hmax);
+}
+template <class C, int GRP>
+__device__ __forceinline__ void epilogue_h3t_store(const uint32_t (&pk)[C::NS][2][2], char* img, int eo) {
+#pragma unroll
+    for (int j = 0; j < grp_n(GRP); ++j) {
+        char* d = img + grp_sq(GRP, j) * (nn::kSB * h3::kRowB) + eo;
+        *reinterpret_cast<uint2*>(d) = uint2{pk[j][0][0], pk[j][0][1]};
+        *reinterpret_cast<uint2*>(d + h3::kPlaneB) = uint2{pk[j][1][0], pk[j][1][1]};
+    }
+}
+
 // The whole forward for the waves of square group GRP.
 template <class C, int GRP>
 __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
@@ -1435,10 +1743,13 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
 #pragma unroll
     for (int k = 0; k < 2; ++k) eo[k] = h3::elem_off(kq * 4 + 2 * k + (co & 1), co & ~1);
     const int lo[2] = {h3::chunk_off(i, kq), h3::chunk_off(i, 4 + kq)};
+    const int cq = nt * 16 + 4 * kq;  // TR: this lane's 4 channels cq .. cq + 3 of position i
+    const int eot = h3::chunk_off(i, cq >> 3) + (cq & 7) * 2;
 
     f32x4 acc[NS];
     f32x4 skip[NS];
     float vmax = 0.0f;
+    uint32_t hmax = 0;  // TR: largest hi bit patterns (two u16 halves)
     uint64_t ph[6] = {0, 0, 0, 0, 0, 0};  // DBG 2: first layer, conv, barrier 1, epilogue, barrier 2, heads
     uint64_t tm = C::DBG == 2 ? __builtin_amdgcn_s_memtime() : 0;
     auto stamp = [&](int k) {
@@ -1461,13 +1772,19 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
             pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
         }
         const float bias1 = blob[nn::kL1B + co];
+        const f32x4 bias1t = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};  // skip: finite for the fma in the epilogue
         first_layer_x6<C, GRP>(acc, l1, blob + nn::kL1B + nn::kCh, bb, pinfo[i], lane, nt);
         uint32_t pk[NS][2][2];
-        epilogue_h3_pack<C, GRP>(acc, pk, bias1, 1.0f, skip, co, false, true, vmax);
-        epilogue_h3_store<C, GRP>(pk, img, eo);
+        if constexpr (C::TR) {
+            epilogue_h3t_pack<C, GRP, true>(acc, pk, bias1t, f32x4{1.0f, 1.0f, 1.0f, 1.0f}, skip, false, hmax);
+            epilogue_h3t_store<C, GRP>(pk, img, eot);
+        } else {
+            epilogue_h3_pack<C, GRP>(acc, pk, bias1, 1.0f, skip, co, false, true, vmax);
+            epilogue_h3_store<C, GRP>(pk, img, eo);
+        }
         __syncthreads();
     }
     // 2 * blocks convs through one call site (small block 1: conv + BN + ReLU; small block 2:
@@ -1476,18 +1793,31 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
     const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
     for (int c = 0; c < 2 * blocks; ++c) {
         const float bb = p[h3::kW + co], sc = p[h3::kW + nn::kCh + co];  // in flight during the conv
+        const f32x4 bbt = *reinterpret_cast<const f32x4*>(p + h3::kW + cq);
+        const f32x4 sct = *reinterpret_cast<const f32x4*>(p + h3::kW + nn::kCh + cq);
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = f32x4{};
-        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt), lo,
-                            std::make_integer_sequence<int, X6PlanOf<GRP, C::KH>::P.nbat>{});
+        uint32_t pk[NS][2][2];
+        const bool res = c & 1;
+        auto epi = [&](auto jc) {  // an earlier phase's square: its pack runs between MFMAs
+            constexpr int j = decltype(jc)::value;
+            h3t_pack_one<false>(acc[j], pk[j], bbt, sct, skip[j], res, hmax);
+        };
+        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt), lo, epi,
+                            std::make_integer_sequence<int, H3P<C, GRP>::P.nbat>{});
         stamp(1);
         p += h3::kW + 2 * nn::kCh;
-        uint32_t pk[NS][2][2];
-        epilogue_h3_pack<C, GRP>(acc, pk, bb, sc, skip, co, c & 1, c & 1, vmax);
+        if constexpr (C::TR) {
+            epilogue_h3t_pack<C, GRP, false>(acc, pk, bbt, sct, skip, res, hmax, H3P<C, GRP>::P.tail);
+        } else
+            epilogue_h3_pack<C, GRP>(acc, pk, bb, sc, skip, co, c & 1, c & 1, vmax);
         stamp(3);
         __syncthreads();
         stamp(2);
-        epilogue_h3_store<C, GRP>(pk, img, eo);
+        if constexpr (C::TR)
+            epilogue_h3t_store<C, GRP>(pk, img, eot);
+        else
+            epilogue_h3_store<C, GRP>(pk, img, eo);
         stamp(3);
         __syncthreads();
         stamp(4);
@@ -1504,6 +1834,13 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
 #pragma unroll
             for (int pc = 0; pc < 2; ++pc) hb[m][pc] = HB[(m * 2 + pc) * 64 + lane];
         const float hs = hp[2 * 2 * 64 * 4 + (i < 3 ? i : 0)];
+        // MLP weights in flight during the head convs (after hb: vmcnt is in order)
+        HeadRegs hr;
+        HeadMM hm;
+        if constexpr (C::WAVES == 8 && C::HV == 0)
+            heads_mm_fetch(hm, p, wave, lane);
+        else
+            heads_fetch(hr, p, lane);
         constexpr int kSqPerWave = (25 + C::WAVES - 1) / C::WAVES;
         f32x4 hacc[kSqPerWave];
 #pragma unroll
@@ -1536,17 +1873,22 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
                 }
         }
         __syncthreads();
-        constexpr int NP = nn::kSB / C::WAVES;  // positions per wave
-        const float* fq[NP];
-        int bq[NP];
+        if constexpr (C::WAVES == 8 && C::HV == 0) {
+            heads_mm(hm, feat, feat + nn::kSB * 80, wave, lane, b0, B, policy, value);
+        } else {
+            constexpr int NP = nn::kSB / C::WAVES;  // positions per wave
+            const float* fq[NP];
+            int bq[NP];
 #pragma unroll
-        for (int q = 0; q < NP; ++q) {
-            fq[q] = feat + (wave + q * C::WAVES) * 80;
-            bq[q] = b0 + wave + q * C::WAVES;
+            for (int q = 0; q < NP; ++q) {
+                fq[q] = feat + (wave + q * C::WAVES) * 80;
+                bq[q] = b0 + wave + q * C::WAVES;
+            }
+            heads_mlp_r<NP>(hr, fq, bq, lane, B, policy, value);
         }
-        heads_mlp<NP>(fq, bq, p, lane, B, policy, value);
     }
     if (vmax >= 65504.0f) atomicOr(range_flag, 1u);  // an fp16 hi term overflowed (or would have)
+    if (C::TR && ((hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u)) atomicOr(range_flag, 1u);  // hi = inf
     if constexpr (C::DBG == 2) {
         stamp(5);
         __syncthreads();
@@ -1582,20 +1924,25 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
     if (w.precision == OAZ_FP32_SPLIT16) {
         if (!w.range_flag) return hipErrorInvalidValue;
-        // default: 8 waves, uneven 15 / 10 square split, batches of <= 4 squares; OAZ_NN_X6_V
-        // selects the A/B alternatives
-        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1>>;
+        // default: 8 waves, uneven 15 / 10 square split, batches of <= 4 squares, transposed C/D
+        // tiles (TR epilogue); OAZ_NN_X6_V selects the A/B alternatives (DESIGN.md perf log)
+        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1>>;
         int waves = 8;
         switch (w.x6_variant) {
-            case 1: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 1>>; break;  // both pieces one batch ahead
-            case 2: k = k_nn_h3<X6Cfg<8, 6, 1, 0, 1>>; break;
-            case 3: k = k_nn_h3<X6Cfg<8, 6, 2, 0, 1>>; break;
-            case 4: k = k_nn_h3<X6Cfg<8, 5, 1, 0, 1>>; break;
-            case 5: k = k_nn_h3<X6Cfg<8, 4, 1>>; break;  // even 13 / 12 split
-            case 6: k = k_nn_h3<X6Cfg<8, 8, 1, 0, 1>>; break;
-            case 7: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 2>>; break;  // 16 / 9 split
-            case 8: k = k_nn_h3<X6Cfg<4, 8, 1>>; waves = 4; break;  // one 512-VGPR wave per SIMD
-            case 10: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1>>; break;     // timing only: phase stamps
+            case 1: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 1, 1>>; break;  // both pieces one batch ahead
+            case 2: k = k_nn_h3<X6Cfg<8, 6, 1, 0, 1, 1>>; break;
+            case 3: k = k_nn_h3<X6Cfg<8, 6, 2, 0, 1, 1>>; break;
+            case 4: k = k_nn_h3<X6Cfg<8, 5, 1, 0, 1, 1>>; break;
+            case 5: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 0, 1>>; break;  // even 13 / 12 split
+            case 6: k = k_nn_h3<X6Cfg<8, 8, 1, 0, 1, 1>>; break;
+            case 7: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 2, 1>>; break;  // 16 / 9 split
+            case 8: k = k_nn_h3<X6Cfg<4, 8, 1, 0, 0, 1>>; waves = 4; break;  // one 512-VGPR wave per SIMD
+            case 10: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1, 1>>; break;  // timing only: phase stamps
+            case 11: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1>>; break;  // lane-per-channel C/D tiles (DPP pair stores)
+            case 12: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1>>; break;     // timing only: phase stamps, variant 11
+            case 13: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1, 2>>; break;  // younger group in 2 phases (slower)
+            case 17: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1, 1, 1>>; break;  // heads MLPs on the VALU
+            case 14: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1, 1, 2>>; break;  // timing only: phase stamps
             default: break;
         }
         hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value,

@@ -1,4 +1,4 @@
-"""Per-wave phase breakdown of k_nn_x6 / k_nn_h3 (timing build OAZ_NN_X6_V=10: s_memtime sums per
+"""Per-wave phase breakdown of k_nn_x6 / k_nn_h3 (timing build OAZ_NN_X6_V=10 (default layout; 12: variant 11): s_memtime sums per
 phase, written over each workgroup's first policy rows). Output: mean cycles per wave per phase.
 Usage: python tools/nn_phases.py [B] [blocks] [x6|h3]"""
 import json
