@@ -1918,11 +1918,342 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __rest
         nn_h3_body<C, 1>(states, B, blob, blocks, policy, value, range_flag, lds);
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_nn_p8 (OAZ_FP32_SPLIT16, OAZ_NN_X6_V=20): the k_nn_h3 arithmetic (fp16 hi/lo split, 3 products,
+// transposed C/D tiles, per-channel weight scales, range guard) on 8 positions per workgroup, so
+// that two workgroups share a CU (53 KB of LDS each) and one's epilogues, barriers, first layer
+// and heads run beside the other's conv MFMAs. A 16-row MFMA tile is two squares x 8 positions;
+// the 13 tiles pair squares whose on-board tap sets nest (interior / edge pairs: equal sets; a
+// corner with an edge square that contains its set; square 18 with the zero slot), so a tile's
+// (tap) list is the union and only the half whose neighbour is off the board reads the zero slot:
+// 93 tile-taps per conv instead of the ideal 84.5. 4 waves, wave = N-tile over all 13 tiles.
+namespace p8 {
+constexpr int kP = 8;
+constexpr int kZ = 9;                       // zero slot (tile 4, half 1), never written non-zero
+constexpr int kSlotB = kP * 128;            // 8 rows of 64 f16
+constexpr int kPlaneB = 26 * kSlotB;        // 26,624 B
+constexpr int kImageB = 2 * kPlaneB;        // 53,248 B
+constexpr int8_t kTileSq[13][2] = {{6, 7},  {11, 12}, {16, 17}, {8, 13},  {18, 25}, {1, 2},  {21, 22},
+                                   {5, 10}, {9, 14},  {4, 3},   {24, 19}, {20, 23}, {0, 15}};
+constexpr int slot_of(int sq) {
+    for (int k = 0; k < 13; ++k)
+        for (int h = 0; h < 2; ++h)
+            if (kTileSq[k][h] == sq) return 2 * k + h;
+    return kZ;
+}
+constexpr int nb_sq(int sq, int t) {
+    if (sq >= 25) return -1;
+    const int r = sq / 5 + t / 3 - 1, c = sq % 5 + t % 3 - 1;
+    return (r >= 0 && r < 5 && c >= 0 && c < 5) ? r * 5 + c : -1;
+}
+struct Batch {
+    int t, m, n, first, nstep;
+    int8_t j[8], sa[8], sb[8];  // tile, neighbour slot of half 0 / half 1 (kZ when off the board)
+};
+struct Plan {
+    int nbat;
+    Batch b[96];
+};
+constexpr Plan make_plan(int kh) {
+    Plan P{};
+    for (int s = 0; s < 18; ++s) {
+        const int t = s / 2;
+        int tl[13] = {}, nt = 0;
+        for (int k = 0; k < 13; ++k)
+            if (nb_sq(kTileSq[k][0], t) >= 0 || nb_sq(kTileSq[k][1], t) >= 0) tl[nt++] = k;
+        const int nb = (nt + kh - 1) / kh;
+        int q = 0;
+        for (int i = 0; i < nb; ++i) {
+            const int m = (nt - q) / (nb - i);
+            Batch B{};
+            B.t = t;
+            B.m = s % 2;
+            B.n = m;
+            B.first = i == 0;
+            B.nstep = -1;
+            for (int e = 0; e < m; ++e) {
+                const int k = tl[q + e];
+                const int na = nb_sq(kTileSq[k][0], t), nbb = nb_sq(kTileSq[k][1], t);
+                B.j[e] = (int8_t)k;
+                B.sa[e] = (int8_t)(na >= 0 ? slot_of(na) : kZ);
+                B.sb[e] = (int8_t)(nbb >= 0 ? slot_of(nbb) : kZ);
+            }
+            q += m;
+            P.b[P.nbat++] = B;
+        }
+    }
+    int next = -1;
+    for (int k = P.nbat - 1; k >= 0; --k)
+        if (P.b[k].first) {
+            P.b[k].nstep = next;
+            next = P.b[k].t * 2 + P.b[k].m;
+        }
+    return P;
+}
+template <int KH>
+struct PlanOf {
+    static constexpr Plan P = make_plan(KH);
+};
+}  // namespace p8
+
+// image fragment loads of batch K: lane (half h, position p, k-group kq) reads its half's neighbour
+// slot: base lb[m] + h * (sb - sa) * 1 KiB, immediate sa * 1 KiB + piece plane
+template <int KH, int K>
+__device__ __forceinline__ void p8_load(f16x8 (&a)[KH], const char* img, const int (&lb)[2], bool h, int piece) {
+    constexpr p8::Batch B = p8::PlanOf<KH>::P.b[K];
+#pragma unroll
+    for (int q = 0; q < KH; ++q)
+        if (q < B.n) {
+            const int d = h ? (B.sb[q] - B.sa[q]) * p8::kSlotB : 0;
+            a[q] = *reinterpret_cast<const f16x8*>(img + lb[B.m] + d + B.sa[q] * p8::kSlotB + piece * p8::kPlaneB);
+        }
+}
+template <int KH, int K>
+__device__ __forceinline__ void p8_mfma(f32x4 (&acc)[13], const f16x8 (&a)[KH], const f16x8& w) {
+    constexpr p8::Batch B = p8::PlanOf<KH>::P.b[K];
+#pragma unroll
+    for (int q = 0; q < KH; ++q)
+        if (q < B.n) acc[B.j[q]] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w, a[q], acc[B.j[q]], 0, 0, 0);
+}
+template <int KH, int K>
+__device__ __forceinline__ void p8_batch(f32x4 (&acc)[13], const char* img, const X6W& W, f16x8 (&b)[2],
+                                         f16x8 (&bn)[2], f16x8 (&X)[KH], f16x8 (&Y)[KH], const int (&lb)[2], bool h) {
+    constexpr p8::Plan P = p8::PlanOf<KH>::P;
+    constexpr p8::Batch B = P.b[K];
+    if constexpr (B.first && K > 0) {
+        b[0] = bn[0];
+        b[1] = bn[1];
+    }
+    if constexpr (B.first && B.nstep >= 0) {
+        bn[0] = h3_ldb(W, (B.nstep * 2 + 0) * 4);
+        bn[1] = h3_ldb(W, (B.nstep * 2 + 1) * 4);
+    }
+    p8_load<KH, K>(Y, img, lb, h, 0);
+    p8_mfma<KH, K>(acc, X, b[0]);  // lo * Bhi
+    if constexpr (K + 1 < P.nbat) p8_load<KH, K + 1>(X, img, lb, h, 1);
+    p8_mfma<KH, K>(acc, Y, b[0]);  // hi * Bhi
+    p8_mfma<KH, K>(acc, Y, b[1]);  // hi * Blo
+    __builtin_amdgcn_sched_barrier(0);
+}
+// PIPE 2: both pieces of batch K+1 load during batch K (four buffers, roles swap with K's parity)
+template <int KH, int K>
+__device__ __forceinline__ void p8_batch2(f32x4 (&acc)[13], const char* img, const X6W& W, f16x8 (&b)[2],
+                                          f16x8 (&bn)[2], f16x8 (&L)[KH], f16x8 (&H)[KH], f16x8 (&Ln)[KH],
+                                          f16x8 (&Hn)[KH], const int (&lb)[2], bool h) {
+    constexpr p8::Plan P = p8::PlanOf<KH>::P;
+    constexpr p8::Batch B = P.b[K];
+    constexpr bool more = K + 1 < P.nbat;
+    if constexpr (B.first && K > 0) {
+        b[0] = bn[0];
+        b[1] = bn[1];
+    }
+    if constexpr (B.first && B.nstep >= 0) {
+        bn[0] = h3_ldb(W, (B.nstep * 2 + 0) * 4);
+        bn[1] = h3_ldb(W, (B.nstep * 2 + 1) * 4);
+    }
+    p8_mfma<KH, K>(acc, L, b[0]);  // lo * Bhi
+    if constexpr (more) p8_load<KH, K + 1>(Ln, img, lb, h, 1);
+    p8_mfma<KH, K>(acc, H, b[0]);  // hi * Bhi
+    if constexpr (more) p8_load<KH, K + 1>(Hn, img, lb, h, 0);
+    p8_mfma<KH, K>(acc, H, b[1]);  // hi * Blo
+    __builtin_amdgcn_sched_barrier(0);
+}
+template <int KH, int PIPE, int... K>
+__device__ __forceinline__ void p8_conv(f32x4 (&acc)[13], const char* img, const X6W& W, const int (&lb)[2], bool h,
+                                        std::integer_sequence<int, K...>) {
+    constexpr p8::Batch B0 = p8::PlanOf<KH>::P.b[0];
+    f16x8 b[2], bn[2];
+    b[0] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 0) * 4);
+    b[1] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 1) * 4);
+    if constexpr (PIPE == 2) {
+        f16x8 L[KH], H[KH], L2[KH], H2[KH];
+        p8_load<KH, 0>(L, img, lb, h, 1);
+        p8_load<KH, 0>(H, img, lb, h, 0);
+        ((K % 2 == 0 ? p8_batch2<KH, K>(acc, img, W, b, bn, L, H, L2, H2, lb, h)
+                     : p8_batch2<KH, K>(acc, img, W, b, bn, L2, H2, L, H, lb, h)),
+         ...);
+    } else {
+        f16x8 X[KH], Y[KH];
+        p8_load<KH, 0>(X, img, lb, h, 1);
+        (p8_batch<KH, K>(acc, img, W, b, bn, X, Y, lb, h), ...);
+    }
+}
+// the pack of tile 4's half 1 (the zero slot) is forced to 0
+__device__ __forceinline__ void p8_store(uint32_t (&pk)[13][2][2], char* img, int est, bool h) {
+    if (h) pk[4][0][0] = pk[4][0][1] = pk[4][1][0] = pk[4][1][1] = 0u;
+#pragma unroll
+    for (int k = 0; k < 13; ++k) {
+        char* d = img + k * 2 * p8::kSlotB + est;
+        *reinterpret_cast<uint2*>(d) = uint2{pk[k][0][0], pk[k][0][1]};
+        *reinterpret_cast<uint2*>(d + p8::kPlaneB) = uint2{pk[k][1][0], pk[k][1][1]};
+    }
+}
+
+template <int KH, int PIPE>
+__global__ void __launch_bounds__(256) k_nn_p8(const oaz_state* __restrict__ states, int B,
+                                               const float* __restrict__ blob, int blocks,
+                                               float* __restrict__ policy, float* __restrict__ value,
+                                               uint32_t* __restrict__ range_flag) {
+    __shared__ __attribute__((aligned(16))) char img[p8::kImageB];
+    __shared__ int pinfo[p8::kP];
+    const int tid = threadIdx.x, nt = tid >> 6, lane = tid & 63;
+    const int n = lane & 15, pp = n & 7, kq = lane >> 4;
+    const bool h = n >= 8;
+    const int b0 = blockIdx.x * p8::kP;
+    const int cq = nt * 16 + 4 * kq;  // this lane's 4 output channels (TR C/D tiles), position (h, pp)
+    int lb[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) lb[m] = pp * 128 + (((kq + 4 * m) ^ pp) << 4);
+    const int est = (h ? p8::kSlotB : 0) + pp * 128 + (((cq >> 3) ^ pp) << 4) + (cq & 7) * 2;
+    f32x4 acc[13], skip[13];
+    uint32_t hmax = 0;
+    {  // encoder + first layer: exact fp32 MFMA (0/1 inputs); K = the 4 bitboards per tap, then the
+       // constant planes as K = (half, plane) over the two squares' table rows (9 k-steps)
+        float w1[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) w1[t] = blob[(t * 4 + nt) * 64 + lane];
+        const int b = b0 + pp < B ? b0 + pp : b0;
+        const uint32_t* sw = reinterpret_cast<const uint32_t*>(&states[b]);
+        const uint32_t bb = kq == 0 ? sw[2] : kq == 1 ? sw[0] : kq == 2 ? sw[3] : sw[1];
+        if (tid < p8::kP) {
+            const oaz_state st = states[b0 + tid < B ? b0 + tid : b0];
+            const int blue = st.to_move & 1;
+            const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
+            pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
+        }
+        const f32x4 bias1 = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
+        const float* table = blob + nn::kL1B + nn::kCh;
+        const int ch = nt * 16 + n;  // A-operand row (output channel) of this lane
+        float tb[2][9];
+        auto fetch = [&](float (&d)[9], int k) {  // table rows of tile k: k-step kk, lane k-group kq
+#pragma unroll
+            for (int kk = 0; kk < 9; ++kk) {
+                const int kx = 4 * kk + kq, hh = kx >= 17, pl = kx - 17 * hh;
+                const int sq = p8::kTileSq[k][hh];  // (compile-time per (k, kk) up to the lane's hh)
+                d[kk] = (kx < 34 && sq < 25) ? table[(size_t)sq * 17 * nn::kCh + pl * nn::kCh + ch] : 0.0f;
+            }
+        };
+        fetch(tb[0], 0);
+        __syncthreads();
+        const int ci = pinfo[pp];
+        const int c0 = ci & 15, c1 = (ci >> 4) & 15, blue = (ci >> 8) & 1;
+        float ac[9];
+#pragma unroll
+        for (int kk = 0; kk < 9; ++kk) {
+            const int kx = 4 * kk + kq, hh = kx >= 17, pl = kx - 17 * hh;
+            const float v = pl < 16 ? ((pl == c0 || pl == c1) ? 1.0f : 0.0f) : (float)blue;
+            ac[kk] = (kx < 34 && hh == (int)h) ? v : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < 13; ++k) {
+            acc[k] = skip[k] = f32x4{};
+            if (k + 1 < 13) fetch(tb[(k + 1) & 1], k + 1);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int na = p8::nb_sq(p8::kTileSq[k][0], t), nbq = p8::nb_sq(p8::kTileSq[k][1], t);
+                if (na >= 0 || nbq >= 0) {
+                    const int sh = h ? (nbq >= 0 ? 31 - nbq : 0) : (na >= 0 ? 31 - na : 0);  // bit 0 is never set
+                    const float a = (float)((bb >> sh) & 1u);
+                    acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[t], a, acc[k], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int kk = 0; kk < 9; ++kk)
+                acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[k & 1][kk], ac[kk], acc[k], 0, 0, 0);
+        }
+        uint32_t pk[13][2][2];
+#pragma unroll
+        for (int k = 0; k < 13; ++k)
+            h3t_pack_one<true>(acc[k], pk[k], bias1, f32x4{1.0f, 1.0f, 1.0f, 1.0f}, skip[k], false, hmax);
+        p8_store(pk, img, est, h);
+        __syncthreads();
+    }
+    const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
+    for (int c = 0; c < 2 * blocks; ++c) {
+        const f32x4 bbt = *reinterpret_cast<const f32x4*>(p + h3::kW + cq);
+        const f32x4 sct = *reinterpret_cast<const f32x4*>(p + h3::kW + nn::kCh + cq);
+#pragma unroll
+        for (int k = 0; k < 13; ++k) acc[k] = f32x4{};
+        // opaque per iteration: the ~90 per-(tile, tap) half-select addresses must not be hoisted out of
+        // the conv loop as loop invariants (they would stay live in registers)
+        int hv = h, lb2[2] = {lb[0], lb[1]};
+        asm volatile("" : "+v"(hv), "+v"(lb2[0]), "+v"(lb2[1]));
+        p8_conv<KH, PIPE>(acc, img, h3_w(p, lane, nt), lb2, hv != 0,
+                    std::make_integer_sequence<int, p8::PlanOf<KH>::P.nbat>{});
+        p += h3::kW + 2 * nn::kCh;
+        uint32_t pk[13][2][2];
+        const bool res = c & 1;
+#pragma unroll
+        for (int k = 0; k < 13; ++k) h3t_pack_one<false>(acc[k], pk[k], bbt, sct, skip[k], res, hmax);
+        __syncthreads();
+        p8_store(pk, img, est, h);
+        __syncthreads();
+    }
+    {  // heads: 1x1 convs as split MFMAs per tile (rows = (half, position), columns = value, policy
+       // planes 0 / 1), feature table [8][80] in LDS, then the MLPs (2 positions per wave)
+        const float* hp = p + nn::kValueF + nn::kPolicyF;
+        const f16x8* HB = reinterpret_cast<const f16x8*>(hp);
+        f16x8 hb[2][2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int pc = 0; pc < 2; ++pc) hb[m][pc] = HB[(m * 2 + pc) * 64 + lane];
+        const float hs = hp[2 * 2 * 64 * 4 + (n < 3 ? n : 0)];
+        HeadRegs hr;
+        heads_fetch(hr, p, lane);
+        f32x4 hacc[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            hacc[q] = f32x4{};
+            const int k = nt + 4 * q;
+            if (k < 13) {
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    // A operand: rows (half, position) = lane & 15 -> own half's slot of tile k
+                    const char* a = img + k * 2 * p8::kSlotB + (h ? p8::kSlotB : 0) + lb[m];
+                    const f16x8 ah = *reinterpret_cast<const f16x8*>(a);
+                    const f16x8 al = *reinterpret_cast<const f16x8*>(a + p8::kPlaneB);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, hb[m][0], hacc[q], 0, 0, 0);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][0], hacc[q], 0, 0, 0);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][1], hacc[q], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();  // the image is no longer read: its first 2.5 KB become the feature table
+        float* feat = reinterpret_cast<float*>(img);  // [8 positions][80]
+        const float hbias = n == 0 ? p[64] : n == 1 ? p[nn::kValueF + 128] : p[nn::kValueF + 129];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = nt + 4 * q;
+            if (k < 13 && n < 3)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = kq * 4 + r, sq = p8::kTileSq[k][row >> 3];  // C/D row = (half, position)
+                    const float v = __builtin_fmaf(hacc[q][r], hs, hbias);
+                    if (sq < 25) feat[(row & 7) * 80 + n * 25 + sq] = v > 0.0f ? v : 0.0f;
+                }
+        }
+        __syncthreads();
+        const float* fq[2] = {feat + nt * 80, feat + (nt + 4) * 80};
+        const int bq[2] = {b0 + nt, b0 + nt + 4};
+        heads_mlp_r<2>(hr, fq, bq, lane, B, policy, value);
+    }
+    if ((hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u) atomicOr(range_flag, 1u);  // an fp16 hi = inf
+}
+
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy, float* value,
                              hipStream_t st) {
     if (B <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
-    if (w.precision == OAZ_FP32_SPLIT16) {
+    if (w.precision == OAZ_FP32_SPLIT16 && w.x6_variant >= 20) {
+        if (!w.range_flag) return hipErrorInvalidValue;
+        const unsigned g8 = (unsigned)((B + p8::kP - 1) / p8::kP);
+        // measured 1.40 vs 1.25 ms (C3 batch): the two workgroups per CU overlap, but a single wave
+        // per SIMD per workgroup leaves the MFMA pipe waiting on its own LDS reads (69 % busy, as
+        // k_nn_h3), and the paired tiles add 10 % conv and 43 % first-layer MFMA work
+        auto k = k_nn_p8<4, 1>;
+        hipLaunchKernelGGL(k, dim3(g8), dim3(256), 0, st, s, B, w.blob, w.blocks, policy, value, w.range_flag);
+    } else if (w.precision == OAZ_FP32_SPLIT16) {
         if (!w.range_flag) return hipErrorInvalidValue;
         // default: 8 waves, uneven 15 / 10 square split, batches of <= 4 squares, transposed C/D
         // tiles (TR epilogue); OAZ_NN_X6_V selects the A/B alternatives (DESIGN.md perf log)
