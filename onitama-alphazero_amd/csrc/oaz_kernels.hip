@@ -11,6 +11,9 @@
 // The f64 PUCT arithmetic is the reference's expression order, compiled with
 // -ffp-contract=off; sqrt(N) comes from a host-built table so every bit matches the oracle.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include <utility>
 
 #include "oaz_device.h"
 #include "oaz_kernels.h"
@@ -433,6 +436,304 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup(TreeView t, const oaz_
     }
 }
 
+// ---- segmented tree kernels: FOUR GAMES PER WAVE (16-lane segments) ----------------------
+// The select / expand-backup walks are chains of dependent memory round trips (one per tree
+// level), so their time is the number of such chains in flight per CU, not bandwidth: with one
+// game per wave a CU holds 32 games, with one per 16-lane segment 128. A segment is active or
+// idle as a whole (every branch condition below is uniform over its 16 lanes), and segment-wide
+// reductions use DPP row operations (quad swaps, half-row and row mirrors), which never leave
+// the 16-lane row. Results are bit-identical to k_select / k_expand_backup (same f64 expressions,
+// same sequential fold and summation orders); tests/test_gpu.py compares whole trees to the oracle.
+constexpr int kSegLanes = 16;
+__device__ __forceinline__ int seg_lane() { return (int)(threadIdx.x & 15); }
+__device__ __forceinline__ int seg_base() { return (int)(threadIdx.x & 63) & ~15; }
+__device__ __forceinline__ uint32_t seg_game() {
+    return (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 4 + ((threadIdx.x >> 4) & 3);
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
+// argmax of (key, idx) over the segment, the larger idx winning among equal keys (max_by)
+template <int CTRL>
+__device__ __forceinline__ void seg_amax_step(int64_t& key, int& idx) {
+    const uint64_t kb = (uint64_t)key;
+    const uint32_t lo = dpp_u32<CTRL>((uint32_t)kb), hi = dpp_u32<CTRL>((uint32_t)(kb >> 32));
+    const int64_t ok = (int64_t)(((uint64_t)hi << 32) | lo);
+    const int oi = (int)dpp_u32<CTRL>((uint32_t)idx);
+    if (ok > key || (ok == key && oi > idx)) {
+        key = ok;
+        idx = oi;
+    }
+}
+__device__ __forceinline__ int seg_argmax_last(int64_t key, int idx) {
+    seg_amax_step<0xB1>(key, idx);   // quad_perm [1,0,3,2]
+    seg_amax_step<0x4E>(key, idx);   // quad_perm [2,3,0,1]
+    seg_amax_step<0x141>(key, idx);  // row_half_mirror
+    seg_amax_step<0x140>(key, idx);  // row_mirror
+    return idx;
+}
+__device__ __forceinline__ uint32_t seg_or(uint32_t v) {
+    v |= dpp_u32<0xB1>(v);
+    v |= dpp_u32<0x4E>(v);
+    v |= dpp_u32<0x141>(v);
+    v |= dpp_u32<0x140>(v);
+    return v;
+}
+__device__ __forceinline__ uint32_t seg_incl_scan(uint32_t v) {  // row_shr 1, 2, 4, 8 (zero fill)
+    v += dpp_u32<0x111>(v);
+    v += dpp_u32<0x112>(v);
+    v += dpp_u32<0x114>(v);
+    v += dpp_u32<0x118>(v);
+    return v;
+}
+__device__ __forceinline__ double shfl_f64(double v, int src) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)b, src), hi = (uint32_t)__shfl((int)(uint32_t)(b >> 32), src);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <class T>
+__device__ __forceinline__ T pick3(int c, const T& a, const T& b, const T& d) {
+    return c == 0 ? a : c == 1 ? b : d;
+}
+
+// lane n of every 16-lane row, to the whole row (DPP row_newbcast)
+template <int N>
+__device__ __forceinline__ double bcast_f64(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x150 + N, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x150 + N, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// comparison j of the root fold (k_select): operand a = the running best with comparison j's
+// fresh draw, operand b = child j with its own draw
+template <int J>
+__device__ __forceinline__ void fold_step(int& acc, double& qa, double& ba, double& sa, int K, const double (&na)[3],
+                                          const double (&ubl)[3], const double (&q)[3], const double (&base)[3],
+                                          const double (&sq)[3], const SearchParams& prm) {
+    constexpr int c = J >> 4, n = J & 15;
+    const double ua = qa + prm.c_puct * (ba + bcast_f64<n>(na[c]) * prm.eps) * sa;
+    const double ub = bcast_f64<n>(ubl[c]);
+    const double qj = bcast_f64<n>(q[c]), bj = bcast_f64<n>(base[c]), sj = bcast_f64<n>(sq[c]);
+    if (J < K && !(total_key(ua) > total_key(ub))) {
+        acc = J;
+        qa = qj;
+        ba = bj;
+        sa = sj;
+    }
+}
+template <int... I>
+__device__ __forceinline__ void fold_steps(int& acc, double& qa, double& ba, double& sa, int K, int Kmax,
+                                           const double (&na)[3], const double (&ubl)[3], const double (&q)[3],
+                                           const double (&base)[3], const double (&sq)[3], const SearchParams& prm,
+                                           std::integer_sequence<int, I...>) {
+    // j = I + 1 = 1 .. 39; stop once every segment's K is passed (wave-uniform)
+    ((I + 1 < Kmax ? (fold_step<I + 1>(acc, qa, ba, sa, K, na, ubl, q, base, sq, prm), true) : false) && ...);
+}
+
+// k_select with 16 lanes per game: lane sl holds children j = 16c + sl (c < 3, K <= 40).
+__global__ void __launch_bounds__(kBlock) k_select_seg(TreeView t, const oaz_state* __restrict__ roots,
+                                                       const uint8_t* __restrict__ active,
+                                                       const float* __restrict__ noise, SearchParams prm) {
+    const uint32_t g = seg_game();
+    const int sl = seg_lane(), sb = seg_base();
+    const bool on = g < t.G && !(active && active[g] != 1);
+    const bool fold_mode = prm.train_noise && noise;
+    oaz_node* T = t.nodes + (size_t)(on ? g : 0) * t.cap;
+    uint32_t* path = t.path + (size_t)(on ? g : 0) * t.pathcap;
+    oaz_state s = load_state(&roots[on ? g : 0]);
+    int color = s.to_move & 1;
+    NodeRegs nd = load_node(&T[0]);
+    uint32_t node = 0, depth = 0;
+    if (on && sl == 0) path[0] = 0;
+    bool stuck = false;
+    bool go = on && (node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2);
+    while (__builtin_amdgcn_read_exec() && __ballot(go)) {  // some segment is still walking
+        const int K = go ? node_nch(nd.misc) : 0;
+        if (go && K == 0) {  // reference would panic in select (Q6): stop here, treat as a leaf
+            stuck = true;
+            go = false;
+        }
+        NodeRegs ch[3];
+        double q[3], sq[3];
+        int64_t bkey = INT64_MIN;
+        int bidx = sl;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int j = 16 * c + sl;
+            ch[c].W = 0.0;
+            ch[c].P = 0.0;
+            ch[c].N = 0;
+            ch[c].first = 0;
+            ch[c].misc = 0;
+            if (go && j < K) ch[c] = load_node(&T[nd.first + j]);
+        }
+        const double sqn = go ? t.sqrt_tab[nd.N] : 0.0;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int j = 16 * c + sl;
+            q[c] = ch[c].N ? ch[c].W / (double)ch[c].N : 0.0;
+            sq[c] = sqn / (double)(ch[c].N + 1);
+            if (go && j < K && !(depth == 0 && fold_mode)) {
+                const double u = q[c] + prm.c_puct * ch[c].P * sq[c];  // mcts_arena.rs:204-207
+                const int64_t key = total_key(u);
+                if (key >= bkey) {  // ascending j: the last maximum
+                    bkey = key;
+                    bidx = j;
+                }
+            }
+        }
+        int best = 0;
+        if (depth == 0 && fold_mode) {
+            // root with noise: the sequential Iterator::max_by fold (see k_select), one segment
+            // at a time on wave-uniform v_readlane values
+            double base[3], ubl[3], na[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int j = 16 * c + sl;
+                double a = 0.0, b = 0.0;
+                if (go && j >= 1 && j < K) {
+                    a = (double)noise[(size_t)g * kNoiseStride + 2 * j];
+                    b = (double)noise[(size_t)g * kNoiseStride + 2 * j + 1];
+                }
+                na[c] = a;
+                base[c] = ch[c].P * (1.0 - prm.eps);
+                ubl[c] = q[c] + prm.c_puct * (base[c] + b * prm.eps) * sq[c];
+            }
+            // the four segments fold in parallel: child j's operands are broadcast within each
+            // 16-lane row by DPP row_newbcast (j compile-time: the fold is unrolled over j)
+            const int Kmax = max(max(__builtin_amdgcn_readlane(K, 0), __builtin_amdgcn_readlane(K, 16)),
+                                 max(__builtin_amdgcn_readlane(K, 32), __builtin_amdgcn_readlane(K, 48)));
+            int acc = 0;
+            double qa = bcast_f64<0>(q[0]), ba = bcast_f64<0>(base[0]), sa = bcast_f64<0>(sq[0]);
+            fold_steps(acc, qa, ba, sa, K, Kmax, na, ubl, q, base, sq, prm, std::make_integer_sequence<int, 39>{});
+            best = acc;
+        } else {
+            best = seg_argmax_last(bkey, bidx);
+        }
+        // the chosen child's node from the lane that holds it (chunk best >> 4 of lane best & 15)
+        const int bc = best >> 4, src = sb + (best & 15);
+        NodeRegs c;
+        c.W = shfl_f64(pick3(bc, ch[0].W, ch[1].W, ch[2].W), src);
+        c.P = shfl_f64(pick3(bc, ch[0].P, ch[1].P, ch[2].P), src);
+        c.N = (uint32_t)__shfl((int)pick3(bc, ch[0].N, ch[1].N, ch[2].N), src);
+        c.first = (uint32_t)__shfl((int)pick3(bc, ch[0].first, ch[1].first, ch[2].first), src);
+        c.misc = (uint32_t)__shfl((int)pick3(bc, ch[0].misc, ch[1].misc, ch[2].misc), src);
+        if (go) {
+            const uint32_t cidx = nd.first + (uint32_t)best;
+            const int res = make_move(s, mv_from(c.misc), mv_to(c.misc), mv_piece(c.misc), mv_slot(c.misc), color);
+            color ^= 1;  // game_state.player_color.switch()
+            if (is_win(res)) {
+                c.misc |= 2u << 24;
+                if (sl == 0) *flags_ptr(&T[cidx]) = (uint8_t)(node_flags(c.misc));
+            }
+            ++depth;
+            if (sl == 0 && depth < t.pathcap) path[depth] = cidx;
+            node = cidx;
+            nd = c;
+            go = (node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2);
+        }
+    }
+    s.to_move = (uint8_t)color;
+    if (on && sl == 0) {
+        store_state(&t.leaf_state[g], s);
+        t.leaf[g] = node;
+        t.depth[g] = depth;
+        uint64_t* st = t.stats + (size_t)g * GS_COUNT;
+        st[GS_SIMS] += 1;
+        st[GS_DEPTH] += depth;
+        if (stuck) st[GS_STUCK] += 1;
+    }
+}
+
+// k_expand_backup with 16 lanes per game: lane sl generates the moves of (card, from) combos
+// 4 sl .. 4 sl + 3 (combo = card * 25 + from, the reference order), one segment scan places them.
+__global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const oaz_state* __restrict__ roots,
+                                                              const uint8_t* __restrict__ active,
+                                                              const float* __restrict__ policy,
+                                                              const float* __restrict__ value) {
+    const uint32_t g = seg_game();
+    const int sl = seg_lane();
+    if (g >= t.G) return;                  // whole segments (G is not a multiple of 4 only at the end)
+    if (active && active[g] != 1) return;  // uniform over the segment
+    oaz_node* T = t.nodes + (size_t)g * t.cap;
+    const uint32_t* path = t.path + (size_t)g * t.pathcap;
+    const oaz_state s = load_state(&t.leaf_state[g]);
+    const uint32_t leaf = t.leaf[g], depth = t.depth[g];
+    const NodeRegs nd = load_node(&T[leaf]);
+    uint64_t* st = t.stats + (size_t)g * GS_COUNT;
+    const float* pol = policy + (size_t)g * 50;
+
+    if (!(node_flags(nd.misc) & 3)) {
+        const int color = s.to_move & 1;
+        const uint32_t pawns = s.pawns[color], king = s.kings[color], own = pawns | king;
+        uint32_t mask[4];
+        uint32_t cnt = 0, r0 = 0, r1 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int cb = 4 * sl + i, k = cb >= 25 ? 1 : 0, from = cb - 25 * k;
+            uint32_t m = 0;
+            if (cb < 50 && (own & sq_bit(from))) m = c_attack.m[color][s.cards[(color ? 2 : 0) + k] & 15][from] & ~own;
+            mask[i] = m;
+            cnt += (uint32_t)__popc(m);
+            if (k) r1 |= m; else r0 |= m;
+        }
+        const uint32_t incl = seg_incl_scan(cnt);
+        const uint32_t K = (uint32_t)__shfl((int)incl, seg_base() + 15);
+        const uint32_t row0 = seg_or(r0), row1 = seg_or(r1);
+        // per-card renormalisation; sequential f64 sums in square order (mcts_arena.rs:288-301)
+        double sum0 = 0.0, sum1 = 0.0;
+        for (int sq = 0; sq < 25; ++sq) {
+            if (row0 & sq_bit(sq)) sum0 += (double)pol[sq];
+            if (row1 & sq_bit(sq)) sum1 += (double)pol[25 + sq];
+        }
+        const uint32_t base = t.n_nodes[g];
+        uint32_t o = incl - cnt;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int cb = 4 * sl + i, k = cb >= 25 ? 1 : 0, from = cb - 25 * k;
+            const int slot = (color ? 2 : 0) + k;
+            const int piece = (pawns & sq_bit(from)) ? OAZ_PAWN : OAZ_KING;
+            const double rs = k ? sum1 : sum0;
+            uint32_t mm = mask[i];
+            while (mm) {
+                const int to = __clz(mm);
+                mm &= ~sq_bit(to);
+                double p = (double)pol[k * 25 + to];
+                if (rs > 0.0) p = p / rs;
+                store_fresh_node(&T[base + o], p, pack_move(from, to, slot, piece));
+                ++o;
+            }
+        }
+        if (sl == 0) {
+            t.n_nodes[g] = base + K;
+            T[leaf].first = base;
+            T[leaf].nch = (uint8_t)K;
+            T[leaf].flags = 1;
+            st[GS_EXPANSIONS] += 1;
+            st[GS_CHILDREN] += K;
+            if (base + K > st[GS_MAXNODES]) st[GS_MAXNODES] = base + K;
+        }
+    }
+    const int res = current_state(s);
+    double r;
+    if (is_win(res)) {
+        const int root_color = roots[g].to_move & 1;
+        const int pc = depth == 0 ? root_color : (root_color ^ (int)((depth - 1) & 1));
+        r = reward(res, pc);
+        if (sl == 0) st[GS_TERMINAL] += 1;
+    } else {
+        r = (double)value[g];
+    }
+    const uint32_t plen = depth < t.pathcap ? depth : t.pathcap - 1;
+    for (uint32_t k = (uint32_t)sl; k <= plen; k += kSegLanes) {
+        const uint32_t n = path[k];
+        const double rk = ((depth - k) & 1) ? -r : r;
+        T[n].N += 1;
+        T[n].W += rk;
+    }
+}
+
 // calculate_priors (mcts_arena.rs:104-124) + best child (87-94) for every root.
 __device__ __forceinline__ void root_pi_best(const oaz_node* T, float* pi_out /*50, may be null*/,
                                              float& pi_lane, int& best_lane, int& K_out,
@@ -646,9 +947,18 @@ hipError_t launch_tree_reset(const TreeView& t, hipStream_t st) {
     hipLaunchKernelGGL(k_tree_reset, dim3(thread_grid(t.G, kBlock)), dim3(kBlock), 0, st, t);
     return hipGetLastError();
 }
+// OAZ_TREE_SEG=0 selects the one-game-per-wave kernels (the default is four games per wave)
+static bool tree_seg() {
+    static const bool v = !(getenv("OAZ_TREE_SEG") && getenv("OAZ_TREE_SEG")[0] == '0');
+    return v;
+}
 hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                          const float* noise, SearchParams p, hipStream_t st) {
-    hipLaunchKernelGGL(k_select, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, roots, active, noise, p);
+    if (tree_seg())
+        hipLaunchKernelGGL(k_select_seg, dim3(wave_grid((t.G + 3) / 4)), dim3(kBlock), 0, st, t, roots, active, noise,
+                           p);
+    else
+        hipLaunchKernelGGL(k_select, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, roots, active, noise, p);
     return hipGetLastError();
 }
 hipError_t launch_root_noise(const oaz_state* roots, const uint8_t* active, const uint64_t* game_id,
@@ -660,8 +970,12 @@ hipError_t launch_root_noise(const oaz_state* roots, const uint8_t* active, cons
 }
 hipError_t launch_expand_backup(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                                 const float* policy, const float* value, hipStream_t st) {
-    hipLaunchKernelGGL(k_expand_backup, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, roots,
-                       active, policy, value);
+    if (tree_seg())
+        hipLaunchKernelGGL(k_expand_backup_seg, dim3(wave_grid((t.G + 3) / 4)), dim3(kBlock), 0, st, t, roots, active,
+                           policy, value);
+    else
+        hipLaunchKernelGGL(k_expand_backup, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, roots, active, policy,
+                           value);
     return hipGetLastError();
 }
 hipError_t launch_search_finalize(const TreeView& t, const oaz_state* roots, oaz_move* out_move,
