@@ -505,17 +505,35 @@ __device__ __forceinline__ double bcast_f64(double v) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x150 + N, 0xF, 0xF, false);
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+// Root fold operands of this lane's child in one chunk: q, base = P (1 - eps), sq = sqrt(N_parent)
+// / (N + 1), nae = (operand-a draw) * eps and kub = total_key(operand b) -- everything of
+// comparison j that does not depend on the running best, computed in parallel per child.
+struct FoldCh {
+    double q, base, sq, nae, kub;
+};
+__device__ __forceinline__ FoldCh fold_chunk(const NodeRegs& ch, float na, float nb, double sqn, const SearchParams& prm) {
+    FoldCh f;
+    f.q = ch.N ? ch.W / (double)ch.N : 0.0;
+    f.sq = sqn / (double)(ch.N + 1);
+    f.base = ch.P * (1.0 - prm.eps);
+    f.nae = (double)na * prm.eps;
+    const double ub = f.q + prm.c_puct * (f.base + (double)nb * prm.eps) * f.sq;
+    f.kub = __builtin_bit_cast(double, total_key(ub));  // the key, carried in a double
+    return f;
+}
 // comparison j of the root fold (k_select): operand a = the running best with comparison j's
-// fresh draw, operand b = child j with its own draw
+// fresh draw, operand b = child j with its own draw. A chunk's operands are built when the fold
+// reaches it (j = 16, 32), so only one chunk's are live at a time.
 template <int J>
-__device__ __forceinline__ void fold_step(int& acc, double& qa, double& ba, double& sa, int K, const double (&na)[3],
-                                          const double (&ubl)[3], const double (&q)[3], const double (&base)[3],
-                                          const double (&sq)[3], const SearchParams& prm) {
+__device__ __forceinline__ void fold_step(int& acc, double& qa, double& ba, double& sa, int K, FoldCh& f,
+                                          const NodeRegs (&ch)[3], const float (&na)[3], const float (&nb)[3],
+                                          double sqn, const SearchParams& prm) {
     constexpr int c = J >> 4, n = J & 15;
-    const double ua = qa + prm.c_puct * (ba + bcast_f64<n>(na[c]) * prm.eps) * sa;
-    const double ub = bcast_f64<n>(ubl[c]);
-    const double qj = bcast_f64<n>(q[c]), bj = bcast_f64<n>(base[c]), sj = bcast_f64<n>(sq[c]);
-    if (J < K && !(total_key(ua) > total_key(ub))) {
+    if constexpr (n == 0) f = fold_chunk(ch[c], na[c], nb[c], sqn, prm);
+    const double ua = qa + prm.c_puct * (ba + bcast_f64<n>(f.nae)) * sa;
+    const int64_t kb = __builtin_bit_cast(int64_t, bcast_f64<n>(f.kub));
+    const double qj = bcast_f64<n>(f.q), bj = bcast_f64<n>(f.base), sj = bcast_f64<n>(f.sq);
+    if (J < K && !(total_key(ua) > kb)) {
         acc = J;
         qa = qj;
         ba = bj;
@@ -523,16 +541,19 @@ __device__ __forceinline__ void fold_step(int& acc, double& qa, double& ba, doub
     }
 }
 template <int... I>
-__device__ __forceinline__ void fold_steps(int& acc, double& qa, double& ba, double& sa, int K, int Kmax,
-                                           const double (&na)[3], const double (&ubl)[3], const double (&q)[3],
-                                           const double (&base)[3], const double (&sq)[3], const SearchParams& prm,
-                                           std::integer_sequence<int, I...>) {
+__device__ __forceinline__ int root_fold(int K, int Kmax, const NodeRegs (&ch)[3], const float (&na)[3],
+                                         const float (&nb)[3], double sqn, const SearchParams& prm,
+                                         std::integer_sequence<int, I...>) {
+    FoldCh f = fold_chunk(ch[0], na[0], nb[0], sqn, prm);
+    int acc = 0;
+    double qa = bcast_f64<0>(f.q), ba = bcast_f64<0>(f.base), sa = bcast_f64<0>(f.sq);
     // j = I + 1 = 1 .. 39; stop once every segment's K is passed (wave-uniform)
-    ((I + 1 < Kmax ? (fold_step<I + 1>(acc, qa, ba, sa, K, na, ubl, q, base, sq, prm), true) : false) && ...);
+    ((I + 1 < Kmax ? (fold_step<I + 1>(acc, qa, ba, sa, K, f, ch, na, nb, sqn, prm), true) : false) && ...);
+    return acc;
 }
 
 // k_select with 16 lanes per game: lane sl holds children j = 16c + sl (c < 3, K <= 40).
-__global__ void __launch_bounds__(kBlock) k_select_seg(TreeView t, const oaz_state* __restrict__ roots,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) k_select_seg(TreeView t, const oaz_state* __restrict__ roots,
                                                        const uint8_t* __restrict__ active,
                                                        const float* __restrict__ noise, SearchParams prm) {
     const uint32_t g = seg_game();
@@ -555,7 +576,6 @@ __global__ void __launch_bounds__(kBlock) k_select_seg(TreeView t, const oaz_sta
             go = false;
         }
         NodeRegs ch[3];
-        double q[3], sq[3];
         int64_t bkey = INT64_MIN;
         int bidx = sl;
 #pragma unroll
@@ -569,53 +589,46 @@ __global__ void __launch_bounds__(kBlock) k_select_seg(TreeView t, const oaz_sta
             if (go && j < K) ch[c] = load_node(&T[nd.first + j]);
         }
         const double sqn = go ? t.sqrt_tab[nd.N] : 0.0;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const int j = 16 * c + sl;
-            q[c] = ch[c].N ? ch[c].W / (double)ch[c].N : 0.0;
-            sq[c] = sqn / (double)(ch[c].N + 1);
-            if (go && j < K && !(depth == 0 && fold_mode)) {
-                const double u = q[c] + prm.c_puct * ch[c].P * sq[c];  // mcts_arena.rs:204-207
-                const int64_t key = total_key(u);
-                if (key >= bkey) {  // ascending j: the last maximum
-                    bkey = key;
-                    bidx = j;
-                }
-            }
-        }
         int best = 0;
         if (depth == 0 && fold_mode) {
-            // root with noise: the sequential Iterator::max_by fold (see k_select), one segment
-            // at a time on wave-uniform v_readlane values
-            double base[3], ubl[3], na[3];
+            // root with noise: the sequential Iterator::max_by fold of k_select, every segment's
+            // fold state (acc, operand a) held uniformly across its 16 lanes; child j's operands
+            // are broadcast within each 16-lane row by DPP row_newbcast (j compile-time)
+            float na[3], nb[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const int j = 16 * c + sl;
-                double a = 0.0, b = 0.0;
+                na[c] = nb[c] = 0.0f;
                 if (go && j >= 1 && j < K) {
-                    a = (double)noise[(size_t)g * kNoiseStride + 2 * j];
-                    b = (double)noise[(size_t)g * kNoiseStride + 2 * j + 1];
+                    na[c] = noise[(size_t)g * kNoiseStride + 2 * j];
+                    nb[c] = noise[(size_t)g * kNoiseStride + 2 * j + 1];
                 }
-                na[c] = a;
-                base[c] = ch[c].P * (1.0 - prm.eps);
-                ubl[c] = q[c] + prm.c_puct * (base[c] + b * prm.eps) * sq[c];
             }
-            // the four segments fold in parallel: child j's operands are broadcast within each
-            // 16-lane row by DPP row_newbcast (j compile-time: the fold is unrolled over j)
             const int Kmax = max(max(__builtin_amdgcn_readlane(K, 0), __builtin_amdgcn_readlane(K, 16)),
                                  max(__builtin_amdgcn_readlane(K, 32), __builtin_amdgcn_readlane(K, 48)));
-            int acc = 0;
-            double qa = bcast_f64<0>(q[0]), ba = bcast_f64<0>(base[0]), sa = bcast_f64<0>(sq[0]);
-            fold_steps(acc, qa, ba, sa, K, Kmax, na, ubl, q, base, sq, prm, std::make_integer_sequence<int, 39>{});
-            best = acc;
+            best = root_fold(K, Kmax, ch, na, nb, sqn, prm, std::make_integer_sequence<int, 39>{});
         } else {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int j = 16 * c + sl;
+                if (go && j < K) {
+                    const double q = ch[c].N ? ch[c].W / (double)ch[c].N : 0.0;
+                    const double sq = sqn / (double)(ch[c].N + 1);
+                    const double u = q + prm.c_puct * ch[c].P * sq;  // mcts_arena.rs:204-207
+                    const int64_t key = total_key(u);
+                    if (key >= bkey) {  // ascending j: the last maximum
+                        bkey = key;
+                        bidx = j;
+                    }
+                }
+            }
             best = seg_argmax_last(bkey, bidx);
         }
         // the chosen child's node from the lane that holds it (chunk best >> 4 of lane best & 15)
         const int bc = best >> 4, src = sb + (best & 15);
-        NodeRegs c;
-        c.W = shfl_f64(pick3(bc, ch[0].W, ch[1].W, ch[2].W), src);
-        c.P = shfl_f64(pick3(bc, ch[0].P, ch[1].P, ch[2].P), src);
+        NodeRegs c;  // (the walk reads only N, first and misc of the node it descends to)
+        c.W = 0.0;
+        c.P = 0.0;
         c.N = (uint32_t)__shfl((int)pick3(bc, ch[0].N, ch[1].N, ch[2].N), src);
         c.first = (uint32_t)__shfl((int)pick3(bc, ch[0].first, ch[1].first, ch[2].first), src);
         c.misc = (uint32_t)__shfl((int)pick3(bc, ch[0].misc, ch[1].misc, ch[2].misc), src);
