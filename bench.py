@@ -122,6 +122,35 @@ def pmc_traffic(args, cfg):
             "raw_kb": kb, "note": "rocprofv3 --pmc, separate passes; FETCH_SIZE x2 (gfx950 wide-read correction)"}
 
 
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+
+
+def tree_roofline(kt, sims, expansions, depth, branching, cfg):
+    """Achieved HBM-side bytes of the tree kernels (tree-kernel GB/s vs HBM peak),
+    from the run's mean walk depth D and branching K and the 32-byte node layout:
+    select reads the root state (24 B) and node (32 B), per level K children (32 B each), sqrt(N)
+    (8 B) and writes a path entry (4 B), at the root K noise pairs (8 B each, training noise), and
+    writes the leaf record (24 + 8 B) and two counters (16 B); expand/backup reads the leaf record
+    and node (64 B) and the value (4 B), on expansion the policy row (200 B) and writes K fresh
+    children (32 B each) and the header (16 B), and per path node reads the path entry (4 B) and
+    updates N and W (12 B read + 12 B written)."""
+    if not kt.select_n or not kt.expand_n:
+        return None
+    D, K = depth, branching
+    per_launch = sims / kt.select_n
+    noise = 8.0 * K if cfg.get("noise", True) else 0.0
+    sel = 24 + 32 + D * (32 * K + 8 + 4) + noise + 32 + 16
+    exp = 64 + 4 + (expansions / max(1, sims)) * (200 + 32 * K + 16) + (D + 1) * (4 + 24)
+    out = {"bound": "latency (one dependent HBM round trip per tree level; 4 games per wave)",
+           "peak_GBps": HBM_PEAK_GBPS, "sims_per_launch": per_launch}
+    for name, ms, n, b in (("select", kt.select_ms, kt.select_n, sel), ("expand_backup", kt.expand_ms, kt.expand_n, exp)):
+        t = ms / n * 1e-3
+        gbps = per_launch * b / t / 1e9
+        out[name] = {"avg_launch_us": t * 1e6, "algorithmic_bytes_per_sim": b, "achieved_GBps": gbps,
+                     "frac": gbps / HBM_PEAK_GBPS}
+    return out
+
+
 def cpu_baseline(cfg, seconds, threads):
     """Reference-equivalent CPU baseline: the C restatement (oracle) playing self-play with the
     reference's execution shape — one game per worker thread, sequential search, one batch-1
@@ -477,6 +506,7 @@ def main():
                                        "fp32_split": "BF16 dense MFMA peak / 6 products per fp32 MAC",
                                        "fp32_split16": "FP16 dense MFMA peak / 3 products per fp32 MAC"}[cfg["precision"]],
                          "frac_of_fp32_mfma_peak": achieved / PEAK_TFLOPS["fp32"]},
+            "tree_kernels": tree_roofline(kt, sims, expansions, depth, branching, cfg),
             "allgather": allgather,
         }
         if not args.no_cpu_baseline and world == 1:

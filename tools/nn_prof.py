@@ -12,12 +12,12 @@ from onitama_az import _abi  # noqa: E402
 from onitama_az.engine import Engine  # noqa: E402
 from onitama_az.weights import random_weights  # noqa: E402
 
-PREC = {"fp32": _abi.FP32, "bf16": _abi.BF16, "fp32x6": _abi.FP32_SPLIT}
+PREC = {"fp32": _abi.FP32, "bf16": _abi.BF16, "fp32x6": _abi.FP32_SPLIT, "fp32h3": _abi.FP32_SPLIT16}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--precision", default="fp32x6", choices=sorted(PREC))
+    ap.add_argument("--precision", default="fp32h3", choices=sorted(PREC))
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--blocks", type=int, default=3)
     ap.add_argument("--launches", type=int, default=3)
