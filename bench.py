@@ -125,7 +125,7 @@ def pmc_traffic(args, cfg):
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 
-def tree_roofline(kt, sims, expansions, depth, branching, cfg):
+def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg):
     """Achieved HBM-side bytes of the tree kernels (tree-kernel GB/s vs HBM peak),
     from the run's mean walk depth D and branching K and the 32-byte node layout:
     select reads the root state (24 B) and node (32 B), per level K children (32 B each), sqrt(N)
@@ -137,7 +137,7 @@ def tree_roofline(kt, sims, expansions, depth, branching, cfg):
     if not kt.select_n or not kt.expand_n:
         return None
     D, K = depth, branching
-    per_launch = sims / kt.select_n
+    per_launch = sims / max(1, sim_steps)  # games per select / expand launch
     noise = 8.0 * K if cfg.get("noise", True) else 0.0
     sel = 24 + 32 + D * (32 * K + 8 + 4) + noise + 32 + 16
     exp = 64 + 4 + (expansions / max(1, sims)) * (200 + 32 * K + 16) + (D + 1) * (4 + 24)
@@ -427,7 +427,9 @@ def main():
     barrier_sync()
     st0 = eng.selfplay_stats()
     eng.kernel_times_reset()
-    eng.set_timing(True)
+    # HIP events around the kernels of every 8th simulation step: an event pair around every launch
+    # costs ~2 % of the step (measured), sampling keeps the live per-kernel averages nearly free
+    eng.set_timing(int(os.environ.get("OAZ_BENCH_TIMING_EVERY", "8")))
     barrier_sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -463,6 +465,7 @@ def main():
                      "backend": ("gloo (rehearsal)" if rehearse else "nccl(RCCL)") if world > 1 else "local"}
 
     if rank == 0:
+        sims_steps = cfg["sims"]  # simulation steps (select -> NN -> expand launches) per bench step
         nn_avg_ms = kt.nn_ms / max(1, kt.nn_n)
         flops_launch = FLOP_PER_SIM[cfg["blocks"]] * (kt.nn_samples / max(1, kt.nn_n))
         achieved = flops_launch / (nn_avg_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
@@ -491,9 +494,13 @@ def main():
             "sims_per_s_per_gpu": sims_all / T / world, "stagger": stagger,
             "games_per_s": games_all / T, "plies_per_s": plies_all / T,
             "true_expansions_per_s": exp_all / T, "mean_select_depth": depth, "mean_branching": branching,
-            "kernel_ms_per_step": {"select": kt.select_ms / args.steps, "nn": kt.nn_ms / args.steps,
-                                   "expand_backup": kt.expand_ms / args.steps, "move": kt.finalize_ms / args.steps,
-                                   "root_noise_stream2": kt.noise_ms / args.steps},
+            "kernel_ms_per_step": {
+                "select": kt.select_ms / max(1, kt.select_n) * sims_steps,
+                "nn": kt.nn_ms / max(1, kt.nn_n) * sims_steps,
+                "expand_backup": kt.expand_ms / max(1, kt.expand_n) * sims_steps,
+                "move": kt.finalize_ms / args.steps, "root_noise_stream2": kt.noise_ms / args.steps},
+            "kernel_timing": "HIP events around the kernels of every %s-th simulation step (per-kernel means x "
+                             "simulation steps per bench step)" % os.environ.get("OAZ_BENCH_TIMING_EVERY", "8"),
             "roofline": {"bound": "mfma", "kernel": NN_KERNEL[cfg["precision"]],
                          "achieved": achieved, "peak": PEAK_TFLOPS[cfg["precision"]], "unit": "TFLOP/s",
                          "frac": achieved / PEAK_TFLOPS[cfg["precision"]],
@@ -506,7 +513,7 @@ def main():
                                        "fp32_split": "BF16 dense MFMA peak / 6 products per fp32 MAC",
                                        "fp32_split16": "FP16 dense MFMA peak / 3 products per fp32 MAC"}[cfg["precision"]],
                          "frac_of_fp32_mfma_peak": achieved / PEAK_TFLOPS["fp32"]},
-            "tree_kernels": tree_roofline(kt, sims, expansions, depth, branching, cfg),
+            "tree_kernels": tree_roofline(kt, sims, args.steps * sims_steps, expansions, depth, branching, cfg),
             "allgather": allgather,
         }
         if not args.no_cpu_baseline and world == 1:

@@ -567,6 +567,8 @@ struct oaz_engine {
     uint64_t quota = 0;
     // timing
     bool timing = false;
+    int timing_every = 1;     // time the kernels of every N-th simulation step (events cost ~2 % each)
+    bool timing_skip = false; // run_sims: this simulation step is not sampled
     std::vector<TimedLaunch> pending;
     std::vector<hipEvent_t> pool;
     oaz_kernel_times times{};
@@ -658,7 +660,7 @@ static void accumulate(oaz_engine* e, const TimedLaunch& p, float ms) {
 template <class F>
 static int timed(oaz_engine* e, int kind, uint32_t samples, F&& launch, hipStream_t st = nullptr) {
     if (!st) st = e->stream;
-    if (!e->timing) {
+    if (!e->timing || e->timing_skip) {
         HIP_TRY(launch());
         return 0;
     }
@@ -840,7 +842,9 @@ extern "C" int oaz_sync(oaz_engine* e) {
 
 extern "C" int oaz_set_timing(oaz_engine* e, int enable) {
     if (!e) return oaz_set_err(OAZ_ERR_ARG, "set_timing: null");
+    if (enable < 0) return oaz_set_err(OAZ_ERR_ARG, "set_timing: enable=%d < 0", enable);
     e->timing = enable != 0;
+    e->timing_every = enable > 1 ? enable : 1;
     return 0;
 }
 
@@ -946,6 +950,7 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
     const uint32_t nchunks = (sims + kNoiseChunk - 1) / kNoiseChunk;
     auto produce = [&](uint32_t c) -> int {
         if (c >= 2) HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[c & 1], 0));
+        e->timing_skip = false;  // every noise launch is timed (once per chunk)
         const uint32_t s0 = c * kNoiseChunk, n = sims - s0 < kNoiseChunk ? sims - s0 : kNoiseChunk;
         float* buf = e->noise + (c & 1) * slot_elems;
         if (int rc = timed(e, 4, t.G * n, [&] {
@@ -985,6 +990,8 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
         }
         const uint32_t s0 = c * kNoiseChunk, s1 = s0 + kNoiseChunk < sims ? s0 + kNoiseChunk : sims;
         for (uint32_t s = s0; s < s1; ++s) {
+            // sampled steps sit mid-chunk: a chunk's first select also waits for its noise
+            e->timing_skip = e->timing_every > 1 && s % (uint32_t)e->timing_every != (uint32_t)e->timing_every / 2;
             for (int h = 0; h < nh; ++h) {
                 const TreeView& th = tv[h];
                 const size_t go = g0[h];
@@ -1014,6 +1021,7 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
         }
         if (noise) HIP_TRY(hipEventRecord(e->ev_consumed[c & 1], e->stream));
     }
+    e->timing_skip = false;
     if (split) {
         HIP_TRY(hipEventRecord(e->ev_join, e->stream3));
         HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));

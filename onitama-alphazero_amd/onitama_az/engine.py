@@ -128,8 +128,9 @@ class Engine:
         return out[: n.value], st
 
     # -- timing --
-    def set_timing(self, on: bool) -> None:
-        _abi.check(self._lib.oaz_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, on) -> None:
+        """False/True: off / every launch; an int N > 1: the kernels of every N-th simulation step."""
+        _abi.check(self._lib.oaz_set_timing(self._h, int(on) if not isinstance(on, bool) else (1 if on else 0)))
 
     def kernel_times(self) -> _abi.oaz_kernel_times:
         t = _abi.oaz_kernel_times()

@@ -493,8 +493,8 @@ static inline int64_t tkey(double x) {
  * Marsaglia-Tsang, small-shape boost u^(1/shape)). The reference's thread_rng is unseedable, so
  * noise parity is distributional; this restates the engine's f32 log-domain formulation
  * (oaz_device.h root_noise) op for op so that the engine's draws can be checked bit for bit:
- * log X = log G(1+a) + log(U)/a, eta = 1/(1 + exp(log Y - log X)), with polynomial log/exp
- * (+, -, *, /, sqrt and bit operations only; built with -ffp-contract=off). */
+ * the same Beta marginal by Johnk's method, with polynomial log/exp (+, -, *, / and bit
+ * operations only; built with -ffp-contract=off). */
 typedef struct {
     uint64_t seed, game;
     uint32_t c2;
@@ -528,44 +528,23 @@ static float nz_exp(float x) {
     return q * f_from_u((uint32_t)((int)k + 127) << 23);
 }
 
-static void gamma_ctr(const noise_key* k, uint32_t idx, uint32_t which, uint32_t t, uint32_t out[4]) {
-    uint32_t ctr[4] = {(uint32_t)k->game, (uint32_t)(k->game >> 32), k->c2,
-                       (idx << 12) | (which << 11) | (t & 2047u)};
-    orc_philox(k->seed, ctr, out);
-}
-
-/* log of a Gamma(shape >= 1) variate: Marsaglia-Tsang with a polar-method normal (words 0, 1)
- * and the acceptance uniform (word 2) of attempt t's Philox block */
-static float log_gamma_large(const noise_key* k, uint32_t idx, uint32_t which, float shape) {
-    const float d = shape - 0.333333333f;
-    const float c = 1.0f / sqrtf(9.0f * d);
-    for (uint32_t t = 0; t < 1000u; t++) {
-        uint32_t r[4];
-        gamma_ctr(k, idx, which, t, r);
-        const float v1 = 2.0f * nz_u(r[0]) - 1.0f, v2 = 2.0f * nz_u(r[1]) - 1.0f;
-        const float s = v1 * v1 + v2 * v2;
-        if (s >= 1.0f || s == 0.0f) continue;
-        const float x = v1 * sqrtf(-2.0f * nz_log(s) / s);
-        const float vc = 1.0f + c * x;
-        if (vc <= 0.0f) continue;
-        const float lv = 3.0f * nz_log(vc), v = vc * vc * vc;
-        const float u = nz_u(r[2]), x2 = x * x;
-        if (u < 1.0f - 0.0331f * (x2 * x2) || nz_log(u) < 0.5f * x2 + d * (1.0f - v + lv)) return nz_log(d) + lv;
-    }
-    return nz_log(d);
-}
-
-static float log_gamma(const noise_key* k, uint32_t idx, uint32_t which, float shape) {
-    if (shape >= 1.0f) return log_gamma_large(k, idx, which, shape);
-    uint32_t r[4];
-    gamma_ctr(k, idx, which, 2047u, r);
-    return log_gamma_large(k, idx, which, 1.0f + shape) + nz_log(nz_u(r[0])) / shape;
-}
-
+/* Beta(a, b), a = alpha, b = (K-1) alpha, by Johnk's method (exact): X = U^(1/a), Y = V^(1/b),
+ * accept X + Y <= 1, eta = X / (X + Y); in the log domain with products by the rounded
+ * reciprocals; attempt t uses Philox block (game lo, game hi, c2, idx << 12 | t), words 0, 1 then
+ * 2, 3 (oaz_device.h root_noise, op for op). */
 static double beta_noise(const noise_key* k, uint32_t idx, double alpha, int nchild) {
-    const float lx = log_gamma(k, idx, 0, (float)alpha);
-    const float ly = log_gamma(k, idx, 1, (float)alpha * (float)(nchild - 1));
-    return (double)(1.0f / (1.0f + nz_exp(ly - lx)));
+    const float a = (float)alpha;
+    const float ia = 1.0f / a, ib = 1.0f / (a * (float)(nchild - 1));
+    for (uint32_t t = 0; t < 1024u; t++) {
+        uint32_t r[4];
+        const uint32_t ctr[4] = {(uint32_t)k->game, (uint32_t)(k->game >> 32), k->c2, (idx << 12) | t};
+        orc_philox(k->seed, ctr, r);
+        const float lx = nz_log(nz_u(r[0])) * ia, ly = nz_log(nz_u(r[1])) * ib;
+        if (nz_exp(lx) + nz_exp(ly) <= 1.0f) return (double)(1.0f / (1.0f + nz_exp(ly - lx)));
+        const float lx2 = nz_log(nz_u(r[2])) * ia, ly2 = nz_log(nz_u(r[3])) * ib;
+        if (nz_exp(lx2) + nz_exp(ly2) <= 1.0f) return (double)(1.0f / (1.0f + nz_exp(ly2 - lx2)));
+    }
+    return (double)(1.0f / (float)nchild);
 }
 
 double orc_root_noise(uint64_t seed, uint64_t game_id, uint32_t c2, uint32_t draw, double alpha, int nchild) {

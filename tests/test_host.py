@@ -147,5 +147,7 @@ def test_root_noise_host_matches_oracle_and_distribution():
         assert 0.0 <= a <= 1.0
     for K in (2, 12, 40):
         xs = np.array([lib.oaz_root_noise(7, g, 0, s, 3, 0.03, K) for g in range(40) for s in range(100)])
-        se = np.sqrt((1.0 / K) * (1 - 1.0 / K) / (0.03 * K + 1) / len(xs))  # Beta variance
+        var = (1.0 / K) * (1 - 1.0 / K) / (0.03 * K + 1)  # Beta(a, b) variance, a + b = 0.03 K
+        se = np.sqrt(var / len(xs))
         assert abs(xs.mean() - 1.0 / K) < 5 * se, (K, xs.mean())
+        assert abs(xs.var() / var - 1.0) < 0.2, (K, xs.var(), var)
