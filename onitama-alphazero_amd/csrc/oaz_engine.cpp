@@ -403,6 +403,52 @@ static int pack_weights(const float* raw, int blocks, int precision, std::vector
         out.resize(base + h.size() / 2);
         memcpy(out.data() + base, h.data(), h.size() * sizeof(uint16_t));
         for (int k = 0; k < 4; ++k) out.push_back(inv[k]);
+        // k_nn_h3 first layer, constant planes on fp16 MFMA: A fragments [square][piece][N-tile][lane]
+        // f16x8, lane l supplying A[row co = 16nt + (l&15)][k = 8(l>>4) + e] = piece of s_co T[sq][k][co]
+        // (k < 17: the 16 card planes and the colour plane; T = the first-layer table above), then
+        // s[64] (applied to the fp32 bitboard weights in the kernel) and 1/s[64]; s = 2^k per output
+        // channel over the bitboard weights and the table
+        const float* r1 = raw;  // (fold advances its pointer)
+        FoldedConv f1 = fold(r1, 64, 21, 9);
+        std::vector<float> T((size_t)25 * 17 * 64);
+        for (int sq = 0; sq < 25; ++sq)
+            for (int c = 0; c < 17; ++c) {
+                const int plane = c < 16 ? 4 + c : 20;
+                for (int co = 0; co < 64; ++co) {
+                    double acc = 0.0;
+                    for (int t = 0; t < 9; ++t) {
+                        const int r = sq / 5 + t / 3 - 1, cc = sq % 5 + t % 3 - 1;
+                        if (r < 0 || r > 4 || cc < 0 || cc > 4) continue;
+                        acc += (double)f1.w[((size_t)co * 21 + plane) * 9 + t];
+                    }
+                    T[((size_t)sq * 17 + c) * 64 + co] = (float)acc;
+                }
+            }
+        float s1[64], inv1[64];
+        for (int co = 0; co < 64; ++co) {
+            float mx = 0.0f;
+            for (int pl = 0; pl < 4; ++pl)
+                for (int t = 0; t < 9; ++t) mx = fmaxf(mx, fabsf(f1.w[((size_t)co * 21 + pl) * 9 + t]));
+            for (int sq = 0; sq < 25; ++sq)
+                for (int c = 0; c < 17; ++c) mx = fmaxf(mx, fabsf(T[((size_t)sq * 17 + c) * 64 + co]));
+            s1[co] = pow2_scale(&mx, 1, 1, &inv1[co]);
+        }
+        std::vector<uint16_t> h1;
+        for (int sq = 0; sq < 25; ++sq)
+            for (int pcs = 0; pcs < 2; ++pcs)
+                for (int nt = 0; nt < 4; ++nt)
+                    for (int l = 0; l < 64; ++l)
+                        for (int e = 0; e < 8; ++e) {
+                            const int co = nt * 16 + (l & 15), k = 8 * (l >> 4) + e;
+                            uint16_t sp[2];
+                            split16_host(k < 17 ? T[((size_t)sq * 17 + k) * 64 + co] * s1[co] : 0.0f, sp);
+                            h1.push_back(sp[pcs]);
+                        }
+        const size_t b1 = out.size();
+        out.resize(b1 + h1.size() / 2);
+        memcpy(out.data() + b1, h1.data(), h1.size() * sizeof(uint16_t));
+        for (int co = 0; co < 64; ++co) out.push_back(s1[co]);
+        for (int co = 0; co < 64; ++co) out.push_back(inv1[co]);
     }
     if (out.size() != nn_packed_floats(blocks, precision)) return oaz_set_err(OAZ_ERR_STATE, "pack: size mismatch");
     if ((size_t)(p - raw) != oaz_weight_count(blocks, 64, 21)) return oaz_set_err(OAZ_ERR_STATE, "pack: raw size mismatch");

@@ -103,12 +103,14 @@ constexpr int kImageB = 2 * kPlaneB;           // 102,400 B
 constexpr int kLdsFloats = kImageB / 4 + nn::kWaves * nn::kScratch;  // 26,624 floats = 106,496 B
 constexpr size_t kW = 9 * 2 * 2 * 4 * 64 * 4;
 constexpr size_t kHeadB = 2 * 2 * 64 * 4 + 4;
+// first layer, constant planes: [square][piece][N-tile][lane] f16x8 of the scaled table, s[64], 1/s[64]
+constexpr size_t kL1C = 25 * 2 * 4 * 64 * 4 + 2 * nn::kCh;
 }  // namespace h3
 
 size_t nn_packed_floats(int blocks, int precision) {
     if (precision == OAZ_FP32_SPLIT16)
         return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) + nn::kValueF +
-               nn::kPolicyF + h3::kHeadB;
+               nn::kPolicyF + h3::kHeadB + h3::kL1C;
     const size_t w = precision == OAZ_BF16 ? nn::kW64h : precision == OAZ_FP32_SPLIT ? x6::kW : nn::kW64;
     return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (w + nn::kCh) + nn::kValueF + nn::kPolicyF +
            (precision == OAZ_FP32_SPLIT ? x6::kHeadB : 0);
@@ -1726,6 +1728,65 @@ __device__ __forceinline__ void epilogue_h3t_store(const uint32_t (&pk)[C::NS][2
     }
 }
 
+// k_nn_h3 (TR) first layer: the bitboard part as k_nn_x6 (exact fp32 16x16x4 MFMAs, weights scaled
+// by s per output channel: exact), the 17 constant planes as ONE fp16 K-step per square: A = the
+// scaled table T[sq] split hi / lo (two 16x16x32 MFMAs), B = the position's 0/1 plane indicators
+// (exact in fp16, the same for every square). 2 x 16 instead of 5 x 32 MFMA cycles per square.
+template <class C, int GRP>
+__device__ __forceinline__ void first_layer_h3t(f32x4 (&acc)[C::NS], const L1Regs<GRP>& R, const float* l1c,
+                                                uint32_t bb, int cinfo, int lane, int nt) {
+    constexpr int n = grp_n(GRP), kB = 4;  // squares per batch of A-fragment loads
+    const int kq = lane >> 4;
+    X6W A;
+    A.r = __builtin_amdgcn_make_buffer_rsrc((void*)l1c, (short)0, (int)(25 * 2 * 4 * 64 * 16), 0x00020000);
+    A.voff = (nt * 64 + lane) * 16;
+    auto ld = [&](int sq, int pc) {  // fragment [sq][pc][nt][lane]
+        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(A.r, A.voff, (sq * 2 + pc) * 4 * 64 * 16, 0));
+    };
+    f16x8 fa[2][kB][2];
+#pragma unroll
+    for (int q = 0; q < kB; ++q)
+        if (q < n) {
+            fa[0][q][0] = ld(grp_sq(GRP, q), 0);
+            fa[0][q][1] = ld(grp_sq(GRP, q), 1);
+        }
+    const float s = l1c[25 * 2 * 4 * 64 * 4 + nt * 16 + (lane & 15)];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < n; ++j) {
+            const int sq = grp_sq(GRP, j);
+            const int r = sq / 5 + t / 3 - 1, c = sq % 5 + t % 3 - 1;
+            if (r >= 0 && r < 5 && c >= 0 && c < 5) {
+                const float a = (float)((bb >> (31 - (r * 5 + c))) & 1u);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(R.w[t] * s, a, acc[j], 0, 0, 0);
+            }
+        }
+    const int c0 = cinfo & 15, c1 = (cinfo >> 4) & 15, blue = (cinfo >> 8) & 1;
+    f16x8 bc;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int k = 8 * kq + e;
+        bc[e] = (_Float16)(k < 16 ? ((k == c0 || k == c1) ? 1.0f : 0.0f) : (k == 16 ? (float)blue : 0.0f));
+    }
+#pragma unroll
+    for (int j0 = 0, b = 0; j0 < n; j0 += kB, b ^= 1) {
+        if (j0 + kB < n)
+#pragma unroll
+            for (int q = 0; q < kB; ++q)
+                if (j0 + kB + q < n) {
+                    fa[b ^ 1][q][0] = ld(grp_sq(GRP, j0 + kB + q), 0);
+                    fa[b ^ 1][q][1] = ld(grp_sq(GRP, j0 + kB + q), 1);
+                }
+#pragma unroll
+        for (int q = 0; q < kB; ++q)
+            if (j0 + q < n) {
+                acc[j0 + q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[b][q][0], bc, acc[j0 + q], 0, 0, 0);
+                acc[j0 + q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[b][q][1], bc, acc[j0 + q], 0, 0, 0);
+            }
+    }
+}
+
 // The whole forward for the waves of square group GRP.
 template <class C, int GRP>
 __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
@@ -1776,10 +1837,16 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};  // skip: finite for the fma in the epilogue
-        first_layer_x6<C, GRP>(acc, l1, blob + nn::kL1B + nn::kCh, bb, pinfo[i], lane, nt);
+        const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
+                           nn::kValueF + nn::kPolicyF + h3::kHeadB;
+        if constexpr (C::TR)
+            first_layer_h3t<C, GRP>(acc, l1, l1c, bb, pinfo[i], lane, nt);
+        else
+            first_layer_x6<C, GRP>(acc, l1, blob + nn::kL1B + nn::kCh, bb, pinfo[i], lane, nt);
         uint32_t pk[NS][2][2];
         if constexpr (C::TR) {
-            epilogue_h3t_pack<C, GRP, true>(acc, pk, bias1t, f32x4{1.0f, 1.0f, 1.0f, 1.0f}, skip, false, hmax);
+            const f32x4 inv1 = *reinterpret_cast<const f32x4*>(l1c + 25 * 2 * 4 * 64 * 4 + nn::kCh + cq);
+            epilogue_h3t_pack<C, GRP, true>(acc, pk, bias1t, inv1, skip, false, hmax);
             epilogue_h3t_store<C, GRP>(pk, img, eot);
         } else {
             epilogue_h3_pack<C, GRP>(acc, pk, bias1, 1.0f, skip, co, false, true, vmax);
