@@ -904,13 +904,16 @@ constexpr int8_t kSqOrder[25] = {0, 4, 20, 24, 1, 3, 21, 23, 6, 8, 12, 16, 18,
 // the younger fills its gaps, so equal halves leave the younger finishing alone.
 constexpr int8_t kSqOrderU[25] = {6, 7, 8, 11, 12, 13, 16, 17, 18, 0, 4, 20, 24, 2, 22,
                                   1, 3, 5, 10, 9, 14, 15, 19, 21, 23};
-// GRP 5 / 6: 16 / 9 squares (115 / 54 taps), same order with one more edge in the first group.
+// GRP 5 / 6: 16 / 9 squares (115 / 54 taps), same order with one more edge in the first group;
+// GRP 7 / 8: 17 / 8 (the default, measured 1-2 % faster than 15 / 10), GRP 9 / 10: 18 / 7.
 constexpr int grp_n(int grp) {
-    return grp == 0 ? nn::kTPW : grp == 1 ? 25 - nn::kTPW : grp == 3 ? 15 : grp == 4 ? 10 : grp == 5 ? 16 : grp == 6 ? 9 : 25;
+    return grp == 0 ? nn::kTPW : grp == 1 ? 25 - nn::kTPW : grp == 3 ? 15 : grp == 4 ? 10 : grp == 5 ? 16 : grp == 6 ? 9
+         : grp == 7 ? 17 : grp == 8 ? 8 : grp == 9 ? 18 : grp == 10 ? 7 : 25;
 }
 constexpr int grp_sq(int grp, int j) {
-    return grp == 2 ? j : grp >= 5 ? kSqOrderU[(grp - 5) * 16 + j] : grp >= 3 ? kSqOrderU[(grp - 3) * 15 + j]
-                                                                            : kSqOrder[grp * nn::kTPW + j];
+    return grp == 2 ? j : grp >= 9 ? kSqOrderU[(grp - 9) * 18 + j] : grp >= 7 ? kSqOrderU[(grp - 7) * 17 + j]
+         : grp >= 5 ? kSqOrderU[(grp - 5) * 16 + j]
+         : grp >= 3 ? kSqOrderU[(grp - 3) * 15 + j] : kSqOrder[grp * nn::kTPW + j];
 }
 
 // On-board squares of group GRP for tap T: the conv is straight-line code per (group, tap), with no
@@ -1053,7 +1056,7 @@ struct X6Cfg {
     static constexpr int PH = PH_;  // h3 + TR: square phases of the second (younger) group
     static constexpr int WAVES = WAVES_;
     static constexpr int UNEVEN = UNEVEN_;
-    static constexpr int NS = WAVES_ == 8 ? (UNEVEN_ == 2 ? 16 : UNEVEN_ ? 15 : nn::kTPW) : 25;  // tiles per wave
+    static constexpr int NS = WAVES_ == 8 ? (UNEVEN_ == 4 ? 18 : UNEVEN_ == 3 ? 17 : UNEVEN_ == 2 ? 16 : UNEVEN_ ? 15 : nn::kTPW) : 25;  // tiles per wave
     static constexpr int KH = KH_;
     static constexpr int PIPE = PIPE_;
     static constexpr int DBG = DBG_;
@@ -1456,7 +1459,7 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_x6(const oaz_state* __rest
     if constexpr (C::WAVES == 4) {
         nn_x6_body<C, 2>(states, B, blob, blocks, policy, value, lds);
     } else if constexpr (C::UNEVEN) {
-        constexpr int g0 = C::UNEVEN == 2 ? 5 : 3;
+        constexpr int g0 = C::UNEVEN == 4 ? 9 : C::UNEVEN == 3 ? 7 : C::UNEVEN == 2 ? 5 : 3;
         if ((threadIdx.x >> 8) == 0) {
             __builtin_amdgcn_s_setprio(1);
             nn_x6_body<C, g0>(states, B, blob, blocks, policy, value, lds);
@@ -1972,7 +1975,7 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __rest
     if constexpr (C::WAVES == 4) {
         nn_h3_body<C, 2>(states, B, blob, blocks, policy, value, range_flag, lds);
     } else if constexpr (C::UNEVEN) {
-        constexpr int g0 = C::UNEVEN == 2 ? 5 : 3;
+        constexpr int g0 = C::UNEVEN == 4 ? 9 : C::UNEVEN == 3 ? 7 : C::UNEVEN == 2 ? 5 : 3;
         if ((threadIdx.x >> 8) == 0) {
             __builtin_amdgcn_s_setprio(1);
             nn_h3_body<C, g0>(states, B, blob, blocks, policy, value, range_flag, lds);
@@ -2322,9 +2325,9 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
         hipLaunchKernelGGL(k, dim3(g8), dim3(256), 0, st, s, B, w.blob, w.blocks, policy, value, w.range_flag);
     } else if (w.precision == OAZ_FP32_SPLIT16) {
         if (!w.range_flag) return hipErrorInvalidValue;
-        // default: 8 waves, uneven 15 / 10 square split, batches of <= 4 squares, transposed C/D
+        // default: 8 waves, uneven 17 / 8 square split, batches of <= 4 squares, transposed C/D
         // tiles (TR epilogue); OAZ_NN_X6_V selects the A/B alternatives (DESIGN.md perf log)
-        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1>>;
+        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1>>;
         int waves = 8;
         switch (w.x6_variant) {
             case 1: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 1, 1>>; break;  // both pieces one batch ahead
@@ -2335,11 +2338,13 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             case 6: k = k_nn_h3<X6Cfg<8, 8, 1, 0, 1, 1>>; break;
             case 7: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 2, 1>>; break;  // 16 / 9 split
             case 8: k = k_nn_h3<X6Cfg<4, 8, 1, 0, 0, 1>>; waves = 4; break;  // one 512-VGPR wave per SIMD
-            case 10: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1, 1>>; break;  // timing only: phase stamps
+            case 10: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 3, 1>>; break;  // timing only: phase stamps
             case 11: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1>>; break;  // lane-per-channel C/D tiles (DPP pair stores)
             case 12: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1>>; break;     // timing only: phase stamps, variant 11
             case 13: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1, 2>>; break;  // younger group in 2 phases (slower)
             case 17: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1, 1, 1>>; break;  // heads MLPs on the VALU
+            case 18: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1>>; break;  // 15 / 10 split (the previous default)
+            case 19: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 4, 1>>; break;  // 18 / 7 split
             case 14: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1, 1, 2>>; break;  // timing only: phase stamps
             default: break;
         }
