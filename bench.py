@@ -58,7 +58,8 @@ NN_KERNEL = {"fp32": "k_nn_sq16<fp32> (fused ResNet, exact fp32 v_mfma_f32_16x16
                            "v_mfma_f32_16x16x32_bf16, fp32 accumulate)",
              "fp32_split16": "k_nn_h3 (fused ResNet, fp32 operands split into hi+lo fp16 terms, 3 products on "
                              "v_mfma_f32_16x16x32_f16, fp32 accumulate)",
-             "bf16": "k_nn_bf16g<2> (fused ResNet, 8 waves x 2 N-tiles, v_mfma_f32_16x16x32_bf16)"}
+             "bf16": "k_nn_h3 in bf16 mode (fused ResNet, transposed tiles, one bf16 product on "
+                     "v_mfma_f32_16x16x32_bf16, fp32 accumulate)"}
 METRIC = "MCTS node-expansions/sec/GPU @400 sims; self-play games/sec at 1/2/4/8 GPU"
 
 

@@ -381,6 +381,21 @@ static int pack_weights(const float* raw, int blocks, int precision, std::vector
         out.resize(base + h.size() / 2);
         memcpy(out.data() + base, h.data(), h.size() * sizeof(uint16_t));
     }
+    if (precision == OAZ_BF16) {
+        // k_nn_h3 in bf16 mode (k_nn_h1): head 1x1 convs as [K-half m][lane] bf16x8, lane l supplying
+        // B[k = 8(l>>4) + e][col n = l&15] for channel 32m + 8(l>>4) + e, columns n = 0 value conv,
+        // 1 / 2 policy conv planes, 3..15 zero
+        std::vector<uint16_t> h;
+        for (int m = 0; m < 2; ++m)
+            for (int l = 0; l < 64; ++l)
+                for (int e = 0; e < 8; ++e) {
+                    const int c = 32 * m + 8 * (l >> 4) + e, n = l & 15;
+                    h.push_back(f32_to_bf16(n == 0 ? vc.w[c] : n <= 2 ? pc.w[(n - 1) * 64 + c] : 0.0f));
+                }
+        const size_t base = out.size();
+        out.resize(base + h.size() / 2);
+        memcpy(out.data() + base, h.data(), h.size() * sizeof(uint16_t));
+    }
     if (precision == OAZ_FP32_SPLIT16) {
         // k_nn_h3 head 1x1 convs: [K-half m][piece][lane] f16x8 of the column-scaled weights
         // (column n = 0 value conv, 1 / 2 policy conv planes, 3..15 zero), then 1/s per column (+pad)
@@ -934,7 +949,7 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
     w.precision = e->cfg.precision;
     {
         const char* v1 = getenv("OAZ_NN_BF16_V1");
-        w.bf16_v1 = v1 ? atoi(v1) : 0;  // 0: 8 waves x 2 N-tiles, 1: k_nn_sq16<bf16>, 2: 4 waves x 4 N-tiles
+        w.bf16_v1 = v1 ? atoi(v1) : 0;  // 0: k_nn_h3 in bf16 mode, 1: k_nn_sq16<bf16>, 2: k_nn_bf16g<4>, 3: k_nn_bf16g<2>
         const char* xv = getenv("OAZ_NN_X6_V");
         w.x6_variant = xv ? atoi(xv) : 0;
     }

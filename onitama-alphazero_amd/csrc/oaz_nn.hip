@@ -113,7 +113,7 @@ size_t nn_packed_floats(int blocks, int precision) {
                nn::kPolicyF + h3::kHeadB + h3::kL1C;
     const size_t w = precision == OAZ_BF16 ? nn::kW64h : precision == OAZ_FP32_SPLIT ? x6::kW : nn::kW64;
     return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (w + nn::kCh) + nn::kValueF + nn::kPolicyF +
-           (precision == OAZ_FP32_SPLIT ? x6::kHeadB : 0);
+           (precision == OAZ_FP32_SPLIT ? x6::kHeadB : 0) + (precision == OAZ_BF16 ? 2 * 64 * 4 : 0);
 }
 
 // Square groups: 4 corners + 4 edges + 5 interior (85 on-board taps) | 8 edges + 4 interior (84).
@@ -1049,8 +1049,10 @@ struct H3PlanOf {
 // wrong results): per-wave s_memtime phase sums over the first policy rows (tools/nn_phases.py).
 // UNEVEN (8 waves): square groups 3 / 4 (15 / 10 squares) instead of 0 / 1, the bigger group at
 // s_setprio 1.
-template <int WAVES_, int KH_, int PIPE_, int DBG_ = 0, int UNEVEN_ = 0, int TR_ = 0, int PH_ = 1, int HV_ = 0>
+template <int WAVES_, int KH_, int PIPE_, int DBG_ = 0, int UNEVEN_ = 0, int TR_ = 0, int PH_ = 1, int HV_ = 0,
+          int BF_ = 0>
 struct X6Cfg {
+    static constexpr int BF = BF_;  // h3 + TR: OAZ_BF16 mode (one bf16 piece, one product; C5)
     static constexpr int HV = HV_;  // h3 heads: 0 MLPs on MFMA (8 waves), 1 per-position VALU MLPs
     static constexpr int TR = TR_;
     static constexpr int PH = PH_;  // h3 + TR: square phases of the second (younger) group
@@ -1497,6 +1499,7 @@ __device__ __forceinline__ int elem_off(int row, int c) { return chunk_off(row, 
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 // Phases of group GRP's squares (C::PH for the second group of the TR kernel, else 1).
 template <class C, int GRP>
@@ -1528,8 +1531,11 @@ __device__ __forceinline__ void h3_mfma(f32x4 (&acc)[C::NS], const f16x8 (&a)[N]
 #pragma unroll
     for (int q = 0; q < N; ++q)
         if (q < B.n)
-            acc[B.j[q]] = C::TR ? __builtin_amdgcn_mfma_f32_16x16x32_f16(bv, a[q], acc[B.j[q]], 0, 0, 0)
-                                : __builtin_amdgcn_mfma_f32_16x16x32_f16(a[q], bv, acc[B.j[q]], 0, 0, 0);
+            acc[B.j[q]] = C::BF ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bv),
+                                                                          __builtin_bit_cast(bf16x8, a[q]), acc[B.j[q]],
+                                                                          0, 0, 0)
+                          : C::TR ? __builtin_amdgcn_mfma_f32_16x16x32_f16(bv, a[q], acc[B.j[q]], 0, 0, 0)
+                                  : __builtin_amdgcn_mfma_f32_16x16x32_f16(a[q], bv, acc[B.j[q]], 0, 0, 0);
 }
 
 // the packs of earlier-phase squares that batch K runs (compile-time list)
@@ -1540,9 +1546,9 @@ __device__ __forceinline__ void h3_epi(E& epi, std::integer_sequence<int, I...>)
 }
 
 // B pieces of (tap, K-half) step S for N-tile nt: [step][piece][N-tile][lane] f16x8, buffer loads
-__device__ __forceinline__ X6W h3_w(const float* p, int lane, int nt) {
+__device__ __forceinline__ X6W h3_w(const float* p, int lane, int nt, int bytes = (int)(h3::kW * 4)) {
     X6W w;
-    w.r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(h3::kW * 4), 0x00020000);
+    w.r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, bytes, 0x00020000);
     w.voff = (nt * 64 + lane) * 16;
     return w;
 }
@@ -1558,9 +1564,25 @@ __device__ __forceinline__ void h3_step_b(const X6W& W, f16x8 (&b)[2], f16x8 (&b
         b[1] = bn[1];
     }
     if constexpr (B.first && B.nstep >= 0) {  // prefetch the next step run's B pieces
-        bn[0] = h3_ldb(W, (B.nstep * 2 + 0) * 4);
-        bn[1] = h3_ldb(W, (B.nstep * 2 + 1) * 4);
+        if constexpr (C::BF) {  // BF: [step][N-tile][lane] bf16x8, one piece
+            bn[0] = h3_ldb(W, B.nstep * 4);
+        } else {
+            bn[0] = h3_ldb(W, (B.nstep * 2 + 0) * 4);
+            bn[1] = h3_ldb(W, (B.nstep * 2 + 1) * 4);
+        }
     }
+}
+
+// BF batch K: one piece, one product; the next batch's fragments load during this one's MFMAs
+// (two buffers, roles swap with K's parity)
+template <class C, int GRP, int K>
+__device__ __forceinline__ void conv_h1_batch(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
+                                              f16x8 (&bn)[2], f16x8 (&X)[C::KH], f16x8 (&Xn)[C::KH],
+                                              const int (&ab)[2][2]) {
+    h3_step_b<C, GRP, K>(W, b, bn);
+    if constexpr (K + 1 < H3P<C, GRP>::P.nbat) h3_load<C, GRP, K + 1>(Xn, img, ab, 0);
+    h3_mfma<C, GRP, K>(acc, X, b[0]);
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // PIPE 1, batch K (X holds its lo pieces on entry and the next batch's on exit):
@@ -1607,6 +1629,16 @@ __device__ __forceinline__ void conv_h3_run(f32x4 (&acc)[C::NS], const char* img
         for (int sg = 0; sg < 2; ++sg) ab[m][sg] = lo[m] + sg * 65536;
     constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
     f16x8 b[2], bn[2];
+    if constexpr (C::BF) {
+        b[0] = h3_ldb(W, (B0.t * 2 + B0.m) * 4);
+        f16x8 X[C::KH], X2[C::KH];
+        h3_load<C, GRP, 0>(X, img, ab, 0);
+        ((K % 2 == 0 ? conv_h1_batch<C, GRP, K>(acc, img, W, b, bn, X, X2, ab)
+                     : conv_h1_batch<C, GRP, K>(acc, img, W, b, bn, X2, X, ab)),
+         ...);
+        (void)epi;
+        return;
+    }
     b[0] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 0) * 4);
     b[1] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 1) * 4);
     if constexpr (C::PIPE == 2) {
@@ -1689,7 +1721,7 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 // selects makes the allocator spill.)
 // vmax: the largest hi bit pattern (v >= 0 after ReLU, so the u16 order is the value order; an
 // overflowed hi is +inf = 0x7C00).
-template <bool FIRST>
+template <bool FIRST, bool BF = false>
 __device__ __forceinline__ void h3t_pack_one(const f32x4& acc, uint32_t (&pk)[2][2], const f32x4& bb, const f32x4& sc,
                                              f32x4& skip, bool res, uint32_t& hmax) {
     const f32x2 rf = {res ? 1.0f : 0.0f, res ? 1.0f : 0.0f};  // fma(skip, rf, v) = v + skip or v, exactly
@@ -1705,12 +1737,17 @@ __device__ __forceinline__ void h3t_pack_one(const f32x4& acc, uint32_t (&pk)[2]
             skip[2 * k] = v[0];
             skip[2 * k + 1] = v[1];
         }
-        uint32_t hi;  // (RNE; one packed conversion)
-        asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(hi) : "v"(v[0]), "v"(v[1]));
-        hmax = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, hmax),
-                                                                      __builtin_bit_cast(u16x2, hi)));
-        pk[0][k] = hi;
-        pk[1][k] = h3_lo_pair(hi, v[0], v[1]);
+        if constexpr (BF) {  // one bf16 piece (RNE), no range limit below fp32's
+            pk[0][k] = __builtin_bit_cast(uint32_t, bf16x2{(__bf16)v[0], (__bf16)v[1]});
+            pk[1][k] = 0u;
+        } else {
+            uint32_t hi;  // (RNE; one packed conversion)
+            asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(hi) : "v"(v[0]), "v"(v[1]));
+            hmax = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, hmax),
+                                                                          __builtin_bit_cast(u16x2, hi)));
+            pk[0][k] = hi;
+            pk[1][k] = h3_lo_pair(hi, v[0], v[1]);
+        }
     }
 }
 template <class C, int GRP, bool FIRST>
@@ -1719,7 +1756,7 @@ __device__ __forceinline__ void epilogue_h3t_pack(const f32x4 (&acc)[C::NS], uin
                                                   uint32_t& hmax, int from = 0) {
 #pragma unroll
     for (int j = 0; j < grp_n(GRP); ++j)
-        if (j >= from) h3t_pack_one<FIRST>(acc[j], pk[j], bb, sc, skip[j], res, hmax);
+        if (j >= from) h3t_pack_one<FIRST, (bool)C::BF>(acc[j], pk[j], bb, sc, skip[j], res, hmax);
 }
 template <class C, int GRP>
 __device__ __forceinline__ void epilogue_h3t_store(const uint32_t (&pk)[C::NS][2][2], char* img, int eo) {
@@ -1727,7 +1764,7 @@ __device__ __forceinline__ void epilogue_h3t_store(const uint32_t (&pk)[C::NS][2
     for (int j = 0; j < grp_n(GRP); ++j) {
         char* d = img + grp_sq(GRP, j) * (nn::kSB * h3::kRowB) + eo;
         *reinterpret_cast<uint2*>(d) = uint2{pk[j][0][0], pk[j][0][1]};
-        *reinterpret_cast<uint2*>(d + h3::kPlaneB) = uint2{pk[j][1][0], pk[j][1][1]};
+        if constexpr (!C::BF) *reinterpret_cast<uint2*>(d + h3::kPlaneB) = uint2{pk[j][1][0], pk[j][1][1]};
     }
 }
 
@@ -1842,13 +1879,14 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
         for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};  // skip: finite for the fma in the epilogue
         const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
                            nn::kValueF + nn::kPolicyF + h3::kHeadB;
-        if constexpr (C::TR)
+        if constexpr (C::TR && !C::BF)
             first_layer_h3t<C, GRP>(acc, l1, l1c, bb, pinfo[i], lane, nt);
         else
             first_layer_x6<C, GRP>(acc, l1, blob + nn::kL1B + nn::kCh, bb, pinfo[i], lane, nt);
         uint32_t pk[NS][2][2];
         if constexpr (C::TR) {
-            const f32x4 inv1 = *reinterpret_cast<const f32x4*>(l1c + 25 * 2 * 4 * 64 * 4 + nn::kCh + cq);
+            const f32x4 inv1 = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f}
+                                     : *reinterpret_cast<const f32x4*>(l1c + 25 * 2 * 4 * 64 * 4 + nn::kCh + cq);
             epilogue_h3t_pack<C, GRP, true>(acc, pk, bias1t, inv1, skip, false, hmax);
             epilogue_h3t_store<C, GRP>(pk, img, eot);
         } else {
@@ -1863,8 +1901,9 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
     const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
     for (int c = 0; c < 2 * blocks; ++c) {
         const float bb = p[h3::kW + co], sc = p[h3::kW + nn::kCh + co];  // in flight during the conv
-        const f32x4 bbt = *reinterpret_cast<const f32x4*>(p + h3::kW + cq);
-        const f32x4 sct = *reinterpret_cast<const f32x4*>(p + h3::kW + nn::kCh + cq);
+        constexpr size_t kWc = C::BF ? nn::kW64h : h3::kW;  // B fragments of one conv
+        const f32x4 bbt = *reinterpret_cast<const f32x4*>(p + kWc + cq);
+        const f32x4 sct = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f} : *reinterpret_cast<const f32x4*>(p + kWc + nn::kCh + cq);
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = f32x4{};
         uint32_t pk[NS][2][2];
@@ -1873,10 +1912,10 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
             constexpr int j = decltype(jc)::value;
             h3t_pack_one<false>(acc[j], pk[j], bbt, sct, skip[j], res, hmax);
         };
-        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt), lo, epi,
+        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt, (int)(kWc * 4)), lo, epi,
                             std::make_integer_sequence<int, H3P<C, GRP>::P.nbat>{});
         stamp(1);
-        p += h3::kW + 2 * nn::kCh;
+        p += C::BF ? nn::kW64h + nn::kCh : h3::kW + 2 * nn::kCh;
         if constexpr (C::TR) {
             epilogue_h3t_pack<C, GRP, false>(acc, pk, bbt, sct, skip, res, hmax, H3P<C, GRP>::P.tail);
         } else
@@ -1902,8 +1941,8 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
-            for (int pc = 0; pc < 2; ++pc) hb[m][pc] = HB[(m * 2 + pc) * 64 + lane];
-        const float hs = hp[2 * 2 * 64 * 4 + (i < 3 ? i : 0)];
+            for (int pc = 0; pc < 2; ++pc) hb[m][pc] = HB[(C::BF ? m : m * 2 + pc) * 64 + lane];  // BF: [m][lane]
+        const float hs = C::BF ? 1.0f : hp[2 * 2 * 64 * 4 + (i < 3 ? i : 0)];
         // MLP weights in flight during the head convs (after hb: vmcnt is in order)
         HeadRegs hr;
         HeadMM hm;
@@ -1922,6 +1961,11 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
                 for (int m = 0; m < 2; ++m) {
                     const char* a = img + sq * (nn::kSB * h3::kRowB) + lo[m];
                     const f16x8 ah = *reinterpret_cast<const f16x8*>(a);
+                    if constexpr (C::BF) {
+                        hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, hb[m][0]), hacc[q], 0, 0, 0);
+                        continue;
+                    }
                     const f16x8 al = *reinterpret_cast<const f16x8*>(a + h3::kPlaneB);
                     hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, hb[m][0], hacc[q], 0, 0, 0);
                     hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][0], hacc[q], 0, 0, 0);
@@ -2368,10 +2412,14 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
         }
         hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value);
     }
+    else if (w.precision == OAZ_BF16 && w.bf16_v1 == 0) {  // the k_nn_h3 structure, one bf16 product (k_nn_h1)
+        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 1>>;
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value, w.range_flag);
+    }
     else if (w.precision == OAZ_BF16 && w.bf16_v1 == 1)
         hipLaunchKernelGGL(k_nn_sq16<true>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
                            value);
-    else if (w.precision == OAZ_BF16 && w.bf16_v1 == 0)
+    else if (w.precision == OAZ_BF16 && w.bf16_v1 == 3)
         hipLaunchKernelGGL(k_nn_bf16g<2>, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value);
     else if (w.precision == OAZ_BF16)
         hipLaunchKernelGGL(k_nn_bf16g<4>, dim3(grid), dim3(64 * 4), 0, st, s, B, w.blob, w.blocks, policy, value);
