@@ -100,7 +100,7 @@ def pmc_traffic(args, cfg):
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None
-    kb = {}
+    kb, tree_kb = {}, {"select": {}, "expand_backup": {}}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         with tempfile.TemporaryDirectory() as d:
             cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
@@ -110,23 +110,38 @@ def pmc_traffic(args, cfg):
                 subprocess.run(cmd, timeout=600, capture_output=True, check=True)
             except (subprocess.SubprocessError, OSError):
                 return None
-            vals = []
+            vals, tv = [], {"select": [], "expand_backup": []}
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 for r in csv.DictReader(open(f)):
-                    if "k_nn_" in r["Kernel_Name"] and r["Counter_Name"] == ctr:
+                    if r["Counter_Name"] != ctr:
+                        continue
+                    if "k_nn_" in r["Kernel_Name"]:
                         vals.append(float(r["Counter_Value"]))
+                    elif "k_select" in r["Kernel_Name"]:
+                        tv["select"].append(float(r["Counter_Value"]))
+                    elif "k_expand_backup" in r["Kernel_Name"]:
+                        tv["expand_backup"].append(float(r["Counter_Value"]))
             if not vals:
                 return None
             kb[ctr] = sum(vals) / len(vals)
+            for k, v in tv.items():
+                if v:
+                    tree_kb[k][ctr] = sum(v) / len(v)
     fetch, write = 2.0 * kb["FETCH_SIZE"] * 1024.0, kb["WRITE_SIZE"] * 1024.0
+    tree = {}
+    for k, v in tree_kb.items():  # per game: launches cover every game of the child run
+        if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            tree[k] = {"fetch_bytes_per_sim": 2.0 * v["FETCH_SIZE"] * 1024.0 / cfg["games"],
+                       "write_bytes_per_sim": v["WRITE_SIZE"] * 1024.0 / cfg["games"]}
     return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
-            "raw_kb": kb, "note": "rocprofv3 --pmc, separate passes; FETCH_SIZE x2 (gfx950 wide-read correction)"}
+            "raw_kb": kb, "tree_pmc": tree,
+            "note": "rocprofv3 --pmc, separate passes; FETCH_SIZE x2 (gfx950 wide-read correction)"}
 
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 
-def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg):
+def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg, pmc=None):
     """Achieved HBM-side bytes of the tree kernels (tree-kernel GB/s vs HBM peak),
     from the run's mean walk depth D and branching K and the 32-byte node layout:
     select reads the root state (24 B) and node (32 B), per level K children (32 B each), sqrt(N)
@@ -149,6 +164,10 @@ def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg):
         gbps = per_launch * b / t / 1e9
         out[name] = {"avg_launch_us": t * 1e6, "algorithmic_bytes_per_sim": b, "achieved_GBps": gbps,
                      "frac": gbps / HBM_PEAK_GBPS}
+        if pmc and name in pmc:
+            out[name]["pmc"] = dict(pmc[name], note="rocprofv3 FETCH/WRITE_SIZE of the profiled child run (the "
+                                    "first move's first 2 simulations: shallow trees); writes are small scattered "
+                                    "records (leaf record, counters, path entries), each a whole write transaction")
     return out
 
 
@@ -514,7 +533,8 @@ def main():
                                        "fp32_split": "BF16 dense MFMA peak / 6 products per fp32 MAC",
                                        "fp32_split16": "FP16 dense MFMA peak / 3 products per fp32 MAC"}[cfg["precision"]],
                          "frac_of_fp32_mfma_peak": achieved / PEAK_TFLOPS["fp32"]},
-            "tree_kernels": tree_roofline(kt, sims, args.steps * sims_steps, expansions, depth, branching, cfg),
+            "tree_kernels": tree_roofline(kt, sims, args.steps * sims_steps, expansions, depth, branching, cfg,
+                                          traffic.get("tree_pmc") if traffic else None),
             "allgather": allgather,
         }
         if not args.no_cpu_baseline and world == 1:
