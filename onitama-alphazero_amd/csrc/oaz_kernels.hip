@@ -659,6 +659,24 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))
     }
 }
 
+template <int N>
+__device__ __forceinline__ float bcast_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + N, 0xF, 0xF, false));
+}
+template <int SQ>
+__device__ __forceinline__ void policy_sum_step(const float (&polr)[4], uint32_t row0, uint32_t row1, double& sum0,
+                                                double& sum1) {
+    constexpr int i0 = SQ, i1 = 25 + SQ;
+    const float v0 = bcast_f32<(i0 & 15)>(polr[i0 >> 4]), v1 = bcast_f32<(i1 & 15)>(polr[i1 >> 4]);
+    sum0 += (row0 & sq_bit(SQ)) ? (double)v0 : 0.0;
+    sum1 += (row1 & sq_bit(SQ)) ? (double)v1 : 0.0;
+}
+template <int... SQ>
+__device__ __forceinline__ void policy_sums(const float (&polr)[4], uint32_t row0, uint32_t row1, double& sum0,
+                                            double& sum1, std::integer_sequence<int, SQ...>) {
+    (policy_sum_step<SQ>(polr, row0, row1, sum0, sum1), ...);
+}
+
 // k_expand_backup with 16 lanes per game: lane sl generates the moves of (card, from) combos
 // 4 sl .. 4 sl + 3 (combo = card * 25 + from, the reference order), one segment scan places them.
 __global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const oaz_state* __restrict__ roots,
@@ -678,6 +696,17 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const 
     const float* pol = policy + (size_t)g * 50;
 
     if (!(node_flags(nd.misc) & 3)) {
+        // the leaf's 50 policy values in one round trip (lane sl: entries sl, 16+sl, 32+sl, 48+sl),
+        // kept in registers for the renormalisation sums and in LDS for the children's priors
+        __shared__ float spol[kWavesPerBlock * 4][52];
+        float* sp = spol[(threadIdx.x >> 4) & 15];
+        float polr[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int idx = 16 * c + sl;
+            polr[c] = idx < 50 ? pol[idx] : 0.0f;
+            if (idx < 50) sp[idx] = polr[c];
+        }
         const int color = s.to_move & 1;
         const uint32_t pawns = s.pawns[color], king = s.kings[color], own = pawns | king;
         uint32_t mask[4];
@@ -694,12 +723,11 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const 
         const uint32_t incl = seg_incl_scan(cnt);
         const uint32_t K = (uint32_t)__shfl((int)incl, seg_base() + 15);
         const uint32_t row0 = seg_or(r0), row1 = seg_or(r1);
-        // per-card renormalisation; sequential f64 sums in square order (mcts_arena.rs:288-301)
+        // per-card renormalisation; sequential f64 sums in square order (mcts_arena.rs:288-301).
+        // Entry idx comes from lane idx & 15 by DPP row_newbcast; an unset square adds +0.0, which
+        // leaves a non-negative sum unchanged bit for bit (the old loop loaded and waited 50 times).
         double sum0 = 0.0, sum1 = 0.0;
-        for (int sq = 0; sq < 25; ++sq) {
-            if (row0 & sq_bit(sq)) sum0 += (double)pol[sq];
-            if (row1 & sq_bit(sq)) sum1 += (double)pol[25 + sq];
-        }
+        policy_sums(polr, row0, row1, sum0, sum1, std::make_integer_sequence<int, 25>{});
         const uint32_t base = t.n_nodes[g];
         uint32_t o = incl - cnt;
 #pragma unroll
@@ -712,7 +740,7 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const 
             while (mm) {
                 const int to = __clz(mm);
                 mm &= ~sq_bit(to);
-                double p = (double)pol[k * 25 + to];
+                double p = (double)sp[k * 25 + to];
                 if (rs > 0.0) p = p / rs;
                 store_fresh_node(&T[base + o], p, pack_move(from, to, slot, piece));
                 ++o;
