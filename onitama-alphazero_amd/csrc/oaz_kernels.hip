@@ -594,15 +594,16 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))
             // root with noise: the sequential Iterator::max_by fold of k_select, every segment's
             // fold state (acc, operand a) held uniformly across its 16 lanes; child j's operands
             // are broadcast within each 16-lane row by DPP row_newbcast (j compile-time)
+            // the three chunks' draw pairs load unconditionally (index clamped inside the game's
+            // slot) so they are one round trip, not three; unused lanes then select 0
             float na[3], nb[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                const int j = 16 * c + sl;
-                na[c] = nb[c] = 0.0f;
-                if (go && j >= 1 && j < K) {
-                    na[c] = noise[(size_t)g * kNoiseStride + 2 * j];
-                    nb[c] = noise[(size_t)g * kNoiseStride + 2 * j + 1];
-                }
+                const int j = 16 * c + sl, jj = j < OAZ_MAX_MOVES ? j : OAZ_MAX_MOVES - 1;
+                const float2 d = *reinterpret_cast<const float2*>(noise + (size_t)(on ? g : 0) * kNoiseStride + 2 * jj);
+                const bool use = go && j >= 1 && j < K;
+                na[c] = use ? d.x : 0.0f;
+                nb[c] = use ? d.y : 0.0f;
             }
             const int Kmax = max(max(__builtin_amdgcn_readlane(K, 0), __builtin_amdgcn_readlane(K, 16)),
                                  max(__builtin_amdgcn_readlane(K, 32), __builtin_amdgcn_readlane(K, 48)));
