@@ -406,3 +406,34 @@ def test_agent_api_mirror(orc):
     assert len(data) > 0 and data[0].state.shape == (21, 5, 5)
     for d in data[:20]:
         assert d.z in (-1.0, 0.0, 1.0) and d.pi.shape == (2, 25)
+
+
+def test_legacy_one_game_per_wave_tree_kernels_match_oracle(tmp_path):
+    """OAZ_TREE_SEG=0 selects the one-game-per-wave k_select / k_expand_backup (the default runs four
+    games per wave). The switch is read once per process, so the check runs in a child process:
+    noise-on searches whose trees must equal the oracle's node for node, as the default path's."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    code = f"""
+import sys
+sys.path.insert(0, {str(root / 'onitama-alphazero_amd')!r}); sys.path.insert(0, {str(root / 'tests')!r})
+import numpy as np
+import oracle_ffi as orc
+from conftest import random_positions
+from onitama_az import _abi
+from onitama_az.engine import Engine
+orc.load()
+roots = random_positions(orc, 10, seed=4242)
+with Engine(games=10, sims=40, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=31) as e:
+    e.search(roots)
+    for g in range(10):
+        cfg = orc.search_cfg(sims=40, c_puct=5.0, evaluator=orc.EVAL_HASH, train_noise=1, seed=31, game_id=g, ply=0)
+        _, _, nodes, _ = orc.search(cfg, roots[g])
+        assert e.tree(g).tobytes() == nodes.tobytes(), g
+print("legacy ok")
+"""
+    env = dict(__import__("os").environ, OAZ_TREE_SEG="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "legacy ok" in r.stdout, r.stdout + r.stderr
