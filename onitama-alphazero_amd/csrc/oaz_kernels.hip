@@ -548,7 +548,7 @@ __device__ __forceinline__ int root_fold(int K, int Kmax, const NodeRegs (&ch)[3
     int acc = 0;
     double qa = bcast_f64<0>(f.q), ba = bcast_f64<0>(f.base), sa = bcast_f64<0>(f.sq);
     // j = I + 1 = 1 .. 39; stop once every segment's K is passed (wave-uniform)
-    ((I + 1 < Kmax ? (fold_step<I + 1>(acc, qa, ba, sa, K, f, ch, na, nb, sqn, prm), true) : false) && ...);
+    (void)((I + 1 < Kmax ? (fold_step<I + 1>(acc, qa, ba, sa, K, f, ch, na, nb, sqn, prm), true) : false) && ...);
     return acc;
 }
 
