@@ -553,9 +553,9 @@ __device__ __forceinline__ int root_fold(int K, int Kmax, const NodeRegs (&ch)[3
 }
 
 // k_select with 16 lanes per game: lane sl holds children j = 16c + sl (c < 3, K <= 40).
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) k_select_seg(TreeView t, const oaz_state* __restrict__ roots,
-                                                       const uint8_t* __restrict__ active,
-                                                       const float* __restrict__ noise, SearchParams prm) {
+__device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_state* __restrict__ roots,
+                                                const uint8_t* __restrict__ active, const float* __restrict__ noise,
+                                                const SearchParams& prm) {
     const uint32_t g = seg_game();
     const int sl = seg_lane(), sb = seg_base();
     const bool on = g < t.G && !(active && active[g] != 1);
@@ -658,6 +658,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))
         st[GS_DEPTH] += depth;
         if (stuck) st[GS_STUCK] += 1;
     }
+}
+
+// register budgets: 80 VGPRs = 6 waves/SIMD (default), 72 = 7 waves/SIMD (a few dwords spilled)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6)))
+k_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
+             const float* __restrict__ noise, SearchParams prm) {
+    select_seg_body(t, roots, active, noise, prm);
+}
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7)))
+k_select_seg7(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
+              const float* __restrict__ noise, SearchParams prm) {
+    select_seg_body(t, roots, active, noise, prm);
 }
 
 template <int N>
@@ -996,7 +1008,11 @@ static bool tree_seg() {
 }
 hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                          const float* noise, SearchParams p, hipStream_t st) {
-    if (tree_seg())
+    static const bool w7 = getenv("OAZ_SELECT_W7") && getenv("OAZ_SELECT_W7")[0] == '1';
+    if (tree_seg() && w7)
+        hipLaunchKernelGGL(k_select_seg7, dim3(wave_grid((t.G + 3) / 4)), dim3(kBlock), 0, st, t, roots, active, noise,
+                           p);
+    else if (tree_seg())
         hipLaunchKernelGGL(k_select_seg, dim3(wave_grid((t.G + 3) / 4)), dim3(kBlock), 0, st, t, roots, active, noise,
                            p);
     else
