@@ -80,6 +80,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--no-exact", action="store_true", help="skip the exact-fp32 comparison leg")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
     ap.add_argument("--no-noise", action="store_true", help=argparse.SUPPRESS)  # experiments only: not C3
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -384,6 +385,43 @@ def pure_mcts_main(args, world, rank, local):
         dist.destroy_process_group()
 
 
+def exact_fp32_leg(args, cfg, device):
+    """The same workload on the exact-fp32 NN kernel (k_nn_sq16: fp32 MFMA products), so the
+    headline's precision trade is visible in the same line: a short run (2 warmup + 2 timed steps,
+    no staggered starts) with the NN kernel timed by HIP events on the engine stream."""
+    from onitama_az import _abi
+    from onitama_az.engine import Engine
+    from onitama_az.weights import random_weights
+    with Engine(device=device, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0,
+                train_noise=0 if args.no_noise else 1, max_plies=150, evaluator=_abi.EVAL_NN, precision=_abi.FP32,
+                fixed_deck=cfg["fixed_deck"], deck=[0, 1, 2, 3, 4], seed=20260101,
+                sample_capacity=cfg["games"] * 8) as e:
+        e.load_weights(random_weights(0, cfg["blocks"]))
+        e.selfplay_reset()
+        e.selfplay_step(2)
+        e.sync()
+        st0 = e.selfplay_stats()
+        e.kernel_times_reset()
+        e.set_timing(8)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e.selfplay_step(2)
+        e.sync()
+        dt = time.perf_counter() - t0
+        e.set_timing(False)
+        kt = e.kernel_times()
+        st1 = e.selfplay_stats()
+    sims = st1.search.sims - st0.search.sims
+    nn_ms = kt.nn_ms / max(1, kt.nn_n)
+    fl = FLOP_PER_SIM[cfg["blocks"]] * kt.nn_samples / max(1, kt.nn_n)
+    tf = fl / (nn_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
+    return {"kernel": NN_KERNEL["fp32"], "value": sims / dt, "unit": "sims/s", "ms_per_step": 1e3 * dt / 2,
+            "steps": 2, "warmup": 2, "nn_avg_launch_ms": nn_ms, "nn_achieved_TFLOPs": tf,
+            "nn_frac_of_fp32_mfma_peak": tf / PEAK_TFLOPS["fp32"],
+            "note": "same workload, exact fp32 MFMA products (no operand splitting); short run without staggered "
+                    "starts (the NN dominates the step)"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -427,7 +465,8 @@ def main():
                             "fp32_split16": _abi.FP32_SPLIT16}.get(cfg["precision"], _abi.FP32),
                  fixed_deck=cfg["fixed_deck"],
                  deck=[0, 1, 2, 3, 4], seed=20260101, rank=rank, world=world,
-                 sample_capacity=cfg["games"] * 24, stagger=0 if args.pmc_child else stagger)
+                 # every sample of every game that can finish in warmup + steps plies fits (checked below)
+                 sample_capacity=cfg["games"] * (args.warmup + args.steps + 2), stagger=0 if args.pmc_child else stagger)
     eng.load_weights(random_weights(0, cfg["blocks"]))  # random-init weights (seed 0), SURVEY.md 8d
     eng.selfplay_reset()
     if args.pmc_child:  # profiled pass: one move of a couple of simulations, NN launches at full batch
@@ -467,22 +506,35 @@ def main():
     depth = (st1.search.depth_sum - st0.search.depth_sum) / max(1, sims)
     branching = (st1.search.children - st0.search.children) / max(1, expansions)
     cdev = "cpu" if rehearse else "cuda"
-    tot = torch.tensor([float(sims), float(games_done), float(plies), float(expansions)], dtype=torch.float64, device=cdev)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    fallbacks = eng.nn_fallbacks()
+    tot = torch.tensor([float(sims), float(games_done), float(plies), float(expansions), float(st1.samples_dropped),
+                        float(fallbacks)], dtype=torch.float64, device=cdev)
+    tmax = torch.tensor([elapsed, float(st1.search.max_nodes)], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    sims_all, games_all, plies_all, exp_all = (float(x) for x in tot.tolist())
-    T = float(tmax.item())
+    sims_all, games_all, plies_all, exp_all, dropped_all, fallbacks_all = (float(x) for x in tot.tolist())
+    T, max_nodes_all = (float(x) for x in tmax.tolist())
+
+    # validity of the measured run over all ranks (the process exits non-zero if a check fails):
+    # no sample lost to the device buffer, no tree beyond its capacity, every rank simulated
+    cap_nodes = 1 + 40 * cfg["sims"]
+    checks = {"samples_dropped": int(dropped_all), "max_nodes": int(max_nodes_all), "tree_capacity": cap_nodes,
+              "nn_fp16_range_fallback_tiles": int(fallbacks_all),
+              "ok": bool(dropped_all == 0 and max_nodes_all <= cap_nodes and sims_all > 0)}
 
     allgather = None
     if not args.no_allgather:  # C4: RCCL all-gather of (s, pi, z) after the timed region
-        from onitama_az.dist import allgather_samples
+        from onitama_az.dist import Comm, allgather_samples
+        comm = None if rehearse else Comm.create(rank, world, local)
         t1 = time.perf_counter()
-        got = allgather_samples(eng, world, torch.device("cuda", local), host=rehearse)
+        got = allgather_samples(eng, world, torch.device("cuda", local), comm=comm)
         torch.cuda.synchronize()
-        allgather = {"samples_total": int(got), "bytes_per_sample": 228, "seconds": time.perf_counter() - t1,
-                     "backend": ("gloo (rehearsal)" if rehearse else "nccl(RCCL)") if world > 1 else "local"}
+        allgather = {"samples_total": int(len(got)), "bytes_per_sample": 228, "seconds": time.perf_counter() - t1,
+                     "backend": "gloo (rehearsal, host copies)" if rehearse else
+                                "oaz_allgather_samples (C ABI: RCCL counts all-gather + grouped broadcasts)"}
+        if comm is not None:
+            comm.close()
 
     if rank == 0:
         sims_steps = cfg["sims"]  # simulation steps (select -> NN -> expand launches) per bench step
@@ -496,7 +548,9 @@ def main():
         out = {
             "metric": METRIC, "value": sims_all / T, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * T / args.steps, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16" if cfg["precision"] == "bf16" else "fp32",
+            "vs_baseline": None,
+            "dtype": {"bf16": "bf16", "fp32": "fp32", "fp32_split": "fp32 (bf16x6 split)",
+                      "fp32_split16": "fp32 (fp16x3 split)"}[cfg["precision"]],
             "nn_arithmetic": {"fp32": "exact fp32 MFMA products, fp32 accumulate",
                               "fp32_split": "fp32 operands split exactly into hi+mid+lo bf16 terms, the 6 products "
                                             "above 2^-24 relative on bf16 MFMA, fp32 accumulate (error vs float64 = "
@@ -504,7 +558,9 @@ def main():
                               "fp32_split16": "fp32 operands split into hi = fp16(x) and lo = fp16(x - hi) (weights "
                                               "pre-scaled per output channel by a power of two), the 3 products "
                                               "hi*hi, hi*lo, lo*hi on fp16 MFMA, fp32 accumulate (within 1e-5 of the "
-                                              "fp32 goldens, tests/test_gpu.py; range-checked: OAZ_ERR_RANGE)",
+                                              "fp32 goldens, tests/test_gpu.py); a 16-position tile whose activations "
+                                              "leave the fp16 range is recomputed in-kernel with the bf16x6 split "
+                                              "(counted in checks.nn_fp16_range_fallback_tiles)",
                               "bf16": "bf16 MFMA inputs, fp32 accumulate"}[cfg["precision"]],
             "data": "synthetic (random-init weights seed 0, seeded deals)",
             "config": {"workload": f"{args.config}: {cfg['games']} self-play games/GPU x {cfg['sims']} sims/move, "
@@ -536,14 +592,21 @@ def main():
             "tree_kernels": tree_roofline(kt, sims, args.steps * sims_steps, expansions, depth, branching, cfg,
                                           traffic.get("tree_pmc") if traffic else None),
             "allgather": allgather,
+            "checks": checks,
         }
+    eng.close()
+    if rank == 0:
+        if not args.no_exact and world == 1 and cfg["precision"] in ("fp32_split16", "fp32_split"):
+            out["exact_fp32"] = exact_fp32_leg(args, cfg, local)
         if not args.no_cpu_baseline and world == 1:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, threads)
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
+    if not checks["ok"]:
+        print(f"bench: invalid run: {checks}", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

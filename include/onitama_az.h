@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define OAZ_ABI_VERSION 1
+#define OAZ_ABI_VERSION 2
 
 /* ---- enums mirroring the reference --------------------------------------- */
 enum { OAZ_RED = 0, OAZ_BLUE = 1 };                 /* PlayerColor, player_color.rs:7-10 */
@@ -72,7 +72,8 @@ enum {
     OAZ_ERR_CAPACITY = -4,
     OAZ_ERR_STATE = -5,
     OAZ_ERR_WEIGHTS = -6,
-    OAZ_ERR_RANGE = -7      /* OAZ_FP32_SPLIT16: an activation left the fp16 range (|x| >= 65504) */
+    OAZ_ERR_RANGE = -7,     /* ABI 1 only: ABI 2 recomputes fp16-range tiles instead (oaz_nn_fallbacks) */
+    OAZ_ERR_COMM = -8       /* RCCL communicator error (oaz_comm_*, oaz_allgather_samples) */
 };
 
 enum { OAZ_EVAL_NN = 0, OAZ_EVAL_HASH = 1 };        /* leaf evaluator (HASH: test evaluator, below) */
@@ -83,9 +84,10 @@ enum { OAZ_EVAL_NN = 0, OAZ_EVAL_HASH = 1 };        /* leaf evaluator (HASH: tes
  * operands split into two fp16 terms (hi = fp16(x), lo = fp16(x - hi): 22 significant bits), the
  * three products hi*hi, hi*lo, lo*hi on fp16 MFMA, fp32 accumulate; conv weights are pre-scaled per
  * output channel by a power of two (exact). Errors vs a float64 forward are at the fp32 level
- * (DESIGN.md "fp16 split") at half the MFMA work of OAZ_FP32_SPLIT. Activations must stay below
- * 65504 in magnitude: an engine that saw one beyond returns OAZ_ERR_RANGE from its next
- * synchronising call (nn_forward, search, selfplay stats / samples), never a silent result. */
+ * (DESIGN.md "fp16 split") at half the MFMA work of OAZ_FP32_SPLIT. fp16 terms cover |x| < 65504:
+ * a workgroup whose 16 positions split an activation beyond that recomputes them in the same launch
+ * with the OAZ_FP32_SPLIT arithmetic (fp32 range), so no result is ever silently wrong and no run
+ * fails; oaz_nn_fallbacks() counts the recomputed 16-position tiles. */
 enum { OAZ_FP32 = 0, OAZ_BF16 = 1, OAZ_FP32_SPLIT = 2, OAZ_FP32_SPLIT16 = 3 };
 
 /* ---- PODs ----------------------------------------------------------------- */
@@ -246,6 +248,9 @@ int oaz_kernel_times_reset(oaz_engine* eng);
 
 /* policy [B][2][25] (softmax over all 50), value [B]. Host pointers. B <= cfg.games. */
 int oaz_nn_forward(oaz_engine* eng, const oaz_state* s, int B, float* policy, float* value);
+/* OAZ_FP32_SPLIT16: 16-position tiles recomputed with the OAZ_FP32_SPLIT arithmetic because an
+ * activation left the fp16 range, since the engine was created (0 for other precisions). */
+int oaz_nn_fallbacks(oaz_engine* eng, uint64_t* tiles);
 
 /* One search per root (root colour = roots[i].to_move), cfg.sims simulations each, all
  * G searches advanced together. out_pi [G][50] f32, out_root_value [G] = an extra NN
@@ -264,10 +269,43 @@ int oaz_samples_fetch(oaz_engine* eng, oaz_sample* out, size_t cap, size_t* n_ou
 /* Device-to-device copy of up to cap_bytes/sizeof(oaz_sample) buffered samples into a
  * device buffer on the engine's GPU (e.g. a tensor that is then all-gathered over RCCL). */
 int oaz_samples_export_device(oaz_engine* eng, void* dev_dst, size_t cap_bytes, size_t* n_out);
-/* self_play(): play exactly n_games games (slot g plays games until the total is
- * reached) and return their samples. */
+/* self_play(): play exactly n_games games and return their samples. n_games counts global game
+ * ids over all ranks (cfg.world): this rank plays the ids below n_games that it owns
+ * ((k * world + rank) * games + slot) and returns when those are finished. */
 int oaz_selfplay_run(oaz_engine* eng, int n_games, oaz_sample* out, size_t cap,
                      size_t* n_out, oaz_selfplay_stats* stats);
+
+/* ---- multi-GPU: RCCL over xGMI ------------------------------
+ * One process (or host thread) per GPU, one engine per GPU, games sharded by global game id with
+ * no exchange inside the simulation loop. The one data exchange of the path replaces the
+ * reference's join of its self-play workers' buffers (alphazero-training/src/train.rs:241-244:
+ * `for handle in handles { data_buffer.extend(handle.join()) }`): every rank ends with every
+ * rank's (s, pi, z) records. The communicator wraps an RCCL communicator (librccl.so.1, loaded on
+ * first use); rank 0 makes the id and the host sends it to the other ranks out of band (a file,
+ * a socket, torch.distributed, MPI). All oaz_comm_* calls with a `comm` are collective. */
+typedef struct oaz_comm oaz_comm;
+typedef struct oaz_comm_id { char internal[128]; } oaz_comm_id;  /* = ncclUniqueId */
+
+int oaz_comm_unique_id(oaz_comm_id* out);
+/* Joins `world` ranks on GPU `device`; blocks until all ranks joined. NULL on error. */
+oaz_comm* oaz_comm_init(const oaz_comm_id* id, int rank, int world, int device);
+void oaz_comm_destroy(oaz_comm* comm);
+/* All-gather of the engines' buffered samples: every rank's samples_ready records land in
+ * dev_out (device memory on the engine's GPU, cap records) in rank order, and are dropped from each
+ * engine's buffer (as oaz_samples_fetch does). counts_out[world] (host, optional) = records per
+ * rank; *n_total = their sum. Counts are all-gathered first, then each rank's block is one
+ * broadcast into its offset, all in one RCCL group: an all-gatherv with no padding and no scratch.
+ * OAZ_ERR_CAPACITY (on every rank alike) when the total exceeds cap; nothing is consumed then. */
+int oaz_allgather_samples(oaz_engine* eng, oaz_comm* comm, oaz_sample* dev_out, size_t cap, size_t* n_total,
+                          uint64_t* counts_out);
+/* In-place sum all-reduce of n floats in device memory (data-parallel gradients), on `stream`
+ * (a hipStream_t; NULL = the communicator's own stream); returns when enqueued. */
+int oaz_comm_allreduce_sum_f32(oaz_comm* comm, float* dev, size_t n, void* stream);
+/* In-place broadcast of `bytes` bytes of device memory from `root` (new best weights),
+ * on `stream` (NULL = the communicator's stream); returns when enqueued. */
+int oaz_comm_broadcast(oaz_comm* comm, void* dev, size_t bytes, int root, void* stream);
+/* Waits for the communicator's own stream. */
+int oaz_comm_sync(oaz_comm* comm);
 
 /* ---- training step ---------------------------------
  * One trainer = one GPU. Parameters live on the device in the canonical blob

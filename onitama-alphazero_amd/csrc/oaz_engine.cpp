@@ -467,7 +467,19 @@ static int pack_weights(const float* raw, int blocks, int precision, std::vector
     }
     if (out.size() != nn_packed_floats(blocks, precision)) return oaz_set_err(OAZ_ERR_STATE, "pack: size mismatch");
     if ((size_t)(p - raw) != oaz_weight_count(blocks, 64, 21)) return oaz_set_err(OAZ_ERR_STATE, "pack: raw size mismatch");
+    if (precision == OAZ_FP32_SPLIT16) {
+        // k_nn_h3 recomputes fp16-range tiles with the k_nn_x6 body: the OAZ_FP32_SPLIT blob follows
+        std::vector<float> x6;
+        if (int rc = pack_weights(raw, blocks, OAZ_FP32_SPLIT, x6)) return rc;
+        out.insert(out.end(), x6.begin(), x6.end());
+    }
     return 0;
+}
+
+// Device floats of an engine's packed weights (SPLIT16 carries the SPLIT blob for its fallback).
+static size_t weights_floats(int blocks, int precision) {
+    return nn_packed_floats(blocks, precision) +
+           (precision == OAZ_FP32_SPLIT16 ? nn_packed_floats(blocks, OAZ_FP32_SPLIT) : 0);
 }
 
 // ---- rules context (no engine needed) ----------------------------------------------------------
@@ -606,7 +618,7 @@ struct oaz_engine {
     float *policy = nullptr, *value = nullptr;
     float* weights = nullptr;
     bool have_weights = false;
-    uint32_t* range_flag = nullptr;      // OAZ_FP32_SPLIT16: an activation reached the fp16 range limit
+    unsigned long long* nn_fallback = nullptr;  // OAZ_FP32_SPLIT16: tiles recomputed by k_nn_x6 (fp16 range)
     // search mode
     oaz_state* s_roots = nullptr;
     oaz_move* s_move = nullptr;
@@ -816,12 +828,12 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         dalloc(&e->depth, G) || dalloc(&e->leaf, G) || dalloc(&e->leaf_state, G) ||
         dalloc(&e->stats, G * GS_COUNT) || dalloc(&e->stats_sum, (size_t)GS_COUNT) ||
         dalloc(&e->sqrt_tab, (size_t)cfg->sims + 2) || dalloc(&e->policy, G * 50) ||
-        dalloc(&e->value, G) || dalloc(&e->weights, nn_packed_floats(cfg->blocks, cfg->precision)) ||
+        dalloc(&e->value, G) || dalloc(&e->weights, weights_floats(cfg->blocks, cfg->precision)) ||
         dalloc(&e->s_roots, G) || dalloc(&e->s_move, G) || dalloc(&e->s_pi, G * 50) ||
         dalloc(&e->s_rootv, G) || dalloc(&e->s_rootp, G * 50) || dalloc(&e->s_ply, G) ||
         dalloc(&e->root, G) || dalloc(&e->ply, G) || dalloc(&e->seq, G) ||
         dalloc(&e->game_id, G) || dalloc(&e->active, G) || dalloc(&e->hist, G * e->hcap) ||
-        dalloc(&e->out, (size_t)e->out_cap) || dalloc(&e->out_count, (size_t)1) || dalloc(&e->range_flag, (size_t)1) ||
+        dalloc(&e->out, (size_t)e->out_cap) || dalloc(&e->out_count, (size_t)1) || dalloc(&e->nn_fallback, (size_t)1) ||
         (cfg->train_noise && dalloc(&e->noise, 2 * kNoiseChunk * G * kNoiseStride)))
         return fail();
     // sqrt((double)n) from the host libm (IEEE correctly rounded), so device PUCT = oracle PUCT
@@ -830,7 +842,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
     if (hipMemcpy(e->sqrt_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(e->stats, 0, G * GS_COUNT * sizeof(uint64_t)) != hipSuccess ||
         hipMemset(e->out_count, 0, sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(e->range_flag, 0, sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(e->nn_fallback, 0, sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(e->active, 0, G) != hipSuccess) {
         oaz_set_err(OAZ_ERR_HIP, "create: init copies failed");
         return fail();
@@ -863,7 +875,7 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     void* ptrs[] = {e->nodes, e->n_nodes, e->path, e->depth, e->leaf, e->leaf_state, e->stats,
                     e->stats_sum, e->sqrt_tab, e->policy, e->value, e->weights, e->s_roots,
                     e->s_move, e->s_pi, e->s_rootv, e->s_rootp, e->s_ply, e->root, e->ply,
-                    e->seq, e->game_id, e->active, e->hist, e->out, e->out_count, e->noise, e->range_flag};
+                    e->seq, e->game_id, e->active, e->hist, e->out, e->out_count, e->noise, e->nn_fallback};
     for (void* p : ptrs) dfree(p);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
@@ -887,7 +899,6 @@ extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
     if (int rc = pack_weights(blob, e->cfg.blocks, e->cfg.precision, packed)) return rc;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipMemcpyAsync(e->weights, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
-    HIP_TRY(hipMemsetAsync(e->range_flag, 0, sizeof(uint32_t), e->stream));  // new weights: a fresh range check
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->have_weights = true;
     return 0;
@@ -947,28 +958,29 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
     w.blob = e->weights;
     w.blocks = e->cfg.blocks;
     w.precision = e->cfg.precision;
+    w.bf16_v1 = 0;
+    w.x6_variant = 0;
+#if OAZ_AB  // A/B build only: kernel alternatives by environment variable
     {
         const char* v1 = getenv("OAZ_NN_BF16_V1");
         w.bf16_v1 = v1 ? atoi(v1) : 0;  // 0: k_nn_h3 in bf16 mode, 1: k_nn_sq16<bf16>, 2: k_nn_bf16g<4>, 3: k_nn_bf16g<2>
         const char* xv = getenv("OAZ_NN_X6_V");
         w.x6_variant = xv ? atoi(xv) : 0;
     }
-    w.range_flag = e->range_flag;
+#endif
+    w.blob_x6 = e->cfg.precision == OAZ_FP32_SPLIT16 ? e->weights + nn_packed_floats(e->cfg.blocks, OAZ_FP32_SPLIT16)
+                                                     : nullptr;
+    w.fallback = e->nn_fallback;
     return timed(e, 1, B, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, st); }, st);
 }
 
-// OAZ_FP32_SPLIT16: did any NN launch so far see an activation beyond the fp16 range? Called after
-// the engine's stream has been synchronised; the flag stays set (every later call fails too) until
-// new weights are loaded.
-static int check_range(oaz_engine* e) {
-    if (e->cfg.precision != OAZ_FP32_SPLIT16 || e->cfg.evaluator != OAZ_EVAL_NN) return 0;
-    uint32_t f = 0;
-    HIP_TRY(hipMemcpyAsync(&f, e->range_flag, sizeof(f), hipMemcpyDeviceToHost, e->stream));
+extern "C" int oaz_nn_fallbacks(oaz_engine* e, uint64_t* tiles) {
+    if (!e || !tiles) return oaz_set_err(OAZ_ERR_ARG, "nn_fallbacks: null");
+    HIP_TRY(hipSetDevice(e->device));
+    unsigned long long n = 0;
+    HIP_TRY(hipMemcpyAsync(&n, e->nn_fallback, sizeof(n), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    if (f)
-        return oaz_set_err(OAZ_ERR_RANGE,
-                           "NN activation reached the fp16 range (|x| >= 65504) under OAZ_FP32_SPLIT16; "
-                           "results since the last weight load are invalid: use OAZ_FP32_SPLIT or OAZ_FP32");
+    *tiles = (uint64_t)n;
     return 0;
 }
 
@@ -982,7 +994,7 @@ extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* p
     if (policy) HIP_TRY(hipMemcpyAsync(policy, e->s_rootp, (size_t)B * 50 * 4, hipMemcpyDeviceToHost, e->stream));
     if (value) HIP_TRY(hipMemcpyAsync(value, e->s_rootv, (size_t)B * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    return check_range(e);
+    return 0;
 }
 
 // All cfg.sims simulations of one move for every game: select -> evaluate -> expand/backup,
@@ -1030,7 +1042,11 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
     // halves alternating and each half's select / expand-backup running beside the other half's NN.
     // Measured no faster on MI355X (C3 11.88 vs 11.93 M sims/s; the tree kernels slow down 4x
     // beside the NN), so one stream is the default.
+#if OAZ_AB
     const bool split = t.G >= 4096 && getenv("OAZ_SPLIT_HALVES") && getenv("OAZ_SPLIT_HALVES")[0] == '1';
+#else
+    const bool split = false;
+#endif
     const uint32_t GA = split ? (t.G / 2 + 63) / 64 * 64 : t.G;
     hipStream_t sh[2] = {e->stream, e->stream3};
     TreeView tv[2] = {t, t};
@@ -1132,7 +1148,6 @@ extern "C" int oaz_search(oaz_engine* e, const oaz_state* roots, int G, oaz_move
     if (out_move) HIP_TRY(hipMemcpyAsync(out_move, e->s_move, (size_t)G * sizeof(oaz_move), hipMemcpyDeviceToHost, e->stream));
     if (out_pi) HIP_TRY(hipMemcpyAsync(out_pi, e->s_pi, (size_t)G * 50 * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    if (int rc = check_range(e)) return rc;
     if (stats) {
         uint64_t s[GS_COUNT];
         if (int rc = reduce_stats(e, (uint32_t)G, s)) return rc;
@@ -1190,7 +1205,6 @@ extern "C" int oaz_selfplay_stats_get(oaz_engine* e, oaz_selfplay_stats* o) {
     HIP_TRY(hipSetDevice(e->device));
     uint64_t s[GS_COUNT];
     if (int rc = reduce_stats(e, e->G, s)) return rc;
-    if (int rc = check_range(e)) return rc;
     unsigned long long cnt = 0;
     HIP_TRY(hipMemcpy(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost));
     memset(o, 0, sizeof(*o));
@@ -1212,7 +1226,6 @@ static int samples_copy(oaz_engine* e, void* dst, size_t cap, size_t* n_out, hip
     unsigned long long cnt = 0;
     HIP_TRY(hipMemcpyAsync(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    if (int rc = check_range(e)) return rc;
     const unsigned long long avail = (cnt < e->out_cap ? cnt : e->out_cap);
     const size_t ready = avail > e->out_read ? (size_t)(avail - e->out_read) : 0;
     const size_t n = ready < cap ? ready : cap;
@@ -1228,6 +1241,37 @@ static int samples_copy(oaz_engine* e, void* dst, size_t cap, size_t* n_out, hip
     return 0;
 }
 
+// Internal (oaz_host.h), for oaz_allgather_samples: the engine's buffered samples as one contiguous
+// device range [*dev, *dev + *n), after the engine's work so far is complete.
+int oaz_engine_samples_peek(oaz_engine* e, const oaz_sample** dev, size_t* n, int* device) {
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream2));
+    unsigned long long cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    const unsigned long long avail = (cnt < e->out_cap ? cnt : e->out_cap);
+    *n = avail > e->out_read ? (size_t)(avail - e->out_read) : 0;
+    *dev = e->out + e->out_read;
+    *device = e->device;
+    return 0;
+}
+
+// Drops the first n peeked samples (the caller's copies of them are complete).
+int oaz_engine_samples_consume(oaz_engine* e, size_t n) {
+    HIP_TRY(hipSetDevice(e->device));
+    unsigned long long cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    const unsigned long long avail = (cnt < e->out_cap ? cnt : e->out_cap);
+    e->out_read += n;
+    if (e->out_read == avail && cnt >= e->out_read) {  // buffer drained: rewind
+        HIP_TRY(hipMemsetAsync(e->out_count, 0, sizeof(unsigned long long), e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        e->out_read = 0;
+    }
+    return 0;
+}
+
 extern "C" int oaz_samples_fetch(oaz_engine* e, oaz_sample* out, size_t cap, size_t* n_out) {
     if (!e || (!out && cap)) return oaz_set_err(OAZ_ERR_ARG, "samples_fetch: bad arguments");
     return samples_copy(e, out, cap, n_out, hipMemcpyDeviceToHost);
@@ -1238,10 +1282,20 @@ extern "C" int oaz_samples_export_device(oaz_engine* e, void* dev_dst, size_t ca
     return samples_copy(e, dev_dst, cap_bytes / sizeof(oaz_sample), n_out, hipMemcpyDeviceToDevice);
 }
 
+// Games of the first `quota` global ids that this rank plays: rank r owns the ids
+// seq * world * G + r * G + g (g < G, seq >= 0; SlotView, k_selfplay_move).
+static uint64_t rank_share(const oaz_engine* e, uint64_t quota) {
+    const uint64_t G = e->G, W = (uint64_t)(e->cfg.world > 0 ? e->cfg.world : 1), r = (uint64_t)e->cfg.rank;
+    const uint64_t full = quota / (W * G), rem = quota % (W * G);
+    const uint64_t lo = r * G;
+    return full * G + (rem > lo ? (rem - lo < G ? rem - lo : G) : 0);
+}
+
 extern "C" int oaz_selfplay_run(oaz_engine* e, int n_games, oaz_sample* out, size_t cap, size_t* n_out,
                                 oaz_selfplay_stats* stats) {
     if (!e || n_games < 0) return oaz_set_err(OAZ_ERR_ARG, "selfplay_run: bad arguments");
     e->quota = (uint64_t)n_games;  // slots stop dealing at global game index >= n_games
+    const uint64_t mine = rank_share(e, e->quota);  // this rank's share of the n_games (global) games
     int rc = oaz_selfplay_reset(e);
     if (rc) {
         e->quota = 0;
@@ -1251,7 +1305,7 @@ extern "C" int oaz_selfplay_run(oaz_engine* e, int n_games, oaz_sample* out, siz
     for (;;) {
         oaz_selfplay_stats st;
         if ((rc = oaz_selfplay_stats_get(e, &st))) break;
-        if (st.games_finished >= (uint64_t)n_games) {
+        if (st.games_finished >= mine) {
             if (stats) *stats = st;
             break;
         }

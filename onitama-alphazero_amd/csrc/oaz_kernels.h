@@ -77,9 +77,10 @@ struct NNView {
     int32_t blocks;
     int32_t precision;  // OAZ_FP32 (exact fp32 MFMA), OAZ_BF16 (bf16 inputs), OAZ_FP32_SPLIT (bf16x6 split),
                         // OAZ_FP32_SPLIT16 (fp16x3 split)
-    int32_t x6_variant; // fp32-split kernel variant (OAZ_NN_X6_V, A/B testing)
-    int32_t bf16_v1;    // bf16 kernel variant (OAZ_NN_BF16_V1): 0 k_nn_bf16g<2>, 1 k_nn_sq16<bf16>, 2 k_nn_bf16g<4>
-    uint32_t* range_flag;  // OAZ_FP32_SPLIT16: set to 1 when an activation reached the fp16 range limit
+    int32_t x6_variant; // A/B build only (OAZ_NN_X6_V): split kernel variant
+    int32_t bf16_v1;    // A/B build only (OAZ_NN_BF16_V1): 1 k_nn_sq16<bf16>, 2 k_nn_bf16g<4>, 3 k_nn_bf16g<2>
+    const float* blob_x6;             // OAZ_FP32_SPLIT16: the OAZ_FP32_SPLIT blob of the same weights
+    unsigned long long* fallback;     // OAZ_FP32_SPLIT16: tiles recomputed by the k_nn_x6 body (fp16 range)
 };
 
 // rules

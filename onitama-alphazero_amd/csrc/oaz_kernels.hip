@@ -666,11 +666,13 @@ k_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __r
              const float* __restrict__ noise, SearchParams prm) {
     select_seg_body(t, roots, active, noise, prm);
 }
+#if OAZ_AB
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7)))
 k_select_seg7(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
               const float* __restrict__ noise, SearchParams prm) {
     select_seg_body(t, roots, active, noise, prm);
 }
+#endif
 
 template <int N>
 __device__ __forceinline__ float bcast_f32(float v) {
@@ -918,6 +920,10 @@ __global__ void __launch_bounds__(kBlock) k_selfplay_move(TreeView t, SlotView s
     const bool over = is_win(res) || (int)nply >= sv.max_plies + 2;
     if (l == 0) st[GS_MOVES] += 1;
     if (over) {
+        // lanes reload history records other lanes of this wave wrote (pi from lanes 0..49, the
+        // state from lane 0): order those global writes before the reads under the memory model
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t n = nply < sv.hcap ? nply : sv.hcap;
         unsigned long long base = 0;
         if (l == 0) base = atomicAdd(sv.out_count, (unsigned long long)n);
@@ -1008,11 +1014,15 @@ static bool tree_seg() {
 }
 hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                          const float* noise, SearchParams p, hipStream_t st) {
+#if OAZ_AB  // A/B build only: 7 waves/SIMD (spills; measured 10 % slower)
     static const bool w7 = getenv("OAZ_SELECT_W7") && getenv("OAZ_SELECT_W7")[0] == '1';
-    if (tree_seg() && w7)
+    if (tree_seg() && w7) {
         hipLaunchKernelGGL(k_select_seg7, dim3(wave_grid((t.G + 3) / 4)), dim3(kBlock), 0, st, t, roots, active, noise,
                            p);
-    else if (tree_seg())
+        return hipGetLastError();
+    }
+#endif
+    if (tree_seg())
         hipLaunchKernelGGL(k_select_seg, dim3(wave_grid((t.G + 3) / 4)), dim3(kBlock), 0, st, t, roots, active, noise,
                            p);
     else

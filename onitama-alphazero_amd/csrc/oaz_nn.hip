@@ -639,6 +639,7 @@ __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __
     for (int s = wave; s < nn::kSB; s += nn::kWaves) heads<BF16>(act, scratch, s, p, lane, b0 + s, B, policy, value);
 }
 
+#if OAZ_AB  // A/B build only (make AB=1): the earlier C5 kernels, superseded by k_nn_h3 in bf16 mode
 // ---- bf16, 4 waves x 4 N-tiles ------------------------------------------------------------------
 // Each wave owns all 64 output channels (4 N-tiles) of one square group, so every A fragment read
 // from LDS (one (square, tap) of 16 positions x 64 channels) feeds 8 MFMAs instead of 2: LDS
@@ -842,6 +843,7 @@ __global__ void __launch_bounds__(64 * 16 / NPW) k_nn_bf16g(const oaz_state* __r
     float* scratch = lds + kImageFloats + wave * nn::kScratch;
     for (int s = wave; s < nn::kSB; s += kWaves) heads<true>(act, scratch, s, p, lane, b0 + s, B, policy, value);
 }
+#endif  // OAZ_AB
 
 // ---- fp32 split (OAZ_FP32_SPLIT): bf16x6 MFMA with fp32-level error ------------------------------
 // Every fp32 operand x (activation or folded weight) is split EXACTLY into three bf16 terms,
@@ -1828,10 +1830,12 @@ __device__ __forceinline__ void first_layer_h3t(f32x4 (&acc)[C::NS], const L1Reg
 }
 
 // The whole forward for the waves of square group GRP.
+// Returns true in a lane that split an activation beyond the fp16 range (an fp16 hi term that
+// overflowed, or would have): the tile's results are then invalid and k_nn_h3 recomputes them.
 template <class C, int GRP>
-__device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
+__device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
                                            int blocks, float* __restrict__ policy, float* __restrict__ value,
-                                           uint32_t* __restrict__ range_flag, float* lds) {
+                                           float* lds) {
     constexpr int NS = C::NS;
     char* img = reinterpret_cast<char*>(lds);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -2001,37 +2005,76 @@ __device__ __forceinline__ void nn_h3_body(const oaz_state* __restrict__ states,
             heads_mlp_r<NP>(hr, fq, bq, lane, B, policy, value);
         }
     }
-    if (vmax >= 65504.0f) atomicOr(range_flag, 1u);  // an fp16 hi term overflowed (or would have)
-    if (C::TR && ((hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u)) atomicOr(range_flag, 1u);  // hi = inf
     if constexpr (C::DBG == 2) {
         stamp(5);
         __syncthreads();
         if (lane < 6 && b0 + nn::kSB <= B) policy[(size_t)b0 * 50 + wave * 6 + lane] = (float)ph[lane];
     }
+    if constexpr (C::BF) return false;  // bf16 pieces have fp32's exponent range
+    return vmax >= 65504.0f || (C::TR && ((hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u));  // hi = inf
+}
+
+// fp16-range fallback: a workgroup in which any lane split an activation beyond the fp16 range
+// recomputes its 16 positions with the k_nn_x6 body (the exact three-term bf16 split: fp32's
+// exponent range, the same fp32-level error) from the OAZ_FP32_SPLIT blob `xblob`, in the same
+// launch, and counts the tile in *fallback. Results are therefore never silently wrong and no run
+// dies on a range trip; the common path pays one __syncthreads_or at the end of the workgroup
+// (the LDS is released only when every wave is done anyway). x6's LDS image (157.7 KB) bounds the
+// kernel's LDS; h3's 106.5 KB already allowed one workgroup per CU only, so occupancy is unchanged.
+template <class C>
+struct H3Fallback {
+    static constexpr bool kOn = !C::BF && C::DBG == 0;
+    using X = X6Cfg<C::WAVES, C::WAVES == 4 ? 8 : 4, 1, 0, C::WAVES == 4 ? 0 : 1>;
+    static constexpr int kLds = kOn && x6::kLdsFloats > h3::kLdsFloats ? x6::kLdsFloats : h3::kLdsFloats;
+};
+
+// Out of line, so that the fallback's register allocation (k_nn_x6 spills a few VGPRs at 8 waves)
+// cannot touch the k_nn_h3 body's: the call is the rare path.
+template <class X, int GRP>
+__device__ __noinline__ void nn_h3_fallback(const oaz_state* __restrict__ states, int B, const float* __restrict__ xblob,
+                                            int blocks, float* __restrict__ policy, float* __restrict__ value,
+                                            float* lds) {
+    nn_x6_body<X, GRP>(states, B, xblob, blocks, policy, value, lds);
 }
 
 template <class C>
 __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __restrict__ states, int B,
                                                         const float* __restrict__ blob, int blocks,
                                                         float* __restrict__ policy, float* __restrict__ value,
-                                                        uint32_t* __restrict__ range_flag) {
-    __shared__ __attribute__((aligned(16))) float lds[h3::kLdsFloats];
+                                                        const float* __restrict__ xblob,
+                                                        unsigned long long* __restrict__ fallback) {
+    __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
+    bool ovf;
+    const bool g0 = (threadIdx.x >> 8) == 0;  // 8 waves: waves 0-3 square group A, waves 4-7 group B
     if constexpr (C::WAVES == 4) {
-        nn_h3_body<C, 2>(states, B, blob, blocks, policy, value, range_flag, lds);
+        ovf = nn_h3_body<C, 2>(states, B, blob, blocks, policy, value, lds);
     } else if constexpr (C::UNEVEN) {
-        constexpr int g0 = C::UNEVEN == 4 ? 9 : C::UNEVEN == 3 ? 7 : C::UNEVEN == 2 ? 5 : 3;
-        if ((threadIdx.x >> 8) == 0) {
+        constexpr int ga = C::UNEVEN == 4 ? 9 : C::UNEVEN == 3 ? 7 : C::UNEVEN == 2 ? 5 : 3;
+        if (g0) {
             __builtin_amdgcn_s_setprio(1);
-            nn_h3_body<C, g0>(states, B, blob, blocks, policy, value, range_flag, lds);
+            ovf = nn_h3_body<C, ga>(states, B, blob, blocks, policy, value, lds);
         } else {
-            nn_h3_body<C, g0 + 1>(states, B, blob, blocks, policy, value, range_flag, lds);
+            ovf = nn_h3_body<C, ga + 1>(states, B, blob, blocks, policy, value, lds);
         }
-    } else if ((threadIdx.x >> 8) == 0)  // waves 0-3: square group 0, waves 4-7: group 1
-        nn_h3_body<C, 0>(states, B, blob, blocks, policy, value, range_flag, lds);
+    } else if (g0)
+        ovf = nn_h3_body<C, 0>(states, B, blob, blocks, policy, value, lds);
     else
-        nn_h3_body<C, 1>(states, B, blob, blocks, policy, value, range_flag, lds);
+        ovf = nn_h3_body<C, 1>(states, B, blob, blocks, policy, value, lds);
+    if constexpr (H3Fallback<C>::kOn) {
+        using X = typename H3Fallback<C>::X;
+        if (__syncthreads_or(ovf)) {  // uniform over the workgroup; also the barrier before LDS reuse
+            if constexpr (C::WAVES == 4)
+                nn_h3_fallback<X, 2>(states, B, xblob, blocks, policy, value, lds);
+            else if (g0)
+                nn_h3_fallback<X, 3>(states, B, xblob, blocks, policy, value, lds);
+            else
+                nn_h3_fallback<X, 4>(states, B, xblob, blocks, policy, value, lds);
+            if (threadIdx.x == 0) atomicAdd(fallback, 1ull);
+        }
+    }
 }
 
+#if OAZ_AB
 // ---------------------------------------------------------------------------------------------
 // k_nn_p8 (OAZ_FP32_SPLIT16, OAZ_NN_X6_V=20): the k_nn_h3 arithmetic (fp16 hi/lo split, 3 products,
 // transposed C/D tiles, per-channel weight scales, range guard) on 8 positions per workgroup, so
@@ -2207,7 +2250,7 @@ template <int KH, int PIPE>
 __global__ void __launch_bounds__(256) k_nn_p8(const oaz_state* __restrict__ states, int B,
                                                const float* __restrict__ blob, int blocks,
                                                float* __restrict__ policy, float* __restrict__ value,
-                                               uint32_t* __restrict__ range_flag) {
+                                               unsigned long long* __restrict__ range_flag) {
     __shared__ __attribute__((aligned(16))) char img[p8::kImageB];
     __shared__ int pinfo[p8::kP];
     const int tid = threadIdx.x, nt = tid >> 6, lane = tid & 63;
@@ -2352,27 +2395,25 @@ __global__ void __launch_bounds__(256) k_nn_p8(const oaz_state* __restrict__ sta
         const int bq[2] = {b0 + nt, b0 + nt + 4};
         heads_mlp_r<2>(hr, fq, bq, lane, B, policy, value);
     }
-    if ((hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u) atomicOr(range_flag, 1u);  // an fp16 hi = inf
+    // A/B-only kernel: no recompute; the counter records the overflow (the tile's results are invalid)
+    if ((hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u) atomicAdd(range_flag, 1ull);  // an fp16 hi = inf
 }
+#endif  // OAZ_AB
 
+// One kernel per precision in the product build. The A/B build (make AB=1, -DOAZ_AB=1) adds the
+// measured alternatives of the DESIGN.md perf log, selected by OAZ_NN_X6_V / OAZ_NN_BF16_V1; the
+// product build ignores those variables.
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy, float* value,
                              hipStream_t st) {
     if (B <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
-    if (w.precision == OAZ_FP32_SPLIT16 && w.x6_variant >= 20) {
-        if (!w.range_flag) return hipErrorInvalidValue;
-        const unsigned g8 = (unsigned)((B + p8::kP - 1) / p8::kP);
-        // measured 1.40 vs 1.25 ms (C3 batch): the two workgroups per CU overlap, but a single wave
-        // per SIMD per workgroup leaves the MFMA pipe waiting on its own LDS reads (69 % busy, as
-        // k_nn_h3), and the paired tiles add 10 % conv and 43 % first-layer MFMA work
-        auto k = k_nn_p8<4, 1>;
-        hipLaunchKernelGGL(k, dim3(g8), dim3(256), 0, st, s, B, w.blob, w.blocks, policy, value, w.range_flag);
-    } else if (w.precision == OAZ_FP32_SPLIT16) {
-        if (!w.range_flag) return hipErrorInvalidValue;
-        // default: 8 waves, uneven 17 / 8 square split, batches of <= 4 squares, transposed C/D
-        // tiles (TR epilogue); OAZ_NN_X6_V selects the A/B alternatives (DESIGN.md perf log)
+    if (w.precision == OAZ_FP32_SPLIT16) {
+        if (!w.fallback || !w.blob_x6) return hipErrorInvalidValue;
+        // 8 waves, uneven 17 / 8 square split, batches of <= 4 squares, transposed C/D tiles, in-kernel
+        // k_nn_x6 recompute of fp16-range tiles
         auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1>>;
         int waves = 8;
+#if OAZ_AB
         switch (w.x6_variant) {
             case 1: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 1, 1>>; break;  // both pieces one batch ahead
             case 2: k = k_nn_h3<X6Cfg<8, 6, 1, 0, 1, 1>>; break;
@@ -2390,15 +2431,22 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             case 18: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1>>; break;  // 15 / 10 split (the previous default)
             case 19: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 4, 1>>; break;  // 18 / 7 split
             case 14: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1, 1, 2>>; break;  // timing only: phase stamps
+            case 20: {  // 8 positions per workgroup, 2 workgroups per CU (measured 1.40 vs 1.25 ms)
+                const unsigned g8 = (unsigned)((B + p8::kP - 1) / p8::kP);
+                hipLaunchKernelGGL((k_nn_p8<4, 1>), dim3(g8), dim3(256), 0, st, s, B, w.blob, w.blocks, policy, value,
+                                   w.fallback);
+                return hipGetLastError();
+            }
             default: break;
         }
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value,
-                           w.range_flag);
+#endif
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value, w.blob_x6,
+                           w.fallback);
     } else if (w.precision == OAZ_FP32_SPLIT) {
-        // default: 8 waves, uneven 15 / 10 square split, pipelined batches of <= 4 squares
-        // (DESIGN.md perf log); OAZ_NN_X6_V selects the A/B alternatives
+        // 8 waves, uneven 15 / 10 square split, pipelined batches of <= 4 squares
         auto k = k_nn_x6<X6Cfg<8, 4, 1, 0, 1>>;
         int waves = 8;
+#if OAZ_AB
         switch (w.x6_variant) {
             case 1: k = k_nn_x6<X6Cfg<4, 8, 1>>; waves = 4; break;  // one 512-VGPR wave per SIMD
             case 2: k = k_nn_x6<X6Cfg<4, 8, 2>>; waves = 4; break;  // + three piece buffers
@@ -2410,22 +2458,27 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             case 13: k = k_nn_x6<X6Cfg<8, 4, 1, 2, 1>>; break;  // timing only: phase stamps
             default: break;
         }
+#endif
         hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value);
-    }
-    else if (w.precision == OAZ_BF16 && w.bf16_v1 == 0) {  // the k_nn_h3 structure, one bf16 product (k_nn_h1)
+    } else if (w.precision == OAZ_BF16) {
+#if OAZ_AB
+        if (w.bf16_v1 == 1)
+            hipLaunchKernelGGL(k_nn_sq16<true>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks,
+                               policy, value);
+        else if (w.bf16_v1 == 2)
+            hipLaunchKernelGGL(k_nn_bf16g<4>, dim3(grid), dim3(64 * 4), 0, st, s, B, w.blob, w.blocks, policy, value);
+        else if (w.bf16_v1 == 3)
+            hipLaunchKernelGGL(k_nn_bf16g<2>, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value);
+        if (w.bf16_v1 >= 1 && w.bf16_v1 <= 3) return hipGetLastError();
+#endif
+        // the k_nn_h3 structure with one bf16 piece and one product (k_nn_h1)
         auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 1>>;
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value, w.range_flag);
-    }
-    else if (w.precision == OAZ_BF16 && w.bf16_v1 == 1)
-        hipLaunchKernelGGL(k_nn_sq16<true>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
-                           value);
-    else if (w.precision == OAZ_BF16 && w.bf16_v1 == 3)
-        hipLaunchKernelGGL(k_nn_bf16g<2>, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value);
-    else if (w.precision == OAZ_BF16)
-        hipLaunchKernelGGL(k_nn_bf16g<4>, dim3(grid), dim3(64 * 4), 0, st, s, B, w.blob, w.blocks, policy, value);
-    else
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value, nullptr,
+                           nullptr);
+    } else {
         hipLaunchKernelGGL(k_nn_sq16<false>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
                            value);
+    }
     return hipGetLastError();
 }
 

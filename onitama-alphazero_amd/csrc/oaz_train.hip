@@ -993,10 +993,12 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
     t->nconv = 1 + 2 * cfg->blocks;
     t->maxB = cfg->max_batch;
     t->L = make_layout(cfg->blocks);
+#if OAZ_AB  // A/B build only: conv row-group override
     if (const char* e = getenv("OAZ_CONV_RG")) {
         const int v = atoi(e);
         if (v == 1 || v == 2 || v == 4) t->conv_rg = v;
     }
+#endif
     t->nparam = t->L.total;
     const size_t R = (size_t)t->maxB * 25;
     auto fail = [&]() -> oaz_trainer* { delete t; return nullptr; };
@@ -1341,7 +1343,12 @@ extern "C" int oaz_trainer_train(oaz_trainer* t, int first, int count) {
     // Plain stream launches by default: on this stack replaying the captured step (~65 kernels on
     // two streams) measured slower (1.06 vs 0.87 ms at batch 512, 5 blocks); OAZ_TRAIN_GRAPH=1
     // selects the graph path.
-    if (!getenv("OAZ_TRAIN_GRAPH")) {
+#if OAZ_AB
+    const bool graph = getenv("OAZ_TRAIN_GRAPH") != nullptr;
+#else
+    const bool graph = false;
+#endif
+    if (!graph) {
         for (int b = first; b < first + count; ++b) {
             if (int rc = backward(t, b)) return rc;
             if (int rc = apply(t, 1.0f)) return rc;

@@ -19,7 +19,10 @@ PAWN, KING = 0, 1
 CAPTURE, RED_WIN, BLUE_WIN, IN_PROGRESS = 0, 1, 2, 3
 EVAL_NN, EVAL_HASH = 0, 1
 FP32, BF16, FP32_SPLIT, FP32_SPLIT16 = 0, 1, 2, 3  # OAZ_FP32 / OAZ_BF16 / OAZ_FP32_SPLIT / OAZ_FP32_SPLIT16
-ERR_RANGE = -7  # OAZ_ERR_RANGE (onitama_az.h)
+ERR_RANGE = -7  # OAZ_ERR_RANGE (ABI 1 only; ABI 2 recomputes fp16-range tiles, oaz_nn_fallbacks)
+ERR_CAPACITY = -4
+ERR_COMM = -8
+ABI_VERSION = 2
 MAX_MOVES = 40
 
 
@@ -157,6 +160,10 @@ class oaz_pure_mcts_stats(C.Structure):
                                           "rollouts_capped", "max_nodes", "tree_full")]
 
 
+class oaz_comm_id(C.Structure):
+    _fields_ = [("internal", C.c_char * 128)]
+
+
 assert C.sizeof(oaz_state) == 24
 assert C.sizeof(oaz_move) == 4
 assert C.sizeof(oaz_node) == 32
@@ -204,6 +211,7 @@ _PROTOS = {
     "oaz_kernel_times_get": (C.c_int, [_VOIDP, _P(oaz_kernel_times)]),
     "oaz_kernel_times_reset": (C.c_int, [_VOIDP]),
     "oaz_nn_forward": (C.c_int, [_VOIDP, _VOIDP, C.c_int, _VOIDP, _VOIDP]),
+    "oaz_nn_fallbacks": (C.c_int, [_VOIDP, _P(C.c_uint64)]),
     "oaz_search": (C.c_int, [_VOIDP, _VOIDP, C.c_int, _VOIDP, _VOIDP, _VOIDP, _P(oaz_search_stats)]),
     "oaz_tree_dump": (C.c_int, [_VOIDP, C.c_int, _VOIDP, C.c_int, _P(C.c_int)]),
     "oaz_selfplay_reset": (C.c_int, [_VOIDP]),
@@ -212,6 +220,13 @@ _PROTOS = {
     "oaz_samples_fetch": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t, _P(C.c_size_t)]),
     "oaz_samples_export_device": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t, _P(C.c_size_t)]),
     "oaz_selfplay_run": (C.c_int, [_VOIDP, C.c_int, _VOIDP, C.c_size_t, _P(C.c_size_t), _P(oaz_selfplay_stats)]),
+    "oaz_comm_unique_id": (C.c_int, [_P(oaz_comm_id)]),
+    "oaz_comm_init": (_VOIDP, [_P(oaz_comm_id), C.c_int, C.c_int, C.c_int]),
+    "oaz_comm_destroy": (None, [_VOIDP]),
+    "oaz_allgather_samples": (C.c_int, [_VOIDP, _VOIDP, _VOIDP, C.c_size_t, _P(C.c_size_t), _VOIDP]),
+    "oaz_comm_allreduce_sum_f32": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t, _VOIDP]),
+    "oaz_comm_broadcast": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t, C.c_int, _VOIDP]),
+    "oaz_comm_sync": (C.c_int, [_VOIDP]),
     "oaz_pure_mcts_config_default": (None, [_P(oaz_pure_mcts_config)]),
     "oaz_pure_mcts_tree_capacity": (C.c_size_t, [_P(oaz_pure_mcts_config)]),
     "oaz_pure_mcts_search": (C.c_int, [_VOIDP, C.c_int, _P(oaz_pure_mcts_config), _VOIDP, _VOIDP,
@@ -244,7 +259,8 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # OAZ_LIB: another in-tree build of the same ABI (the A/B build, `make AB=1`, for tools/ only)
+    p = Path(path) if path else Path(os.environ["OAZ_LIB"]) if os.environ.get("OAZ_LIB") else LIB_PATH
     if not p.exists():
         raise OazError(f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
@@ -252,7 +268,7 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.oaz_abi_version() != 1:
+    if lib.oaz_abi_version() != ABI_VERSION:
         raise OazError("ABI version mismatch")
     if path is None:
         _lib = lib

@@ -78,6 +78,12 @@ class Engine:
         _abi.check(self._lib.oaz_nn_forward(self._h, _abi.ptr(states), B, _abi.ptr(pol), _abi.ptr(val)))
         return pol, val
 
+    def nn_fallbacks(self) -> int:
+        """OAZ_FP32_SPLIT16: 16-position tiles recomputed with the bf16x6 split (fp16 range)."""
+        n = C.c_uint64(0)
+        _abi.check(self._lib.oaz_nn_fallbacks(self._h, C.byref(n)))
+        return int(n.value)
+
     # -- search --
     def search(self, roots: np.ndarray, root_value: bool = False) -> SearchResult:
         roots = np.ascontiguousarray(roots, dtype=_abi.STATE_DTYPE)

@@ -897,6 +897,85 @@ int64_t orc_selfplay_bench(const orc_selfplay_cfg* cfg, int threads, double seco
 }
 
 
+/* Batch of independent searches on host threads (the checker for bench-size GPU searches): root i
+ * runs orc_search with game_id = game_ids[i] (or cfg->game_id + i); workers take roots from a
+ * shared counter. */
+typedef struct {
+    const orc_search_cfg* cfg;
+    const oaz_state* roots;
+    const uint64_t* game_ids;
+    int n;
+    oaz_move* out_move;
+    float* out_pi;
+    int* next;
+    pthread_mutex_t* mu;
+    oaz_search_stats st;
+    int rc;
+} batch_arg;
+
+static void* batch_worker(void* p) {
+    batch_arg* a = (batch_arg*)p;
+    orc_search_cfg c = *a->cfg;
+    for (;;) {
+        pthread_mutex_lock(a->mu);
+        const int i = (*a->next)++;
+        pthread_mutex_unlock(a->mu);
+        if (i >= a->n) break;
+        c.game_id = a->game_ids ? a->game_ids[i] : a->cfg->game_id + (uint64_t)i;
+        oaz_search_stats st;
+        memset(&st, 0, sizeof(st));
+        const int rc = orc_search(&c, &a->roots[i], &a->out_move[i], a->out_pi + (size_t)i * 50, NULL, 0, NULL, &st);
+        if (rc < 0) a->rc = rc;
+        a->st.sims += st.sims;
+        a->st.expansions += st.expansions;
+        a->st.children += st.children;
+        a->st.terminal_leaves += st.terminal_leaves;
+        a->st.depth_sum += st.depth_sum;
+        a->st.stuck_leaves += st.stuck_leaves;
+        if (st.max_nodes > a->st.max_nodes) a->st.max_nodes = st.max_nodes;
+    }
+    return NULL;
+}
+
+int orc_search_batch(const orc_search_cfg* cfg, const oaz_state* roots, const uint64_t* game_ids, int n, int threads,
+                     oaz_move* out_move, float* out_pi, oaz_search_stats* stats) {
+    if (!cfg || !roots || n < 0 || !out_move || !out_pi) return OAZ_ERR_ARG;
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    batch_arg* args = (batch_arg*)calloc((size_t)threads, sizeof(batch_arg));
+    pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+    int next = 0;
+    for (int i = 0; i < threads; i++) {
+        args[i].cfg = cfg;
+        args[i].roots = roots;
+        args[i].game_ids = game_ids;
+        args[i].n = n;
+        args[i].out_move = out_move;
+        args[i].out_pi = out_pi;
+        args[i].next = &next;
+        args[i].mu = &mu;
+        pthread_create(&th[i], NULL, batch_worker, &args[i]);
+    }
+    int rc = 0;
+    oaz_search_stats sum;
+    memset(&sum, 0, sizeof(sum));
+    for (int i = 0; i < threads; i++) {
+        pthread_join(th[i], NULL);
+        if (args[i].rc < 0) rc = args[i].rc;
+        sum.sims += args[i].st.sims;
+        sum.expansions += args[i].st.expansions;
+        sum.children += args[i].st.children;
+        sum.terminal_leaves += args[i].st.terminal_leaves;
+        sum.depth_sum += args[i].st.depth_sum;
+        sum.stuck_leaves += args[i].st.stuck_leaves;
+        if (args[i].st.max_nodes > sum.max_nodes) sum.max_nodes = args[i].st.max_nodes;
+    }
+    free(th);
+    free(args);
+    if (stats) *stats = sum;
+    return rc;
+}
+
 /* ---- pure MCTS (onitama-game/src/ai/mcts/mcts_arena.rs) ---------------------------------- */
 typedef struct {
     uint64_t seed;

@@ -81,6 +81,13 @@ int orc_search(const orc_search_cfg* cfg, const oaz_state* root, oaz_move* out_m
                float out_pi[50], oaz_node* out_nodes, int cap, int* n_nodes,
                oaz_search_stats* stats);
 
+/* n independent searches on `threads` host threads; root i uses game_id = game_ids[i], or
+ * cfg->game_id + i when game_ids is NULL (the GPU's search mode keys root i's noise by batch index
+ * i). out_move[n], out_pi[n*50]; stats summed (max_nodes: maximum). The evaluator must be
+ * thread-safe (HASH or NN; not a Python callback). */
+int orc_search_batch(const orc_search_cfg* cfg, const oaz_state* roots, const uint64_t* game_ids, int n, int threads,
+                     oaz_move* out_move, float* out_pi, oaz_search_stats* stats);
+
 typedef struct orc_selfplay_cfg {
     orc_search_cfg search;
     int max_plies;

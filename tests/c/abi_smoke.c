@@ -8,6 +8,12 @@
 
 #include "onitama_az.h"
 
+/* A host allocates the device buffer the all-gather writes into with HIP itself (the Rust host
+ * links libamdhip64 too); plain-C prototypes of the three calls used (extern "C" in HIP). */
+int hipMalloc(void** ptr, size_t size);
+int hipFree(void* ptr);
+int hipMemcpy(void* dst, const void* src, size_t bytes, int kind); /* kind 2 = device to host */
+
 #define CHECK(c)                                                                   \
     do {                                                                           \
         if (!(c)) {                                                                \
@@ -73,6 +79,36 @@ int main(void) {
     oaz_selfplay_stats sp;
     CHECK(oaz_selfplay_run(e, 4, buf, 4 * 152, &n, &sp) == 0 && sp.games_finished + sp.games_cut == 4 && n > 0);
     printf("OK selfplay %zu samples\n", n);
+    /* RCCL communicator at world 1: all-gather the buffered samples device to device */
+    CHECK(oaz_selfplay_reset(e) == 0 && oaz_selfplay_step(e, 40) == 0 && oaz_selfplay_stats_get(e, &sp) == 0);
+    const size_t ready = sp.samples_ready;
+    CHECK(ready > 0);
+    oaz_comm_id cid;
+    CHECK(oaz_comm_unique_id(&cid) == 0);
+    oaz_comm* comm = oaz_comm_init(&cid, 0, 1, 0);
+    CHECK(comm != NULL);
+    void* dev = NULL;
+    CHECK(hipMalloc(&dev, ready * sizeof(oaz_sample)) == 0);
+    size_t total = 0;
+    uint64_t counts[1] = {0};
+    CHECK(oaz_allgather_samples(e, comm, (oaz_sample*)dev, ready - 1, &total, counts) == OAZ_ERR_CAPACITY &&
+          total == ready);
+    CHECK(oaz_allgather_samples(e, comm, (oaz_sample*)dev, ready, &total, counts) == 0 && total == ready &&
+          counts[0] == ready);
+    oaz_sample* hs = (oaz_sample*)malloc(ready * sizeof(oaz_sample));
+    CHECK(hipMemcpy(hs, dev, ready * sizeof(oaz_sample), 2) == 0);
+    for (size_t i = 0; i < ready; ++i) {
+        float sum = 0;
+        for (int k = 0; k < 50; ++k) sum += hs[i].pi[k];
+        CHECK(sum > 0.999f && sum < 1.001f && (hs[i].z == 0.0f || hs[i].z == 1.0f || hs[i].z == -1.0f));
+    }
+    CHECK(oaz_selfplay_stats_get(e, &sp) == 0 && sp.samples_ready == 0); /* consumed */
+    CHECK(oaz_comm_allreduce_sum_f32(comm, (float*)dev, 16, NULL) == 0 && oaz_comm_sync(comm) == 0);
+    CHECK(oaz_comm_broadcast(comm, dev, 64, 0, NULL) == 0 && oaz_comm_sync(comm) == 0);
+    oaz_comm_destroy(comm);
+    hipFree(dev);
+    free(hs);
+    printf("OK comm %zu samples\n", ready);
     /* pure MCTS agent */
     oaz_pure_mcts_config pc;
     oaz_pure_mcts_config_default(&pc);

@@ -76,6 +76,7 @@ def load() -> C.CDLL:
         "orc_weight_count": (C.c_size_t, [C.c_int]),
         "orc_nn_forward": (C.c_int, [V, C.c_int, V, C.c_int, V, V]),
         "orc_search": (C.c_int, [P(orc_search_cfg), V, V, V, V, C.c_int, P(C.c_int), P(_abi.oaz_search_stats)]),
+        "orc_search_batch": (C.c_int, [P(orc_search_cfg), V, V, C.c_int, C.c_int, V, V, P(_abi.oaz_search_stats)]),
         "orc_selfplay_game": (C.c_int, [P(orc_selfplay_cfg), C.c_uint64, V, C.c_int, P(C.c_int), P(C.c_int),
                                         P(_abi.oaz_search_stats)]),
         "orc_selfplay_bench": (C.c_int64, [P(orc_selfplay_cfg), C.c_int, C.c_double, P(C.c_int64), P(C.c_int64)]),
@@ -211,6 +212,32 @@ def search(cfg: orc_search_cfg, root: np.ndarray, tree: bool = True):
                            cap if tree else 0, C.byref(n), C.byref(st))
     assert rc == 0, rc
     return mv[0], pi.reshape(2, 25), (nodes[: n.value] if tree else None), st
+
+
+def host_threads() -> int:
+    """Worker threads for the checker: the CPUs this process may run on, at most 16 (the GPU
+    box's CPU share per GPU)."""
+    import os
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def search_batch(cfg: orc_search_cfg, roots: np.ndarray, threads: int = 0, game_ids=None):
+    """orc_search_batch: root i searched with game_id = game_ids[i] (default cfg.game_id + i).
+    Returns (moves, pi [n,2,25], summed stats)."""
+    roots = np.ascontiguousarray(roots, dtype=_abi.STATE_DTYPE)
+    n = len(roots)
+    ids = None if game_ids is None else np.ascontiguousarray(game_ids, dtype=np.uint64)
+    mv = np.zeros(n, dtype=_abi.MOVE_DTYPE)
+    pi = np.zeros((n, 50), dtype=np.float32)
+    st = _abi.oaz_search_stats()
+    rc = load().orc_search_batch(C.byref(cfg), P_(roots), P_(ids) if ids is not None else None, n,
+                                 threads or host_threads(), P_(mv), P_(pi), C.byref(st))
+    assert rc == 0, rc
+    return mv, pi.reshape(n, 2, 25), st
 
 
 def selfplay_game(search: orc_search_cfg, game_id: int, max_plies=150, deck=None):

@@ -19,8 +19,10 @@ def _build(tmp_path) -> Path:
         pytest.skip("no C compiler")
     exe = tmp_path / "abi_smoke"
     lib_dir = _abi.LIB_PATH.parent
+    rocm = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / "lib"
     subprocess.run([cc, "-O1", "-Wall", "-o", str(exe), str(ROOT / "tests/c/abi_smoke.c"), f"-I{ROOT / 'include'}",
-                    f"-L{lib_dir}", "-lonitama_az", f"-Wl,-rpath,{lib_dir}"], check=True)
+                    f"-L{lib_dir}", "-lonitama_az", f"-Wl,-rpath,{lib_dir}", f"-L{rocm}", "-lamdhip64",
+                    f"-Wl,-rpath,{rocm}"], check=True)
     return exe
 
 
@@ -40,5 +42,5 @@ def test_c_host_without_device(tmp_path):
 def test_c_host_on_gpu(tmp_path):
     r = _run(_build(tmp_path))
     assert r.returncode == 0, r.stdout + r.stderr
-    for tag in ("OK search", "OK selfplay", "OK pure_mcts", "OK train"):
+    for tag in ("OK search", "OK selfplay", "OK comm", "OK pure_mcts", "OK train"):
         assert tag in r.stdout, r.stdout

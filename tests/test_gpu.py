@@ -124,26 +124,63 @@ def test_nn_split16_error_at_fp32_level(nn_golden, trained3, name, blocks):
     assert err[_abi.FP32_SPLIT16] <= 4 * err[_abi.FP32] + 1e-6, err
 
 
-def test_nn_split16_range_guard(nn_golden, trained3):
-    """An activation beyond the fp16 range fails loudly (OAZ_ERR_RANGE) instead of returning
-    garbage, and a later load of sane weights clears the condition."""
+def test_nn_split16_range_fallback_recomputes_all_tiles(nn_golden, trained3):
+    """Activations beyond the fp16 range (here every position's: BN-folded first-layer bias 1e5) make
+    each workgroup recompute its 16 positions with the bf16x6 split inside the same launch: the
+    results equal the OAZ_FP32_SPLIT engine's bit for bit, and the fallback counts every tile."""
     from onitama_az.weights import blob_from_named, named_from_blob
     named = {k: v.copy() for k, v in named_from_blob(trained3.copy(), 3).items()}
     named["bn1|bias"][:] = 1.0e5  # first-layer activations ~1e5 > 65504
     bad = blob_from_named(named, 3)
-    states = nn_golden["states"][:32]
+    states = nn_golden["states"][:64]
     with Engine(games=64, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT16) as e:
         e.load_weights(bad)
-        with pytest.raises(_abi.OazError, match="fp16 range"):
-            e.nn_forward(states)
+        p16, v16 = e.nn_forward(states)
+        assert e.nn_fallbacks() == 4  # 64 positions = 4 tiles of 16
         e.load_weights(trained3)
         p, _ = e.nn_forward(states)
-    assert np.abs(p - nn_golden["policy_trained3"][:32]).max() < 1e-5
-    # the exact kernels have no such limit: same weights, finite softmax
+        assert e.nn_fallbacks() == 4  # sane weights: no further tile
+    assert np.abs(p - nn_golden["policy_trained3"][:64]).max() < 1e-5
     with Engine(games=64, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT) as e:
         e.load_weights(bad)
-        p, v = e.nn_forward(states)
-    assert np.isfinite(p).all() and np.isfinite(v).all()
+        px, vx = e.nn_forward(states)
+    assert np.isfinite(px).all() and np.isfinite(vx).all()
+    assert np.array_equal(p16, px) and np.array_equal(v16, vx)
+
+
+def test_nn_split16_range_fallback_only_overflowing_tiles(nn_golden, trained3):
+    """Only positions whose mover holds card 7 (Rooster) overflow (its first-layer plane weights are
+    scaled by 1e6): exactly the tiles containing such a position are recomputed (bit-equal to the
+    OAZ_FP32_SPLIT kernel), the other tiles keep the fp16x3 result (bit-equal to a batch of those
+    positions alone, and within 1e-5 of exact fp32)."""
+    from onitama_az.game import encode_batch
+    from onitama_az.weights import blob_from_named, named_from_blob
+    named = {k: v.copy() for k, v in named_from_blob(trained3.copy(), 3).items()}
+    named["conv_init_1|weight"][:, 4 + 7] *= 1.0e6
+    bad = blob_from_named(named, 3)
+    states = nn_golden["states"]
+    planes = encode_batch(states)
+    hot = planes[:, 4 + 7].reshape(256, -1).max(1) > 0  # the mover holds card 7
+    tiles_hot = hot.reshape(16, 16).any(1)
+    assert 0 < tiles_hot.sum() < 16
+    out = {}
+    for prec in (_abi.FP32_SPLIT16, _abi.FP32_SPLIT, _abi.FP32):
+        with Engine(games=256, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=prec) as e:
+            e.load_weights(bad)
+            out[prec] = e.nn_forward(states)
+            if prec == _abi.FP32_SPLIT16:
+                assert e.nn_fallbacks() == int(tiles_hot.sum())
+    p16, px, pf = out[_abi.FP32_SPLIT16][0], out[_abi.FP32_SPLIT][0], out[_abi.FP32][0]
+    rows = np.repeat(tiles_hot, 16)
+    assert np.array_equal(p16[rows], px[rows])
+    assert np.abs(p16[~rows] - pf[~rows]).max() < 1e-5
+    # the cold tiles alone in a clean batch: the same fp16x3 bits
+    cold = np.ascontiguousarray(states[~rows])
+    with Engine(games=256, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT16) as e:
+        e.load_weights(bad)
+        pc, _ = e.nn_forward(cold)
+        assert e.nn_fallbacks() == 0
+    assert np.array_equal(pc, p16[~rows])
 
 
 @pytest.mark.parametrize("name,blocks", [("trained3", 3), ("random3", 3), ("random6", 6)])

@@ -18,7 +18,7 @@ HEADER = ROOT / "include" / "onitama_az.h"
 def declared_functions():
     text = HEADER.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(oaz_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(oaz_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_header_functions_exported(lib):
@@ -30,7 +30,7 @@ def test_header_functions_exported(lib):
 
 
 def test_abi_version_and_structs(lib):
-    assert lib.oaz_abi_version() == 1
+    assert lib.oaz_abi_version() == _abi.ABI_VERSION == 2
     assert C.sizeof(_abi.oaz_config) == 112 or C.sizeof(_abi.oaz_config) > 0
 
 

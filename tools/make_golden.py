@@ -3,6 +3,7 @@ reference is mounted; the GPU box only reads the committed outputs).
 
   weights_3block_trained.npy   the reference's trained 3-block net (models/model_5e-3_3_resnet.ot)
                                as a canonical fp32 blob, read with the no-unpickling .ot reader
+  weights_5block_trained.npy   the reference's trained 5-block net (models/model_5e-3.ot), likewise
   nn_golden.npz                seeded positions (random play driven by the C oracle's rules) and
                                torch-CPU outputs of the net.rs op graph (F.conv2d, F.batch_norm
                                eval eps=1e-5, relu, linear, tanh, softmax) for:
@@ -32,6 +33,7 @@ from onitama_az.weights import (blob_from_named, named_from_blob, random_weights
 
 GOLD = ROOT / "tests" / "golden"
 REF_MODEL = Path("/root/reference/models/model_5e-3_3_resnet.ot")
+REF_MODEL5 = Path("/root/reference/models/model_5e-3.ot")
 
 
 def random_positions(n: int, seed: int) -> np.ndarray:
@@ -88,6 +90,7 @@ def main():
     trained = read_ot(str(REF_MODEL))
     w3 = blob_from_named(trained, 3)
     np.save(GOLD / "weights_3block_trained.npy", w3)
+    np.save(GOLD / "weights_5block_trained.npy", blob_from_named(read_ot(str(REF_MODEL5)), 5))
     states = random_positions(256, seed=7)
     planes = np.stack([orc.encode(s) for s in states])
     out = {"states": states}
