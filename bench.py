@@ -172,25 +172,72 @@ def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg, pmc=No
     return out
 
 
-def cpu_baseline(cfg, seconds, threads):
-    """Reference-equivalent CPU baseline: the C restatement (oracle) playing self-play with the
-    reference's execution shape — one game per worker thread, sequential search, one batch-1
-    fp32 forward per simulation (train.rs:218-245, mcts_arena.rs:267-269)."""
-    sys.path.insert(0, str(ROOT / "tests"))
-    import oracle_ffi as orc
-    from onitama_az.weights import random_weights
+def host_cpu():
+    """Physical cores this process may use (its CPU affinity, one per (package, core) pair,
+    capped by a cgroup CPU quota) and the CPU model: the reference runs one self-play worker per
+    core (train.rs:122,147 thread_amnt = available_parallelism; BASELINE.md 4: physical cores)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = list(range(os.cpu_count() or 1))
+    cores = set()
+    for c in cpus:
+        try:
+            t = Path(f"/sys/devices/system/cpu/cpu{c}/topology")
+            cores.add(((t / "physical_package_id").read_text().strip(), (t / "core_id").read_text().strip()))
+        except OSError:
+            cores.add(("?", str(c)))
+    n, how = len(cores), f"{len(cores)} physical cores in the affinity mask ({len(cpus)} logical CPUs)"
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max" and int(q) // int(per) < n:
+            n = max(1, int(q) // int(per))
+            how += f", capped by the cgroup CPU quota ({q}/{per})"
+    except (OSError, ValueError):
+        pass
+    share = os.environ.get("OMP_NUM_THREADS")  # the GPU box's CPU share per GPU (16): a pool rule
+    if share and share.isdigit() and 0 < int(share) < n:
+        n = int(share)
+        how += f", capped by this host's CPU share per GPU (OMP_NUM_THREADS={share})"
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return n, how, model
 
-    w = random_weights(0, cfg["blocks"])
-    sc = orc.search_cfg(sims=cfg["sims"], c_puct=5.0, train_noise=1, evaluator=orc.EVAL_NN, weights=w,
-                        blocks=cfg["blocks"], seed=20260101)
-    t0 = time.perf_counter()
-    sims, games, plies = orc.selfplay_bench(sc, threads, seconds, max_plies=150,
-                                            deck=[0, 1, 2, 3, 4] if cfg["fixed_deck"] else None)
-    dt = time.perf_counter() - t0
-    return {"value": sims / dt, "unit": "sims/s", "cores": threads, "kind": "port",
-            "sample": f"{dt:.1f}s of self-play on {threads} host threads (oracle C restatement, batch-1 fp32 NN per "
-                      f"simulation, {cfg['blocks']}-block random-init, {cfg['sims']} sims/move): {sims} sims, "
-                      f"{plies} plies, {games} games finished"}
+
+def cpu_baseline(cfg, seconds, threads):
+    """Reference-equivalent CPU baseline: oracle/build/oaz_cpu_baseline plays the
+    reference's self-play execution shape — one game per worker thread, workers = physical cores,
+    sequential MCTS (the C restatement of mcts_arena.rs), one batch-1 libtorch-CPU (ATen) forward per
+    simulation (mcts_arena.rs:267-269 -> net.rs:215-232, the ops tch calls), intra-op threads 1 —
+    on a bounded sample of the configuration, plus BASELINE's C1 row (1 game, 50 sims, 1 thread)."""
+    from onitama_az.weights import random_weights
+    exe = ROOT / "oracle" / "build" / "oaz_cpu_baseline"
+    n, how, model = host_cpu()
+    threads = threads or n
+    with tempfile.TemporaryDirectory() as d:
+        wf = Path(d) / f"w{cfg['blocks']}.f32"
+        random_weights(0, cfg["blocks"]).astype("float32").tofile(wf)
+        run = lambda *a: json.loads(subprocess.run([str(exe), *map(str, a)], capture_output=True, text=True,
+                                                   check=True, timeout=600).stdout)
+        b = run("bench", wf, cfg["blocks"], cfg["sims"], threads, seconds, cfg["fixed_deck"])
+        w3 = Path(d) / "w3.f32"
+        random_weights(0, 3).astype("float32").tofile(w3)
+        c1 = run("c1", w3, 3, 50)
+    return {"value": b["sims_per_s"], "unit": "sims/s", "cores": threads, "kind": "port",
+            "games_per_s": b["games_per_s"], "cpu_model": model, "cores_detected": how,
+            "sample": f"{b['seconds']:.1f}s of self-play on {threads} worker threads (one game each, searches "
+                      f"sequential, batch-1 libtorch-CPU forward per simulation, intra-op threads 1; "
+                      f"{cfg['blocks']}-block random-init, {cfg['sims']} sims/move, c_puct 5, root noise): "
+                      f"{b['sims']} sims, {b['plies']} plies, {b['games']} games finished",
+            "c1": dict(c1, config="BASELINE C1: 1 game, 50 sims/move, 3-block random-init, fixed deck, 1 thread"),
+            "implementation": "oracle/cpu_baseline.cpp (C restatement of mcts_arena.rs + ATen CPU ops; the Rust/tch "
+                              "binary cannot be built here)"}
 
 
 TRAIN_METRIC = "training samples/sec (SGD steps of batch 512, forward(train) + alphaloss + backward + SGD)"
@@ -599,8 +646,7 @@ def main():
         if not args.no_exact and world == 1 and cfg["precision"] in ("fp32_split16", "fp32_split"):
             out["exact_fp32"] = exact_fp32_leg(args, cfg, local)
         if not args.no_cpu_baseline and world == 1:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, threads)
+            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -253,8 +253,11 @@ static void pack_conv64_split(const FoldedConv& f, std::vector<float>& out) {
 }
 
 // fp16 split (OAZ_FP32_SPLIT16): hi = fp16(x) (round to nearest even), lo = fp16(x - hi); the same
-// split as epilogue_h3_pack in oaz_nn.hip. Weights are first scaled by s = 2^k per output channel
-// (max |w s| in [1, 2)); 1/s is stored for the epilogue.
+// split as epilogue_h3_pack in oaz_nn.hip. Weights are first scaled by s = 2^k per output channel so
+// that max |w s| lies in [2^14, 2^15): the top of fp16's range (products with activations < 65504
+// stay far inside fp32), which keeps hi normal for weights down to 2^-28 of the channel's largest and
+// bounds each weight's representation error by 2^-25 / s = 2^-39 max|w| (a channel with one huge
+// weight no longer pushes its ordinary weights into fp16 subnormals). 1/s is stored for the epilogue.
 static void split16_host(float x, uint16_t out[2]) {
     const _Float16 h = (_Float16)x;
     const _Float16 l = (_Float16)(x - (float)h);
@@ -270,8 +273,9 @@ static float pow2_scale(const float* w, size_t n, size_t stride, float* inv) {
     }
     int e = 0;
     (void)frexpf(mx, &e);  // mx = f 2^e, f in [0.5, 1)
-    *inv = ldexpf(1.0f, e - 1);
-    return ldexpf(1.0f, 1 - e);
+    if (e < -100) e = -100;  // keep s and 1/s normal floats
+    *inv = ldexpf(1.0f, e - 15);
+    return ldexpf(1.0f, 15 - e);
 }
 
 // Split16 B fragments: [tap][K-half m][piece p][N-tile][lane] f16x8, lane l supplying

@@ -1483,7 +1483,7 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_x6(const oaz_state* __rest
 // v_mfma_f32_16x16x32_f16 (fp16 x fp16 products are exact in fp32, fp32 accumulation); lo*lo is
 // below 2^-22 relative. One K=32 block costs 3 x 16 cycles (half of k_nn_x6's six products).
 // fp16's exponent range is the price: conv weights are scaled per output channel by a power of two
-// s (max |w s| in [1, 2), exact) and the epilogue multiplies by 1/s (exact); activations below 2^-14
+// s (max |w s| in [2^14, 2^15), exact) and the epilogue multiplies by 1/s (exact); activations below 2^-14
 // fall into fp16 subnormals (absolute error <= 2^-25 per term, below the fp32 rounding of the dot
 // products); an activation >= 65504 would overflow, so every lane tracks the largest value it
 // splits and raises range_flag (the engine reports OAZ_ERR_RANGE, never a silent result).

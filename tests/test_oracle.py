@@ -157,3 +157,22 @@ def test_oracle_selfplay_game_semantics(orc):
             assert plies == 152 and np.all(samples["z"] == 0)
     samples, res, plies, _ = orc.selfplay_game(cfg, 0, max_plies=2)  # cut after max_plies + 2 plies
     assert plies <= 4 and (res in (1, 2) or (plies == 4 and np.all(samples["z"] == 0)))
+
+
+def test_cpu_baseline_libtorch_evaluator_matches_goldens(nn_golden, trained3, tmp_path):
+    """bench.py's cpu_baseline program (oracle/cpu_baseline.cpp: batch-1 ATen CPU forwards, the
+    reference's execution shape) evaluates the golden positions within 1e-5 of the torch goldens,
+    so its sims/s are those of the same network."""
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "build" / "oaz_cpu_baseline"
+    if not exe.exists():
+        pytest.skip("oaz_cpu_baseline not built (torch headers absent)")
+    wf, sf, of = tmp_path / "w.f32", tmp_path / "s.bin", tmp_path / "o.f32"
+    trained3.astype(np.float32).tofile(wf)
+    nn_golden["states"].tofile(sf)
+    subprocess.run([str(exe), "nn", str(wf), "3", str(sf), str(of)], check=True, timeout=120)
+    out = np.fromfile(of, dtype=np.float32).reshape(-1, 51)
+    assert len(out) == 256
+    assert np.abs(out[:, :50] - nn_golden["policy_trained3"].reshape(256, 50)).max() < 1e-5
+    assert np.abs(out[:, 50] - nn_golden["value_trained3"]).max() < 1e-5
