@@ -237,6 +237,11 @@ int oaz_encode(const oaz_state* s, int n, float* planes);
 oaz_engine* oaz_create(const oaz_config* cfg, int device);
 void oaz_destroy(oaz_engine* eng);
 int oaz_get_config(const oaz_engine* eng, oaz_config* out);
+/* Per-agent search parameters for the following searches / self-play plies (AlphaZeroMctsConfig,
+ * alphazero_mcts/mod.rs:26-43: max_playouts <= the creation cfg.sims, exploration_c, train), so
+ * agents with different configs can share one engine as the reference's agents share one
+ * Arc<Mutex<ConvResNet>> (mod.rs:84,124). */
+int oaz_set_search_params(oaz_engine* eng, int sims, double c_puct, int train_noise);
 /* Weights in canonical order (n == oaz_weight_count). BN is folded on the host. */
 int oaz_load_weights(oaz_engine* eng, const float* blob, size_t n);
 int oaz_sync(oaz_engine* eng);
@@ -354,6 +359,14 @@ int oaz_trainer_grads(oaz_trainer* t, float** dev_grads, size_t* n);
 int oaz_trainer_get_grads(oaz_trainer* t, float* host, size_t n);
 /* SGD step on the gradient buffer (scaled by grad_scale, e.g. 1/world after a sum all-reduce). */
 int oaz_trainer_apply(oaz_trainer* t, float grad_scale);
+/* BN running statistics (running_mean + running_var of every BN layer, canonical order) as one
+ * contiguous device range of oaz_trainer_bn_stats_count(blocks) floats, so a data-parallel host can
+ * average them over ranks (pack, oaz_comm_allreduce_sum_f32, unpack with scale = 1/world) and every
+ * rank keeps identical inference weights (ranks' batch statistics differ; DDP without SyncBN). Both
+ * run on the trainer's stream. */
+size_t oaz_trainer_bn_stats_count(int blocks);
+int oaz_trainer_bn_stats_pack(oaz_trainer* t, float* dev_out);
+int oaz_trainer_bn_stats_unpack(oaz_trainer* t, const float* dev_in, float scale);
 /* backward(b) + apply(1) for batches [first, first+count). */
 int oaz_trainer_train(oaz_trainer* t, int first, int count);
 /* Loss sums since the last call: out[0] value loss, out[1] policy loss, out[2] steps. */

@@ -612,6 +612,7 @@ struct oaz_engine {
     hipEvent_t ev_nn[2] = {nullptr, nullptr}, ev_join = nullptr;
     float* noise = nullptr;              // [2][kNoiseChunk][G][kNoiseStride]
     uint32_t G = 0, cap = 0, pathcap = 0, hcap = 0, out_cap = 0;
+    int32_t sims_cap = 0;                // cfg.sims at creation: trees and paths are sized for it
     // trees
     oaz_node* nodes = nullptr;
     uint32_t *n_nodes = nullptr, *path = nullptr, *depth = nullptr, *leaf = nullptr;
@@ -798,6 +799,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
     e->cfg = *cfg;
     e->device = device;
     e->G = (uint32_t)cfg->games;
+    e->sims_cap = cfg->sims;
     e->cap = 1u + (uint32_t)cfg->sims * OAZ_MAX_MOVES;  // each playout expands <= 1 node of <= 40 children
     e->pathcap = (uint32_t)cfg->sims + 1;               // depth grows by <= 1 per playout
     e->hcap = (uint32_t)cfg->max_plies + 2;             // train.rs:74-79 cut after max_plies+2 plies
@@ -885,6 +887,23 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->stream3) (void)hipStreamDestroy(e->stream3);
     delete e;
+}
+
+extern "C" int oaz_set_search_params(oaz_engine* e, int sims, double c_puct, int train_noise) {
+    if (!e) return oaz_set_err(OAZ_ERR_ARG, "set_search_params: null");
+    if (sims < 1 || sims > e->sims_cap)
+        return oaz_set_err(OAZ_ERR_ARG, "set_search_params: sims %d outside [1, %d] (the creation budget)", sims,
+                           e->sims_cap);
+    if (!(c_puct >= 0.0) || !std::isfinite(c_puct)) return oaz_set_err(OAZ_ERR_ARG, "set_search_params: bad c_puct");
+    if (train_noise && !e->noise) {  // the engine was made without root noise: its ring comes now
+        HIP_TRY(hipSetDevice(e->device));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        if (dalloc(&e->noise, 2 * kNoiseChunk * (size_t)e->G * kNoiseStride)) return OAZ_ERR_HIP;
+    }
+    e->cfg.sims = sims;
+    e->cfg.c_puct = c_puct;
+    e->cfg.train_noise = train_noise ? 1 : 0;
+    return 0;
 }
 
 extern "C" int oaz_get_config(const oaz_engine* e, oaz_config* out) {

@@ -1301,6 +1301,55 @@ static int apply(oaz_trainer* t, float scale) {
     return 0;
 }
 
+// BN running statistics <-> one contiguous range (data-parallel epoch-end average over ranks).
+// Segments: per conv layer running_mean[64] running_var[64] (adjacent in the canonical blob), then
+// the value head's (1 + 1) and the policy head's (2 + 2).
+struct BnSegs {
+    int n;
+    int off[kMaxConv + 2], len[kMaxConv + 2];
+};
+static BnSegs bn_segs(const oaz_trainer* t) {
+    BnSegs s{};
+    for (int l = 0; l < t->nconv; ++l) {
+        s.off[s.n] = (int)t->L.brm[l];
+        s.len[s.n++] = 2 * kC;
+    }
+    s.off[s.n] = t->L.h.vrm;
+    s.len[s.n++] = 2;
+    s.off[s.n] = t->L.h.prm;
+    s.len[s.n++] = 4;
+    return s;
+}
+__global__ void k_bn_stats_io(float* P, float* buf, BnSegs s, int unpack, float scale) {
+    int base = 0;
+    for (int k = 0; k < s.n; ++k) {
+        for (int i = threadIdx.x; i < s.len[k]; i += blockDim.x) {
+            if (unpack) P[s.off[k] + i] = scale * buf[base + i];
+            else buf[base + i] = P[s.off[k] + i];
+        }
+        base += s.len[k];
+    }
+}
+
+extern "C" size_t oaz_trainer_bn_stats_count(int blocks) { return (size_t)(1 + 2 * blocks) * 2 * kC + 2 + 4; }
+
+extern "C" int oaz_trainer_bn_stats_pack(oaz_trainer* t, float* dev_out) {
+    if (!t || !dev_out) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
+    HIP_TRY(hipSetDevice(t->device));
+    hipLaunchKernelGGL(k_bn_stats_io, dim3(1), dim3(256), 0, t->st, t->P, dev_out, bn_segs(t), 0, 1.0f);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+extern "C" int oaz_trainer_bn_stats_unpack(oaz_trainer* t, const float* dev_in, float scale) {
+    if (!t || !dev_in) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
+    HIP_TRY(hipSetDevice(t->device));
+    hipLaunchKernelGGL(k_bn_stats_io, dim3(1), dim3(256), 0, t->st, t->P, const_cast<float*>(dev_in), bn_segs(t), 1,
+                       scale);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 extern "C" int oaz_trainer_apply(oaz_trainer* t, float grad_scale) {
     if (!t) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
     HIP_TRY(hipSetDevice(t->device));

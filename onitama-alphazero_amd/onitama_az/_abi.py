@@ -205,6 +205,7 @@ _PROTOS = {
     "oaz_create": (_VOIDP, [_P(oaz_config), C.c_int]),
     "oaz_destroy": (None, [_VOIDP]),
     "oaz_get_config": (C.c_int, [_VOIDP, _P(oaz_config)]),
+    "oaz_set_search_params": (C.c_int, [_VOIDP, C.c_int, C.c_double, C.c_int]),
     "oaz_load_weights": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
     "oaz_sync": (C.c_int, [_VOIDP]),
     "oaz_set_timing": (C.c_int, [_VOIDP, C.c_int]),
@@ -244,6 +245,9 @@ _PROTOS = {
     "oaz_trainer_grads": (C.c_int, [_VOIDP, _P(C.c_void_p), _P(C.c_size_t)]),
     "oaz_trainer_get_grads": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
     "oaz_trainer_apply": (C.c_int, [_VOIDP, C.c_float]),
+    "oaz_trainer_bn_stats_count": (C.c_size_t, [C.c_int]),
+    "oaz_trainer_bn_stats_pack": (C.c_int, [_VOIDP, _VOIDP]),
+    "oaz_trainer_bn_stats_unpack": (C.c_int, [_VOIDP, _VOIDP, C.c_float]),
     "oaz_trainer_train": (C.c_int, [_VOIDP, C.c_int, C.c_int]),
     "oaz_trainer_losses": (C.c_int, [_VOIDP, _P(C.c_double * 3)]),
     "oaz_trainer_sync": (C.c_int, [_VOIDP]),

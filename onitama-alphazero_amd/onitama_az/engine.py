@@ -65,6 +65,10 @@ class Engine:
         blob = np.ascontiguousarray(blob, dtype=np.float32)
         _abi.check(self._lib.oaz_load_weights(self._h, _abi.ptr(blob), blob.size))
 
+    def set_search_params(self, sims: int, c_puct: float, train_noise: bool) -> None:
+        """Per-agent AlphaZeroMctsConfig for the next searches (sims <= the creation budget)."""
+        _abi.check(self._lib.oaz_set_search_params(self._h, int(sims), float(c_puct), int(bool(train_noise))))
+
     def sync(self) -> None:
         _abi.check(self._lib.oaz_sync(self._h))
 

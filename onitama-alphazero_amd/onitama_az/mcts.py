@@ -94,18 +94,23 @@ class ConvResNet:
 
 
 def _search_engine(cache: dict, config: AlphaZeroMctsConfig, model: ConvResNet, games: int) -> Engine:
-    key = (games, config.max_playouts, config.exploration_c, config.train, model.config.resnet_block_amnt,
-           model.options.device, id(model.weights))
-    eng = cache.get("engine")
-    if eng is None or cache.get("key") != key:
+    """The model's search engine, shared by every agent that uses the model (the reference shares
+    one Arc<Mutex<ConvResNet>> between agent clones, mod.rs:84,124): it is rebuilt only when the
+    batch or the simulation budget outgrows it; each agent's AlphaZeroMctsConfig is applied with
+    oaz_set_search_params before its search."""
+    shared = model.__dict__.setdefault("_search", {})
+    key = (model.config.resnet_block_amnt, model.options.device, model.options.precision, id(model.weights))
+    eng = shared.get("engine")
+    if eng is None or shared.get("key") != key or shared["games"] < games or shared["sims"] < config.max_playouts:
         if eng is not None:
             eng.close()
-        eng = Engine(device=model.options.device, games=games, sims=config.max_playouts,
-                     c_puct=config.exploration_c, train_noise=int(config.train),
-                     blocks=model.config.resnet_block_amnt, evaluator=_abi.EVAL_NN,
+        g, n = max(games, shared.get("games", 0)), max(config.max_playouts, shared.get("sims", 0))
+        eng = Engine(device=model.options.device, games=g, sims=n, c_puct=config.exploration_c,
+                     train_noise=int(config.train), blocks=model.config.resnet_block_amnt, evaluator=_abi.EVAL_NN,
                      precision=model.options.precision)
         eng.load_weights(model.weights)
-        cache["engine"], cache["key"] = eng, key
+        shared.update(engine=eng, key=key, games=g, sims=n)
+    eng.set_search_params(config.max_playouts, config.exploration_c, config.train)
     return eng
 
 

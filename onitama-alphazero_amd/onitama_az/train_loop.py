@@ -5,6 +5,13 @@ Per iteration: self-play with the best model (all games in parallel on the GPU, 
 across iterations as the reference keeps `opt`), every `evaluation_checkpoint` iterations a pit
 against the best model, random and MCTS (promotion when the winrate beats `winrate_percent`), and
 `.ot` checkpoints with `save_vs` names. Statistics mirror `stats.rs` (saved as JSON).
+
+Multi-GPU (one process per GPU under torchrun, `rank`/`world`): every rank self-plays its share of
+the iteration's games (global game ids, `oaz_selfplay_run`), the samples are all-gathered so every
+rank holds the whole buffer in the same order (the join of train.rs:241-244), the epochs run data
+parallel (`train_epochs_dp`: sharded batches, gradient all-reduce, BN statistics averaged), so every
+rank ends the epochs with identical weights; rank 0 plays the pit and broadcasts the promotion
+decision and ratings, and only rank 0 writes checkpoints and statistics.
 """
 from __future__ import annotations
 
@@ -22,7 +29,7 @@ from .engine import Engine
 from .evaluator import EvaluatorConfig, Evaluator, PitStatistics
 from .game import Deck
 from .mcts import AlphaZeroMctsConfig, ConvResNet, ConvResNetConfig, Options
-from .trainer import Trainer, train_epochs
+from .trainer import Trainer, train_epochs, train_epochs_dp
 from .weights import checkpoint_path, random_weights, save_blob_ot
 
 
@@ -62,13 +69,30 @@ class Stats:  # stats.rs:7-24
             json.dump(dataclasses.asdict(self), f, default=float)
 
 
+def _bcast(obj, world: int):
+    """Rank 0's object on every rank (the pit result, the new best weights)."""
+    if world == 1:
+        return obj
+    import torch.distributed as dist
+    box = [obj]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
+
+
 def train(config: LoopConfig, folder: Optional[str] = None, options: Options = None,
-          initial_weights: Optional[np.ndarray] = None, eval_sims: int = 400) -> Stats:
-    """train.rs:158-412. Returns the statistics (also written to <folder>/stats.json)."""
+          initial_weights: Optional[np.ndarray] = None, eval_sims: int = 400, rank: int = 0, world: int = 1,
+          comm=None, on_iteration=None) -> Stats:
+    """train.rs:158-412. Returns the statistics (also written to <folder>/stats.json by rank 0).
+    world > 1: an initialised torch.distributed group (rank, world); `comm` (onitama_az.dist.Comm,
+    RCCL) carries the sample all-gather and the gradient all-reduce, without it they go over the
+    default group through host copies (gloo tests / one-GPU rehearsals). on_iteration(it, new, best),
+    if given, sees each iteration's trained and best weights (tests)."""
+    from .dist import allgather_samples
     options = options or Options()
     blocks = config.model_config.resnet_block_amnt
-    folder = folder or os.path.join("models", time.strftime("%Y%m%d_%H%M%S"))
-    os.makedirs(folder, exist_ok=True)
+    folder = _bcast(folder or os.path.join("models", time.strftime("%Y%m%d_%H%M%S")), world)
+    if rank == 0:
+        os.makedirs(folder, exist_ok=True)
     weights = np.asarray(initial_weights if initial_weights is not None else random_weights(config.seed, blocks),
                          dtype=np.float32)
     best = weights.copy()
@@ -81,18 +105,29 @@ def train(config: LoopConfig, folder: Optional[str] = None, options: Options = N
         tr.set_weights(weights)
         for it in range(1, config.iterations + 1):
             # self-play with the best model (train.rs:210-250)
-            kw = dict(games=max(1, min(n_games, 65536)), sims=mc.max_playouts, c_puct=mc.exploration_c,
+            per_rank = (n_games + world - 1) // world
+            kw = dict(games=max(1, min(per_rank, 65536)), sims=mc.max_playouts, c_puct=mc.exploration_c,
                       train_noise=int(mc.train), blocks=blocks, max_plies=config.max_plies, evaluator=_abi.EVAL_NN,
-                      precision=options.precision, seed=config.seed + it)
+                      precision=options.precision, seed=config.seed + it, rank=rank, world=world,
+                      sample_capacity=max(1, per_rank) * (config.max_plies + 2))
             if config.deck is not None:
                 kw.update(fixed_deck=1, deck=config.deck.indices())
             with Engine(device=options.device, **kw) as eng:
                 eng.load_weights(best)
-                samples, _ = eng.selfplay_run(n_games, cap=n_games * (config.max_plies + 2))
+                if world == 1:
+                    samples, _ = eng.selfplay_run(n_games, cap=n_games * (config.max_plies + 2))
+                else:  # this rank's share, left on the device, then every rank's samples in rank order
+                    import torch
+                    eng.selfplay_run(n_games, cap=0)
+                    samples = allgather_samples(eng, world, torch.device("cuda", options.device), comm=comm)
             stats.games_played.append({"games_amnt": n_games, "positions_retrieved": int(len(samples))})
             # training epochs (train.rs:257-325)
-            hist = train_epochs(tr, samples, epochs=config.training_epochs, batch=config.train_batch_size,
-                                seed=config.seed + 1000 + it)
+            if world == 1:
+                hist = train_epochs(tr, samples, epochs=config.training_epochs, batch=config.train_batch_size,
+                                    seed=config.seed + 1000 + it)
+            else:
+                hist = train_epochs_dp(tr, samples, epochs=config.training_epochs, batch=config.train_batch_size,
+                                       seed=config.seed + 1000 + it, rank=rank, world=world, comm=comm)
             k = max(1, len(hist))
             stats.iteration.append(it)
             stats.loss.append(sum(h.loss for h in hist) / k)
@@ -101,19 +136,27 @@ def train(config: LoopConfig, folder: Optional[str] = None, options: Options = N
             new = tr.get_weights()
             # evaluation (train.rs:340-377)
             if it % config.evaluation_checkpoint == 0:
-                ev = Evaluator(config.evaluator_config, ConvResNet(config.model_config, options, best),
-                               ConvResNet(config.model_config, options, new), ratings)
-                pit, promote = ev.pit(sims=eval_sims)
+                if rank == 0:
+                    ev = Evaluator(config.evaluator_config, ConvResNet(config.model_config, options, best),
+                                   ConvResNet(config.model_config, options, new), ratings)
+                    pit, promote = ev.pit(sims=eval_sims)
+                else:
+                    pit, promote = None, None
+                pit, promote = _bcast((pit, promote), world)  # one decision for every rank
                 ratings = [(pit.self_fight.rating_a, pit.self_fight.rating_b),
                            (pit.random_fight.rating_a, pit.random_fight.rating_b),
                            (pit.mcts_fight.rating_a, pit.mcts_fight.rating_b)]
                 stats.was_best_change.append(bool(promote))
                 stats.fight_statistics.append(pit)
                 if promote:
-                    save_blob_ot(checkpoint_path(folder, it, True, time.strftime("%Y%m%d_%H%M%S")), new, blocks)
+                    if rank == 0:
+                        save_blob_ot(checkpoint_path(folder, it, True, time.strftime("%Y%m%d_%H%M%S")), new, blocks)
                     best = new.copy()
                     ratings[0] = (ratings[0][0], ratings[0][0])  # best inherits the new rating (train.rs:366-367)
-            if it % config.save_checkpoint == 0:
+            if it % config.save_checkpoint == 0 and rank == 0:
                 save_blob_ot(checkpoint_path(folder, it, False, time.strftime("%Y%m%d_%H%M%S")), new, blocks)
-            stats.save(os.path.join(folder, "stats.json"))
+            if rank == 0:
+                stats.save(os.path.join(folder, "stats.json"))
+            if on_iteration is not None:
+                on_iteration(it, new, best)
     return stats

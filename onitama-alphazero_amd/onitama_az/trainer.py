@@ -7,9 +7,10 @@ replacement; seeded numpy here, the reference uses thread_rng), each one
 weight decay l2_const (train.rs:181-186). Every step runs in libonitama_az.so
 (oaz_trainer_*, csrc/oaz_train.hip); this module only draws indices and keeps statistics.
 
-Data-parallel training (`world > 1`): every rank runs backward on its own batch shard, the
-flat gradient buffer is all-reduced (torch.distributed, RCCL on ROCm) on the trainer's stream,
-then every rank applies the same SGD step (grad_scale = 1/world).
+Data-parallel training (`world > 1`, train_epochs_dp): every rank runs backward on its own batch
+shard, the flat gradient buffer is all-reduced (the C ABI's RCCL communicator, oaz_comm_*) on the
+trainer's stream, then every rank applies the same SGD step (grad_scale = 1/world); BN running
+statistics and losses are averaged over ranks after each epoch.
 """
 from __future__ import annotations
 
@@ -156,19 +157,39 @@ class _DeviceArray:
                                          "strides": None}
 
 
-def train_epochs_dp(trainer: Trainer, samples: np.ndarray, epochs: int, batch: int, seed: int, rank: int,
-                    world: int) -> List[EpochLoss]:
-    """Data-parallel epochs: the global batch `batch` is split into `world` shards of
-    batch/world samples; the gradient buffer is summed with an RCCL all-reduce and applied with
-    grad_scale 1/world. All ranks draw the same index stream (same seed) and take their shard.
-    BN batch statistics are per shard (as DDP without SyncBatchNorm)."""
+def _allreduce_sum(t, comm, stream: int) -> None:
+    """Sum over ranks in place: the C ABI's RCCL communicator on `stream`, or (no comm: gloo CPU
+    tests / one-GPU rehearsals) torch.distributed through a host copy."""
     import torch
     import torch.distributed as dist
+    if comm is not None:
+        comm.allreduce_sum_(t, stream)
+        return
+    torch.cuda.current_stream().synchronize()
+    h = t.cpu()
+    dist.all_reduce(h)
+    t.copy_(h.to(t.device))
+
+
+def train_epochs_dp(trainer: Trainer, samples: np.ndarray, epochs: int, batch: int, seed: int, rank: int,
+                    world: int, comm=None) -> List[EpochLoss]:
+    """Data-parallel epochs (train.rs:264-325 over `world` GPUs): the global batch `batch` is split
+    into `world` shards of batch/world samples; the gradient buffer is summed over ranks (RCCL via
+    `comm`, an onitama_az.dist.Comm) and applied with grad_scale 1/world, so every rank takes the
+    same SGD step. All ranks draw the same index stream (same seed, same gathered `samples`) and take
+    their shard. BN batch statistics are per shard (DDP without SyncBatchNorm); the running
+    statistics are averaged over ranks after each epoch, and the reported losses are the global
+    ones, so every rank ends each epoch with identical weights and statistics."""
+    import torch
     assert batch % world == 0 and (batch // world) % 16 == 0
     shard = batch // world
-    trainer.set_stream(torch.cuda.current_stream().cuda_stream)
+    stream = torch.cuda.current_stream().cuda_stream
+    trainer.set_stream(stream)
+    dev = f"cuda:{torch.cuda.current_device()}"
     ptr, n = trainer.grads_device()
-    grads = torch.as_tensor(_DeviceArray(ptr, n), device=f"cuda:{torch.cuda.current_device()}")
+    grads = torch.as_tensor(_DeviceArray(ptr, n), device=dev)
+    nbn = int(trainer._lib.oaz_trainer_bn_stats_count(trainer.blocks))
+    bn = torch.empty(nbn, dtype=torch.float32, device=dev)
     rng = np.random.default_rng(seed)
     trainer.load_samples(samples)
     out: List[EpochLoss] = []
@@ -180,8 +201,19 @@ def train_epochs_dp(trainer: Trainer, samples: np.ndarray, epochs: int, batch: i
         trainer.set_batches(idx)
         for b in range(nb):
             trainer.backward(b)
-            dist.all_reduce(grads)
+            if world > 1:
+                _allreduce_sum(grads, comm, stream)
             trainer.apply(1.0 / world)
         v, p, k = trainer.losses()
+        if world > 1:
+            trainer._check(trainer._lib.oaz_trainer_bn_stats_pack(trainer._h, C.c_void_p(bn.data_ptr())))
+            _allreduce_sum(bn, comm, stream)
+            trainer._check(trainer._lib.oaz_trainer_bn_stats_unpack(trainer._h, C.c_void_p(bn.data_ptr()),
+                                                                    C.c_float(1.0 / world)))
+            tot = torch.tensor([v, p], dtype=torch.float32, device=dev)
+            _allreduce_sum(tot, comm, stream)
+            torch.cuda.current_stream().synchronize()
+            v, p = (float(x) / world for x in tot.tolist())
         out.append(EpochLoss((v + p) / k, v / k, p / k, k))
+    trainer.sync()
     return out

@@ -474,3 +474,19 @@ print("legacy ok")
     env = dict(__import__("os").environ, OAZ_TREE_SEG="0")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "legacy ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_set_search_params_per_agent_config(orc):
+    """oaz_set_search_params: one engine (created for 64 sims, no noise) serves searches with other
+    AlphaZeroMctsConfigs (32 sims, c = 2, noise on) exactly as an engine made for them would."""
+    roots = random_positions(orc, 6, seed=1212)
+    with Engine(games=6, sims=64, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0, seed=5) as e:
+        e.set_search_params(32, 2.0, True)
+        r = e.search(roots)
+        for g in range(6):
+            cfg = orc.search_cfg(sims=32, c_puct=2.0, evaluator=orc.EVAL_HASH, train_noise=1, seed=5, game_id=g, ply=0)
+            mv, pi, nodes, _ = orc.search(cfg, roots[g])
+            _compare_trees(e, g, nodes)
+            assert _mv(r.moves[g]) == _mv(mv)
+        with pytest.raises(_abi.OazError):
+            e.set_search_params(65, 2.0, False)  # beyond the creation budget
