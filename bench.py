@@ -305,7 +305,9 @@ def train_main(args, world, rank, local):
     samples["z"] = rng.integers(-1, 2, n_samples).astype(np.float32)
     tr = Trainer(blocks=blocks, max_batch=shard, device=local)
     tr.set_weights(random_weights(0, blocks))
-    tr.set_stream(torch.cuda.current_stream().cuda_stream)
+    ts = torch.cuda.Stream()  # explicit: handle 0 would leave the trainer on its own, unordered stream
+    torch.cuda.set_stream(ts)
+    tr.set_stream(ts.cuda_stream)
     tr.load_samples(samples)
     nb = args.warmup + args.steps
     idx = choose_batches(np.random.default_rng(1), n_samples, B, nb)[:, rank * shard:(rank + 1) * shard]

@@ -183,7 +183,19 @@ def train_epochs_dp(trainer: Trainer, samples: np.ndarray, epochs: int, batch: i
     import torch
     assert batch % world == 0 and (batch // world) % 16 == 0
     shard = batch // world
-    stream = torch.cuda.current_stream().cuda_stream
+    # one explicit stream for the trainer's kernels, the collectives and the torch copies (the legacy
+    # default stream, handle 0, would mean "the trainer's own stream" to oaz_trainer_set_stream and
+    # leave the all-reduce unordered against backward / apply)
+    ts = torch.cuda.Stream()
+    with torch.cuda.stream(ts):
+        out = _epochs_dp(trainer, samples, epochs, batch, seed, rank, world, comm, shard, ts.cuda_stream)
+    trainer.sync()
+    trainer.set_stream(None)
+    return out
+
+
+def _epochs_dp(trainer, samples, epochs, batch, seed, rank, world, comm, shard, stream) -> List[EpochLoss]:
+    import torch
     trainer.set_stream(stream)
     dev = f"cuda:{torch.cuda.current_device()}"
     ptr, n = trainer.grads_device()
@@ -215,5 +227,4 @@ def train_epochs_dp(trainer: Trainer, samples: np.ndarray, epochs: int, batch: i
             torch.cuda.current_stream().synchronize()
             v, p = (float(x) / world for x in tot.tolist())
         out.append(EpochLoss((v + p) / k, v / k, p / k, k))
-    trainer.sync()
     return out
