@@ -422,11 +422,12 @@ static int pack_weights(const float* raw, int blocks, int precision, std::vector
         out.resize(base + h.size() / 2);
         memcpy(out.data() + base, h.data(), h.size() * sizeof(uint16_t));
         for (int k = 0; k < 4; ++k) out.push_back(inv[k]);
-        // k_nn_h3 first layer, constant planes on fp16 MFMA: A fragments [square][piece][N-tile][lane]
-        // f16x8, lane l supplying A[row co = 16nt + (l&15)][k = 8(l>>4) + e] = piece of s_co T[sq][k][co]
-        // (k < 17: the 16 card planes and the colour plane; T = the first-layer table above), then
-        // s[64] (applied to the fp32 bitboard weights in the kernel) and 1/s[64]; s = 2^k per output
-        // channel over the bitboard weights and the table
+        // k_nn_h3 first layer on fp16 MFMA: K block 0 = [piece][N-tile][lane] f16x8, lane l supplying
+        // A[row co = 16nt + (l&15)][k = 8q + e] (q = l>>4) = piece of s_co W[co][bitboard plane q][tap e];
+        // K block 1 per square = [square][piece][N-tile][lane] f16x8 with k = 8q + e: e = 0 tap 8 of
+        // plane q, e >= 1 the table T[sq][c = 7q + e - 1][co] (c < 17: the 16 card planes and the
+        // colour plane summed over the square's on-board taps); then 1/s[64]. s = 2^k per output
+        // channel over all of them (max |s w| in [2^14, 2^15)).
         const float* r1 = raw;  // (fold advances its pointer)
         FoldedConv f1 = fold(r1, 64, 21, 9);
         std::vector<float> T((size_t)25 * 17 * 64);
@@ -452,21 +453,27 @@ static int pack_weights(const float* raw, int blocks, int precision, std::vector
                 for (int c = 0; c < 17; ++c) mx = fmaxf(mx, fabsf(T[((size_t)sq * 17 + c) * 64 + co]));
             s1[co] = pow2_scale(&mx, 1, 1, &inv1[co]);
         }
-        std::vector<uint16_t> h1;
-        for (int sq = 0; sq < 25; ++sq)
+        auto frag = [&](int blk, int sq, std::vector<uint16_t>& h1) {  // blk 0 (sq unused) or 1
             for (int pcs = 0; pcs < 2; ++pcs)
                 for (int nt = 0; nt < 4; ++nt)
                     for (int l = 0; l < 64; ++l)
                         for (int e = 0; e < 8; ++e) {
-                            const int co = nt * 16 + (l & 15), k = 8 * (l >> 4) + e;
+                            const int co = nt * 16 + (l & 15), q = l >> 4;
+                            float w = 0.0f;
+                            if (blk == 0) w = f1.w[((size_t)co * 21 + q) * 9 + e];
+                            else if (e == 0) w = f1.w[((size_t)co * 21 + q) * 9 + 8];
+                            else if (7 * q + e - 1 < 17) w = T[((size_t)sq * 17 + 7 * q + e - 1) * 64 + co];
                             uint16_t sp[2];
-                            split16_host(k < 17 ? T[((size_t)sq * 17 + k) * 64 + co] * s1[co] : 0.0f, sp);
+                            split16_host(w * s1[co], sp);  // exact scaling
                             h1.push_back(sp[pcs]);
                         }
+        };
+        std::vector<uint16_t> h1;
+        frag(0, 0, h1);
+        for (int sq = 0; sq < 25; ++sq) frag(1, sq, h1);
         const size_t b1 = out.size();
         out.resize(b1 + h1.size() / 2);
         memcpy(out.data() + b1, h1.data(), h1.size() * sizeof(uint16_t));
-        for (int co = 0; co < 64; ++co) out.push_back(s1[co]);
         for (int co = 0; co < 64; ++co) out.push_back(inv1[co]);
     }
     if (out.size() != nn_packed_floats(blocks, precision)) return oaz_set_err(OAZ_ERR_STATE, "pack: size mismatch");

@@ -103,8 +103,14 @@ constexpr int kImageB = 2 * kPlaneB;           // 102,400 B
 constexpr int kLdsFloats = kImageB / 4 + nn::kWaves * nn::kScratch;  // 26,624 floats = 106,496 B
 constexpr size_t kW = 9 * 2 * 2 * 4 * 64 * 4;
 constexpr size_t kHeadB = 2 * 2 * 64 * 4 + 4;
-// first layer, constant planes: [square][piece][N-tile][lane] f16x8 of the scaled table, s[64], 1/s[64]
-constexpr size_t kL1C = 25 * 2 * 4 * 64 * 4 + 2 * nn::kCh;
+// first layer on fp16 MFMA (k_nn_h3, TR): K block 0 [piece][N-tile][lane] f16x8 (bitboard taps 0-7 of
+// plane q = lane >> 4, square-independent), K block 1 [square][piece][N-tile][lane] f16x8 (tap 8 of
+// plane q, then the 17 constant planes' table T[square]), all scaled by s = 2^k per output channel;
+// then 1/s[64]. The 0/1 B operands are built in-kernel (lut: LDS table of the 8-tap bit patterns).
+constexpr size_t kL1Frag = 2 * 4 * 64 * 4;            // one K block: 2 pieces x 4 N-tiles x 64 lanes x f16x8
+constexpr size_t kL1C = 26 * kL1Frag + nn::kCh;
+constexpr int kLutB = 256 * 16;                       // 256 patterns x f16x8
+constexpr int kLutOff = kLdsFloats * 4;               // after the image + scratch (the fallback's LDS)
 }  // namespace h3
 
 size_t nn_packed_floats(int blocks, int precision) {
@@ -1052,8 +1058,9 @@ struct H3PlanOf {
 // UNEVEN (8 waves): square groups 3 / 4 (15 / 10 squares) instead of 0 / 1, the bigger group at
 // s_setprio 1.
 template <int WAVES_, int KH_, int PIPE_, int DBG_ = 0, int UNEVEN_ = 0, int TR_ = 0, int PH_ = 1, int HV_ = 0,
-          int BF_ = 0>
+          int BF_ = 0, int PF_ = 0>
 struct X6Cfg {
+    static constexpr int PF = PF_;  // h3 + TR: the next conv's first B pieces load during this conv's last steps
     static constexpr int BF = BF_;  // h3 + TR: OAZ_BF16 mode (one bf16 piece, one product; C5)
     static constexpr int HV = HV_;  // h3 heads: 0 MLPs on MFMA (8 waves), 1 per-position VALU MLPs
     static constexpr int TR = TR_;
@@ -1557,6 +1564,9 @@ __device__ __forceinline__ X6W h3_w(const float* p, int lane, int nt, int bytes 
 __device__ __forceinline__ f16x8 h3_ldb(const X6W& w, int entry) {  // entry = (step * 2 + piece) * 4
     return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(w.r, w.voff, entry * 64 * 16, 0));
 }
+__device__ __forceinline__ f16x8 h3_ldb_at(const X6W& w, int bytes) {
+    return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(w.r, w.voff, bytes, 0));
+}
 
 template <class C, int GRP, int K>
 __device__ __forceinline__ void h3_step_b(const X6W& W, f16x8 (&b)[2], f16x8 (&bn)[2]) {
@@ -1592,8 +1602,17 @@ __device__ __forceinline__ void conv_h1_batch(f32x4 (&acc)[C::NS], const char* i
 template <class C, int GRP, int K, class E>
 __device__ __forceinline__ void conv_h3_batch(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
                                               f16x8 (&bn)[2], f16x8 (&X)[C::KH], f16x8 (&Y)[C::KH],
-                                              const int (&ab)[2][2], E& epi) {
+                                              const int (&ab)[2][2], E& epi, f16x8 (*carry)[2] = nullptr) {
     h3_step_b<C, GRP, K>(W, b, bn);
+    if constexpr (C::PF) {  // the last step run: prefetch the next conv's first pieces (one conv further on)
+        constexpr H3Batch B = H3P<C, GRP>::P.b[K];
+        constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
+        if constexpr (B.first && B.nstep < 0) {
+            constexpr int next = (int)((h3::kW + 2 * nn::kCh) * 4);  // bytes per conv
+            (*carry)[0] = h3_ldb_at(W, next + ((B0.t * 2 + B0.m) * 2 + 0) * 4 * 64 * 16);
+            (*carry)[1] = h3_ldb_at(W, next + ((B0.t * 2 + B0.m) * 2 + 1) * 4 * 64 * 16);
+        }
+    }
     h3_load<C, GRP, K>(Y, img, ab, 0);
     h3_mfma<C, GRP, K>(acc, X, b[0]);  // lo*hi
     if constexpr (K + 1 < H3P<C, GRP>::P.nbat) h3_load<C, GRP, K + 1>(X, img, ab, 1);
@@ -1623,7 +1642,7 @@ __device__ __forceinline__ void conv_h3_batch2(f32x4 (&acc)[C::NS], const char* 
 
 template <class C, int GRP, class E, int... K>
 __device__ __forceinline__ void conv_h3_run(f32x4 (&acc)[C::NS], const char* img, const X6W& W, const int (&lo)[2],
-                                            E& epi, std::integer_sequence<int, K...>) {
+                                            E& epi, std::integer_sequence<int, K...>, f16x8 (*carry)[2] = nullptr) {
     int ab[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -1641,8 +1660,13 @@ __device__ __forceinline__ void conv_h3_run(f32x4 (&acc)[C::NS], const char* img
         (void)epi;
         return;
     }
-    b[0] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 0) * 4);
-    b[1] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 1) * 4);
+    if constexpr (C::PF) {  // this conv's first pieces were loaded during the previous conv
+        b[0] = (*carry)[0];
+        b[1] = (*carry)[1];
+    } else {
+        b[0] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 0) * 4);
+        b[1] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 1) * 4);
+    }
     if constexpr (C::PIPE == 2) {
         f16x8 L[C::KH], H[C::KH], L2[C::KH], H2[C::KH];
         h3_load<C, GRP, 0>(L, img, ab, 1);
@@ -1653,7 +1677,7 @@ __device__ __forceinline__ void conv_h3_run(f32x4 (&acc)[C::NS], const char* img
     } else {
         f16x8 X[C::KH], Y[C::KH];
         h3_load<C, GRP, 0>(X, img, ab, 1);
-        (conv_h3_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab, epi), ...);
+        (conv_h3_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab, epi, carry), ...);
     }
 }
 
@@ -1830,6 +1854,84 @@ __device__ __forceinline__ void first_layer_h3t(f32x4 (&acc)[C::NS], const L1Reg
 }
 
 // The whole forward for the waves of square group GRP.
+// k_nn_h3 (TR) first layer, all on fp16 MFMA (conv_init_1, net.rs:16-27 / 119-131): for output square
+// sq the K dimension is (plane q, tap t) of the 4 bitboard planes and the 17 constant planes (the
+// mover's two cards and the colour plane, common.rs:26-80, summed over sq's on-board taps on the
+// host: T[sq]). Block 0 = taps 0-7 of plane q (k = 8q + t), block 1 = tap 8 of plane q (k = 32 + 8q)
+// and the constant planes (k = 32 + 8q + 1..7). A = weights (hi / lo of s * W), B = the 0/1 inputs,
+// exact in fp16: 4 MFMAs of 16 cycles per square instead of 9 fp32 16x16x4 MFMAs of 32 cycles. The
+// lane's 8 tap bits of block 0 are three 3-bit row fields of its plane's bitboard (rows of the board
+// are 5 contiguous bits, bit of square i = 1 << (31 - i)), gathered into an 8-bit index (board-edge
+// masks are compile-time per square) that selects the f16x8 operand from an LDS table.
+template <int SQ>
+__device__ __forceinline__ uint32_t l1_pattern(uint32_t bb) {
+    constexpr int r = SQ / 5, c = SQ % 5;
+    // index bits: 0 = tap 2, 1 = tap 1, 2 = tap 0, 3 = tap 5, 4 = tap 4, 5 = tap 3, 6 = tap 7, 7 = tap 6
+    uint32_t a = 0, d = 0;
+    if constexpr (r > 0) a = (bb >> (35 - SQ)) & 7u;  // squares SQ-6, SQ-5, SQ-4 (bits 2, 1, 0)
+    const uint32_t m = (bb >> (30 - SQ)) & 7u;        // SQ-1, SQ, SQ+1
+    if constexpr (r < 4) d = (bb >> (26 - SQ)) & 3u;  // SQ+4, SQ+5 (bits 1, 0)
+    const uint32_t idx = a | (m << 3) | (d << 6);
+    constexpr uint32_t mask = (c == 0 ? ~0xA4u : ~0u) & (c == 4 ? ~0x09u : ~0u) & 0xFFu;
+    return idx & mask;
+}
+template <int SQ>
+__device__ __forceinline__ uint32_t l1_tap8(uint32_t bb) {  // square SQ+6 (tap 8) as an fp16 0 / 1.0
+    if constexpr (SQ / 5 == 4 || SQ % 5 == 4) return 0u;
+    else return ((bb >> (25 - SQ)) & 1u) ? 0x3C00u : 0u;
+}
+__device__ __forceinline__ void l1_lut_build(char* lds, int tid) {  // entry P, element t: bit pos(t) of P
+    constexpr int pos[8] = {2, 1, 0, 5, 4, 3, 7, 6};
+    const int P = tid >> 1, h = tid & 1;
+    uint32_t w[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int t0 = 4 * h + 2 * k;
+        w[k] = (((P >> pos[t0]) & 1) ? 0x3C00u : 0u) | (((P >> pos[t0 + 1]) & 1) ? 0x3C000000u : 0u);
+    }
+    *reinterpret_cast<uint2*>(lds + h3::kLutOff + P * 16 + h * 8) = uint2{w[0], w[1]};
+}
+template <class C, int GRP, int... J>
+__device__ __forceinline__ void first_layer_h3f(f32x4 (&acc)[C::NS], const float* l1c, uint32_t bb, int cinfo,
+                                                int lane, int nt, const char* lds, std::integer_sequence<int, J...>) {
+    const int q = lane >> 4;
+    X6W A;
+    A.r = __builtin_amdgcn_make_buffer_rsrc((void*)l1c, (short)0, (int)(26 * h3::kL1Frag * 4), 0x00020000);
+    A.voff = (nt * 64 + lane) * 16;
+    auto ld = [&](int blk, int pc) {  // [blk][pc][nt][lane]
+        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(A.r, A.voff, (blk * 2 + pc) * 4 * 64 * 16, 0));
+    };
+    const f16x8 a0h = ld(0, 0), a0l = ld(0, 1);
+    f16x8 a1[grp_n(GRP)][2];
+    ((a1[J][0] = ld(1 + grp_sq(GRP, J), 0), a1[J][1] = ld(1 + grp_sq(GRP, J), 1)), ...);
+    // block 1 constants: element e >= 1 of quarter q is constant plane c = 7q + e - 1
+    const int c0 = cinfo & 15, c1 = (cinfo >> 4) & 15, blue = (cinfo >> 8) & 1;
+    uint32_t kw[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int e = 2 * w + h, c = 7 * q + e - 1;
+            const bool one = e > 0 && (c < 16 ? (c == c0 || c == c1) : (c == 16 && blue));
+            v |= one ? (0x3C00u << (16 * h)) : 0u;
+        }
+        kw[w] = v;
+    }
+    const char* lut = lds + h3::kLutOff;
+    auto sq_mfma = [&](auto jc) {
+        constexpr int j = decltype(jc)::value, sq = grp_sq(GRP, j);
+        const f16x8 b0 = *reinterpret_cast<const f16x8*>(lut + l1_pattern<sq>(bb) * 16);
+        uint4 w1 = uint4{kw[0] | l1_tap8<sq>(bb), kw[1], kw[2], kw[3]};
+        const f16x8 b1 = __builtin_bit_cast(f16x8, w1);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0h, b0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0l, b0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[j][0], b1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[j][1], b1, acc[j], 0, 0, 0);
+    };
+    (sq_mfma(std::integral_constant<int, J>{}), ...);
+}
+
 // Returns true in a lane that split an activation beyond the fp16 range (an fp16 hi term that
 // overflowed, or would have): the tile's results are then invalid and k_nn_h3 recomputes them.
 template <class C, int GRP>
@@ -1864,6 +1966,13 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
             tm = t;
         }
     };
+    f16x8 carry[2];  // PF: the first B pieces of the next conv (conv 0's load under the first layer)
+    if constexpr (C::PF && !C::BF) {
+        constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
+        const X6W W0 = h3_w(blob + nn::kL1B + nn::kCh + nn::kL1Table, lane, nt);
+        carry[0] = h3_ldb(W0, ((B0.t * 2 + B0.m) * 2 + 0) * 4);
+        carry[1] = h3_ldb(W0, ((B0.t * 2 + B0.m) * 2 + 1) * 4);
+    }
     {  // encoder + first layer (exact fp32 MFMA on the 0/1 inputs, as k_nn_x6)
         L1Regs<GRP> l1;
         first_layer_x6_fetch<GRP>(l1, blob, lane, nt);
@@ -1876,6 +1985,8 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
             const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
             pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
         }
+        if constexpr (C::TR && !C::BF)
+            for (int t = tid; t < 512; t += 64 * C::WAVES) l1_lut_build(img, t);
         const float bias1 = blob[nn::kL1B + co];
         const f32x4 bias1t = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
         __syncthreads();
@@ -1884,13 +1995,14 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
                            nn::kValueF + nn::kPolicyF + h3::kHeadB;
         if constexpr (C::TR && !C::BF)
-            first_layer_h3t<C, GRP>(acc, l1, l1c, bb, pinfo[i], lane, nt);
+            first_layer_h3f<C, GRP>(acc, l1c, bb, pinfo[i], lane, nt, reinterpret_cast<const char*>(lds),
+                                    std::make_integer_sequence<int, grp_n(GRP)>{});
         else
             first_layer_x6<C, GRP>(acc, l1, blob + nn::kL1B + nn::kCh, bb, pinfo[i], lane, nt);
         uint32_t pk[NS][2][2];
         if constexpr (C::TR) {
             const f32x4 inv1 = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f}
-                                     : *reinterpret_cast<const f32x4*>(l1c + 25 * 2 * 4 * 64 * 4 + nn::kCh + cq);
+                                     : *reinterpret_cast<const f32x4*>(l1c + 26 * h3::kL1Frag + cq);
             epilogue_h3t_pack<C, GRP, true>(acc, pk, bias1t, inv1, skip, false, hmax);
             epilogue_h3t_store<C, GRP>(pk, img, eot);
         } else {
@@ -1916,8 +2028,8 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
             constexpr int j = decltype(jc)::value;
             h3t_pack_one<false>(acc[j], pk[j], bbt, sct, skip[j], res, hmax);
         };
-        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt, (int)(kWc * 4)), lo, epi,
-                            std::make_integer_sequence<int, H3P<C, GRP>::P.nbat>{});
+        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt, (int)(C::PF ? 2 * (h3::kW + 2 * nn::kCh) * 4 : kWc * 4)), lo,
+                            epi, std::make_integer_sequence<int, H3P<C, GRP>::P.nbat>{}, &carry);
         stamp(1);
         p += C::BF ? nn::kW64h + nn::kCh : h3::kW + 2 * nn::kCh;
         if constexpr (C::TR) {
@@ -2025,7 +2137,8 @@ template <class C>
 struct H3Fallback {
     static constexpr bool kOn = !C::BF && C::DBG == 0;
     using X = X6Cfg<C::WAVES, C::WAVES == 4 ? 8 : 4, 1, 0, C::WAVES == 4 ? 0 : 1>;
-    static constexpr int kLds = kOn && x6::kLdsFloats > h3::kLdsFloats ? x6::kLdsFloats : h3::kLdsFloats;
+    static constexpr int kBase = h3::kLdsFloats + (C::TR && !C::BF ? h3::kLutB / 4 : 0);  // + the first-layer LUT
+    static constexpr int kLds = kOn && x6::kLdsFloats > kBase ? x6::kLdsFloats : kBase;
 };
 
 // Out of line, so that the fallback's register allocation (k_nn_x6 spills a few VGPRs at 8 waves)
@@ -2431,6 +2544,8 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             case 18: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1>>; break;  // 15 / 10 split (the previous default)
             case 19: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 4, 1>>; break;  // 18 / 7 split
             case 14: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1, 1, 2>>; break;  // timing only: phase stamps
+            case 21: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 1>>; break;  // PF: cross-conv B prefetch
+            case 22: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 3, 1, 1, 0, 0, 1>>; break;  // timing only: PF phase stamps
             case 20: {  // 8 positions per workgroup, 2 workgroups per CU (measured 1.40 vs 1.25 ms)
                 const unsigned g8 = (unsigned)((B + p8::kP - 1) / p8::kP);
                 hipLaunchKernelGGL((k_nn_p8<4, 1>), dim3(g8), dim3(256), 0, st, s, B, w.blob, w.blocks, policy, value,

@@ -10,7 +10,7 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "onitama-alphazero_amd"))
-os.environ["OAZ_NN_X6_V"] = os.environ.get("OAZ_NN_X6_V", "10")
+os.environ["OAZ_NN_X6_V"] = os.environ.get("OAZ_NN_X6_V", "10")  # (A/B build: OAZ_LIB)
 from onitama_az import _abi  # noqa: E402
 from onitama_az.engine import Engine  # noqa: E402
 from onitama_az.weights import random_weights  # noqa: E402

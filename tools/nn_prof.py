@@ -1,6 +1,6 @@
-"""NN kernel driver for rocprofv3 PMC passes: `launches` forwards of one precision at one batch.
-Usage: rocprofv3 --pmc ... -- python tools/nn_prof.py [--precision fp32x6] [--batch 65536] [--blocks 3]"""
-import argparse
+"""NN kernel driver for rocprofv3 passes: nn_forward at a given batch, a few launches.
+Usage: python tools/nn_prof.py [B] [blocks] [fp32h3|fp32x6|bf16|fp32] [reps]  (OAZ_NN_X6_V selects a variant
+in the A/B build, OAZ_LIB=.../libonitama_az_ab.so)."""
 import sys
 from pathlib import Path
 
@@ -12,23 +12,15 @@ from onitama_az import _abi  # noqa: E402
 from onitama_az.engine import Engine  # noqa: E402
 from onitama_az.weights import random_weights  # noqa: E402
 
-PREC = {"fp32": _abi.FP32, "bf16": _abi.BF16, "fp32x6": _abi.FP32_SPLIT, "fp32h3": _abi.FP32_SPLIT16}
-
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--precision", default="fp32h3", choices=sorted(PREC))
-    ap.add_argument("--batch", type=int, default=65536)
-    ap.add_argument("--blocks", type=int, default=3)
-    ap.add_argument("--launches", type=int, default=3)
-    a = ap.parse_args()
-    g = np.load(ROOT / "tests/golden/nn_golden.npz")
-    states = np.concatenate([g["states"]] * (a.batch // len(g["states"]) + 1))[: a.batch]
-    with Engine(games=a.batch, sims=1, blocks=a.blocks, evaluator=_abi.EVAL_NN, precision=PREC[a.precision]) as e:
-        e.load_weights(random_weights(0, a.blocks))
-        for _ in range(a.launches):
-            e.nn_forward(states)
-
-
-if __name__ == "__main__":
-    main()
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+blocks = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+prec = {"fp32h3": _abi.FP32_SPLIT16, "fp32x6": _abi.FP32_SPLIT, "bf16": _abi.BF16, "fp32": _abi.FP32}[
+    sys.argv[3] if len(sys.argv) > 3 else "fp32h3"]
+reps = int(sys.argv[4]) if len(sys.argv) > 4 else 5
+g = np.load(ROOT / "tests/golden/nn_golden.npz")
+states = np.concatenate([g["states"]] * (B // len(g["states"]) + 1))[:B]
+with Engine(games=B, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN, precision=prec) as e:
+    e.load_weights(random_weights(0, blocks))
+    for _ in range(reps):
+        e.nn_forward(states)
+print("ok")
