@@ -84,6 +84,7 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
     ap.add_argument("--no-noise", action="store_true", help=argparse.SUPPRESS)  # experiments only: not C3
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-plies", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--mode", default="selfplay", choices=["selfplay", "train", "pure_mcts"],
                     help="train: SGD steps of the training loop (SURVEY 8f #2), not the headline metric")
     ap.add_argument("--train-blocks", type=int, default=5, help="train mode: residual blocks (bin/train.rs:60)")
@@ -94,49 +95,60 @@ def parse():
 
 
 def pmc_traffic(args, cfg):
-    """HBM bytes per k_nn_sq16 launch from rocprofv3 PMC counters, one counter per pass (TCC slots:
-    FETCH_SIZE and WRITE_SIZE do not fit one pass). Runs as child processes BEFORE this process
-    touches the GPU. gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half the
-    bytes of wide (16 B/lane) coalesced reads -> doubled; WRITE_SIZE is taken as reported."""
+    """HBM bytes per launch of k_nn_h3 and the tree kernels from rocprofv3 PMC counters, one counter
+    per pass (TCC slots: FETCH_SIZE and WRITE_SIZE do not fit one pass). Each pass profiles a child
+    that plays the bench's warm-up plies (same stagger, full sims) unprofiled and collects counters
+    only on the simulation steps of the NEXT ply (--kernel-iteration-range, per kernel), so the
+    tree kernels are measured on steady-state trees, as timed. Runs as child processes BEFORE this
+    process touches the GPU. gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half
+    the bytes of wide (16 B/lane) coalesced reads -> doubled; WRITE_SIZE is taken as reported."""
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None
-    kb, tree_kb = {}, {"select": {}, "expand_backup": {}}
+    plies = args.warmup
+    first, last = plies * cfg["sims"] + 1, (plies + 1) * cfg["sims"]  # 1-based launch index of each kernel
+    kb, tree_kb, counts = {}, {"select": {}, "expand_backup": {}}, {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         with tempfile.TemporaryDirectory() as d:
-            cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
-                   str(Path(__file__).resolve()), "--pmc-child", "--config", args.config, "--games", str(cfg["games"]),
-                   "--sims", "2", "--fp32-kernel", args.fp32_kernel]
+            cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "k_nn_|k_select|k_expand_backup",
+                   "--kernel-iteration-range", f"[{first}-{last}]", "--output-format", "csv", "-d", d, "-o", "pmc",
+                   "--", sys.executable, str(Path(__file__).resolve()), "--pmc-child", "--pmc-plies", str(plies),
+                   "--stagger", str(args.stagger), "--warmup", str(args.warmup), "--config", args.config, "--games", str(cfg["games"]),
+                   "--sims", str(cfg["sims"]), "--fp32-kernel", args.fp32_kernel]
             try:
                 subprocess.run(cmd, timeout=600, capture_output=True, check=True)
             except (subprocess.SubprocessError, OSError):
                 return None
-            vals, tv = [], {"select": [], "expand_backup": []}
+            rows = {"nn": [], "select": [], "expand_backup": []}
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 for r in csv.DictReader(open(f)):
                     if r["Counter_Name"] != ctr:
                         continue
-                    if "k_nn_" in r["Kernel_Name"]:
-                        vals.append(float(r["Counter_Value"]))
-                    elif "k_select" in r["Kernel_Name"]:
-                        tv["select"].append(float(r["Counter_Value"]))
-                    elif "k_expand_backup" in r["Kernel_Name"]:
-                        tv["expand_backup"].append(float(r["Counter_Value"]))
-            if not vals:
+                    k = ("nn" if "k_nn_" in r["Kernel_Name"] else "select" if "k_select" in r["Kernel_Name"]
+                         else "expand_backup" if "k_expand_backup" in r["Kernel_Name"] else None)
+                    if k:
+                        rows[k].append((int(r.get("Dispatch_Id", 0) or 0), float(r["Counter_Value"])))
+            if not rows["nn"]:
                 return None
-            kb[ctr] = sum(vals) / len(vals)
-            for k, v in tv.items():
-                if v:
-                    tree_kb[k][ctr] = sum(v) / len(v)
+            for k, v in rows.items():  # the last ply's launches only (also if the range was not applied)
+                v.sort()
+                rows[k] = [x for _, x in v[-cfg["sims"]:]]
+                counts[k] = len(rows[k])
+            kb[ctr] = sum(rows["nn"]) / len(rows["nn"])
+            for k in ("select", "expand_backup"):
+                if rows[k]:
+                    tree_kb[k][ctr] = sum(rows[k]) / len(rows[k])
     fetch, write = 2.0 * kb["FETCH_SIZE"] * 1024.0, kb["WRITE_SIZE"] * 1024.0
     tree = {}
-    for k, v in tree_kb.items():  # per game: launches cover every game of the child run
+    for k, v in tree_kb.items():  # per game: every launch covers every game slot
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
             tree[k] = {"fetch_bytes_per_sim": 2.0 * v["FETCH_SIZE"] * 1024.0 / cfg["games"],
                        "write_bytes_per_sim": v["WRITE_SIZE"] * 1024.0 / cfg["games"]}
     return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
-            "raw_kb": kb, "tree_pmc": tree,
-            "note": "rocprofv3 --pmc, separate passes; FETCH_SIZE x2 (gfx950 wide-read correction)"}
+            "raw_kb": kb, "tree_pmc": tree, "launches_profiled": counts,
+            "note": f"rocprofv3 --pmc, separate passes, on the {cfg['sims']} simulation steps of ply {plies + 1} "
+                    f"(after {plies} warm-up plies, stagger {args.stagger}); FETCH_SIZE x2 (gfx950 wide-read "
+                    "correction)"}
 
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
@@ -166,8 +178,8 @@ def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg, pmc=No
         out[name] = {"avg_launch_us": t * 1e6, "algorithmic_bytes_per_sim": b, "achieved_GBps": gbps,
                      "frac": gbps / HBM_PEAK_GBPS}
         if pmc and name in pmc:
-            out[name]["pmc"] = dict(pmc[name], note="rocprofv3 FETCH/WRITE_SIZE of the profiled child run (the "
-                                    "first move's first 2 simulations: shallow trees); writes are small scattered "
+            out[name]["pmc"] = dict(pmc[name], note="rocprofv3 FETCH/WRITE_SIZE per simulation over the launches "
+                                    "of one steady-state ply (after the warm-up plies); writes are small scattered "
                                     "records (leaf record, counters, path entries), each a whole write transaction")
     return out
 
@@ -515,11 +527,12 @@ def main():
                  fixed_deck=cfg["fixed_deck"],
                  deck=[0, 1, 2, 3, 4], seed=20260101, rank=rank, world=world,
                  # every sample of every game that can finish in warmup + steps plies fits (checked below)
-                 sample_capacity=cfg["games"] * (args.warmup + args.steps + 2), stagger=0 if args.pmc_child else stagger)
+                 sample_capacity=cfg["games"] * (max(args.warmup, args.pmc_plies) + args.steps + 2), stagger=stagger)
     eng.load_weights(random_weights(0, cfg["blocks"]))  # random-init weights (seed 0), SURVEY.md 8d
     eng.selfplay_reset()
-    if args.pmc_child:  # profiled pass: one move of a couple of simulations, NN launches at full batch
-        eng.selfplay_step(1)
+    if args.pmc_child:  # profiled pass: the warm-up plies (not collected), then one collected ply
+        for _ in range(args.pmc_plies + 1):
+            eng.selfplay_step(1)
         eng.sync()
         eng.close()
         return
