@@ -154,6 +154,26 @@ def pmc_traffic(args, cfg):
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 
+class _StdoutToStderr:
+    """fd-level redirect of stdout to stderr: RCCL prints its version banner to stdout while a
+    communicator initialises, and the bench's stdout must stay ONE JSON line."""
+
+    def __enter__(self):
+        import ctypes
+        sys.stdout.flush()
+        self._libc = ctypes.CDLL(None)
+        self._libc.fflush(None)
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        self._libc.fflush(None)
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+        return False
+
+
 def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg, pmc=None):
     """Achieved HBM-side bytes of the tree kernels (tree-kernel GB/s vs HBM peak),
     from the run's mean walk depth D and branching K and the 32-byte node layout:
@@ -588,10 +608,11 @@ def main():
     allgather = None
     if not args.no_allgather:  # C4: RCCL all-gather of (s, pi, z) after the timed region
         from onitama_az.dist import Comm, allgather_samples
-        comm = None if rehearse else Comm.create(rank, world, local)
-        t1 = time.perf_counter()
-        got = allgather_samples(eng, world, torch.device("cuda", local), comm=comm)
-        torch.cuda.synchronize()
+        with _StdoutToStderr():
+            comm = None if rehearse else Comm.create(rank, world, local)
+            t1 = time.perf_counter()
+            got = allgather_samples(eng, world, torch.device("cuda", local), comm=comm)
+            torch.cuda.synchronize()
         allgather = {"samples_total": int(len(got)), "bytes_per_sample": 228, "seconds": time.perf_counter() - t1,
                      "backend": "gloo (rehearsal, host copies)" if rehearse else
                                 "oaz_allgather_samples (C ABI: RCCL counts all-gather + grouped broadcasts)"}

@@ -993,7 +993,7 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
 #if OAZ_AB  // A/B build only: kernel alternatives by environment variable
     {
         const char* v1 = getenv("OAZ_NN_BF16_V1");
-        w.bf16_v1 = v1 ? atoi(v1) : 0;  // 0: k_nn_h3 in bf16 mode, 1: k_nn_sq16<bf16>, 2: k_nn_bf16g<4>, 3: k_nn_bf16g<2>
+        w.bf16_v1 = v1 ? atoi(v1) : 0;  // 0: k_nn_h3 in bf16 mode, 1: k_nn_sq16<bf16>, 2: k_nn_bf16g<4>, 3: k_nn_bf16g<2>, 4: k_nn_h3 bf16 without EP
         const char* xv = getenv("OAZ_NN_X6_V");
         w.x6_variant = xv ? atoi(xv) : 0;
     }

@@ -994,13 +994,16 @@ struct H3Plan {
     int nbat, tail;  // tail: first square index packed after the conv
     H3Batch b[160];
 };
-constexpr H3Plan h3_plan(int grp, int kh, int nph) {
+// khf 0: the 18 (tap, K-half) steps interleaved; khf 1 / 2: only the 9 taps of K-half 0 / 1 (the
+// staggered kernel runs each K-half of a conv in its own barrier interval).
+constexpr H3Plan h3_plan(int grp, int kh, int nph, int khf = 0) {
     H3Plan P{};
     const int n = grp_n(grp);
     for (int ph = 0; ph < nph; ++ph) {
         const int lo = ph * n / nph, hi = (ph + 1) * n / nph;
         const int b0 = P.nbat;
-        for (int s = 0; s < 18; ++s) {
+        for (int s0 = 0; s0 < (khf ? 9 : 18); ++s0) {
+            const int s = khf ? s0 * 2 + (khf - 1) : s0;  // step = tap * 2 + K-half
             const TapList L0 = tap_list(grp, s / 2);
             TapList L{};
             for (int q = 0; q < L0.n; ++q)
@@ -1045,9 +1048,9 @@ constexpr H3Plan h3_plan(int grp, int kh, int nph) {
     }
     return P;
 }
-template <int GRP, int KH, int NPH>
+template <int GRP, int KH, int NPH, int KHF = 0>
 struct H3PlanOf {
-    static constexpr H3Plan P = h3_plan(GRP, KH, NPH);
+    static constexpr H3Plan P = h3_plan(GRP, KH, NPH, KHF);
 };
 
 // Kernel configuration. WAVES 8: two waves per SIMD (square groups 0/1 x 4 N-tiles, <= 256 VGPRs);
@@ -1058,8 +1061,15 @@ struct H3PlanOf {
 // UNEVEN (8 waves): square groups 3 / 4 (15 / 10 squares) instead of 0 / 1, the bigger group at
 // s_setprio 1.
 template <int WAVES_, int KH_, int PIPE_, int DBG_ = 0, int UNEVEN_ = 0, int TR_ = 0, int PH_ = 1, int HV_ = 0,
-          int BF_ = 0, int PF_ = 0>
+          int BF_ = 0, int PF_ = 0, int STG_ = 0, int EP_ = 0, int PHA_ = 0>
 struct X6Cfg {
+    // h3 + TR, 8 waves, even 13 / 12 split: waves 0-3 (N-tiles 0, 1) and 4-7 (N-tiles 2, 3) run each
+    // conv's two K-halves and their epilogue in three barrier intervals, waves 4-7 one interval
+    // behind, so one wave's epilogue runs beside its SIMD partner's MFMAs (nn_h3_body). 2: + s_setprio 1
+    // for waves 4-7.
+    static constexpr int STG = STG_;
+    static constexpr int EP = EP_;    // h3 + TR: convs in pairs, the residual parity at compile time
+    static constexpr int PHA = PHA_;  // h3 + TR, UNEVEN 3: the first (17-square) group in PHA phases
     static constexpr int PF = PF_;  // h3 + TR: the next conv's first B pieces load during this conv's last steps
     static constexpr int BF = BF_;  // h3 + TR: OAZ_BF16 mode (one bf16 piece, one product; C5)
     static constexpr int HV = HV_;  // h3 heads: 0 MLPs on MFMA (8 waves), 1 per-position VALU MLPs
@@ -1513,10 +1523,12 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 // Phases of group GRP's squares (C::PH for the second group of the TR kernel, else 1).
 template <class C, int GRP>
 constexpr int h3_nph() {
-    return (C::TR && (GRP == 1 || GRP == 4 || GRP == 6)) ? C::PH : 1;
+    return (C::TR && (GRP == 1 || GRP == 4 || GRP == 6)) ? C::PH : (C::PHA && GRP == 7) ? C::PHA : 1;
 }
+// GRP may carry a K-half filter in bits 5-6 (h3_khalf): the plan functions below then run one K-half.
 template <class C, int GRP>
-using H3P = H3PlanOf<GRP, C::KH, h3_nph<C, GRP>()>;
+using H3P = H3PlanOf<GRP & 31, C::KH, h3_nph<C, GRP & 31>(), (GRP >> 5)>;
+constexpr int h3_khalf(int grp, int m) { return grp | ((m + 1) << 5); }
 
 // A-fragment loads / MFMAs of batch K; the LDS address is one of four per-lane bases
 // ab[m][seg] = lo[m] + seg * 64 KiB plus an immediate offset < 64 KiB (piece 1 = + kPlaneB)
@@ -1747,16 +1759,18 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 // selects makes the allocator spill.)
 // vmax: the largest hi bit pattern (v >= 0 after ReLU, so the u16 order is the value order; an
 // overflowed hi is +inf = 0x7C00).
-template <bool FIRST, bool BF = false>
+// RESC 0 / 1: res known at compile time (the EP kernel's conv pairs): no selects, no multiply by 0.
+template <bool FIRST, bool BF = false, int RESC = -1>
 __device__ __forceinline__ void h3t_pack_one(const f32x4& acc, uint32_t (&pk)[2][2], const f32x4& bb, const f32x4& sc,
-                                             f32x4& skip, bool res, uint32_t& hmax) {
+                                             f32x4& skip, bool res_, uint32_t& hmax) {
+    const bool res = RESC < 0 ? res_ : RESC == 1;
     const f32x2 rf = {res ? 1.0f : 0.0f, res ? 1.0f : 0.0f};  // fma(skip, rf, v) = v + skip or v, exactly
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const f32x2 a2 = {acc[2 * k], acc[2 * k + 1]}, s2 = {sc[2 * k], sc[2 * k + 1]};
         const f32x2 b2 = {bb[2 * k], bb[2 * k + 1]};
         f32x2 v = __builtin_elementwise_fma(a2, s2, b2);
-        if constexpr (!FIRST) v = __builtin_elementwise_fma(f32x2{skip[2 * k], skip[2 * k + 1]}, rf, v);
+        if constexpr (!FIRST && RESC != 0) v = __builtin_elementwise_fma(f32x2{skip[2 * k], skip[2 * k + 1]}, rf, v);
         v[0] = v[0] > 0.0f ? v[0] : 0.0f;
         v[1] = v[1] > 0.0f ? v[1] : 0.0f;
         if (FIRST || res) {
@@ -1776,13 +1790,13 @@ __device__ __forceinline__ void h3t_pack_one(const f32x4& acc, uint32_t (&pk)[2]
         }
     }
 }
-template <class C, int GRP, bool FIRST>
+template <class C, int GRP, bool FIRST, int RESC = -1>
 __device__ __forceinline__ void epilogue_h3t_pack(const f32x4 (&acc)[C::NS], uint32_t (&pk)[C::NS][2][2],
                                                   const f32x4& bb, const f32x4& sc, f32x4 (&skip)[C::NS], bool res,
                                                   uint32_t& hmax, int from = 0) {
 #pragma unroll
     for (int j = 0; j < grp_n(GRP); ++j)
-        if (j >= from) h3t_pack_one<FIRST, (bool)C::BF>(acc[j], pk[j], bb, sc, skip[j], res, hmax);
+        if (j >= from) h3t_pack_one<FIRST, (bool)C::BF, RESC>(acc[j], pk[j], bb, sc, skip[j], res, hmax);
 }
 template <class C, int GRP>
 __device__ __forceinline__ void epilogue_h3t_store(const uint32_t (&pk)[C::NS][2][2], char* img, int eo) {
@@ -1941,7 +1955,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
     constexpr int NS = C::NS;
     char* img = reinterpret_cast<char*>(lds);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int nt = wave & 3;
+    const int nt = C::STG ? wave >> 1 : wave & 3;
     const int b0 = blockIdx.x * nn::kSB;
     int* pinfo = reinterpret_cast<int*>(lds + h3::kImageB / 4);
     const int co = nt * 16 + (lane & 15);
@@ -2015,7 +2029,57 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
     // conv + BN, + skip, ReLU)
     stamp(0);
     const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
-    for (int c = 0; c < 2 * blocks; ++c) {
+    if constexpr (C::STG) {
+        // Staggered convs. Conv c reads the image by K-half (channels 0-31 = the output of waves 0-3,
+        // 32-63 = waves 4-7) and overwrites it in place. A wave's program is h0(c) | h1(c) | E(c)
+        // (K-half 0 MFMAs, K-half 1 MFMAs, epilogue), one barrier interval each; waves 4-7 run it
+        // one interval behind waves 0-3, so each interval pairs one wave's epilogue or K-half with its
+        // SIMD partner's MFMAs:
+        //   interval 3c:     0-3 h0(c)   4-7 E(c-1)   (writes K-half 1: nobody reads it now)
+        //   interval 3c + 1: 0-3 h1(c)   4-7 h0(c)
+        //   interval 3c + 2: 0-3 E(c)    4-7 h1(c)    (0-3 write K-half 0: both h0(c) are done)
+        // Every read of a K-half of conv c's input precedes, by a barrier, the epilogue that overwrites
+        // it, and every epilogue precedes, by a barrier, the first read of what it wrote.
+        static_assert(!C::BF && C::TR && C::WAVES == 8 && !C::UNEVEN, "STG: fp16x3, transposed tiles, 8 waves, 13 / 12");
+        constexpr int kStride = (int)(h3::kW + 2 * nn::kCh);
+        const int nconv = 2 * blocks;
+        const int lag = __builtin_amdgcn_readfirstlane(wave) >> 2;  // 0: waves 0-3, 1: waves 4-7
+        if constexpr (C::STG == 2)
+            if (lag) __builtin_amdgcn_s_setprio(1);
+        f32x4 bbt{}, sct{};
+        auto noepi = [](auto) {};
+        for (int k = 0; k < 3 * nconv + 1; ++k) {
+            const int v = k - lag;  // this wave's interval
+            if (v >= 0 && v < 3 * nconv) {
+                const int c = v / 3, a = v - 3 * c;
+                const float* pc = p + (size_t)c * kStride;
+                const X6W W = h3_w(pc, lane, nt, (int)(h3::kW * 4));
+                if (a == 0) {
+                    bbt = *reinterpret_cast<const f32x4*>(pc + h3::kW + cq);  // in flight during the conv
+                    sct = *reinterpret_cast<const f32x4*>(pc + h3::kW + nn::kCh + cq);
+#pragma unroll
+                    for (int j = 0; j < NS; ++j) acc[j] = f32x4{};
+                    conv_h3_run<C, h3_khalf(GRP, 0)>(acc, img, W, lo, noepi,
+                                                     std::make_integer_sequence<int, H3P<C, h3_khalf(GRP, 0)>::P.nbat>{});
+                    stamp(1);
+                } else if (a == 1) {
+                    conv_h3_run<C, h3_khalf(GRP, 1)>(acc, img, W, lo, noepi,
+                                                     std::make_integer_sequence<int, H3P<C, h3_khalf(GRP, 1)>::P.nbat>{});
+                    stamp(1);
+                } else {
+                    uint32_t pk[NS][2][2];
+                    epilogue_h3t_pack<C, GRP, false>(acc, pk, bbt, sct, skip, c & 1, hmax);
+                    epilogue_h3t_store<C, GRP>(pk, img, eot);
+                    stamp(3);
+                }
+            }
+            __syncthreads();
+            stamp(2);
+        }
+        p += (size_t)nconv * kStride;
+    }
+    auto conv_one = [&](int c, auto resc) {  // RESC: -1 runtime parity, 0 / 1 compile-time (EP)
+        constexpr int RESC = decltype(resc)::value;
         const float bb = p[h3::kW + co], sc = p[h3::kW + nn::kCh + co];  // in flight during the conv
         constexpr size_t kWc = C::BF ? nn::kW64h : h3::kW;  // B fragments of one conv
         const f32x4 bbt = *reinterpret_cast<const f32x4*>(p + kWc + cq);
@@ -2026,14 +2090,14 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         const bool res = c & 1;
         auto epi = [&](auto jc) {  // an earlier phase's square: its pack runs between MFMAs
             constexpr int j = decltype(jc)::value;
-            h3t_pack_one<false>(acc[j], pk[j], bbt, sct, skip[j], res, hmax);
+            h3t_pack_one<false, false, RESC>(acc[j], pk[j], bbt, sct, skip[j], res, hmax);
         };
         conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt, (int)(C::PF ? 2 * (h3::kW + 2 * nn::kCh) * 4 : kWc * 4)), lo,
                             epi, std::make_integer_sequence<int, H3P<C, GRP>::P.nbat>{}, &carry);
         stamp(1);
         p += C::BF ? nn::kW64h + nn::kCh : h3::kW + 2 * nn::kCh;
         if constexpr (C::TR) {
-            epilogue_h3t_pack<C, GRP, false>(acc, pk, bbt, sct, skip, res, hmax, H3P<C, GRP>::P.tail);
+            epilogue_h3t_pack<C, GRP, false, RESC>(acc, pk, bbt, sct, skip, res, hmax, H3P<C, GRP>::P.tail);
         } else
             epilogue_h3_pack<C, GRP>(acc, pk, bb, sc, skip, co, c & 1, c & 1, vmax);
         stamp(3);
@@ -2046,6 +2110,14 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         stamp(3);
         __syncthreads();
         stamp(4);
+    };
+    if constexpr (C::EP) {  // conv pairs: the residual parity at compile time
+        for (int c = 0; c < (C::STG ? 0 : 2 * blocks); c += 2) {
+            conv_one(c, std::integral_constant<int, 0>{});
+            conv_one(c + 1, std::integral_constant<int, 1>{});
+        }
+    } else {
+        for (int c = 0; c < (C::STG ? 0 : 2 * blocks); ++c) conv_one(c, std::integral_constant<int, -1>{});
     }
     // heads: the value / policy 1x1 convs as split MFMAs on the LDS image (one 16x16 tile per
     // square: rows = positions, columns 0 / 1 / 2 = value, policy planes 0 / 1, each scaled by a
@@ -2169,6 +2241,11 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __rest
         } else {
             ovf = nn_h3_body<C, ga + 1>(states, B, blob, blocks, policy, value, lds);
         }
+    } else if constexpr (C::STG) {  // square group = wave parity (the SIMD partners w, w + 4 share it)
+        if (((threadIdx.x >> 6) & 1) == 0)
+            ovf = nn_h3_body<C, 0>(states, B, blob, blocks, policy, value, lds);
+        else
+            ovf = nn_h3_body<C, 1>(states, B, blob, blocks, policy, value, lds);
     } else if (g0)
         ovf = nn_h3_body<C, 0>(states, B, blob, blocks, policy, value, lds);
     else
@@ -2522,9 +2599,9 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
     const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
     if (w.precision == OAZ_FP32_SPLIT16) {
         if (!w.fallback || !w.blob_x6) return hipErrorInvalidValue;
-        // 8 waves, uneven 17 / 8 square split, batches of <= 4 squares, transposed C/D tiles, in-kernel
-        // k_nn_x6 recompute of fp16-range tiles
-        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1>>;
+        // 8 waves, uneven 17 / 8 square split, batches of <= 4 squares, transposed C/D tiles, convs in
+        // pairs (compile-time residual parity), in-kernel k_nn_x6 recompute of fp16-range tiles
+        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 0, 0, 1>>;
         int waves = 8;
 #if OAZ_AB
         switch (w.x6_variant) {
@@ -2546,6 +2623,20 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             case 14: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1, 1, 2>>; break;  // timing only: phase stamps
             case 21: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 1>>; break;  // PF: cross-conv B prefetch
             case 22: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 3, 1, 1, 0, 0, 1>>; break;  // timing only: PF phase stamps
+            case 23: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 0, 1, 1, 0, 0, 0, 1>>; break;  // STG: staggered K-halves
+            case 24: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 0, 1, 1, 0, 0, 0, 2>>; break;  // STG + waves 4-7 at prio 1
+            case 25: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 0, 1, 1, 0, 0, 0, 1>>; break;  // STG, PIPE 2
+            case 26: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 0, 1, 1, 0, 0, 0, 1>>; break;  // timing only: STG phase stamps
+            case 27: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1>>; break;  // the previous default (runtime parity selects)
+            case 28: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 0, 0, 0, 2>>; break;  // PHA 2
+            case 29: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 0, 0, 1, 2>>; break;  // EP + PHA 2
+            case 30: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 0, 0, 0, 3>>; break;  // PHA 3
+            case 31: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 3, 1, 1, 0, 0, 0, 0, 1, 2>>; break;  // timing only: EP + PHA 2
+            case 32: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, PIPE 2
+            case 33: k = k_nn_h3<X6Cfg<8, 5, 1, 0, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, KH 5
+            case 34: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 2, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, 16 / 9
+            case 35: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 4, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, 18 / 7
+            case 36: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // timing only: EP phase stamps
             case 20: {  // 8 positions per workgroup, 2 workgroups per CU (measured 1.40 vs 1.25 ms)
                 const unsigned g8 = (unsigned)((B + p8::kP - 1) / p8::kP);
                 hipLaunchKernelGGL((k_nn_p8<4, 1>), dim3(g8), dim3(256), 0, st, s, B, w.blob, w.blocks, policy, value,
@@ -2586,8 +2677,11 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             hipLaunchKernelGGL(k_nn_bf16g<2>, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value);
         if (w.bf16_v1 >= 1 && w.bf16_v1 <= 3) return hipGetLastError();
 #endif
-        // the k_nn_h3 structure with one bf16 piece and one product (k_nn_h1)
-        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 1>>;
+        // the k_nn_h3 structure with one bf16 piece and one product (k_nn_h1), convs in pairs
+        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 1, 0, 0, 1>>;
+#if OAZ_AB
+        if (w.bf16_v1 == 4) k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 1>>;  // the previous default (runtime parity)
+#endif
         hipLaunchKernelGGL(k, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value, nullptr,
                            nullptr);
     } else {
