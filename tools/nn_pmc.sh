@@ -2,23 +2,23 @@
 # SQ counter passes over the NN kernel (tools/nn_prof.py), one rocprofv3 run per pass, each under its
 # own timeout; summary per counter (per-dispatch mean over the k_nn_ dispatches) in gpurun_out/pmc/summary.txt.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
-mkdir -p gpurun_out/pmc
+OUT=${OUT:-gpurun_out/pmc}; mkdir -p $OUT
 PY=$(command -v python3)
 i=0
 for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VALU" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_MFMA GRBM_GUI_ACTIVE" ; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc/p$i -o run -- "$PY" tools/nn_prof.py ${NN_ARGS:-} > gpurun_out/pmc/p$i.log 2>&1
-  rc=$?; echo "pass $i rc=$rc"; if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/p$i.log; exit $rc; fi
+  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $OUT/p$i -o run -- "$PY" tools/nn_prof.py ${NN_ARGS:-} > $OUT/p$i.log 2>&1
+  rc=$?; echo "pass $i rc=$rc"; if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
 done
-python3 - <<'PY' > gpurun_out/pmc/summary.txt
-import csv, glob, collections
+OUT=$OUT python3 - <<'PY' > $OUT/summary.txt
+import csv, glob, collections, os
 acc = collections.defaultdict(list)
-for f in glob.glob("gpurun_out/pmc/p*/**/*counter_collection.csv", recursive=True):
+for f in glob.glob(os.environ["OUT"] + "/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if "k_nn_" in r["Kernel_Name"]:
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in sorted(acc.items()):
     print(f"{k:28s} {sum(v)/len(v):16.1f}  (n={len(v)})")
 PY
-cat gpurun_out/pmc/summary.txt
+cat $OUT/summary.txt
