@@ -914,12 +914,16 @@ constexpr int8_t kSqOrderU[25] = {6, 7, 8, 11, 12, 13, 16, 17, 18, 0, 4, 20, 24,
                                   1, 3, 5, 10, 9, 14, 15, 19, 21, 23};
 // GRP 5 / 6: 16 / 9 squares (115 / 54 taps), same order with one more edge in the first group;
 // GRP 7 / 8: 17 / 8 (the default, measured 1-2 % faster than 15 / 10), GRP 9 / 10: 18 / 7.
+// GRP 11-14: the four groups of k_nn_q2 (3 interior + 2 edges + 1 corner = 43 on-board taps |
+// 2 interior + 4 edges = 42 | 2 + 4 = 42 | 2 interior + 2 edges + 3 corners = 42)
+constexpr int8_t kSqOrderQ[25] = {0, 1, 2, 6, 7, 8, 3, 5, 10, 11, 12, 15, 9, 13, 14, 16, 19, 21,
+                                  4, 17, 18, 20, 22, 23, 24};
 constexpr int grp_n(int grp) {
-    return grp == 0 ? nn::kTPW : grp == 1 ? 25 - nn::kTPW : grp == 3 ? 15 : grp == 4 ? 10 : grp == 5 ? 16 : grp == 6 ? 9
+    return grp >= 11 ? (grp == 14 ? 7 : 6) : grp == 0 ? nn::kTPW : grp == 1 ? 25 - nn::kTPW : grp == 3 ? 15 : grp == 4 ? 10 : grp == 5 ? 16 : grp == 6 ? 9
          : grp == 7 ? 17 : grp == 8 ? 8 : grp == 9 ? 18 : grp == 10 ? 7 : 25;
 }
 constexpr int grp_sq(int grp, int j) {
-    return grp == 2 ? j : grp >= 9 ? kSqOrderU[(grp - 9) * 18 + j] : grp >= 7 ? kSqOrderU[(grp - 7) * 17 + j]
+    return grp >= 11 ? kSqOrderQ[(grp - 11) * 6 + j] : grp == 2 ? j : grp >= 9 ? kSqOrderU[(grp - 9) * 18 + j] : grp >= 7 ? kSqOrderU[(grp - 7) * 17 + j]
          : grp >= 5 ? kSqOrderU[(grp - 5) * 16 + j]
          : grp >= 3 ? kSqOrderU[(grp - 3) * 15 + j] : kSqOrder[grp * nn::kTPW + j];
 }
@@ -987,7 +991,7 @@ struct X6PlanOf {
 // so only the last phase's packs remain after the conv. first: the batch starts a step run (its
 // B pieces were prefetched); nstep: the step of the next run (its B pieces are prefetched now).
 struct H3Batch {
-    int t, m, n, first, nstep, ne;
+    int t, m, n, first, nstep, ne, nnstep;  // nnstep: the step of the run after next (BD 2)
     int8_t j[16], nb[16], e[16];
 };
 struct H3Plan {
@@ -1039,10 +1043,12 @@ constexpr H3Plan h3_plan(int grp, int kh, int nph, int khf = 0) {
         }
         P.tail = lo;
     }
-    int next = -1;
+    int next = -1, next2 = -1;
     for (int k = P.nbat - 1; k >= 0; --k) {
         if (P.b[k].first) {
             P.b[k].nstep = next;
+            P.b[k].nnstep = next2;
+            next2 = next;
             next = P.b[k].t * 2 + P.b[k].m;
         }
     }
@@ -1061,13 +1067,15 @@ struct H3PlanOf {
 // UNEVEN (8 waves): square groups 3 / 4 (15 / 10 squares) instead of 0 / 1, the bigger group at
 // s_setprio 1.
 template <int WAVES_, int KH_, int PIPE_, int DBG_ = 0, int UNEVEN_ = 0, int TR_ = 0, int PH_ = 1, int HV_ = 0,
-          int BF_ = 0, int PF_ = 0, int STG_ = 0, int EP_ = 0, int PHA_ = 0>
+          int BF_ = 0, int PF_ = 0, int STG_ = 0, int EP_ = 0, int PHA_ = 0, int BD_ = 1, int Q2_ = 0>
 struct X6Cfg {
     // h3 + TR, 8 waves, even 13 / 12 split: waves 0-3 (N-tiles 0, 1) and 4-7 (N-tiles 2, 3) run each
     // conv's two K-halves and their epilogue in three barrier intervals, waves 4-7 one interval
     // behind, so one wave's epilogue runs beside its SIMD partner's MFMAs (nn_h3_body). 2: + s_setprio 1
     // for waves 4-7.
     static constexpr int STG = STG_;
+    static constexpr int BD = BD_;  // h3: B pieces loaded BD step runs ahead (1 or 2)
+    static constexpr int Q2 = Q2_;  // k_nn_q2: two N-tiles per wave over four square groups (GRP 11-14)
     static constexpr int EP = EP_;    // h3 + TR: convs in pairs, the residual parity at compile time
     static constexpr int PHA = PHA_;  // h3 + TR, UNEVEN 3: the first (17-square) group in PHA phases
     static constexpr int PF = PF_;  // h3 + TR: the next conv's first B pieces load during this conv's last steps
@@ -1077,7 +1085,7 @@ struct X6Cfg {
     static constexpr int PH = PH_;  // h3 + TR: square phases of the second (younger) group
     static constexpr int WAVES = WAVES_;
     static constexpr int UNEVEN = UNEVEN_;
-    static constexpr int NS = WAVES_ == 8 ? (UNEVEN_ == 4 ? 18 : UNEVEN_ == 3 ? 17 : UNEVEN_ == 2 ? 16 : UNEVEN_ ? 15 : nn::kTPW) : 25;  // tiles per wave
+    static constexpr int NS = Q2_ ? 7 : WAVES_ == 8 ? (UNEVEN_ == 4 ? 18 : UNEVEN_ == 3 ? 17 : UNEVEN_ == 2 ? 16 : UNEVEN_ ? 15 : nn::kTPW) : 25;  // tiles per wave
     static constexpr int KH = KH_;
     static constexpr int PIPE = PIPE_;
     static constexpr int DBG = DBG_;
@@ -1534,6 +1542,7 @@ constexpr int h3_khalf(int grp, int m) { return grp | ((m + 1) << 5); }
 // ab[m][seg] = lo[m] + seg * 64 KiB plus an immediate offset < 64 KiB (piece 1 = + kPlaneB)
 template <class C, int GRP, int K, int N>
 __device__ __forceinline__ void h3_load(f16x8 (&a)[N], const char* img, const int (&ab)[2][2], int piece) {
+    if constexpr (C::DBG == 3 && K > 1) return;  // ablation (timing only, wrong results): no A reads
     constexpr H3Batch B = H3P<C, GRP>::P.b[K];
 #pragma unroll
     for (int q = 0; q < N; ++q)
@@ -1580,19 +1589,28 @@ __device__ __forceinline__ f16x8 h3_ldb_at(const X6W& w, int bytes) {
     return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(w.r, w.voff, bytes, 0));
 }
 
+// B pieces: b = the current step run's, bn[0..1] = the next run's, bn[2..3] = the run after next
+// (BD 2: loads issued two step runs ahead; BD 1: one)
 template <class C, int GRP, int K>
-__device__ __forceinline__ void h3_step_b(const X6W& W, f16x8 (&b)[2], f16x8 (&bn)[2]) {
+__device__ __forceinline__ void h3_step_b(const X6W& W, f16x8 (&b)[2], f16x8 (&bn)[4]) {
     constexpr H3Batch B = H3P<C, GRP>::P.b[K];
     if constexpr (B.first && K > 0) {
         b[0] = bn[0];
         b[1] = bn[1];
+        if constexpr (C::BD == 2) {
+            bn[0] = bn[2];
+            bn[1] = bn[3];
+        }
     }
-    if constexpr (B.first && B.nstep >= 0) {  // prefetch the next step run's B pieces
+    constexpr int ld = C::BD == 2 ? B.nnstep : B.nstep;
+    constexpr int o = C::BD == 2 ? 2 : 0;
+    if constexpr (B.first && ld >= 0 && C::DBG != 4) {  // prefetch a later step run's B pieces
+                                                         // (DBG 4: ablation, no B loads)
         if constexpr (C::BF) {  // BF: [step][N-tile][lane] bf16x8, one piece
-            bn[0] = h3_ldb(W, B.nstep * 4);
+            bn[o] = h3_ldb(W, ld * 4);
         } else {
-            bn[0] = h3_ldb(W, (B.nstep * 2 + 0) * 4);
-            bn[1] = h3_ldb(W, (B.nstep * 2 + 1) * 4);
+            bn[o] = h3_ldb(W, (ld * 2 + 0) * 4);
+            bn[o + 1] = h3_ldb(W, (ld * 2 + 1) * 4);
         }
     }
 }
@@ -1601,7 +1619,7 @@ __device__ __forceinline__ void h3_step_b(const X6W& W, f16x8 (&b)[2], f16x8 (&b
 // (two buffers, roles swap with K's parity)
 template <class C, int GRP, int K>
 __device__ __forceinline__ void conv_h1_batch(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
-                                              f16x8 (&bn)[2], f16x8 (&X)[C::KH], f16x8 (&Xn)[C::KH],
+                                              f16x8 (&bn)[4], f16x8 (&X)[C::KH], f16x8 (&Xn)[C::KH],
                                               const int (&ab)[2][2]) {
     h3_step_b<C, GRP, K>(W, b, bn);
     if constexpr (K + 1 < H3P<C, GRP>::P.nbat) h3_load<C, GRP, K + 1>(Xn, img, ab, 0);
@@ -1613,7 +1631,7 @@ __device__ __forceinline__ void conv_h1_batch(f32x4 (&acc)[C::NS], const char* i
 //   load Y = hi | lo*Bhi | load X = next lo | hi*Bhi, hi*Blo | earlier-phase packs
 template <class C, int GRP, int K, class E>
 __device__ __forceinline__ void conv_h3_batch(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
-                                              f16x8 (&bn)[2], f16x8 (&X)[C::KH], f16x8 (&Y)[C::KH],
+                                              f16x8 (&bn)[4], f16x8 (&X)[C::KH], f16x8 (&Y)[C::KH],
                                               const int (&ab)[2][2], E& epi, f16x8 (*carry)[2] = nullptr) {
     h3_step_b<C, GRP, K>(W, b, bn);
     if constexpr (C::PF) {  // the last step run: prefetch the next conv's first pieces (one conv further on)
@@ -1638,7 +1656,7 @@ __device__ __forceinline__ void conv_h3_batch(f32x4 (&acc)[C::NS], const char* i
 // parity):  lo*Bhi | load next lo | hi*Bhi | load next hi | hi*Blo
 template <class C, int GRP, int K, class E>
 __device__ __forceinline__ void conv_h3_batch2(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
-                                               f16x8 (&bn)[2], f16x8 (&L)[C::KH], f16x8 (&H)[C::KH],
+                                               f16x8 (&bn)[4], f16x8 (&L)[C::KH], f16x8 (&H)[C::KH],
                                                f16x8 (&Ln)[C::KH], f16x8 (&Hn)[C::KH], const int (&ab)[2][2],
                                                E& epi) {
     constexpr bool more = K + 1 < H3P<C, GRP>::P.nbat;
@@ -1661,7 +1679,15 @@ __device__ __forceinline__ void conv_h3_run(f32x4 (&acc)[C::NS], const char* img
 #pragma unroll
         for (int sg = 0; sg < 2; ++sg) ab[m][sg] = lo[m] + sg * 65536;
     constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
-    f16x8 b[2], bn[2];
+    f16x8 b[2], bn[4];
+    if constexpr (C::BD == 2 && B0.nstep >= 0) {  // the second run's pieces, before the first's are used
+        if constexpr (C::BF) {
+            bn[0] = h3_ldb(W, B0.nstep * 4);
+        } else {
+            bn[0] = h3_ldb(W, (B0.nstep * 2 + 0) * 4);
+            bn[1] = h3_ldb(W, (B0.nstep * 2 + 1) * 4);
+        }
+    }
     if constexpr (C::BF) {
         b[0] = h3_ldb(W, (B0.t * 2 + B0.m) * 4);
         f16x8 X[C::KH], X2[C::KH];
@@ -1905,19 +1931,74 @@ __device__ __forceinline__ void l1_lut_build(char* lds, int tid) {  // entry P, 
     }
     *reinterpret_cast<uint2*>(lds + h3::kLutOff + P * 16 + h * 8) = uint2{w[0], w[1]};
 }
-template <class C, int GRP, int... J>
-__device__ __forceinline__ void first_layer_h3f(f32x4 (&acc)[C::NS], const float* l1c, uint32_t bb, int cinfo,
-                                                int lane, int nt, const char* lds, std::integer_sequence<int, J...>) {
-    const int q = lane >> 4;
+// K block 1 of square sq depends on sq only through its on-board tap set (the constant planes'
+// table T[sq] sums over those taps; tap 8's weights are square-independent): 9 classes (corner,
+// edge and interior rows x columns). A wave loads each of its classes once.
+constexpr int l1_cls(int sq) {
+    const int r = sq / 5, c = sq % 5;
+    return (r == 0 ? 0 : r == 4 ? 2 : 1) * 3 + (c == 0 ? 0 : c == 4 ? 2 : 1);
+}
+struct L1Slots {
+    int n;
+    int8_t slot[25];  // group square j -> its class slot
+    int8_t rep[9];    // class slot -> a square of that class (whose K block 1 is loaded)
+};
+constexpr L1Slots l1_slots(int grp) {
+    L1Slots S{};
+    int cls[9] = {};
+    for (int j = 0; j < grp_n(grp); ++j) {
+        const int c = l1_cls(grp_sq(grp, j));
+        int k = 0;
+        while (k < S.n && cls[k] != c) ++k;
+        if (k == S.n) {
+            cls[S.n] = c;
+            S.rep[S.n] = (int8_t)grp_sq(grp, j);
+            ++S.n;
+        }
+        S.slot[j] = (int8_t)k;
+    }
+    return S;
+}
+template <int GRP>
+struct L1SlotsOf {
+    static constexpr L1Slots S = l1_slots(GRP);
+};
+template <class F, int... K>
+__device__ __forceinline__ void l1_for_slots(F&& f, std::integer_sequence<int, K...>) {
+    (f(std::integral_constant<int, K>{}), ...);
+}
+template <int GRP>
+struct L1H {  // the first layer's A operands (K block 0, and K block 1 of each class the wave touches)
+    f16x8 a0h, a0l;
+    f16x8 a1[L1SlotsOf<GRP>::S.n][2];
+};
+// issued at kernel start, so the loads overlap the state load, the LUT build and the barrier
+template <int GRP>
+__device__ __forceinline__ void first_layer_h3f_fetch(L1H<GRP>& R, const float* l1c, int lane, int nt) {
     X6W A;
     A.r = __builtin_amdgcn_make_buffer_rsrc((void*)l1c, (short)0, (int)(26 * h3::kL1Frag * 4), 0x00020000);
     A.voff = (nt * 64 + lane) * 16;
     auto ld = [&](int blk, int pc) {  // [blk][pc][nt][lane]
         return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(A.r, A.voff, (blk * 2 + pc) * 4 * 64 * 16, 0));
     };
-    const f16x8 a0h = ld(0, 0), a0l = ld(0, 1);
-    f16x8 a1[grp_n(GRP)][2];
-    ((a1[J][0] = ld(1 + grp_sq(GRP, J), 0), a1[J][1] = ld(1 + grp_sq(GRP, J), 1)), ...);
+    R.a0h = ld(0, 0);
+    R.a0l = ld(0, 1);
+    constexpr L1Slots S = L1SlotsOf<GRP>::S;
+    l1_for_slots(
+        [&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            R.a1[k][0] = ld(1 + S.rep[k], 0);
+            R.a1[k][1] = ld(1 + S.rep[k], 1);
+        },
+        std::make_integer_sequence<int, S.n>{});
+}
+template <class C, int GRP, int... J>
+__device__ __forceinline__ void first_layer_h3f(f32x4 (&acc)[C::NS], const L1H<GRP>& R, uint32_t bb, int cinfo,
+                                                int lane, const char* lds, std::integer_sequence<int, J...>) {
+    const int q = lane >> 4;
+    constexpr L1Slots S = L1SlotsOf<GRP>::S;
+    const f16x8 &a0h = R.a0h, &a0l = R.a0l;
+    const auto& a1 = R.a1;
     // block 1 constants: element e >= 1 of quarter q is constant plane c = 7q + e - 1
     const int c0 = cinfo & 15, c1 = (cinfo >> 4) & 15, blue = (cinfo >> 8) & 1;
     uint32_t kw[4];
@@ -1940,14 +2021,91 @@ __device__ __forceinline__ void first_layer_h3f(f32x4 (&acc)[C::NS], const float
         const f16x8 b1 = __builtin_bit_cast(f16x8, w1);
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0h, b0, acc[j], 0, 0, 0);
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0l, b0, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[j][0], b1, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[j][1], b1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[S.slot[j]][0], b1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[S.slot[j]][1], b1, acc[j], 0, 0, 0);
     };
     (sq_mfma(std::integral_constant<int, J>{}), ...);
 }
 
 // Returns true in a lane that split an activation beyond the fp16 range (an fp16 hi term that
 // overflowed, or would have): the tile's results are then invalid and k_nn_h3 recomputes them.
+// heads (k_nn_h3, k_nn_q2): the value / policy 1x1 convs as split MFMAs on the LDS image (one 16x16
+// tile per square: rows = positions, columns 0 / 1 / 2 = value, policy planes 0 / 1, each scaled by a
+// power of two), then the MLPs per position from a feature table in LDS. p: the head parameters
+// (after the convs).
+template <class C>
+__device__ __forceinline__ void h3_heads(const float* p, char* img, const int (&lo)[2], int wave, int lane, int b0,
+                                         int B, float* __restrict__ policy, float* __restrict__ value) {
+    const int i = lane & 15, kq = lane >> 4;
+    {
+        const float* hp = p + nn::kValueF + nn::kPolicyF;
+        const f16x8* HB = reinterpret_cast<const f16x8*>(hp);
+        f16x8 hb[2][2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int pc = 0; pc < 2; ++pc) hb[m][pc] = HB[(C::BF ? m : m * 2 + pc) * 64 + lane];  // BF: [m][lane]
+        const float hs = C::BF ? 1.0f : hp[2 * 2 * 64 * 4 + (i < 3 ? i : 0)];
+        // MLP weights in flight during the head convs (after hb: vmcnt is in order)
+        HeadRegs hr;
+        HeadMM hm;
+        if constexpr (C::WAVES == 8 && C::HV == 0)
+            heads_mm_fetch(hm, p, wave, lane);
+        else
+            heads_fetch(hr, p, lane);
+        constexpr int kSqPerWave = (25 + C::WAVES - 1) / C::WAVES;
+        f32x4 hacc[kSqPerWave];
+#pragma unroll
+        for (int q = 0; q < kSqPerWave; ++q) {
+            hacc[q] = f32x4{};
+            const int sq = wave + q * C::WAVES;
+            if (sq < 25) {
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const char* a = img + sq * (nn::kSB * h3::kRowB) + lo[m];
+                    const f16x8 ah = *reinterpret_cast<const f16x8*>(a);
+                    if constexpr (C::BF) {
+                        hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, hb[m][0]), hacc[q], 0, 0, 0);
+                        continue;
+                    }
+                    const f16x8 al = *reinterpret_cast<const f16x8*>(a + h3::kPlaneB);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, hb[m][0], hacc[q], 0, 0, 0);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][0], hacc[q], 0, 0, 0);
+                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][1], hacc[q], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();  // the image is no longer read: its first 4.8 KB become the feature table
+        float* feat = reinterpret_cast<float*>(img);  // [16 positions][80]
+        const float hbias = i == 0 ? p[64] : i == 1 ? p[nn::kValueF + 128] : p[nn::kValueF + 129];
+#pragma unroll
+        for (int q = 0; q < kSqPerWave; ++q) {
+            const int sq = wave + q * C::WAVES;
+            if (sq < 25 && i < 3)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v = __builtin_fmaf(hacc[q][r], hs, hbias);
+                    feat[(kq * 4 + r) * 80 + i * 25 + sq] = v > 0.0f ? v : 0.0f;
+                }
+        }
+        __syncthreads();
+        if constexpr (C::WAVES == 8 && C::HV == 0) {
+            heads_mm(hm, feat, feat + nn::kSB * 80, wave, lane, b0, B, policy, value);
+        } else {
+            constexpr int NP = nn::kSB / C::WAVES;  // positions per wave
+            const float* fq[NP];
+            int bq[NP];
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                fq[q] = feat + (wave + q * C::WAVES) * 80;
+                bq[q] = b0 + wave + q * C::WAVES;
+            }
+            heads_mlp_r<NP>(hr, fq, bq, lane, B, policy, value);
+        }
+    }
+}
+
 template <class C, int GRP>
 __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
                                            int blocks, float* __restrict__ policy, float* __restrict__ value,
@@ -1971,7 +2129,9 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
     f32x4 skip[NS];
     float vmax = 0.0f;
     uint32_t hmax = 0;  // TR: largest hi bit patterns (two u16 halves)
-    uint64_t ph[6] = {0, 0, 0, 0, 0, 0};  // DBG 2: first layer, conv, barrier 1, epilogue, barrier 2, heads
+    // DBG 2: first layer (MFMA tail + epilogue), conv, barrier 1, epilogue, barrier 2, heads, kernel start (state,
+    // LUT, barrier), first-layer MFMAs (incl. their operand loads)
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tm = C::DBG == 2 ? __builtin_amdgcn_s_memtime() : 0;
     auto stamp = [&](int k) {
         if constexpr (C::DBG == 2) {
@@ -1989,12 +2149,21 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
     }
     {  // encoder + first layer (exact fp32 MFMA on the 0/1 inputs, as k_nn_x6)
         L1Regs<GRP> l1;
-        first_layer_x6_fetch<GRP>(l1, blob, lane, nt);
+        L1H<GRP> l1h;
+        const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
+                           nn::kValueF + nn::kPolicyF + h3::kHeadB;
+        // the state loads first: vmcnt retires in issue order, so the pinfo / LUT work before the
+        // barrier then waits for these and not for the first-layer operands issued after them
         const int b = b0 + i < B ? b0 + i : b0;
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
         const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
+        oaz_state st{};
+        if (tid < nn::kSB) st = states[b];
+        if constexpr (C::TR && !C::BF)
+            first_layer_h3f_fetch<GRP>(l1h, l1c, lane, nt);
+        else
+            first_layer_x6_fetch<GRP>(l1, blob, lane, nt);
         if (tid < nn::kSB) {
-            const oaz_state st = states[b];
             const int blue = st.to_move & 1;
             const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
             pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
@@ -2004,15 +2173,21 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         const float bias1 = blob[nn::kL1B + co];
         const f32x4 bias1t = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
         __syncthreads();
+        stamp(6);
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};  // skip: finite for the fma in the epilogue
-        const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
-                           nn::kValueF + nn::kPolicyF + h3::kHeadB;
         if constexpr (C::TR && !C::BF)
-            first_layer_h3f<C, GRP>(acc, l1c, bb, pinfo[i], lane, nt, reinterpret_cast<const char*>(lds),
+            first_layer_h3f<C, GRP>(acc, l1h, bb, pinfo[i], lane, reinterpret_cast<const char*>(lds),
                                     std::make_integer_sequence<int, grp_n(GRP)>{});
         else
             first_layer_x6<C, GRP>(acc, l1, blob + nn::kL1B + nn::kCh, bb, pinfo[i], lane, nt);
+        if constexpr (C::DBG == 2) {  // the MFMA results, so the stamp follows the MFMAs
+            float z = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) z += acc[j][0];
+            asm volatile("" ::"v"(z));
+        }
+        stamp(7);
         uint32_t pk[NS][2][2];
         if constexpr (C::TR) {
             const f32x4 inv1 = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f}
@@ -2119,80 +2294,11 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
     } else {
         for (int c = 0; c < (C::STG ? 0 : 2 * blocks); ++c) conv_one(c, std::integral_constant<int, -1>{});
     }
-    // heads: the value / policy 1x1 convs as split MFMAs on the LDS image (one 16x16 tile per
-    // square: rows = positions, columns 0 / 1 / 2 = value, policy planes 0 / 1, each scaled by a
-    // power of two), then the MLPs per position on the VALU from a feature table in LDS
-    {
-        const float* hp = p + nn::kValueF + nn::kPolicyF;
-        const f16x8* HB = reinterpret_cast<const f16x8*>(hp);
-        f16x8 hb[2][2];
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int pc = 0; pc < 2; ++pc) hb[m][pc] = HB[(C::BF ? m : m * 2 + pc) * 64 + lane];  // BF: [m][lane]
-        const float hs = C::BF ? 1.0f : hp[2 * 2 * 64 * 4 + (i < 3 ? i : 0)];
-        // MLP weights in flight during the head convs (after hb: vmcnt is in order)
-        HeadRegs hr;
-        HeadMM hm;
-        if constexpr (C::WAVES == 8 && C::HV == 0)
-            heads_mm_fetch(hm, p, wave, lane);
-        else
-            heads_fetch(hr, p, lane);
-        constexpr int kSqPerWave = (25 + C::WAVES - 1) / C::WAVES;
-        f32x4 hacc[kSqPerWave];
-#pragma unroll
-        for (int q = 0; q < kSqPerWave; ++q) {
-            hacc[q] = f32x4{};
-            const int sq = wave + q * C::WAVES;
-            if (sq < 25) {
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    const char* a = img + sq * (nn::kSB * h3::kRowB) + lo[m];
-                    const f16x8 ah = *reinterpret_cast<const f16x8*>(a);
-                    if constexpr (C::BF) {
-                        hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, hb[m][0]), hacc[q], 0, 0, 0);
-                        continue;
-                    }
-                    const f16x8 al = *reinterpret_cast<const f16x8*>(a + h3::kPlaneB);
-                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, hb[m][0], hacc[q], 0, 0, 0);
-                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][0], hacc[q], 0, 0, 0);
-                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][1], hacc[q], 0, 0, 0);
-                }
-            }
-        }
-        __syncthreads();  // the image is no longer read: its first 4.8 KB become the feature table
-        float* feat = reinterpret_cast<float*>(img);  // [16 positions][80]
-        const float hbias = i == 0 ? p[64] : i == 1 ? p[nn::kValueF + 128] : p[nn::kValueF + 129];
-#pragma unroll
-        for (int q = 0; q < kSqPerWave; ++q) {
-            const int sq = wave + q * C::WAVES;
-            if (sq < 25 && i < 3)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float v = __builtin_fmaf(hacc[q][r], hs, hbias);
-                    feat[(kq * 4 + r) * 80 + i * 25 + sq] = v > 0.0f ? v : 0.0f;
-                }
-        }
-        __syncthreads();
-        if constexpr (C::WAVES == 8 && C::HV == 0) {
-            heads_mm(hm, feat, feat + nn::kSB * 80, wave, lane, b0, B, policy, value);
-        } else {
-            constexpr int NP = nn::kSB / C::WAVES;  // positions per wave
-            const float* fq[NP];
-            int bq[NP];
-#pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                fq[q] = feat + (wave + q * C::WAVES) * 80;
-                bq[q] = b0 + wave + q * C::WAVES;
-            }
-            heads_mlp_r<NP>(hr, fq, bq, lane, B, policy, value);
-        }
-    }
+    h3_heads<C>(p, img, lo, wave, lane, b0, B, policy, value);
     if constexpr (C::DBG == 2) {
         stamp(5);
         __syncthreads();
-        if (lane < 6 && b0 + nn::kSB <= B) policy[(size_t)b0 * 50 + wave * 6 + lane] = (float)ph[lane];
+        if (lane < 8 && b0 + nn::kSB <= B) policy[(size_t)b0 * 50 + wave * 8 + lane] = (float)ph[lane];
     }
     if constexpr (C::BF) return false;  // bf16 pieces have fp32's exponent range
     return vmax >= 65504.0f || (C::TR && ((hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u));  // hi = inf
@@ -2256,6 +2362,255 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __rest
             if constexpr (C::WAVES == 4)
                 nn_h3_fallback<X, 2>(states, B, xblob, blocks, policy, value, lds);
             else if (g0)
+                nn_h3_fallback<X, 3>(states, B, xblob, blocks, policy, value, lds);
+            else
+                nn_h3_fallback<X, 4>(states, B, xblob, blocks, policy, value, lds);
+            if (threadIdx.x == 0) atomicAdd(fallback, 1ull);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_nn_q2: the k_nn_h3 arithmetic (fp16x3 split, or one bf16 piece in BF mode; transposed C/D tiles,
+// compile-time batch plans, convs in pairs, in-kernel fp16-range recompute) with TWO N-tiles per
+// wave: 8 waves = 4 square groups (GRP 11-14, 43 / 42 / 42 / 42 on-board taps) x 2 N-tile pairs;
+// waves w and w + 4 share a SIMD and a square group. Every A fragment read from LDS feeds the MFMAs
+// of both N-tiles, so the conv reads half the A bytes of k_nn_h3 (whose four N-tile waves each read
+// the same fragments), at twice the B-piece loads per wave (L2).
+template <class C, int GRP, int K, int N>
+__device__ __forceinline__ void q2_mfma(f32x4 (&acc)[2 * C::NS], const f16x8 (&a)[N], const f16x8& b0v,
+                                        const f16x8& b1v) {
+    constexpr H3Batch B = H3P<C, GRP>::P.b[K];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int q = 0; q < N; ++q)
+            if (q < B.n) {
+                f32x4& d = acc[n * C::NS + B.j[q]];
+                const f16x8& bv = n ? b1v : b0v;
+                d = C::BF ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bv),
+                                                                    __builtin_bit_cast(bf16x8, a[q]), d, 0, 0, 0)
+                          : __builtin_amdgcn_mfma_f32_16x16x32_f16(bv, a[q], d, 0, 0, 0);
+            }
+}
+// B pieces b[n * 2 + piece] of N-tile nt0 + n (the next N-tile is the next 1 KiB entry)
+template <class C, int GRP, int K>
+__device__ __forceinline__ void q2_step_b(const X6W& W, f16x8 (&b)[4], f16x8 (&bn)[4]) {
+    constexpr H3Batch B = H3P<C, GRP>::P.b[K];
+    if constexpr (B.first && K > 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) b[k] = bn[k];
+    }
+    if constexpr (B.first && B.nstep >= 0) {
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            if constexpr (C::BF) {
+                bn[n * 2] = h3_ldb(W, B.nstep * 4 + n);
+            } else {
+                bn[n * 2] = h3_ldb(W, (B.nstep * 2 + 0) * 4 + n);
+                bn[n * 2 + 1] = h3_ldb(W, (B.nstep * 2 + 1) * 4 + n);
+            }
+        }
+    }
+}
+// batch K (X holds its lo pieces on entry and the next batch's on exit; BF: its only piece):
+//   load Y = hi | lo*Bhi (both tiles) | load X = next lo | hi*Bhi, hi*Blo (both tiles)
+template <class C, int GRP, int K>
+__device__ __forceinline__ void q2_batch(f32x4 (&acc)[2 * C::NS], const char* img, const X6W& W, f16x8 (&b)[4],
+                                         f16x8 (&bn)[4], f16x8 (&X)[C::KH], f16x8 (&Y)[C::KH], const int (&ab)[2][2]) {
+    q2_step_b<C, GRP, K>(W, b, bn);
+    if constexpr (C::BF) {  // one piece: X = this batch, Y = the next (roles swap with K's parity)
+        if constexpr (K + 1 < H3P<C, GRP>::P.nbat) h3_load<C, GRP, K + 1>(Y, img, ab, 0);
+        q2_mfma<C, GRP, K>(acc, X, b[0], b[2]);
+    } else {
+        h3_load<C, GRP, K>(Y, img, ab, 0);
+        q2_mfma<C, GRP, K>(acc, X, b[0], b[2]);  // lo*hi
+        if constexpr (K + 1 < H3P<C, GRP>::P.nbat) h3_load<C, GRP, K + 1>(X, img, ab, 1);
+        q2_mfma<C, GRP, K>(acc, Y, b[0], b[2]);  // hi*hi
+        q2_mfma<C, GRP, K>(acc, Y, b[1], b[3]);  // hi*lo
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+template <class C, int GRP, int... K>
+__device__ __forceinline__ void q2_run(f32x4 (&acc)[2 * C::NS], const char* img, const X6W& W, const int (&lo)[2],
+                                       std::integer_sequence<int, K...>) {
+    int ab[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int sg = 0; sg < 2; ++sg) ab[m][sg] = lo[m] + sg * 65536;
+    constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
+    f16x8 b[4], bn[4];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        if constexpr (C::BF) {
+            b[n * 2] = h3_ldb(W, (B0.t * 2 + B0.m) * 4 + n);
+        } else {
+            b[n * 2] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 0) * 4 + n);
+            b[n * 2 + 1] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 1) * 4 + n);
+        }
+    }
+    f16x8 X[C::KH], Y[C::KH];
+    h3_load<C, GRP, 0>(X, img, ab, C::BF ? 0 : 1);
+    if constexpr (C::BF)
+        ((K % 2 == 0 ? q2_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab) : q2_batch<C, GRP, K>(acc, img, W, b, bn, Y, X, ab)),
+         ...);
+    else
+        (q2_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab), ...);
+}
+template <class C>
+using Acc1 = f32x4[C::NS];
+template <class C>
+__device__ __forceinline__ Acc1<C>& q2_tile(f32x4 (&a)[2 * C::NS], int n) {  // N-tile n's accumulators
+    return *reinterpret_cast<Acc1<C>*>(&a[n * C::NS]);
+}
+
+template <class C, int GRP>
+__device__ __forceinline__ bool nn_q2_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
+                                           int blocks, float* __restrict__ policy, float* __restrict__ value,
+                                           float* lds) {
+    constexpr int NS = C::NS;
+    char* img = reinterpret_cast<char*>(lds);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nt0 = (wave >> 2) * 2;  // N-tiles nt0, nt0 + 1
+    const int b0 = blockIdx.x * nn::kSB;
+    int* pinfo = reinterpret_cast<int*>(lds + h3::kImageB / 4);
+    const int i = lane & 15, kq = lane >> 4;
+    const int lo[2] = {h3::chunk_off(i, kq), h3::chunk_off(i, 4 + kq)};
+    int cq[2], eot[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        cq[n] = (nt0 + n) * 16 + 4 * kq;  // this lane's 4 channels of position i in N-tile nt0 + n
+        eot[n] = h3::chunk_off(i, cq[n] >> 3) + (cq[n] & 7) * 2;
+    }
+    f32x4 acc[2 * NS], skip[2 * NS];
+    uint32_t hmax = 0;
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // DBG 2: as nn_h3_body
+    uint64_t tm = C::DBG == 2 ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int k) {
+        if constexpr (C::DBG == 2) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            ph[k] += t - tm;
+            tm = t;
+        }
+    };
+    {  // encoder + first layer
+        const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
+                           nn::kValueF + nn::kPolicyF + h3::kHeadB;
+        const int b = b0 + i < B ? b0 + i : b0;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
+        const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
+        oaz_state st{};
+        if (tid < nn::kSB) st = states[b];
+        L1H<GRP> l1h[C::BF ? 1 : 2];
+        L1Regs<GRP> l1[C::BF ? 2 : 1];
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            if constexpr (C::BF)
+                first_layer_x6_fetch<GRP>(l1[n], blob, lane, nt0 + n);
+            else
+                first_layer_h3f_fetch<GRP>(l1h[n], l1c, lane, nt0 + n);
+        }
+        if (tid < nn::kSB) {
+            const int blue = st.to_move & 1;
+            const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
+            pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
+        }
+        if constexpr (!C::BF)
+            for (int t = tid; t < 512; t += 64 * C::WAVES) l1_lut_build(img, t);
+        f32x4 bias1t[2], inv1[2];
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            bias1t[n] = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq[n]);
+            inv1[n] = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f} : *reinterpret_cast<const f32x4*>(l1c + 26 * h3::kL1Frag + cq[n]);
+        }
+        __syncthreads();
+        stamp(6);
+#pragma unroll
+        for (int j = 0; j < 2 * NS; ++j) acc[j] = skip[j] = f32x4{};
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            if constexpr (C::BF)
+                first_layer_x6<C, GRP>(q2_tile<C>(acc, n), l1[n], blob + nn::kL1B + nn::kCh, bb, pinfo[i], lane, nt0 + n);
+            else
+                first_layer_h3f<C, GRP>(q2_tile<C>(acc, n), l1h[n], bb, pinfo[i], lane, reinterpret_cast<const char*>(lds),
+                                        std::make_integer_sequence<int, grp_n(GRP)>{});
+        }
+        stamp(7);
+        uint32_t pk[2][NS][2][2];
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            epilogue_h3t_pack<C, GRP, true>(q2_tile<C>(acc, n), pk[n], bias1t[n], inv1[n], q2_tile<C>(skip, n), false,
+                                            hmax);
+            epilogue_h3t_store<C, GRP>(pk[n], img, eot[n]);
+        }
+        __syncthreads();
+    }
+    stamp(0);
+    const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
+    constexpr size_t kWc = C::BF ? nn::kW64h : h3::kW;  // B fragments of one conv
+    auto conv_one = [&](auto resc) {  // RESC 0 / 1: the block's first / second conv
+        constexpr int RESC = decltype(resc)::value;
+        f32x4 bbt[2], sct[2];
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            bbt[n] = *reinterpret_cast<const f32x4*>(p + kWc + cq[n]);  // in flight during the conv
+            sct[n] = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f} : *reinterpret_cast<const f32x4*>(p + kWc + nn::kCh + cq[n]);
+        }
+#pragma unroll
+        for (int j = 0; j < 2 * NS; ++j) acc[j] = f32x4{};
+        q2_run<C, GRP>(acc, img, h3_w(p, lane, nt0, (int)(kWc * 4)), lo,
+                       std::make_integer_sequence<int, H3P<C, GRP>::P.nbat>{});
+        stamp(1);
+        p += kWc + 2 * nn::kCh - (C::BF ? nn::kCh : 0);
+        uint32_t pk[2][NS][2][2];
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+            epilogue_h3t_pack<C, GRP, false, RESC>(q2_tile<C>(acc, n), pk[n], bbt[n], sct[n], q2_tile<C>(skip, n),
+                                                   RESC == 1, hmax);
+        stamp(3);
+        __syncthreads();
+        stamp(2);
+#pragma unroll
+        for (int n = 0; n < 2; ++n) epilogue_h3t_store<C, GRP>(pk[n], img, eot[n]);
+        stamp(3);
+        __syncthreads();
+        stamp(4);
+    };
+    for (int c = 0; c < 2 * blocks; c += 2) {
+        conv_one(std::integral_constant<int, 0>{});
+        conv_one(std::integral_constant<int, 1>{});
+    }
+    h3_heads<C>(p, img, lo, wave, lane, b0, B, policy, value);
+    if constexpr (C::DBG == 2) {
+        stamp(5);
+        __syncthreads();
+        if (lane < 8 && b0 + nn::kSB <= B) policy[(size_t)b0 * 50 + wave * 8 + lane] = (float)ph[lane];
+    }
+    if constexpr (C::BF) return false;
+    return (hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u;  // an fp16 hi = inf
+}
+
+template <class C>
+__global__ void __launch_bounds__(64 * C::WAVES) k_nn_q2(const oaz_state* __restrict__ states, int B,
+                                                        const float* __restrict__ blob, int blocks,
+                                                        float* __restrict__ policy, float* __restrict__ value,
+                                                        const float* __restrict__ xblob,
+                                                        unsigned long long* __restrict__ fallback) {
+    static_assert(C::Q2 && C::WAVES == 8 && C::TR && C::EP, "k_nn_q2: 8 waves, transposed tiles, conv pairs");
+    __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
+    bool ovf;
+    switch ((threadIdx.x >> 6) & 3) {  // square group; waves w and w + 4 (one SIMD) share it
+        case 0: ovf = nn_q2_body<C, 11>(states, B, blob, blocks, policy, value, lds); break;
+        case 1: ovf = nn_q2_body<C, 12>(states, B, blob, blocks, policy, value, lds); break;
+        case 2: ovf = nn_q2_body<C, 13>(states, B, blob, blocks, policy, value, lds); break;
+        default: ovf = nn_q2_body<C, 14>(states, B, blob, blocks, policy, value, lds); break;
+    }
+    if constexpr (H3Fallback<C>::kOn) {
+        using X = typename H3Fallback<C>::X;
+        const bool g0 = (threadIdx.x >> 8) == 0;
+        if (__syncthreads_or(ovf)) {  // uniform over the workgroup; also the barrier before LDS reuse
+            if (g0)
                 nn_h3_fallback<X, 3>(states, B, xblob, blocks, policy, value, lds);
             else
                 nn_h3_fallback<X, 4>(states, B, xblob, blocks, policy, value, lds);
@@ -2637,6 +2992,15 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             case 34: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 2, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, 16 / 9
             case 35: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 4, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, 18 / 7
             case 36: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // timing only: EP phase stamps
+            case 42: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 0, 0, 1, 0, 2>>; break;  // EP + BD 2
+            case 43: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1, 1, 0, 0, 0, 0, 1, 0, 2>>; break;  // EP + BD 2, 15 / 10
+            case 44: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 0, 1, 1, 0, 0, 0, 0, 1, 0, 2>>; break;  // EP + BD 2, 13 / 12, PIPE 2
+            case 45: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 0, 1, 1, 0, 0, 0, 0, 1, 0, 2>>; break;  // EP + BD 2, 13 / 12
+            case 50: k = k_nn_q2<X6Cfg<8, 4, 1, 0, 0, 1, 1, 0, 0, 0, 0, 1, 0, 1, 1>>; break;  // Q2: 2 N-tiles per wave
+            case 51: k = k_nn_q2<X6Cfg<8, 3, 1, 0, 0, 1, 1, 0, 0, 0, 0, 1, 0, 1, 1>>; break;  // Q2, KH 3
+            case 52: k = k_nn_q2<X6Cfg<8, 4, 1, 2, 0, 1, 1, 0, 0, 0, 0, 1, 0, 1, 1>>; break;  // timing only: Q2 stamps
+            case 40: k = k_nn_h3<X6Cfg<8, 4, 1, 3, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // ablation: no conv A reads
+            case 41: k = k_nn_h3<X6Cfg<8, 4, 1, 4, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // ablation: no conv B loads
             case 20: {  // 8 positions per workgroup, 2 workgroups per CU (measured 1.40 vs 1.25 ms)
                 const unsigned g8 = (unsigned)((B + p8::kP - 1) / p8::kP);
                 hipLaunchKernelGGL((k_nn_p8<4, 1>), dim3(g8), dim3(256), 0, st, s, B, w.blob, w.blocks, policy, value,
@@ -2681,6 +3045,8 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
         auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 1, 0, 0, 1>>;
 #if OAZ_AB
         if (w.bf16_v1 == 4) k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 1>>;  // the previous default (runtime parity)
+        if (w.bf16_v1 == 5) k = k_nn_q2<X6Cfg<8, 4, 1, 0, 0, 1, 1, 0, 1, 0, 0, 1, 0, 1, 1>>;  // Q2 (2 N-tiles per wave)
+        if (w.bf16_v1 == 6) k = k_nn_q2<X6Cfg<8, 6, 1, 0, 0, 1, 1, 0, 1, 0, 0, 1, 0, 1, 1>>;  // Q2, KH 6
 #endif
         hipLaunchKernelGGL(k, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value, nullptr,
                            nullptr);

@@ -24,8 +24,10 @@ with Engine(games=B, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN, precision=pr
     e.load_weights(random_weights(0, blocks))
     e.nn_forward(states)
     p, _ = e.nn_forward(states)
-flat = p.reshape(B // 16, 800)[:, :48].reshape(-1, 8, 6).astype(np.float64)
-names = ["first_layer", "conv", "barrier1", "epilogue", "barrier2", "heads"]
+h3 = (sys.argv[3] if len(sys.argv) > 3 else "x6") == "h3"
+nph = 8 if h3 else 6  # k_nn_h3 also stamps the kernel start and the first-layer MFMAs
+flat = p.reshape(B // 16, 800)[:, :8 * nph].reshape(-1, 8, nph).astype(np.float64)
+names = ["first_layer", "conv", "barrier1", "epilogue", "barrier2", "heads", "start", "first_layer_mfma"][:nph]
 mean = flat.mean(axis=0)  # [wave][phase]
 out = {"per_wave_mean_cycles": {f"w{w}": dict(zip(names, mean[w].round(0).tolist())) for w in range(8)},
        "all_waves": dict(zip(names, mean.mean(0).round(0).tolist())),
