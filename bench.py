@@ -494,7 +494,8 @@ def exact_fp32_leg(args, cfg, device):
         st1 = e.selfplay_stats()
     sims = st1.search.sims - st0.search.sims
     nn_ms = kt.nn_ms / max(1, kt.nn_n)
-    fl = FLOP_PER_SIM[cfg["blocks"]] * kt.nn_samples / max(1, kt.nn_n)
+    # positions per NN launch: the evaluations the playouts use (leaf compaction), per simulation step
+    fl = FLOP_PER_SIM[cfg["blocks"]] * (st1.search.nn_evals - st0.search.nn_evals) / max(1, 2 * cfg["sims"])
     tf = fl / (nn_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
     return {"kernel": NN_KERNEL["fp32"], "value": sims / dt, "unit": "sims/s", "ms_per_step": 1e3 * dt / 2,
             "steps": 2, "warmup": 2, "nn_avg_launch_ms": nn_ms, "nn_achieved_TFLOPs": tf,
@@ -582,6 +583,7 @@ def main():
     st1 = eng.selfplay_stats()
 
     sims = st1.search.sims - st0.search.sims
+    evals = st1.search.nn_evals - st0.search.nn_evals  # leaves sent to the network (compacted)
     games_done = st1.games_finished - st0.games_finished
     plies = st1.moves - st0.moves
     expansions = st1.search.expansions - st0.search.expansions
@@ -622,11 +624,12 @@ def main():
     if rank == 0:
         sims_steps = cfg["sims"]  # simulation steps (select -> NN -> expand launches) per bench step
         nn_avg_ms = kt.nn_ms / max(1, kt.nn_n)
-        flops_launch = FLOP_PER_SIM[cfg["blocks"]] * (kt.nn_samples / max(1, kt.nn_n))
+        # every simulation step launches the NN once on the compacted leaves of all games
+        positions = evals / max(1, args.steps * sims_steps)
+        flops_launch = FLOP_PER_SIM[cfg["blocks"]] * positions
         achieved = flops_launch / (nn_avg_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
-        nz = nonzero_flop_per_sim(cfg["blocks"]) * (kt.nn_samples / max(1, kt.nn_n))
+        nz = nonzero_flop_per_sim(cfg["blocks"]) * positions
         achieved_nz = nz / (nn_avg_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
-        positions = kt.nn_samples / max(1, kt.nn_n)
         alg_bytes = 0.96e6 + positions * (24 + 204)  # weights once + states in + policy/value out
         out = {
             "metric": METRIC, "value": sims_all / T, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
@@ -653,10 +656,16 @@ def main():
             "sims_per_s_per_gpu": sims_all / T / world, "stagger": stagger,
             "games_per_s": games_all / T, "plies_per_s": plies_all / T,
             "true_expansions_per_s": exp_all / T, "mean_select_depth": depth, "mean_branching": branching,
+            "nn_positions_per_sim": evals / max(1, sims),
+            "nn_evaluation": "every simulation's leaf is evaluated except a won, terminal-flagged leaf, whose evaluation "
+                             "the reference computes and discards (mcts_arena.rs:156-176: no expansion, the reward is "
+                             "backed up); select marks those leaves and k_eval_compact packs the others per 4096-game "
+                             "bucket, so the trees are unchanged and the network runs on nn_positions_per_sim of them",
             "kernel_ms_per_step": {
                 "select": kt.select_ms / max(1, kt.select_n) * sims_steps,
                 "nn": kt.nn_ms / max(1, kt.nn_n) * sims_steps,
                 "expand_backup": kt.expand_ms / max(1, kt.expand_n) * sims_steps,
+                "leaf_compact": kt.compact_ms / max(1, kt.compact_n) * sims_steps,
                 "move": kt.finalize_ms / args.steps, "root_noise_stream2": kt.noise_ms / args.steps},
             "kernel_timing": "HIP events around the kernels of every %s-th simulation step (per-kernel means x "
                              "simulation steps per bench step)" % os.environ.get("OAZ_BENCH_TIMING_EVERY", "8"),

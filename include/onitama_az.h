@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define OAZ_ABI_VERSION 2
+#define OAZ_ABI_VERSION 3
 
 /* ---- enums mirroring the reference --------------------------------------- */
 enum { OAZ_RED = 0, OAZ_BLUE = 1 };                 /* PlayerColor, player_color.rs:7-10 */
@@ -166,6 +166,10 @@ typedef struct oaz_search_stats {
     uint64_t depth_sum;       /* sum of select path depths */
     uint64_t stuck_leaves;    /* expanded nodes with no legal move (reference panics, Q6) */
     uint64_t max_nodes;       /* largest tree seen */
+    uint64_t nn_evals;        /* leaf evaluations whose policy or value the playout uses: every
+                               * playout except those ending on a won, already terminal-flagged
+                               * node, whose evaluation the reference computes and then discards
+                               * (mcts_arena.rs:156-176); only these are sent to the network */
 } oaz_search_stats;
 
 typedef struct oaz_selfplay_stats {
@@ -184,9 +188,12 @@ typedef struct oaz_kernel_times {
      * oaz_set_timing(eng, 1) */
     double select_ms, nn_ms, expand_ms, finalize_ms;
     uint64_t select_n, nn_n, expand_n, finalize_n;
-    uint64_t nn_samples;  /* samples evaluated by the timed nn launches */
+    uint64_t nn_samples;  /* positions of the timed nn launches outside the simulation loop (oaz_nn_forward,
+                           * root values); in the loop the count is on the device: oaz_search_stats.nn_evals */
     double noise_ms;      /* Dirichlet root-noise producer (second stream, overlaps the NN) */
     uint64_t noise_n;
+    double compact_ms;    /* leaf compaction (the positions the NN evaluates, per 4096-game bucket) */
+    uint64_t compact_n;
 } oaz_kernel_times;
 
 typedef struct oaz_engine oaz_engine;

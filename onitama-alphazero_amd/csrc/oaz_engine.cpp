@@ -604,7 +604,7 @@ extern "C" int oaz_encode(const oaz_state* s, int n, float* planes) {
 
 // ---- engine ------------------------------------------------------------------------------------
 struct TimedLaunch {
-    int kind;  // 0 select, 1 nn, 2 expand, 3 finalize, 4 root noise (second stream)
+    int kind;  // 0 select, 1 nn, 2 expand, 3 finalize, 4 root noise (second stream), 5 leaf compaction
     hipEvent_t a, b;
     uint32_t samples;
 };
@@ -614,9 +614,7 @@ struct oaz_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;       // root-noise producer, overlaps the NN kernel
-    hipStream_t stream3 = nullptr;       // second half of the games (tree kernels overlap the other half's NN)
     hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_consumed[2] = {nullptr, nullptr};
-    hipEvent_t ev_nn[2] = {nullptr, nullptr}, ev_join = nullptr;
     float* noise = nullptr;              // [2][kNoiseChunk][G][kNoiseStride]
     uint32_t G = 0, cap = 0, pathcap = 0, hcap = 0, out_cap = 0;
     int32_t sims_cap = 0;                // cfg.sims at creation: trees and paths are sized for it
@@ -627,7 +625,10 @@ struct oaz_engine {
     uint64_t* stats = nullptr;
     uint64_t* stats_sum = nullptr;
     double* sqrt_tab = nullptr;
-    float *policy = nullptr, *value = nullptr;
+    float *policy = nullptr, *value = nullptr;  // evaluations by compacted row (TreeView::slot)
+    uint8_t* need = nullptr;                    // leaf compaction (oaz_kernels.h TreeView)
+    uint32_t *slot = nullptr, *bcnt = nullptr;
+    oaz_state* cstate = nullptr;
     float* weights = nullptr;
     bool have_weights = false;
     unsigned long long* nn_fallback = nullptr;  // OAZ_FP32_SPLIT16: tiles recomputed by k_nn_x6 (fp16 range)
@@ -679,6 +680,10 @@ static TreeView tree_view(oaz_engine* e, uint32_t G) {
     t.leaf_state = e->leaf_state;
     t.stats = e->stats;
     t.sqrt_tab = e->sqrt_tab;
+    t.need = e->need;
+    t.slot = e->slot;
+    t.cstate = e->cstate;
+    t.bcnt = e->bcnt;
     t.cap = e->cap;
     t.pathcap = e->pathcap;
     t.G = G;
@@ -733,10 +738,10 @@ static hipEvent_t ev_get(oaz_engine* e) {
 static constexpr uint32_t kNoiseChunk = 8;  // simulations of root noise produced per launch
 
 static void accumulate(oaz_engine* e, const TimedLaunch& p, float ms) {
-    double* acc[5] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms,
-                      &e->times.noise_ms};
-    uint64_t* cnt[5] = {&e->times.select_n, &e->times.nn_n, &e->times.expand_n, &e->times.finalize_n,
-                        &e->times.noise_n};
+    double* acc[6] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms,
+                      &e->times.noise_ms, &e->times.compact_ms};
+    uint64_t* cnt[6] = {&e->times.select_n, &e->times.nn_n, &e->times.expand_n, &e->times.finalize_n,
+                        &e->times.noise_n, &e->times.compact_n};
     *acc[p.kind] += ms;
     *cnt[p.kind] += 1;
     if (p.kind == 1) e->times.nn_samples += p.samples;
@@ -761,7 +766,6 @@ static int timed(oaz_engine* e, int kind, uint32_t samples, F&& launch, hipStrea
     if (e->pending.size() > 4096) {  // resolve periodically to bound the pool
         HIP_TRY(hipStreamSynchronize(e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream2));
-        HIP_TRY(hipStreamSynchronize(e->stream3));
         for (auto& p : e->pending) {
             float ms = 0.f;
             (void)hipEventElapsedTime(&ms, p.a, p.b);
@@ -822,11 +826,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         return fail();
     }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_nn[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_nn[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) {
         oaz_set_err(OAZ_ERR_HIP, "stream create failed");
         return fail();
     }
@@ -841,7 +841,8 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         dalloc(&e->depth, G) || dalloc(&e->leaf, G) || dalloc(&e->leaf_state, G) ||
         dalloc(&e->stats, G * GS_COUNT) || dalloc(&e->stats_sum, (size_t)GS_COUNT) ||
         dalloc(&e->sqrt_tab, (size_t)cfg->sims + 2) || dalloc(&e->policy, G * 50) ||
-        dalloc(&e->value, G) || dalloc(&e->weights, weights_floats(cfg->blocks, cfg->precision)) ||
+        dalloc(&e->value, G) || dalloc(&e->need, G) || dalloc(&e->slot, G) || dalloc(&e->cstate, G + 16) ||
+        dalloc(&e->bcnt, (size_t)buckets_of((uint32_t)G)) || dalloc(&e->weights, weights_floats(cfg->blocks, cfg->precision)) ||
         dalloc(&e->s_roots, G) || dalloc(&e->s_move, G) || dalloc(&e->s_pi, G * 50) ||
         dalloc(&e->s_rootv, G) || dalloc(&e->s_rootp, G * 50) || dalloc(&e->s_ply, G) ||
         dalloc(&e->root, G) || dalloc(&e->ply, G) || dalloc(&e->seq, G) ||
@@ -856,7 +857,9 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         hipMemset(e->stats, 0, G * GS_COUNT * sizeof(uint64_t)) != hipSuccess ||
         hipMemset(e->out_count, 0, sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(e->nn_fallback, 0, sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(e->active, 0, G) != hipSuccess) {
+        hipMemset(e->active, 0, G) != hipSuccess || hipMemset(e->need, 0, G) != hipSuccess ||
+        hipMemset(e->slot, 0, G * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(e->cstate, 0, (G + 16) * sizeof(oaz_state)) != hipSuccess) {
         oaz_set_err(OAZ_ERR_HIP, "create: init copies failed");
         return fail();
     }
@@ -873,13 +876,10 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->stream2) (void)hipStreamSynchronize(e->stream2);
-    if (e->stream3) (void)hipStreamSynchronize(e->stream3);
     for (int i = 0; i < 2; ++i) {
         if (e->ev_ready[i]) (void)hipEventDestroy(e->ev_ready[i]);
         if (e->ev_consumed[i]) (void)hipEventDestroy(e->ev_consumed[i]);
-        if (e->ev_nn[i]) (void)hipEventDestroy(e->ev_nn[i]);
     }
-    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     for (auto& p : e->pending) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -888,11 +888,11 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     void* ptrs[] = {e->nodes, e->n_nodes, e->path, e->depth, e->leaf, e->leaf_state, e->stats,
                     e->stats_sum, e->sqrt_tab, e->policy, e->value, e->weights, e->s_roots,
                     e->s_move, e->s_pi, e->s_rootv, e->s_rootp, e->s_ply, e->root, e->ply,
-                    e->seq, e->game_id, e->active, e->hist, e->out, e->out_count, e->noise, e->nn_fallback};
+                    e->seq, e->game_id, e->active, e->hist, e->out, e->out_count, e->noise, e->nn_fallback,
+                    e->need, e->slot, e->cstate, e->bcnt};
     for (void* p : ptrs) dfree(p);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
-    if (e->stream3) (void)hipStreamDestroy(e->stream3);
     delete e;
 }
 
@@ -938,7 +938,6 @@ extern "C" int oaz_sync(oaz_engine* e) {
     if (!e) return oaz_set_err(OAZ_ERR_ARG, "sync: null");
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream2));
-    HIP_TRY(hipStreamSynchronize(e->stream3));
     return 0;
 }
 
@@ -953,7 +952,6 @@ extern "C" int oaz_set_timing(oaz_engine* e, int enable) {
 static int resolve_timing(oaz_engine* e) {
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream2));
-    HIP_TRY(hipStreamSynchronize(e->stream3));
     for (auto& p : e->pending) {
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b));
@@ -979,11 +977,14 @@ extern "C" int oaz_kernel_times_reset(oaz_engine* e) {
     return 0;
 }
 
+// B positions d_states[0, B) -> rows [0, B); with tm (compacted leaves, run_sims) the rows of the
+// bucket tiles (the HASH evaluator simply evaluates every row below B).
 static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float* d_pol, float* d_val,
-                    hipStream_t st = nullptr) {
+                    hipStream_t st = nullptr, const TileMap* tm = nullptr) {
     if (!st) st = e->stream;
+    const uint32_t counted = tm ? 0u : B;  // compacted: the count is on the device (GS_EVALS)
     if (e->cfg.evaluator == OAZ_EVAL_HASH)
-        return timed(e, 1, B, [&] { return launch_hash_eval(d_states, (int)B, d_pol, d_val, st); }, st);
+        return timed(e, 1, counted, [&] { return launch_hash_eval(d_states, (int)B, d_pol, d_val, st); }, st);
     NNView w;
     w.blob = e->weights;
     w.blocks = e->cfg.blocks;
@@ -1001,7 +1002,8 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
     w.blob_x6 = e->cfg.precision == OAZ_FP32_SPLIT16 ? e->weights + nn_packed_floats(e->cfg.blocks, OAZ_FP32_SPLIT16)
                                                      : nullptr;
     w.fallback = e->nn_fallback;
-    return timed(e, 1, B, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, st); }, st);
+    w.tm = tm ? *tm : TileMap{nullptr, 0, 0};
+    return timed(e, 1, counted, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, st); }, st);
 }
 
 extern "C" int oaz_nn_fallbacks(oaz_engine* e, uint64_t* tiles) {
@@ -1027,23 +1029,26 @@ extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* p
     return 0;
 }
 
-// All cfg.sims simulations of one move for every game: select -> evaluate -> expand/backup,
-// in lock step. With root noise, k_root_noise fills chunk c+1 of the double-buffered noise
-// ring on stream2 while stream 1 runs chunk c (events order the two ring slots).
-// The trees of games [g0, g0 + n) as a view of their own (every per-game array offset).
-static TreeView slice_view(const TreeView& t, uint32_t g0, uint32_t n) {
-    TreeView v = t;
-    v.nodes = t.nodes + (size_t)g0 * t.cap;
-    v.n_nodes = t.n_nodes + g0;
-    v.path = t.path + (size_t)g0 * t.pathcap;
-    v.depth = t.depth + g0;
-    v.leaf = t.leaf + g0;
-    v.leaf_state = t.leaf_state + g0;
-    v.stats = t.stats + (size_t)g0 * GS_COUNT;
-    v.G = n;
-    return v;
+// Leaf compaction is on unless an A/B-only NN variant without tile maps is selected.
+static bool compact_leaves(const oaz_engine* e) {
+#if OAZ_AB
+    if (e->cfg.evaluator == OAZ_EVAL_NN) {
+        const char* xv = getenv("OAZ_NN_X6_V");
+        const char* v1 = getenv("OAZ_NN_BF16_V1");
+        if ((xv && atoi(xv) == 20) || (v1 && (atoi(v1) == 2 || atoi(v1) == 3))) return false;  // k_nn_p8, k_nn_bf16g
+    }
+#else
+    (void)e;
+#endif
+    return true;
 }
 
+// All cfg.sims simulations of one move for every game, in lock step: select -> leaf compaction ->
+// evaluate -> expand/backup. Select marks the games whose playout uses its leaf evaluation (all
+// but those ending on a won, terminal-flagged node, whose evaluation the reference discards:
+// mcts_arena.rs:156-176) and the compaction kernel packs their leaves per 4096-game bucket, so the
+// network evaluates only those. With root noise, k_root_noise fills chunk c+1 of the
+// double-buffered noise ring on stream2 while stream 1 runs chunk c (events order the ring slots).
 static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, const uint8_t* active,
                     const uint64_t* gids, const uint32_t* plies) {
     const SearchParams prm = search_params(e);
@@ -1068,71 +1073,39 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
         HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[0], 0));
         if (int rc = produce(0)) return rc;
     }
-    // Optional (OAZ_SPLIT_HALVES=1): two halves of the games on two streams, the NN launches of the
-    // halves alternating and each half's select / expand-backup running beside the other half's NN.
-    // Measured no faster on MI355X (C3 11.88 vs 11.93 M sims/s; the tree kernels slow down 4x
-    // beside the NN), so one stream is the default.
-#if OAZ_AB
-    const bool split = t.G >= 4096 && getenv("OAZ_SPLIT_HALVES") && getenv("OAZ_SPLIT_HALVES")[0] == '1';
-#else
-    const bool split = false;
-#endif
-    const uint32_t GA = split ? (t.G / 2 + 63) / 64 * 64 : t.G;
-    hipStream_t sh[2] = {e->stream, e->stream3};
-    TreeView tv[2] = {t, t};
-    uint32_t g0[2] = {0, GA};
-    if (split) {
-        tv[0].G = GA;
-        tv[1] = slice_view(t, GA, t.G - GA);
-        HIP_TRY(hipEventRecord(e->ev_join, e->stream));  // stream3 starts after prior work
-        HIP_TRY(hipStreamWaitEvent(e->stream3, e->ev_join, 0));
+    TreeView tc = t;  // the compaction arrays, or none (rows = game ids)
+    if (!compact_leaves(e)) {
+        tc.need = nullptr;
+        tc.slot = nullptr;
     }
-    const int nh = split ? 2 : 1;
-    bool nn_recorded[2] = {false, false};
+    const TileMap tm{t.bcnt, buckets_of(t.G), (int32_t)t.G + 16};
+    hipStream_t st = e->stream;
     for (uint32_t c = 0; c < nchunks; ++c) {
         if (noise) {
             if (c + 1 < nchunks)
                 if (int rc = produce(c + 1)) return rc;
-            for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(sh[h], e->ev_ready[c & 1], 0));
+            HIP_TRY(hipStreamWaitEvent(st, e->ev_ready[c & 1], 0));
         }
         const uint32_t s0 = c * kNoiseChunk, s1 = s0 + kNoiseChunk < sims ? s0 + kNoiseChunk : sims;
         for (uint32_t s = s0; s < s1; ++s) {
             // sampled steps sit mid-chunk: a chunk's first select also waits for its noise
             e->timing_skip = e->timing_every > 1 && s % (uint32_t)e->timing_every != (uint32_t)e->timing_every / 2;
-            for (int h = 0; h < nh; ++h) {
-                const TreeView& th = tv[h];
-                const size_t go = g0[h];
-                const float* nz = noise ? e->noise + (c & 1) * slot_elems + (size_t)(s - s0) * t.G * kNoiseStride +
-                                               go * kNoiseStride
-                                         : nullptr;
-                const uint8_t* act = active ? active + go : nullptr;  // null in search mode
-                if (int rc = timed(e, 0, th.G, [&] {
-                        return launch_select(th, roots + go, act, nz, prm, sh[h]);
-                    }, sh[h]))
-                    return rc;
-                if (split && nn_recorded[h ^ 1]) HIP_TRY(hipStreamWaitEvent(sh[h], e->ev_nn[h ^ 1], 0));
-                if (int rc = evaluate(e, th.leaf_state, th.G, e->policy + go * 50, e->value + go, sh[h])) return rc;
-                if (split) {
-                    HIP_TRY(hipEventRecord(e->ev_nn[h], sh[h]));
-                    nn_recorded[h] = true;
-                }
-                if (int rc = timed(e, 2, th.G, [&] {
-                        return launch_expand_backup(th, roots + go, act, e->policy + go * 50, e->value + go, sh[h]);
-                    }, sh[h]))
-                    return rc;
+            const float* nz = noise ? e->noise + (c & 1) * slot_elems + (size_t)(s - s0) * t.G * kNoiseStride : nullptr;
+            if (int rc = timed(e, 0, t.G, [&] { return launch_select(tc, roots, active, nz, prm, st); }, st)) return rc;
+            if (tc.need) {
+                if (int rc = timed(e, 5, t.G, [&] { return launch_eval_compact(tc, st); }, st)) return rc;
+                if (int rc = evaluate(e, tc.cstate, t.G, e->policy, e->value, st, &tm)) return rc;
+            } else if (int rc = evaluate(e, tc.leaf_state, t.G, e->policy, e->value, st)) {
+                return rc;
             }
+            if (int rc = timed(e, 2, t.G, [&] {
+                    return launch_expand_backup(tc, roots, active, e->policy, e->value, st);
+                }, st))
+                return rc;
         }
-        if (split) {  // both halves are done with this noise slot
-            HIP_TRY(hipEventRecord(e->ev_join, e->stream3));
-            HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));
-        }
-        if (noise) HIP_TRY(hipEventRecord(e->ev_consumed[c & 1], e->stream));
+        if (noise) HIP_TRY(hipEventRecord(e->ev_consumed[c & 1], st));
     }
     e->timing_skip = false;
-    if (split) {
-        HIP_TRY(hipEventRecord(e->ev_join, e->stream3));
-        HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));
-    }
     return 0;
 }
 
@@ -1151,6 +1124,7 @@ static void fill_search_stats(const uint64_t* s, oaz_search_stats* o) {
     o->depth_sum = s[GS_DEPTH];
     o->stuck_leaves = s[GS_STUCK];
     o->max_nodes = s[GS_MAXNODES];
+    o->nn_evals = s[GS_EVALS];
 }
 
 extern "C" int oaz_search(oaz_engine* e, const oaz_state* roots, int G, oaz_move* out_move, float* out_pi,

@@ -24,6 +24,7 @@ enum GameStat {
     GS_BLUE,
     GS_PASSES,
     GS_DROPPED,
+    GS_EVALS,  // leaves whose evaluation the playout uses (oaz_search_stats.nn_evals)
     GS_COUNT = 16
 };
 
@@ -37,6 +38,11 @@ struct TreeView {
     oaz_state* leaf_state;  // [G] position at the leaf (to_move = leaf colour)
     uint64_t* stats;        // [G][GS_COUNT]
     const double* sqrt_tab; // [sims+1] correctly rounded sqrt(n) (host libm)
+    // leaf compaction (null need: none, the evaluator reads leaf_state[g] and writes row g)
+    uint8_t* need;          // [G] 1 = the playout uses the leaf's evaluation (written by select)
+    uint32_t* slot;         // [G] row of game g's evaluation in the compacted policy / value
+    oaz_state* cstate;      // [G + 16] compacted leaf positions (bucket b's at b * kBucket ..)
+    uint32_t* bcnt;         // [nb] positions per bucket
     uint32_t cap;
     uint32_t pathcap;
     uint32_t G;
@@ -72,6 +78,18 @@ struct SlotView {
     uint32_t stagger;      // slot g waits g % stagger plies before its first game (0: none)
 };
 
+// Evaluator tiles over the compacted leaves: bucket b (games [b * kBucket, (b + 1) * kBucket)) holds
+// its bcnt[b] positions at rows b * kBucket ..; workgroup i takes tile i / nb of bucket i % nb, so the
+// buckets' full tiles come first and the empty tail workgroups exit after their first loads.
+constexpr int kBucketShift = 12;
+constexpr uint32_t kBucket = 1u << kBucketShift;
+struct TileMap {
+    const uint32_t* bcnt;  // null: plain tiles over rows [0, B)
+    int32_t nb;            // buckets
+    int32_t cap;           // readable rows (loads are clamped to it, stores are guarded by the count)
+};
+inline int32_t buckets_of(uint32_t G) { return (int32_t)((G + kBucket - 1) >> kBucketShift); }
+
 struct NNView {
     const float* blob;  // packed, BN-folded weights (DESIGN.md "NN weights layout")
     int32_t blocks;
@@ -81,6 +99,7 @@ struct NNView {
     int32_t bf16_v1;    // A/B build only (OAZ_NN_BF16_V1): 1 k_nn_sq16<bf16>, 2 k_nn_bf16g<4>, 3 k_nn_bf16g<2>
     const float* blob_x6;             // OAZ_FP32_SPLIT16: the OAZ_FP32_SPLIT blob of the same weights
     unsigned long long* fallback;     // OAZ_FP32_SPLIT16: tiles recomputed by the k_nn_x6 body (fp16 range)
+    TileMap tm;                       // compacted leaves (tm.bcnt null: rows [0, B))
 };
 
 // rules
@@ -94,6 +113,8 @@ hipError_t launch_encode(const oaz_state* s, int n, float* planes, hipStream_t s
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy,
                              float* value, hipStream_t st);
 hipError_t launch_hash_eval(const oaz_state* s, int B, float* policy, float* value, hipStream_t st);
+// gather the leaves the playouts use (t.need) into t.cstate / t.slot / t.bcnt, bucket by bucket
+hipError_t launch_eval_compact(const TreeView& t, hipStream_t st);
 size_t nn_packed_floats(int blocks, int precision);
 
 // MCTS

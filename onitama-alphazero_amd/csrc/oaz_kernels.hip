@@ -198,6 +198,56 @@ __global__ void k_hash_eval(const oaz_state* states, int n, float* policy, float
     value[i] = hash_value(h);
 }
 
+// ---- leaf compaction: the positions the NN evaluates ----------------------------------------
+// One workgroup per bucket of kBucket games: the games whose playout uses its leaf evaluation
+// (t.need, written by select) get consecutive rows b * kBucket + j in game order; their leaf
+// positions are gathered to t.cstate, game g's row to t.slot[g], the count to t.bcnt[b]. The
+// evaluator's workgroups then cover bcnt[b] rows per bucket (TileMap) and expand/backup reads
+// row t.slot[g]. Thread tid owns games 4 tid .. 4 tid + 3 of the bucket.
+constexpr int kCompactThreads = (int)(kBucket / 4);
+__global__ void __launch_bounds__(kCompactThreads) k_eval_compact(TreeView t) {
+    __shared__ uint32_t wsum[kCompactThreads / 64];
+    const uint32_t base = blockIdx.x << kBucketShift;
+    const int tid = threadIdx.x, w = tid >> 6;
+    const uint32_t g0 = base + 4 * (uint32_t)tid;
+    // the 4 leaf positions are requested with the flags (contiguous 96 B per thread), so the gather
+    // below is not a second dependent round trip
+    oaz_state ls[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ls[k] = load_state(&t.leaf_state[g0 + k < t.G ? g0 + k : t.G - 1]);
+    uint32_t f = 0;  // need flags of the 4 games, one byte each
+    if (g0 + 4 <= t.G) {
+        f = *reinterpret_cast<const uint32_t*>(t.need + g0);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (g0 + k < t.G) f |= (uint32_t)(t.need[g0 + k] != 0) << (8 * k);
+    }
+    f &= 0x01010101u;
+    const uint32_t cnt = (uint32_t)__popc(f);
+    const uint32_t incl = wave_incl_scan(cnt);
+    if (lane_id() == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kCompactThreads / 64; ++i) {
+        const uint32_t v = wsum[i];
+        off += i < w ? v : 0u;
+        tot += v;
+    }
+    uint32_t j = base + off + incl - cnt;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (f & (1u << (8 * k))) {
+            const uint32_t g = g0 + k;
+            t.slot[g] = j;
+            store_state(&t.cstate[j], ls[k]);
+            ++j;
+        }
+    }
+    if (tid == 0) t.bcnt[blockIdx.x] = tot;
+}
+
 // ---- Dirichlet root noise: root_noise() in oaz_device.h ------------------------------------
 // Dirichlet draws of nsims consecutive simulations for every root: out[(k*G + g)*80 + 2j + {0,1}]
 // holds the noise for comparison j (operand a, operand b) of simulation sim0+k. They depend only
@@ -248,6 +298,12 @@ __device__ __forceinline__ NodeRegs load_node(const oaz_node* p) {
 __device__ __forceinline__ int node_nch(uint32_t misc) { return (misc >> 16) & 0xFF; }
 __device__ __forceinline__ int node_flags(uint32_t misc) { return misc >> 24; }
 __device__ __forceinline__ uint8_t* flags_ptr(oaz_node* n) { return &n->flags; }
+// The playout uses the leaf's evaluation (mcts_arena.rs:156-176) to expand the leaf (neither
+// expanded nor terminal-flagged) or to back up its value (the position is not won). Otherwise the
+// reference evaluates the leaf and discards the result, and the leaf is left out of the NN batch.
+__device__ __forceinline__ bool leaf_needs_eval(uint32_t misc, const oaz_state& s) {
+    return !(node_flags(misc) & 3) || !is_win(current_state(s));
+}
 
 __device__ __forceinline__ void store_fresh_node(oaz_node* p, double P, uint32_t mv) {
     uint4* q = reinterpret_cast<uint4*>(p);
@@ -271,7 +327,10 @@ __global__ void __launch_bounds__(kBlock) k_select(TreeView t, const oaz_state* 
                                                    SearchParams prm) {
     const uint32_t g = wave_game();
     if (g >= t.G) return;
-    if (active && active[g] != 1) return;
+    if (active && active[g] != 1) {
+        if (t.need && lane_id() == 0) t.need[g] = 0;
+        return;
+    }
     const int l = lane_id();
     oaz_node* T = t.nodes + (size_t)g * t.cap;
     uint32_t* path = t.path + (size_t)g * t.pathcap;
@@ -351,12 +410,15 @@ __global__ void __launch_bounds__(kBlock) k_select(TreeView t, const oaz_state* 
     }
     s.to_move = (uint8_t)color;
     if (l == 0) {
+        const bool need = leaf_needs_eval(nd.misc, s);
         store_state(&t.leaf_state[g], s);
         t.leaf[g] = node;
         t.depth[g] = depth;
+        if (t.need) t.need[g] = need;
         uint64_t* st = t.stats + (size_t)g * GS_COUNT;
         st[GS_SIMS] += 1;
         st[GS_DEPTH] += depth;
+        st[GS_EVALS] += need;
         if (stuck) st[GS_STUCK] += 1;
     }
 }
@@ -376,9 +438,10 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup(TreeView t, const oaz_
     const uint32_t* path = t.path + (size_t)g * t.pathcap;
     const oaz_state s = load_state(&t.leaf_state[g]);
     const uint32_t leaf = t.leaf[g], depth = t.depth[g];
+    const uint32_t row = t.slot ? t.slot[g] : g;  // the leaf's evaluation (read only if it was made)
     const NodeRegs nd = load_node(&T[leaf]);
     uint64_t* st = t.stats + (size_t)g * GS_COUNT;
-    const float* pol = policy + (size_t)g * 50;
+    const float* pol = policy + (size_t)row * 50;
 
     if (!(node_flags(nd.misc) & 3)) {
         const LaneMoves m = lane_movegen(s);
@@ -424,7 +487,7 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup(TreeView t, const oaz_
         r = reward(res, pc);
         if (l == 0) st[GS_TERMINAL] += 1;
     } else {
-        r = (double)value[g];
+        r = (double)value[row];
     }
     // back_propagate (mcts_arena.rs:312-323): node at depth k gets (-1)^(depth-k) * r
     const uint32_t plen = depth < t.pathcap ? depth : t.pathcap - 1;
@@ -650,13 +713,18 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
     }
     s.to_move = (uint8_t)color;
     if (on && sl == 0) {
+        const bool need = leaf_needs_eval(nd.misc, s);
         store_state(&t.leaf_state[g], s);
         t.leaf[g] = node;
         t.depth[g] = depth;
+        if (t.need) t.need[g] = need;
         uint64_t* st = t.stats + (size_t)g * GS_COUNT;
         st[GS_SIMS] += 1;
         st[GS_DEPTH] += depth;
+        st[GS_EVALS] += need;
         if (stuck) st[GS_STUCK] += 1;
+    } else if (!on && g < t.G && sl == 0 && t.need) {
+        t.need[g] = 0;  // an idle slot: nothing to evaluate
     }
 }
 
@@ -706,9 +774,10 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const 
     const uint32_t* path = t.path + (size_t)g * t.pathcap;
     const oaz_state s = load_state(&t.leaf_state[g]);
     const uint32_t leaf = t.leaf[g], depth = t.depth[g];
+    const uint32_t row = t.slot ? t.slot[g] : g;  // the leaf's evaluation (read only if it was made)
     const NodeRegs nd = load_node(&T[leaf]);
     uint64_t* st = t.stats + (size_t)g * GS_COUNT;
-    const float* pol = policy + (size_t)g * 50;
+    const float* pol = policy + (size_t)row * 50;
 
     if (!(node_flags(nd.misc) & 3)) {
         // the leaf's 50 policy values in one round trip (lane sl: entries sl, 16+sl, 32+sl, 48+sl),
@@ -779,7 +848,7 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const 
         r = reward(res, pc);
         if (sl == 0) st[GS_TERMINAL] += 1;
     } else {
-        r = (double)value[g];
+        r = (double)value[row];
     }
     const uint32_t plen = depth < t.pathcap ? depth : t.pathcap - 1;
     for (uint32_t k = (uint32_t)sl; k <= plen; k += kSegLanes) {
@@ -1001,6 +1070,11 @@ hipError_t launch_encode(const oaz_state* s, int n, float* planes, hipStream_t s
 hipError_t launch_hash_eval(const oaz_state* s, int B, float* policy, float* value, hipStream_t st) {
     if (B <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_hash_eval, dim3(thread_grid(B, 256)), dim3(256), 0, st, s, B, policy, value);
+    return hipGetLastError();
+}
+hipError_t launch_eval_compact(const TreeView& t, hipStream_t st) {
+    if (t.G == 0 || !t.need) return hipSuccess;
+    hipLaunchKernelGGL(k_eval_compact, dim3((unsigned)buckets_of(t.G)), dim3(kCompactThreads), 0, st, t);
     return hipGetLastError();
 }
 hipError_t launch_tree_reset(const TreeView& t, hipStream_t st) {

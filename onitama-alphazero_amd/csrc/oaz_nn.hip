@@ -83,6 +83,18 @@ template <> struct Act<true> {
 };
 }  // namespace nn
 
+// Rows of this workgroup: [b0, b0 + kSB) below `end`; row loads are clamped to `cap` rows. Plain
+// tiles cover [0, B); over compacted leaves (TileMap, oaz_kernels.h) workgroup i takes tile i / nb of
+// bucket i % nb, and a tile past its bucket's count exits after its first loads.
+struct TileSpan {
+    int b0, end, cap;
+};
+__device__ __forceinline__ TileSpan tile_span(const TileMap& tm, int B) {
+    if (!tm.bcnt) return TileSpan{(int)blockIdx.x * nn::kSB, B, B};
+    const int b = (int)blockIdx.x % tm.nb, t = (int)blockIdx.x / tm.nb, base = b << kBucketShift;
+    return TileSpan{base + t * nn::kSB, base + (int)tm.bcnt[b], tm.cap};
+}
+
 // fp32 split variant (OAZ_FP32_SPLIT): 64->64 conv B fragments are [9 taps][2 K-halves][3 pieces]
 // [4 N-tiles][64 lanes] bf16x8 (the exact 3-term bf16 split of each folded fp32 weight).
 namespace x6 {
@@ -576,7 +588,7 @@ template <bool BF16>
 __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __restrict__ states, int B,
                                                              const float* __restrict__ blob, int blocks,
                                                              float* __restrict__ policy,
-                                                             float* __restrict__ value) {
+                                                             float* __restrict__ value, TileMap tm) {
     using A = nn::Act<BF16>;
     constexpr int kImageFloats = BF16 ? nn::kSB * 25 * nn::kRSh / 2 : nn::kSB * 25 * nn::kRS;
     __shared__ __attribute__((aligned(16))) float lds[BF16 ? nn::kLdsFloatsH : nn::kLdsFloats];
@@ -587,7 +599,9 @@ __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __
     int sq[nn::kTPW];
 #pragma unroll
     for (int j = 0; j < nn::kTPW; ++j) sq[j] = (j < ntiles) ? c_sq_order[grp * nn::kTPW + j] : 0;
-    const int b0 = blockIdx.x * nn::kSB;
+    const TileSpan sp = tile_span(tm, B);
+    const int b0 = sp.b0;
+    B = sp.end;
     // per-position card/colour info for the first-layer table; the area is wave 0's head
     // scratch, free until the heads run
     int* pinfo = reinterpret_cast<int*>(lds + kImageFloats);
@@ -596,7 +610,7 @@ __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __
     // king, blue pawns, blue king); the cards / colour of each position go to LDS
     {
         const int pos = lane & 15, kq = lane >> 4;
-        const int b = b0 + pos < B ? b0 + pos : b0;
+        const int b = min(b0 + pos, sp.cap - 1);  // an empty tile of a bucket starts past cap
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
         const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
         if (tid < nn::kSB) {
@@ -605,6 +619,7 @@ __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __
             const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
             pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
         }
+        if (b0 >= B) return;  // an empty tile of a compacted bucket (uniform over the workgroup)
         __syncthreads();
         f32x4 acc[nn::kTPW];
 #pragma unroll
@@ -1349,14 +1364,15 @@ __device__ __forceinline__ void first_layer_x6(f32x4 (&acc)[C::NS], const L1Regs
 
 // The whole forward for the waves of square group GRP.
 template <class C, int GRP>
-__device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
-                                           int blocks, float* __restrict__ policy, float* __restrict__ value,
-                                           float* lds) {
+__device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states, const TileSpan sp,
+                                           const float* __restrict__ blob, int blocks, float* __restrict__ policy,
+                                           float* __restrict__ value, float* lds) {
+    const int B = sp.end;
     constexpr int NS = C::NS;
     char* img = reinterpret_cast<char*>(lds);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nt = wave & 3;
-    const int b0 = blockIdx.x * nn::kSB;
+    const int b0 = sp.b0;
     int* pinfo = reinterpret_cast<int*>(lds + x6::kImageB / 4);
     const int co = nt * 16 + (lane & 15);
     const int i = lane & 15, kq = lane >> 4;
@@ -1379,7 +1395,7 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
     {  // encoder + first layer
         L1Regs<GRP> l1;
         first_layer_x6_fetch<GRP>(l1, blob, lane, nt);
-        const int b = b0 + i < B ? b0 + i : b0;
+        const int b = min(b0 + i, sp.cap - 1);  // an empty tile of a bucket starts past cap
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
         const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
         if (tid < nn::kSB) {
@@ -1388,6 +1404,7 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
             const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
             pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
         }
+        if (b0 >= B) return;  // an empty tile of a compacted bucket (uniform over the workgroup)
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};  // skip: finite for the fma in epilogue_x6
@@ -1483,22 +1500,24 @@ __device__ __forceinline__ void nn_x6_body(const oaz_state* __restrict__ states,
 template <class C>
 __global__ void __launch_bounds__(64 * C::WAVES) k_nn_x6(const oaz_state* __restrict__ states, int B,
                                                         const float* __restrict__ blob, int blocks,
-                                                        float* __restrict__ policy, float* __restrict__ value) {
+                                                        float* __restrict__ policy, float* __restrict__ value,
+                                                        TileMap tm) {
     __shared__ __attribute__((aligned(16))) float lds[x6::kLdsFloats];
+    const TileSpan sp = tile_span(tm, B);
     if constexpr (C::WAVES == 4) {
-        nn_x6_body<C, 2>(states, B, blob, blocks, policy, value, lds);
+        nn_x6_body<C, 2>(states, sp, blob, blocks, policy, value, lds);
     } else if constexpr (C::UNEVEN) {
         constexpr int g0 = C::UNEVEN == 4 ? 9 : C::UNEVEN == 3 ? 7 : C::UNEVEN == 2 ? 5 : 3;
         if ((threadIdx.x >> 8) == 0) {
             __builtin_amdgcn_s_setprio(1);
-            nn_x6_body<C, g0>(states, B, blob, blocks, policy, value, lds);
+            nn_x6_body<C, g0>(states, sp, blob, blocks, policy, value, lds);
         } else {
-            nn_x6_body<C, g0 + 1>(states, B, blob, blocks, policy, value, lds);
+            nn_x6_body<C, g0 + 1>(states, sp, blob, blocks, policy, value, lds);
         }
     } else if ((threadIdx.x >> 8) == 0)  // waves 0-3: square group 0, waves 4-7: group 1
-        nn_x6_body<C, 0>(states, B, blob, blocks, policy, value, lds);
+        nn_x6_body<C, 0>(states, sp, blob, blocks, policy, value, lds);
     else
-        nn_x6_body<C, 1>(states, B, blob, blocks, policy, value, lds);
+        nn_x6_body<C, 1>(states, sp, blob, blocks, policy, value, lds);
 }
 
 // ---- fp32 split over fp16 (OAZ_FP32_SPLIT16): three f16 MFMA products per fp32 MAC -----------------
@@ -2107,14 +2126,15 @@ __device__ __forceinline__ void h3_heads(const float* p, char* img, const int (&
 }
 
 template <class C, int GRP>
-__device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
-                                           int blocks, float* __restrict__ policy, float* __restrict__ value,
-                                           float* lds) {
+__device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states, const TileSpan sp,
+                                           const float* __restrict__ blob, int blocks, float* __restrict__ policy,
+                                           float* __restrict__ value, float* lds) {
+    const int B = sp.end;
     constexpr int NS = C::NS;
     char* img = reinterpret_cast<char*>(lds);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nt = C::STG ? wave >> 1 : wave & 3;
-    const int b0 = blockIdx.x * nn::kSB;
+    const int b0 = sp.b0;
     int* pinfo = reinterpret_cast<int*>(lds + h3::kImageB / 4);
     const int co = nt * 16 + (lane & 15);
     const int i = lane & 15, kq = lane >> 4;
@@ -2154,7 +2174,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
                            nn::kValueF + nn::kPolicyF + h3::kHeadB;
         // the state loads first: vmcnt retires in issue order, so the pinfo / LUT work before the
         // barrier then waits for these and not for the first-layer operands issued after them
-        const int b = b0 + i < B ? b0 + i : b0;
+        const int b = min(b0 + i, sp.cap - 1);  // an empty tile of a bucket starts past cap
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
         const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
         oaz_state st{};
@@ -2172,6 +2192,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
             for (int t = tid; t < 512; t += 64 * C::WAVES) l1_lut_build(img, t);
         const float bias1 = blob[nn::kL1B + co];
         const f32x4 bias1t = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
+        if (b0 >= B) return false;  // an empty tile of a compacted bucket (uniform over the workgroup)
         __syncthreads();
         stamp(6);
 #pragma unroll
@@ -2322,10 +2343,11 @@ struct H3Fallback {
 // Out of line, so that the fallback's register allocation (k_nn_x6 spills a few VGPRs at 8 waves)
 // cannot touch the k_nn_h3 body's: the call is the rare path.
 template <class X, int GRP>
-__device__ __noinline__ void nn_h3_fallback(const oaz_state* __restrict__ states, int B, const float* __restrict__ xblob,
+__device__ __noinline__ void nn_h3_fallback(const oaz_state* __restrict__ states, const TileSpan sp,
+                                            const float* __restrict__ xblob,
                                             int blocks, float* __restrict__ policy, float* __restrict__ value,
                                             float* lds) {
-    nn_x6_body<X, GRP>(states, B, xblob, blocks, policy, value, lds);
+    nn_x6_body<X, GRP>(states, sp, xblob, blocks, policy, value, lds);
 }
 
 template <class C>
@@ -2333,38 +2355,39 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __rest
                                                         const float* __restrict__ blob, int blocks,
                                                         float* __restrict__ policy, float* __restrict__ value,
                                                         const float* __restrict__ xblob,
-                                                        unsigned long long* __restrict__ fallback) {
+                                                        unsigned long long* __restrict__ fallback, TileMap tm) {
     __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
+    const TileSpan sp = tile_span(tm, B);
     bool ovf;
     const bool g0 = (threadIdx.x >> 8) == 0;  // 8 waves: waves 0-3 square group A, waves 4-7 group B
     if constexpr (C::WAVES == 4) {
-        ovf = nn_h3_body<C, 2>(states, B, blob, blocks, policy, value, lds);
+        ovf = nn_h3_body<C, 2>(states, sp, blob, blocks, policy, value, lds);
     } else if constexpr (C::UNEVEN) {
         constexpr int ga = C::UNEVEN == 4 ? 9 : C::UNEVEN == 3 ? 7 : C::UNEVEN == 2 ? 5 : 3;
         if (g0) {
             __builtin_amdgcn_s_setprio(1);
-            ovf = nn_h3_body<C, ga>(states, B, blob, blocks, policy, value, lds);
+            ovf = nn_h3_body<C, ga>(states, sp, blob, blocks, policy, value, lds);
         } else {
-            ovf = nn_h3_body<C, ga + 1>(states, B, blob, blocks, policy, value, lds);
+            ovf = nn_h3_body<C, ga + 1>(states, sp, blob, blocks, policy, value, lds);
         }
     } else if constexpr (C::STG) {  // square group = wave parity (the SIMD partners w, w + 4 share it)
         if (((threadIdx.x >> 6) & 1) == 0)
-            ovf = nn_h3_body<C, 0>(states, B, blob, blocks, policy, value, lds);
+            ovf = nn_h3_body<C, 0>(states, sp, blob, blocks, policy, value, lds);
         else
-            ovf = nn_h3_body<C, 1>(states, B, blob, blocks, policy, value, lds);
+            ovf = nn_h3_body<C, 1>(states, sp, blob, blocks, policy, value, lds);
     } else if (g0)
-        ovf = nn_h3_body<C, 0>(states, B, blob, blocks, policy, value, lds);
+        ovf = nn_h3_body<C, 0>(states, sp, blob, blocks, policy, value, lds);
     else
-        ovf = nn_h3_body<C, 1>(states, B, blob, blocks, policy, value, lds);
+        ovf = nn_h3_body<C, 1>(states, sp, blob, blocks, policy, value, lds);
     if constexpr (H3Fallback<C>::kOn) {
         using X = typename H3Fallback<C>::X;
         if (__syncthreads_or(ovf)) {  // uniform over the workgroup; also the barrier before LDS reuse
             if constexpr (C::WAVES == 4)
-                nn_h3_fallback<X, 2>(states, B, xblob, blocks, policy, value, lds);
+                nn_h3_fallback<X, 2>(states, sp, xblob, blocks, policy, value, lds);
             else if (g0)
-                nn_h3_fallback<X, 3>(states, B, xblob, blocks, policy, value, lds);
+                nn_h3_fallback<X, 3>(states, sp, xblob, blocks, policy, value, lds);
             else
-                nn_h3_fallback<X, 4>(states, B, xblob, blocks, policy, value, lds);
+                nn_h3_fallback<X, 4>(states, sp, xblob, blocks, policy, value, lds);
             if (threadIdx.x == 0) atomicAdd(fallback, 1ull);
         }
     }
@@ -2466,14 +2489,15 @@ __device__ __forceinline__ Acc1<C>& q2_tile(f32x4 (&a)[2 * C::NS], int n) {  // 
 }
 
 template <class C, int GRP>
-__device__ __forceinline__ bool nn_q2_body(const oaz_state* __restrict__ states, int B, const float* __restrict__ blob,
-                                           int blocks, float* __restrict__ policy, float* __restrict__ value,
-                                           float* lds) {
+__device__ __forceinline__ bool nn_q2_body(const oaz_state* __restrict__ states, const TileSpan sp,
+                                           const float* __restrict__ blob, int blocks, float* __restrict__ policy,
+                                           float* __restrict__ value, float* lds) {
+    const int B = sp.end;
     constexpr int NS = C::NS;
     char* img = reinterpret_cast<char*>(lds);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nt0 = (wave >> 2) * 2;  // N-tiles nt0, nt0 + 1
-    const int b0 = blockIdx.x * nn::kSB;
+    const int b0 = sp.b0;
     int* pinfo = reinterpret_cast<int*>(lds + h3::kImageB / 4);
     const int i = lane & 15, kq = lane >> 4;
     const int lo[2] = {h3::chunk_off(i, kq), h3::chunk_off(i, 4 + kq)};
@@ -2497,7 +2521,7 @@ __device__ __forceinline__ bool nn_q2_body(const oaz_state* __restrict__ states,
     {  // encoder + first layer
         const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
                            nn::kValueF + nn::kPolicyF + h3::kHeadB;
-        const int b = b0 + i < B ? b0 + i : b0;
+        const int b = min(b0 + i, sp.cap - 1);  // an empty tile of a bucket starts past cap
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
         const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
         oaz_state st{};
@@ -2524,6 +2548,7 @@ __device__ __forceinline__ bool nn_q2_body(const oaz_state* __restrict__ states,
             bias1t[n] = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq[n]);
             inv1[n] = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f} : *reinterpret_cast<const f32x4*>(l1c + 26 * h3::kL1Frag + cq[n]);
         }
+        if (b0 >= B) return false;  // an empty tile of a compacted bucket (uniform over the workgroup)
         __syncthreads();
         stamp(6);
 #pragma unroll
@@ -2596,24 +2621,25 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_q2(const oaz_state* __rest
                                                         const float* __restrict__ blob, int blocks,
                                                         float* __restrict__ policy, float* __restrict__ value,
                                                         const float* __restrict__ xblob,
-                                                        unsigned long long* __restrict__ fallback) {
+                                                        unsigned long long* __restrict__ fallback, TileMap tm) {
     static_assert(C::Q2 && C::WAVES == 8 && C::TR && C::EP, "k_nn_q2: 8 waves, transposed tiles, conv pairs");
     __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
+    const TileSpan sp = tile_span(tm, B);
     bool ovf;
     switch ((threadIdx.x >> 6) & 3) {  // square group; waves w and w + 4 (one SIMD) share it
-        case 0: ovf = nn_q2_body<C, 11>(states, B, blob, blocks, policy, value, lds); break;
-        case 1: ovf = nn_q2_body<C, 12>(states, B, blob, blocks, policy, value, lds); break;
-        case 2: ovf = nn_q2_body<C, 13>(states, B, blob, blocks, policy, value, lds); break;
-        default: ovf = nn_q2_body<C, 14>(states, B, blob, blocks, policy, value, lds); break;
+        case 0: ovf = nn_q2_body<C, 11>(states, sp, blob, blocks, policy, value, lds); break;
+        case 1: ovf = nn_q2_body<C, 12>(states, sp, blob, blocks, policy, value, lds); break;
+        case 2: ovf = nn_q2_body<C, 13>(states, sp, blob, blocks, policy, value, lds); break;
+        default: ovf = nn_q2_body<C, 14>(states, sp, blob, blocks, policy, value, lds); break;
     }
     if constexpr (H3Fallback<C>::kOn) {
         using X = typename H3Fallback<C>::X;
         const bool g0 = (threadIdx.x >> 8) == 0;
         if (__syncthreads_or(ovf)) {  // uniform over the workgroup; also the barrier before LDS reuse
             if (g0)
-                nn_h3_fallback<X, 3>(states, B, xblob, blocks, policy, value, lds);
+                nn_h3_fallback<X, 3>(states, sp, xblob, blocks, policy, value, lds);
             else
-                nn_h3_fallback<X, 4>(states, B, xblob, blocks, policy, value, lds);
+                nn_h3_fallback<X, 4>(states, sp, xblob, blocks, policy, value, lds);
             if (threadIdx.x == 0) atomicAdd(fallback, 1ull);
         }
     }
@@ -2951,7 +2977,10 @@ __global__ void __launch_bounds__(256) k_nn_p8(const oaz_state* __restrict__ sta
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy, float* value,
                              hipStream_t st) {
     if (B <= 0) return hipSuccess;
-    const unsigned grid = (unsigned)((B + nn::kSB - 1) / nn::kSB);
+    // compacted leaves (B = games): as many tiles per bucket as its games could fill (the empty ones
+    // exit early); plain: ceil(B / 16)
+    const int per_bucket = ((B < (int)kBucket ? B : (int)kBucket) + nn::kSB - 1) / nn::kSB;
+    const unsigned grid = w.tm.bcnt ? (unsigned)(w.tm.nb * per_bucket) : (unsigned)((B + nn::kSB - 1) / nn::kSB);
     if (w.precision == OAZ_FP32_SPLIT16) {
         if (!w.fallback || !w.blob_x6) return hipErrorInvalidValue;
         // 8 waves, uneven 17 / 8 square split, batches of <= 4 squares, transposed C/D tiles, convs in
@@ -3002,6 +3031,7 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             case 40: k = k_nn_h3<X6Cfg<8, 4, 1, 3, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // ablation: no conv A reads
             case 41: k = k_nn_h3<X6Cfg<8, 4, 1, 4, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // ablation: no conv B loads
             case 20: {  // 8 positions per workgroup, 2 workgroups per CU (measured 1.40 vs 1.25 ms)
+                if (w.tm.bcnt) return hipErrorInvalidValue;  // plain tiles only (the engine does not compact)
                 const unsigned g8 = (unsigned)((B + p8::kP - 1) / p8::kP);
                 hipLaunchKernelGGL((k_nn_p8<4, 1>), dim3(g8), dim3(256), 0, st, s, B, w.blob, w.blocks, policy, value,
                                    w.fallback);
@@ -3011,7 +3041,7 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
         }
 #endif
         hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value, w.blob_x6,
-                           w.fallback);
+                           w.fallback, w.tm);
     } else if (w.precision == OAZ_FP32_SPLIT) {
         // 8 waves, uneven 15 / 10 square split, pipelined batches of <= 4 squares
         auto k = k_nn_x6<X6Cfg<8, 4, 1, 0, 1>>;
@@ -3029,12 +3059,14 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             default: break;
         }
 #endif
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value, w.tm);
     } else if (w.precision == OAZ_BF16) {
 #if OAZ_AB
         if (w.bf16_v1 == 1)
             hipLaunchKernelGGL(k_nn_sq16<true>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks,
-                               policy, value);
+                               policy, value, w.tm);
+        else if ((w.bf16_v1 == 2 || w.bf16_v1 == 3) && w.tm.bcnt)
+            return hipErrorInvalidValue;  // plain tiles only (the engine does not compact)
         else if (w.bf16_v1 == 2)
             hipLaunchKernelGGL(k_nn_bf16g<4>, dim3(grid), dim3(64 * 4), 0, st, s, B, w.blob, w.blocks, policy, value);
         else if (w.bf16_v1 == 3)
@@ -3049,10 +3081,10 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
         if (w.bf16_v1 == 6) k = k_nn_q2<X6Cfg<8, 6, 1, 0, 0, 1, 1, 0, 1, 0, 0, 1, 0, 1, 1>>;  // Q2, KH 6
 #endif
         hipLaunchKernelGGL(k, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value, nullptr,
-                           nullptr);
+                           nullptr, w.tm);
     } else {
         hipLaunchKernelGGL(k_nn_sq16<false>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
-                           value);
+                           value, w.tm);
     }
     return hipGetLastError();
 }

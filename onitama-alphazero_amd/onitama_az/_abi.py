@@ -22,7 +22,7 @@ FP32, BF16, FP32_SPLIT, FP32_SPLIT16 = 0, 1, 2, 3  # OAZ_FP32 / OAZ_BF16 / OAZ_F
 ERR_RANGE = -7  # OAZ_ERR_RANGE (ABI 1 only; ABI 2 recomputes fp16-range tiles, oaz_nn_fallbacks)
 ERR_CAPACITY = -4
 ERR_COMM = -8
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_MOVES = 40
 
 
@@ -96,6 +96,7 @@ class oaz_search_stats(C.Structure):
         ("depth_sum", C.c_uint64),
         ("stuck_leaves", C.c_uint64),
         ("max_nodes", C.c_uint64),
+        ("nn_evals", C.c_uint64),
     ]
 
 
@@ -126,6 +127,8 @@ class oaz_kernel_times(C.Structure):
         ("nn_samples", C.c_uint64),
         ("noise_ms", C.c_double),
         ("noise_n", C.c_uint64),
+        ("compact_ms", C.c_double),
+        ("compact_n", C.c_uint64),
     ]
 
 

@@ -676,12 +676,14 @@ static int playout(search_t* S) {
     }
     eval_result er;
     evaluate(S, &gs, &er);
-    if (!S->ar.a[node].expanded && !S->ar.a[node].terminal)
+    const int expands = !S->ar.a[node].expanded && !S->ar.a[node].terminal;
+    if (expands)
         if (expand(S, node, &er) < 0) return -1;
     const int parent = S->ar.a[node].parent >= 0 ? S->ar.a[node].parent : 0;
     const int reward_color = S->ar.a[parent].color;
     const int mr = orc_current_state(&gs);
     S->st->sims++;
+    S->st->nn_evals += (uint64_t)(expands || !is_win(mr)); /* the evaluation is used (priors or value) */
     S->st->depth_sum += depth;
     if (is_win(mr)) {
         S->st->terminal_leaves++;
@@ -930,6 +932,7 @@ static void* batch_worker(void* p) {
         a->st.expansions += st.expansions;
         a->st.children += st.children;
         a->st.terminal_leaves += st.terminal_leaves;
+        a->st.nn_evals += st.nn_evals;
         a->st.depth_sum += st.depth_sum;
         a->st.stuck_leaves += st.stuck_leaves;
         if (st.max_nodes > a->st.max_nodes) a->st.max_nodes = st.max_nodes;
@@ -966,6 +969,7 @@ int orc_search_batch(const orc_search_cfg* cfg, const oaz_state* roots, const ui
         sum.expansions += args[i].st.expansions;
         sum.children += args[i].st.children;
         sum.terminal_leaves += args[i].st.terminal_leaves;
+        sum.nn_evals += args[i].st.nn_evals;
         sum.depth_sum += args[i].st.depth_sum;
         sum.stuck_leaves += args[i].st.stuck_leaves;
         if (args[i].st.max_nodes > sum.max_nodes) sum.max_nodes = args[i].st.max_nodes;

@@ -223,13 +223,19 @@ def test_search_hash_trees_bitexact(orc, sims, c_puct):
     roots = random_positions(orc, 12, seed=505 + sims)
     with Engine(games=len(roots), sims=sims, c_puct=c_puct, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0) as e:
         r = e.search(roots)
+        evals = terminal = 0
         for g in range(len(roots)):
             cfg = orc.search_cfg(sims=sims, c_puct=c_puct, evaluator=orc.EVAL_HASH)
             mv, pi, nodes, st = orc.search(cfg, roots[g])
             _compare_trees(e, g, nodes)
             assert np.array_equal(r.pi[g].reshape(-1), pi.reshape(-1))
             assert _mv(r.moves[g]) == _mv(mv)
+            evals += st.nn_evals
+            terminal += st.terminal_leaves
     assert r.stats.sims == sims * len(roots)
+    # leaf compaction: the network sees exactly the leaves whose evaluation the playout uses
+    assert (r.stats.nn_evals, r.stats.terminal_leaves) == (evals, terminal)
+    assert r.stats.sims - r.stats.terminal_leaves <= r.stats.nn_evals <= r.stats.sims
 
 
 @pytest.mark.parametrize("precision", [_abi.FP32, _abi.FP32_SPLIT16])

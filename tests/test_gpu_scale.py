@@ -123,8 +123,10 @@ def test_c3_search_every_game_vs_oracle(orc):
         mv, pi, st = orc.search_batch(cfg, roots)
         assert np.array_equal(r.pi.reshape(G, 50), pi.reshape(G, 50))
         assert r.moves.tobytes() == mv.tobytes()
-        assert (st.sims, st.expansions, st.children, st.depth_sum, st.max_nodes) == (
-            r.stats.sims, r.stats.expansions, r.stats.children, r.stats.depth_sum, r.stats.max_nodes)
+        assert (st.sims, st.expansions, st.children, st.depth_sum, st.max_nodes, st.nn_evals) == (
+            r.stats.sims, r.stats.expansions, r.stats.children, r.stats.depth_sum, r.stats.max_nodes,
+            r.stats.nn_evals)
+        assert 0 < r.stats.nn_evals < r.stats.sims  # won leaves are left out of the NN batch
         sample = np.unique(np.concatenate([[0, G - 1], np.random.default_rng(3).integers(0, G, 62)]))
         for g in sample:
             c = orc.search_cfg(sims=sims, c_puct=5.0, evaluator=orc.EVAL_HASH, train_noise=1, seed=SEED,

@@ -30,7 +30,7 @@ def test_header_functions_exported(lib):
 
 
 def test_abi_version_and_structs(lib):
-    assert lib.oaz_abi_version() == _abi.ABI_VERSION == 2
+    assert lib.oaz_abi_version() == _abi.ABI_VERSION == 3
     assert C.sizeof(_abi.oaz_config) == 112 or C.sizeof(_abi.oaz_config) > 0
 
 

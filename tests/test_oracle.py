@@ -134,6 +134,9 @@ def test_oracle_search_invariants(orc):
         cfg = orc.search_cfg(sims=100, c_puct=5.0, evaluator=orc.EVAL_HASH)
         mv, pi, nodes, st = orc.search(cfg, s)
         assert st.sims == 100 and int(nodes[0]["N"]) == 100
+        # a playout's evaluation is unused only when it ends on a won leaf (a won but unflagged leaf,
+        # possible below a random root that is already won, is still expanded with its priors)
+        assert st.sims - st.terminal_leaves <= st.nn_evals <= st.sims
         for i, nd in enumerate(nodes):  # visits of children = visits of parent minus its own eval
             if nd["flags"] & 1 and nd["nch"]:
                 ch = nodes[int(nd["first"]): int(nd["first"]) + int(nd["nch"])]
