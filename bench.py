@@ -107,10 +107,10 @@ def pmc_traffic(args, cfg):
         return None
     plies = args.warmup
     first, last = plies * cfg["sims"] + 1, (plies + 1) * cfg["sims"]  # 1-based launch index of each kernel
-    kb, tree_kb, counts = {}, {"select": {}, "expand_backup": {}}, {}
+    kb, tree_kb, counts = {}, {"backup_select": {}}, {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         with tempfile.TemporaryDirectory() as d:
-            cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "k_nn_|k_select|k_expand_backup",
+            cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "k_nn_|k_backup_select",
                    "--kernel-iteration-range", f"[{first}-{last}]", "--output-format", "csv", "-d", d, "-o", "pmc",
                    "--", sys.executable, str(Path(__file__).resolve()), "--pmc-child", "--pmc-plies", str(plies),
                    "--stagger", str(args.stagger), "--warmup", str(args.warmup), "--config", args.config, "--games", str(cfg["games"]),
@@ -119,13 +119,13 @@ def pmc_traffic(args, cfg):
                 subprocess.run(cmd, timeout=600, capture_output=True, check=True)
             except (subprocess.SubprocessError, OSError):
                 return None
-            rows = {"nn": [], "select": [], "expand_backup": []}
+            rows = {"nn": [], "backup_select": []}
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 for r in csv.DictReader(open(f)):
                     if r["Counter_Name"] != ctr:
                         continue
-                    k = ("nn" if "k_nn_" in r["Kernel_Name"] else "select" if "k_select" in r["Kernel_Name"]
-                         else "expand_backup" if "k_expand_backup" in r["Kernel_Name"] else None)
+                    k = ("nn" if "k_nn_" in r["Kernel_Name"] else "backup_select" if "k_backup_select" in r["Kernel_Name"]
+                         else None)
                     if k:
                         rows[k].append((int(r.get("Dispatch_Id", 0) or 0), float(r["Counter_Value"])))
             if not rows["nn"]:
@@ -135,7 +135,7 @@ def pmc_traffic(args, cfg):
                 rows[k] = [x for _, x in v[-cfg["sims"]:]]
                 counts[k] = len(rows[k])
             kb[ctr] = sum(rows["nn"]) / len(rows["nn"])
-            for k in ("select", "expand_backup"):
+            for k in ("backup_select",):
                 if rows[k]:
                     tree_kb[k][ctr] = sum(rows[k]) / len(rows[k])
     fetch, write = 2.0 * kb["FETCH_SIZE"] * 1024.0, kb["WRITE_SIZE"] * 1024.0
@@ -183,16 +183,18 @@ def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg, pmc=No
     and node (64 B) and the value (4 B), on expansion the policy row (200 B) and writes K fresh
     children (32 B each) and the header (16 B), and per path node reads the path entry (4 B) and
     updates N and W (12 B read + 12 B written)."""
-    if not kt.select_n or not kt.expand_n:
+    if not kt.backup_select_n:
         return None
     D, K = depth, branching
-    per_launch = sims / max(1, sim_steps)  # games per select / expand launch
+    per_launch = sims / max(1, sim_steps)  # games per tree-kernel launch
     noise = 8.0 * K if cfg.get("noise", True) else 0.0
-    sel = 24 + 32 + D * (32 * K + 8 + 4) + noise + 32 + 16
-    exp = 64 + 4 + (expansions / max(1, sims)) * (200 + 32 * K + 16) + (D + 1) * (4 + 24)
+    sel = 24 + 32 + D * (32 * K + 8 + 4) + noise + 32 + 16 + 1  # + the need flag
+    exp = 64 + 4 + 4 + (expansions / max(1, sims)) * (200 + 32 * K + 16) + (D + 1) * (4 + 24)  # + the row
     out = {"bound": "latency (one dependent HBM round trip per tree level; 4 games per wave)",
-           "peak_GBps": HBM_PEAK_GBPS, "sims_per_launch": per_launch}
-    for name, ms, n, b in (("select", kt.select_ms, kt.select_n, sel), ("expand_backup", kt.expand_ms, kt.expand_n, exp)):
+           "peak_GBps": HBM_PEAK_GBPS, "sims_per_launch": per_launch,
+           "kernel": "k_backup_select_seg (expand/backup of simulation s + select of s + 1, one launch per "
+                     "simulation step; the first select and the last expand/backup of a move run alone)"}
+    for name, ms, n, b in (("backup_select", kt.backup_select_ms, kt.backup_select_n, sel + exp),):
         t = ms / n * 1e-3
         gbps = per_launch * b / t / 1e9
         out[name] = {"avg_launch_us": t * 1e6, "algorithmic_bytes_per_sim": b, "achieved_GBps": gbps,
@@ -662,9 +664,10 @@ def main():
                              "backed up); select marks those leaves and k_eval_compact packs the others per 4096-game "
                              "bucket, so the trees are unchanged and the network runs on nn_positions_per_sim of them",
             "kernel_ms_per_step": {
-                "select": kt.select_ms / max(1, kt.select_n) * sims_steps,
+                "backup_select_fused": kt.backup_select_ms / max(1, kt.backup_select_n) * (sims_steps - 1),
+                "select_first": kt.select_ms / max(1, kt.select_n) if kt.select_n else None,
+                "expand_backup_last": kt.expand_ms / max(1, kt.expand_n) if kt.expand_n else None,
                 "nn": kt.nn_ms / max(1, kt.nn_n) * sims_steps,
-                "expand_backup": kt.expand_ms / max(1, kt.expand_n) * sims_steps,
                 "leaf_compact": kt.compact_ms / max(1, kt.compact_n) * sims_steps,
                 "move": kt.finalize_ms / args.steps, "root_noise_stream2": kt.noise_ms / args.steps},
             "kernel_timing": "HIP events around the kernels of every %s-th simulation step (per-kernel means x "

@@ -194,6 +194,9 @@ typedef struct oaz_kernel_times {
     uint64_t noise_n;
     double compact_ms;    /* leaf compaction (the positions the NN evaluates, per 4096-game bucket) */
     uint64_t compact_n;
+    double backup_select_ms; /* expand/backup of simulation s fused with the select of s + 1 (every
+                              * simulation step but the first select and the last expand/backup) */
+    uint64_t backup_select_n;
 } oaz_kernel_times;
 
 typedef struct oaz_engine oaz_engine;

@@ -604,7 +604,8 @@ extern "C" int oaz_encode(const oaz_state* s, int n, float* planes) {
 
 // ---- engine ------------------------------------------------------------------------------------
 struct TimedLaunch {
-    int kind;  // 0 select, 1 nn, 2 expand, 3 finalize, 4 root noise (second stream), 5 leaf compaction
+    int kind;  // 0 select, 1 nn, 2 expand, 3 finalize, 4 root noise (second stream), 5 leaf compaction,
+               // 6 expand/backup + next select (fused)
     hipEvent_t a, b;
     uint32_t samples;
 };
@@ -738,10 +739,10 @@ static hipEvent_t ev_get(oaz_engine* e) {
 static constexpr uint32_t kNoiseChunk = 8;  // simulations of root noise produced per launch
 
 static void accumulate(oaz_engine* e, const TimedLaunch& p, float ms) {
-    double* acc[6] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms,
-                      &e->times.noise_ms, &e->times.compact_ms};
-    uint64_t* cnt[6] = {&e->times.select_n, &e->times.nn_n, &e->times.expand_n, &e->times.finalize_n,
-                        &e->times.noise_n, &e->times.compact_n};
+    double* acc[7] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms,
+                      &e->times.noise_ms, &e->times.compact_ms, &e->times.backup_select_ms};
+    uint64_t* cnt[7] = {&e->times.select_n, &e->times.nn_n, &e->times.expand_n, &e->times.finalize_n,
+                        &e->times.noise_n, &e->times.compact_n, &e->times.backup_select_n};
     *acc[p.kind] += ms;
     *cnt[p.kind] += 1;
     if (p.kind == 1) e->times.nn_samples += p.samples;
@@ -1044,7 +1045,8 @@ static bool compact_leaves(const oaz_engine* e) {
 }
 
 // All cfg.sims simulations of one move for every game, in lock step: select -> leaf compaction ->
-// evaluate -> expand/backup. Select marks the games whose playout uses its leaf evaluation (all
+// evaluate -> expand/backup, where simulation s's expand/backup and simulation s+1's select run as
+// one kernel (k_backup_select_seg; a game's next walk needs only its own backup). Select marks the games whose playout uses its leaf evaluation (all
 // but those ending on a won, terminal-flagged node, whose evaluation the reference discards:
 // mcts_arena.rs:156-176) and the compaction kernel packs their leaves per 4096-game bucket, so the
 // network evaluates only those. With root noise, k_root_noise fills chunk c+1 of the
@@ -1080,6 +1082,11 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
     }
     const TileMap tm{t.bcnt, buckets_of(t.G), (int32_t)t.G + 16};
     hipStream_t st = e->stream;
+#if OAZ_AB  // A/B build only: OAZ_TREE_FUSE=0 runs expand/backup and the next select as two launches
+    static const bool fuse = !(getenv("OAZ_TREE_FUSE") && getenv("OAZ_TREE_FUSE")[0] == '0');
+#else
+    constexpr bool fuse = true;
+#endif
     for (uint32_t c = 0; c < nchunks; ++c) {
         if (noise) {
             if (c + 1 < nchunks)
@@ -1091,22 +1098,32 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
             // sampled steps sit mid-chunk: a chunk's first select also waits for its noise
             e->timing_skip = e->timing_every > 1 && s % (uint32_t)e->timing_every != (uint32_t)e->timing_every / 2;
             const float* nz = noise ? e->noise + (c & 1) * slot_elems + (size_t)(s - s0) * t.G * kNoiseStride : nullptr;
-            if (int rc = timed(e, 0, t.G, [&] { return launch_select(tc, roots, active, nz, prm, st); }, st)) return rc;
+            if (s == 0) {
+                if (int rc = timed(e, 0, t.G, [&] { return launch_select(tc, roots, active, nz, prm, st); }, st))
+                    return rc;
+            } else if (!fuse) {
+                if (int rc = timed(e, 2, t.G, [&] {
+                        return launch_expand_backup(tc, roots, active, e->policy, e->value, st);
+                    }, st))
+                    return rc;
+                if (int rc = timed(e, 0, t.G, [&] { return launch_select(tc, roots, active, nz, prm, st); }, st))
+                    return rc;
+            } else if (int rc = timed(e, 6, t.G, [&] {
+                           return launch_backup_select(tc, roots, active, e->policy, e->value, nz, prm, st);
+                       }, st)) {
+                return rc;
+            }
             if (tc.need) {
                 if (int rc = timed(e, 5, t.G, [&] { return launch_eval_compact(tc, st); }, st)) return rc;
                 if (int rc = evaluate(e, tc.cstate, t.G, e->policy, e->value, st, &tm)) return rc;
             } else if (int rc = evaluate(e, tc.leaf_state, t.G, e->policy, e->value, st)) {
                 return rc;
             }
-            if (int rc = timed(e, 2, t.G, [&] {
-                    return launch_expand_backup(tc, roots, active, e->policy, e->value, st);
-                }, st))
-                return rc;
         }
         if (noise) HIP_TRY(hipEventRecord(e->ev_consumed[c & 1], st));
     }
     e->timing_skip = false;
-    return 0;
+    return timed(e, 2, t.G, [&] { return launch_expand_backup(tc, roots, active, e->policy, e->value, st); }, st);
 }
 
 static int reduce_stats(oaz_engine* e, uint32_t G, uint64_t out[GS_COUNT]) {

@@ -127,6 +127,9 @@ hipError_t launch_root_noise(const oaz_state* roots, const uint8_t* active, cons
                              float* out /* [nsims][G][kNoiseStride] */, hipStream_t st);
 hipError_t launch_expand_backup(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                                 const float* policy, const float* value, hipStream_t st);
+// expand/backup of simulation s, then select of simulation s+1 (noise: its root noise), fused
+hipError_t launch_backup_select(const TreeView& t, const oaz_state* roots, const uint8_t* active, const float* policy,
+                                const float* value, const float* noise, SearchParams p, hipStream_t st);
 hipError_t launch_search_finalize(const TreeView& t, const oaz_state* roots, oaz_move* out_move,
                                   float* out_pi, hipStream_t st);
 hipError_t launch_selfplay_move(const TreeView& t, const SlotView& s, hipStream_t st);

@@ -762,10 +762,10 @@ __device__ __forceinline__ void policy_sums(const float (&polr)[4], uint32_t row
 
 // k_expand_backup with 16 lanes per game: lane sl generates the moves of (card, from) combos
 // 4 sl .. 4 sl + 3 (combo = card * 25 + from, the reference order), one segment scan places them.
-__global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const oaz_state* __restrict__ roots,
-                                                              const uint8_t* __restrict__ active,
-                                                              const float* __restrict__ policy,
-                                                              const float* __restrict__ value) {
+__device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const oaz_state* __restrict__ roots,
+                                                      const uint8_t* __restrict__ active,
+                                                      const float* __restrict__ policy,
+                                                      const float* __restrict__ value) {
     const uint32_t g = seg_game();
     const int sl = seg_lane();
     if (g >= t.G) return;                  // whole segments (G is not a multiple of 4 only at the end)
@@ -857,6 +857,27 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const 
         T[n].N += 1;
         T[n].W += rk;
     }
+}
+
+__global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const oaz_state* __restrict__ roots,
+                                                              const uint8_t* __restrict__ active,
+                                                              const float* __restrict__ policy,
+                                                              const float* __restrict__ value) {
+    expand_backup_seg_body(t, roots, active, policy, value);
+}
+
+// Simulation s's expand/backup and simulation s+1's select of the same four games in one launch:
+// a game's next walk needs only its own backup (the wave's own writes, ordered by a workgroup-scope
+// fence), so every segment goes straight on to its next select instead of waiting for the whole
+// grid; one launch and one grid ramp per simulation step fewer.
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6)))
+k_backup_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
+                    const float* __restrict__ policy, const float* __restrict__ value, const float* __restrict__ noise,
+                    SearchParams prm) {
+    expand_backup_seg_body(t, roots, active, policy, value);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    select_seg_body(t, roots, active, noise, prm);
 }
 
 // calculate_priors (mcts_arena.rs:104-124) + best child (87-94) for every root.
@@ -1118,6 +1139,16 @@ hipError_t launch_expand_backup(const TreeView& t, const oaz_state* roots, const
     else
         hipLaunchKernelGGL(k_expand_backup, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, roots, active, policy,
                            value);
+    return hipGetLastError();
+}
+hipError_t launch_backup_select(const TreeView& t, const oaz_state* roots, const uint8_t* active, const float* policy,
+                                const float* value, const float* noise, SearchParams p, hipStream_t st) {
+    if (!tree_seg()) {  // the one-game-per-wave kernels, one after the other
+        if (hipError_t err = launch_expand_backup(t, roots, active, policy, value, st)) return err;
+        return launch_select(t, roots, active, noise, p, st);
+    }
+    hipLaunchKernelGGL(k_backup_select_seg, dim3(wave_grid((t.G + 3) / 4)), dim3(kBlock), 0, st, t, roots, active,
+                       policy, value, noise, p);
     return hipGetLastError();
 }
 hipError_t launch_search_finalize(const TreeView& t, const oaz_state* roots, oaz_move* out_move,

@@ -2357,6 +2357,8 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __rest
                                                         const float* __restrict__ xblob,
                                                         unsigned long long* __restrict__ fallback, TileMap tm) {
     __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
+    // DBG 5 (timing only): the workgroup's start / end on the constant 100 MHz clock and its CU
+    const uint64_t rt0 = C::DBG == 5 ? __builtin_amdgcn_s_memrealtime() : 0;
     const TileSpan sp = tile_span(tm, B);
     bool ovf;
     const bool g0 = (threadIdx.x >> 8) == 0;  // 8 waves: waves 0-3 square group A, waves 4-7 group B
@@ -2389,6 +2391,21 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __rest
             else
                 nn_h3_fallback<X, 4>(states, sp, xblob, blocks, policy, value, lds);
             if (threadIdx.x == 0) atomicAdd(fallback, 1ull);
+        }
+    }
+    if constexpr (C::DBG == 5) {
+        __syncthreads();  // every wave is done
+        if (threadIdx.x == 0 && sp.b0 < sp.end) {
+            const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+            uint32_t* o = reinterpret_cast<uint32_t*>(policy + (size_t)sp.b0 * 50);
+            o[0] = (uint32_t)rt0;
+            o[1] = (uint32_t)(rt0 >> 32);
+            o[2] = (uint32_t)rt1;
+            o[3] = (uint32_t)(rt1 >> 32);
+            o[4] = hw;
+            o[5] = xcc;
         }
     }
 }
@@ -3021,6 +3038,7 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             case 34: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 2, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, 16 / 9
             case 35: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 4, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, 18 / 7
             case 36: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // timing only: EP phase stamps
+            case 60: k = k_nn_h3<X6Cfg<8, 4, 1, 5, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // timing only: WG timeline
             case 42: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 0, 0, 1, 0, 2>>; break;  // EP + BD 2
             case 43: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1, 1, 0, 0, 0, 0, 1, 0, 2>>; break;  // EP + BD 2, 15 / 10
             case 44: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 0, 1, 1, 0, 0, 0, 0, 1, 0, 2>>; break;  // EP + BD 2, 13 / 12, PIPE 2

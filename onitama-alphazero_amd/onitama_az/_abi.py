@@ -129,6 +129,8 @@ class oaz_kernel_times(C.Structure):
         ("noise_n", C.c_uint64),
         ("compact_ms", C.c_double),
         ("compact_n", C.c_uint64),
+        ("backup_select_ms", C.c_double),
+        ("backup_select_n", C.c_uint64),
     ]
 
 
