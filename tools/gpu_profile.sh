@@ -10,3 +10,6 @@ step bench timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench_
 tail -1 gpurun_out/bench_$TAG.json | cut -c1-600
 step trace timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG/trace -o run -- "$PY" bench.py --steps 2 --no-cpu-baseline --no-allgather --no-pmc --no-exact ${PROF_ARGS:-} > gpurun_out/prof_$TAG/trace.log 2>&1
 find gpurun_out/prof_$TAG -name "*kernel_stats.csv" | head
+# the timed plies only (the --stats summary also averages the staggered warm-up plies)
+T=$(find gpurun_out/prof_$TAG -name "*kernel_trace.csv" | head -1)
+[ -n "$T" ] && python tools/trace_steady.py "$T" $((2 * ${SIMS:-400})) > gpurun_out/prof_$TAG/steady_kernel_stats.csv
