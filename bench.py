@@ -496,8 +496,11 @@ def exact_fp32_leg(args, cfg, device):
         st1 = e.selfplay_stats()
     sims = st1.search.sims - st0.search.sims
     nn_ms = kt.nn_ms / max(1, kt.nn_n)
-    # positions per NN launch: the evaluations the playouts use (leaf compaction), per simulation step
-    fl = FLOP_PER_SIM[cfg["blocks"]] * (st1.search.nn_evals - st0.search.nn_evals) / max(1, 2 * cfg["sims"])
+    # positions per NN launch: all game slots (kt.nn_samples), or with leaf compaction (whose counts
+    # stay on the device) the evaluations the playouts use per simulation step
+    pos = (kt.nn_samples / max(1, kt.nn_n) if kt.nn_samples
+           else (st1.search.nn_evals - st0.search.nn_evals) / max(1, 2 * cfg["sims"]))
+    fl = FLOP_PER_SIM[cfg["blocks"]] * pos
     tf = fl / (nn_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
     return {"kernel": NN_KERNEL["fp32"], "value": sims / dt, "unit": "sims/s", "ms_per_step": 1e3 * dt / 2,
             "steps": 2, "warmup": 2, "nn_avg_launch_ms": nn_ms, "nn_achieved_TFLOPs": tf,
@@ -626,8 +629,9 @@ def main():
     if rank == 0:
         sims_steps = cfg["sims"]  # simulation steps (select -> NN -> expand launches) per bench step
         nn_avg_ms = kt.nn_ms / max(1, kt.nn_n)
-        # every simulation step launches the NN once on the compacted leaves of all games
-        positions = evals / max(1, args.steps * sims_steps)
+        # every simulation step launches the NN once: on every game slot (nn_samples counted by the
+        # engine), or with leaf compaction on the leaves the playouts use (their count: nn_evals)
+        positions = (kt.nn_samples / max(1, kt.nn_n) if kt.nn_samples else evals / max(1, args.steps * sims_steps))
         flops_launch = FLOP_PER_SIM[cfg["blocks"]] * positions
         achieved = flops_launch / (nn_avg_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
         nz = nonzero_flop_per_sim(cfg["blocks"]) * positions
@@ -658,11 +662,13 @@ def main():
             "sims_per_s_per_gpu": sims_all / T / world, "stagger": stagger,
             "games_per_s": games_all / T, "plies_per_s": plies_all / T,
             "true_expansions_per_s": exp_all / T, "mean_select_depth": depth, "mean_branching": branching,
-            "nn_positions_per_sim": evals / max(1, sims),
+            "nn_positions_per_sim": positions * args.steps * sims_steps / max(1, sims),
+            "leaf_compaction": not kt.nn_samples,
             "nn_evaluation": "every simulation's leaf is evaluated except a won, terminal-flagged leaf, whose evaluation "
                              "the reference computes and discards (mcts_arena.rs:156-176: no expansion, the reward is "
-                             "backed up); select marks those leaves and k_eval_compact packs the others per 4096-game "
-                             "bucket, so the trees are unchanged and the network runs on nn_positions_per_sim of them",
+                             "backed up); select marks those leaves and, when that saves NN workgroup rounds (games >= "
+                             "12 x 16 x CUs: leaf_compaction), k_eval_compact packs the others per 4096-game bucket; "
+                             "the trees are unchanged and the network runs on nn_positions_per_sim of the leaves",
             "kernel_ms_per_step": {
                 "backup_select_fused": kt.backup_select_ms / max(1, kt.backup_select_n) * (sims_steps - 1),
                 "select_first": kt.select_ms / max(1, kt.select_n) if kt.select_n else None,

@@ -155,7 +155,10 @@ typedef struct oaz_config {
     int32_t sample_capacity; /* max samples buffered on the device (0: auto) */
     int32_t stagger;         /* self-play: slot g starts playing after g % stagger plies (steady-state
                                 game ages for throughput measurement); 0 = all slots start at once */
-    int32_t reserved[6];
+    int32_t compact;         /* leaf compaction (only the leaves whose evaluation the playout uses go to
+                                the evaluator, Q2): 0 = when it saves NN rounds (games >= 12 * 16 * CUs),
+                                1 = always, -1 = never; results are identical either way */
+    int32_t reserved[5];
 } oaz_config;
 
 typedef struct oaz_search_stats {

@@ -615,6 +615,7 @@ struct oaz_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;       // root-noise producer, overlaps the NN kernel
+    int cus = 256;                       // compute units of the device (leaf-compaction threshold)
     hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_consumed[2] = {nullptr, nullptr};
     float* noise = nullptr;              // [2][kNoiseChunk][G][kNoiseStride]
     uint32_t G = 0, cap = 0, pathcap = 0, hcap = 0, out_cap = 0;
@@ -789,7 +790,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         return nullptr;
     }
     if (cfg->blocks < 0 || cfg->blocks > 64 || cfg->sims < 1 || cfg->sims > 65535 || cfg->games < 1 ||
-        cfg->max_plies < 0 || cfg->max_plies > 100000) {
+        cfg->max_plies < 0 || cfg->max_plies > 100000 || cfg->compact < -1 || cfg->compact > 1) {
         oaz_set_err(OAZ_ERR_ARG, "create: config out of range");
         return nullptr;
     }
@@ -837,6 +838,8 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
             oaz_set_err(OAZ_ERR_HIP, "event create failed");
             return fail();
         }
+    if (hipDeviceGetAttribute(&e->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || e->cus < 1)
+        e->cus = 256;
     const size_t G = e->G;
     if (dalloc(&e->nodes, G * e->cap) || dalloc(&e->n_nodes, G) || dalloc(&e->path, G * e->pathcap) ||
         dalloc(&e->depth, G) || dalloc(&e->leaf, G) || dalloc(&e->leaf_state, G) ||
@@ -1030,16 +1033,18 @@ extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* p
     return 0;
 }
 
-// Leaf compaction is on unless an A/B-only NN variant without tile maps is selected.
-static bool compact_leaves(const oaz_engine* e) {
+// Leaf compaction pays when it can remove whole rounds of NN workgroups (one 16-position tile per
+// CU at a time): at C3 the ~8.7 % won leaves are 1.4 of 16 rounds. Below 12 rounds (G < 12 * 16 *
+// CUs, e.g. C2's 4096 games = one round) it would only add its own launch, so the leaves are then
+// evaluated in place. Also off for the A/B-only NN variants without tile maps.
+static bool compact_leaves(const oaz_engine* e, uint32_t G) {
+    if (e->cfg.compact < 0 || (e->cfg.compact == 0 && G < 12u * 16u * (uint32_t)e->cus)) return false;
 #if OAZ_AB
     if (e->cfg.evaluator == OAZ_EVAL_NN) {
         const char* xv = getenv("OAZ_NN_X6_V");
         const char* v1 = getenv("OAZ_NN_BF16_V1");
         if ((xv && atoi(xv) == 20) || (v1 && (atoi(v1) == 2 || atoi(v1) == 3))) return false;  // k_nn_p8, k_nn_bf16g
     }
-#else
-    (void)e;
 #endif
     return true;
 }
@@ -1076,7 +1081,7 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
         if (int rc = produce(0)) return rc;
     }
     TreeView tc = t;  // the compaction arrays, or none (rows = game ids)
-    if (!compact_leaves(e)) {
+    if (!compact_leaves(e, t.G)) {
         tc.need = nullptr;
         tc.slot = nullptr;
     }

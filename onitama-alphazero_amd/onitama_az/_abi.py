@@ -83,7 +83,8 @@ class oaz_config(C.Structure):
         ("world", C.c_int32),
         ("sample_capacity", C.c_int32),
         ("stagger", C.c_int32),
-        ("reserved", C.c_int32 * 6),
+        ("compact", C.c_int32),
+        ("reserved", C.c_int32 * 5),
     ]
 
 

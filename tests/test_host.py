@@ -151,3 +151,10 @@ def test_root_noise_host_matches_oracle_and_distribution():
         se = np.sqrt(var / len(xs))
         assert abs(xs.mean() - 1.0 / K) < 5 * se, (K, xs.mean())
         assert abs(xs.var() / var - 1.0) < 0.2, (K, xs.var(), var)
+
+
+def test_config_compact_out_of_range_is_an_error():
+    """oaz_config.compact is -1, 0 or 1; anything else fails oaz_create before any device work."""
+    from onitama_az.engine import Engine
+    with pytest.raises(_abi.OazError, match="config out of range"):
+        Engine(games=4, sims=4, compact=2)
