@@ -158,7 +158,10 @@ typedef struct oaz_config {
     int32_t compact;         /* leaf compaction (only the leaves whose evaluation the playout uses go to
                                 the evaluator, Q2): 0 = when it saves NN rounds (games >= 12 * 16 * CUs),
                                 1 = always, -1 = never; results are identical either way */
-    int32_t reserved[5];
+    int32_t parts;           /* the simulation loop runs the games in this many parts (1, 2 or 4), each
+                                on its own stream so one part's tree kernels fill the others' NN gaps;
+                                0 = auto (2 from 2048 games); results are identical either way */
+    int32_t reserved[4];
 } oaz_config;
 
 typedef struct oaz_search_stats {

@@ -603,6 +603,8 @@ extern "C" int oaz_encode(const oaz_state* s, int n, float* planes) {
 }
 
 // ---- engine ------------------------------------------------------------------------------------
+constexpr int kMaxParts = 4;  // run_sims: game parts, each on its own stream (oaz_config.parts)
+
 struct TimedLaunch {
     int kind;  // 0 select, 1 nn, 2 expand, 3 finalize, 4 root noise (second stream), 5 leaf compaction,
                // 6 expand/backup + next select (fused)
@@ -616,6 +618,8 @@ struct oaz_engine {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;       // root-noise producer, overlaps the NN kernel
     int cus = 256;                       // compute units of the device (leaf-compaction threshold)
+    hipStream_t stream3[kMaxParts - 1] = {nullptr, nullptr, nullptr};  // A/B build (OAZ_SPLIT_HALVES): parts 1..
+    hipEvent_t ev_join = nullptr, ev_part[kMaxParts] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_consumed[2] = {nullptr, nullptr};
     float* noise = nullptr;              // [2][kNoiseChunk][G][kNoiseStride]
     uint32_t G = 0, cap = 0, pathcap = 0, hcap = 0, out_cap = 0;
@@ -790,7 +794,8 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         return nullptr;
     }
     if (cfg->blocks < 0 || cfg->blocks > 64 || cfg->sims < 1 || cfg->sims > 65535 || cfg->games < 1 ||
-        cfg->max_plies < 0 || cfg->max_plies > 100000 || cfg->compact < -1 || cfg->compact > 1) {
+        cfg->max_plies < 0 || cfg->max_plies > 100000 || cfg->compact < -1 || cfg->compact > 1 ||
+        (cfg->parts != 0 && cfg->parts != 1 && cfg->parts != 2 && cfg->parts != 4)) {
         oaz_set_err(OAZ_ERR_ARG, "create: config out of range");
         return nullptr;
     }
@@ -828,10 +833,17 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         return fail();
     }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess) {
         oaz_set_err(OAZ_ERR_HIP, "stream create failed");
         return fail();
     }
+    for (int i = 0; i < kMaxParts - 1; ++i)
+        if (hipStreamCreateWithFlags(&e->stream3[i], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_part[i + 1], hipEventDisableTiming) != hipSuccess) {
+            oaz_set_err(OAZ_ERR_HIP, "stream create failed");
+            return fail();
+        }
     for (int i = 0; i < 2; ++i)
         if (hipEventCreateWithFlags(&e->ev_ready[i], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&e->ev_consumed[i], hipEventDisableTiming) != hipSuccess) {
@@ -846,7 +858,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         dalloc(&e->stats, G * GS_COUNT) || dalloc(&e->stats_sum, (size_t)GS_COUNT) ||
         dalloc(&e->sqrt_tab, (size_t)cfg->sims + 2) || dalloc(&e->policy, G * 50) ||
         dalloc(&e->value, G) || dalloc(&e->need, G) || dalloc(&e->slot, G) || dalloc(&e->cstate, G + 16) ||
-        dalloc(&e->bcnt, (size_t)buckets_of((uint32_t)G)) || dalloc(&e->weights, weights_floats(cfg->blocks, cfg->precision)) ||
+        dalloc(&e->bcnt, (size_t)buckets_of((uint32_t)G) + kMaxParts) || dalloc(&e->weights, weights_floats(cfg->blocks, cfg->precision)) ||
         dalloc(&e->s_roots, G) || dalloc(&e->s_move, G) || dalloc(&e->s_pi, G * 50) ||
         dalloc(&e->s_rootv, G) || dalloc(&e->s_rootp, G * 50) || dalloc(&e->s_ply, G) ||
         dalloc(&e->root, G) || dalloc(&e->ply, G) || dalloc(&e->seq, G) ||
@@ -880,10 +892,15 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->stream2) (void)hipStreamSynchronize(e->stream2);
+    for (auto s3 : e->stream3)
+        if (s3) (void)hipStreamSynchronize(s3);
+    for (auto ev : e->ev_part)
+        if (ev) (void)hipEventDestroy(ev);
     for (int i = 0; i < 2; ++i) {
         if (e->ev_ready[i]) (void)hipEventDestroy(e->ev_ready[i]);
         if (e->ev_consumed[i]) (void)hipEventDestroy(e->ev_consumed[i]);
     }
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     for (auto& p : e->pending) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -897,6 +914,8 @@ extern "C" void oaz_destroy(oaz_engine* e) {
     for (void* p : ptrs) dfree(p);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
+    for (auto s3 : e->stream3)
+        if (s3) (void)hipStreamDestroy(s3);
     delete e;
 }
 
@@ -1056,6 +1075,21 @@ static bool compact_leaves(const oaz_engine* e, uint32_t G) {
 // mcts_arena.rs:156-176) and the compaction kernel packs their leaves per 4096-game bucket, so the
 // network evaluates only those. With root noise, k_root_noise fills chunk c+1 of the
 // double-buffered noise ring on stream2 while stream 1 runs chunk c (events order the ring slots).
+static TreeView slice_view(const TreeView& t, uint32_t g0, uint32_t n, int b0);
+
+// Game parts of run_sims (oaz_config.parts; 0 = auto: two from kAutoParts games; the overlap of
+// one part's tree kernels and NN tail with the other's launches measured +3-4 % on C2, C3, C5).
+constexpr uint32_t kAutoParts = 2048;
+static int game_parts(const oaz_engine* e, uint32_t G) {
+    int p = e->cfg.parts ? e->cfg.parts : (G >= kAutoParts ? 2 : 1);
+#if OAZ_AB  // A/B build only: OAZ_SPLIT_HALVES=n overrides
+    if (const char* v = getenv("OAZ_SPLIT_HALVES")) p = atoi(v);
+#endif
+    if (p != 2 && p != 4) p = 1;
+    while (p > 1 && (uint32_t)p > G) p /= 2;
+    return p;
+}
+
 static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, const uint8_t* active,
                     const uint64_t* gids, const uint32_t* plies) {
     const SearchParams prm = search_params(e);
@@ -1085,50 +1119,114 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
         tc.need = nullptr;
         tc.slot = nullptr;
     }
-    const TileMap tm{t.bcnt, buckets_of(t.G), (int32_t)t.G + 16};
-    hipStream_t st = e->stream;
 #if OAZ_AB  // A/B build only: OAZ_TREE_FUSE=0 runs expand/backup and the next select as two launches
     static const bool fuse = !(getenv("OAZ_TREE_FUSE") && getenv("OAZ_TREE_FUSE")[0] == '0');
 #else
     constexpr bool fuse = true;
 #endif
+    // The games in nh parts, each on its own stream: one part's tree kernels, leaf compaction and NN
+    // tail run in the gaps of the others' launches (the NN holds a whole CU per workgroup, so the
+    // tree kernels cannot share a CU with it, only fill the CUs it leaves idle).
+    const int nh = game_parts(e, t.G);
+    const bool split = nh > 1;
+    const uint32_t Gh = (t.G + (uint32_t)nh - 1) / (uint32_t)nh;
+    TreeView tv[kMaxParts];
+    hipStream_t sh[kMaxParts] = {e->stream, e->stream3[0], e->stream3[1], e->stream3[2]};
+    for (int h = 0; h < nh; ++h)
+        tv[h] = split ? slice_view(tc, (uint32_t)h * Gh, (uint32_t)h * Gh + Gh <= t.G ? Gh : t.G - (uint32_t)h * Gh,
+                                   h * buckets_of(Gh))
+                      : tc;
+    if (split) {
+        HIP_TRY(hipEventRecord(e->ev_join, e->stream));  // the other streams start after prior work
+        for (int h = 1; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(sh[h], e->ev_join, 0));
+    }
+    auto join = [&]() -> int {  // stream waits for the other parts' streams
+        for (int h = 1; h < nh; ++h) {
+            HIP_TRY(hipEventRecord(e->ev_part[h], sh[h]));
+            HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_part[h], 0));
+        }
+        return 0;
+    };
     for (uint32_t c = 0; c < nchunks; ++c) {
         if (noise) {
             if (c + 1 < nchunks)
                 if (int rc = produce(c + 1)) return rc;
-            HIP_TRY(hipStreamWaitEvent(st, e->ev_ready[c & 1], 0));
+            for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(sh[h], e->ev_ready[c & 1], 0));
         }
         const uint32_t s0 = c * kNoiseChunk, s1 = s0 + kNoiseChunk < sims ? s0 + kNoiseChunk : sims;
         for (uint32_t s = s0; s < s1; ++s) {
             // sampled steps sit mid-chunk: a chunk's first select also waits for its noise
             e->timing_skip = e->timing_every > 1 && s % (uint32_t)e->timing_every != (uint32_t)e->timing_every / 2;
-            const float* nz = noise ? e->noise + (c & 1) * slot_elems + (size_t)(s - s0) * t.G * kNoiseStride : nullptr;
-            if (s == 0) {
-                if (int rc = timed(e, 0, t.G, [&] { return launch_select(tc, roots, active, nz, prm, st); }, st))
+            for (int h = 0; h < nh; ++h) {
+                const TreeView& th = tv[h];
+                const size_t go = (size_t)h * Gh;
+                if (th.G == 0) continue;
+                const hipStream_t st = sh[h];
+                const oaz_state* rh = roots + go;
+                const uint8_t* ah = active ? active + go : nullptr;  // null in search mode
+                float* pol = e->policy + go * 50;
+                float* val = e->value + go;
+                const float* nz = noise ? e->noise + (c & 1) * slot_elems + ((size_t)(s - s0) * t.G + go) * kNoiseStride
+                                        : nullptr;
+                if (s == 0) {
+                    if (int rc = timed(e, 0, th.G, [&] { return launch_select(th, rh, ah, nz, prm, st); }, st))
+                        return rc;
+                } else if (!fuse) {
+                    if (int rc = timed(e, 2, th.G, [&] { return launch_expand_backup(th, rh, ah, pol, val, st); }, st))
+                        return rc;
+                    if (int rc = timed(e, 0, th.G, [&] { return launch_select(th, rh, ah, nz, prm, st); }, st))
+                        return rc;
+                } else if (int rc = timed(e, 6, th.G, [&] {
+                               return launch_backup_select(th, rh, ah, pol, val, nz, prm, st);
+                           }, st)) {
                     return rc;
-            } else if (!fuse) {
-                if (int rc = timed(e, 2, t.G, [&] {
-                        return launch_expand_backup(tc, roots, active, e->policy, e->value, st);
-                    }, st))
+                }
+                if (th.need) {
+                    const TileMap tm{th.bcnt, buckets_of(th.G), (int32_t)th.G + 16};
+                    if (int rc = timed(e, 5, th.G, [&] { return launch_eval_compact(th, st); }, st)) return rc;
+                    if (int rc = evaluate(e, th.cstate, th.G, pol, val, st, &tm)) return rc;
+                } else if (int rc = evaluate(e, th.leaf_state, th.G, pol, val, st)) {
                     return rc;
-                if (int rc = timed(e, 0, t.G, [&] { return launch_select(tc, roots, active, nz, prm, st); }, st))
-                    return rc;
-            } else if (int rc = timed(e, 6, t.G, [&] {
-                           return launch_backup_select(tc, roots, active, e->policy, e->value, nz, prm, st);
-                       }, st)) {
-                return rc;
-            }
-            if (tc.need) {
-                if (int rc = timed(e, 5, t.G, [&] { return launch_eval_compact(tc, st); }, st)) return rc;
-                if (int rc = evaluate(e, tc.cstate, t.G, e->policy, e->value, st, &tm)) return rc;
-            } else if (int rc = evaluate(e, tc.leaf_state, t.G, e->policy, e->value, st)) {
-                return rc;
+                }
             }
         }
-        if (noise) HIP_TRY(hipEventRecord(e->ev_consumed[c & 1], st));
+        if (split)  // every part is done with this noise slot
+            if (int rc = join()) return rc;
+        if (noise) HIP_TRY(hipEventRecord(e->ev_consumed[c & 1], e->stream));
     }
     e->timing_skip = false;
-    return timed(e, 2, t.G, [&] { return launch_expand_backup(tc, roots, active, e->policy, e->value, st); }, st);
+    for (int h = 0; h < nh; ++h) {
+        const size_t go = (size_t)h * Gh;
+        if (tv[h].G == 0) continue;
+        if (int rc = timed(e, 2, tv[h].G, [&] {
+                return launch_expand_backup(tv[h], roots + go, active ? active + go : nullptr, e->policy + go * 50,
+                                            e->value + go, sh[h]);
+            }, sh[h]))
+            return rc;
+    }
+    if (split)
+        if (int rc = join()) return rc;
+    return 0;
+}
+
+// The trees of games [g0, g0 + n) as a view of their own: every per-game array offset by g0, the
+// part's compaction buckets from bucket counter b0 (its compacted rows start at g0; a part's last
+// tile may read up to 15 rows of the next part's, which it never stores).
+static TreeView slice_view(const TreeView& t, uint32_t g0, uint32_t n, int b0) {
+    TreeView v = t;
+    v.nodes = t.nodes + (size_t)g0 * t.cap;
+    v.n_nodes = t.n_nodes + g0;
+    v.path = t.path + (size_t)g0 * t.pathcap;
+    v.depth = t.depth + g0;
+    v.leaf = t.leaf + g0;
+    v.leaf_state = t.leaf_state + g0;
+    v.stats = t.stats + (size_t)g0 * GS_COUNT;
+    if (t.need) v.need = t.need + g0;
+    if (t.slot) v.slot = t.slot + g0;
+    v.cstate = t.cstate + g0;
+    v.bcnt = t.bcnt + b0;
+    v.G = n;
+    return v;
 }
 
 static int reduce_stats(oaz_engine* e, uint32_t G, uint64_t out[GS_COUNT]) {

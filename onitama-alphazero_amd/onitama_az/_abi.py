@@ -84,7 +84,8 @@ class oaz_config(C.Structure):
         ("sample_capacity", C.c_int32),
         ("stagger", C.c_int32),
         ("compact", C.c_int32),
-        ("reserved", C.c_int32 * 5),
+        ("parts", C.c_int32),
+        ("reserved", C.c_int32 * 4),
     ]
 
 

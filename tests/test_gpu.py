@@ -218,12 +218,13 @@ def _compare_trees(e, g, nodes_ref):
         assert np.array_equal(a, b), f
 
 
-@pytest.mark.parametrize("compact", [0, 1])  # 0: 12 games evaluate in place; 1: leaf compaction forced
+# compact 0: 12 games evaluate in place, 1: leaf compaction forced; parts: the games on 1 or 2 streams
+@pytest.mark.parametrize("compact,parts", [(0, 1), (1, 1), (0, 2), (1, 2)])
 @pytest.mark.parametrize("sims,c_puct", [(64, 5.0), (200, 2.0)])
-def test_search_hash_trees_bitexact(orc, sims, c_puct, compact):
+def test_search_hash_trees_bitexact(orc, sims, c_puct, compact, parts):
     roots = random_positions(orc, 12, seed=505 + sims)
     with Engine(games=len(roots), sims=sims, c_puct=c_puct, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0,
-                compact=compact) as e:
+                compact=compact, parts=parts) as e:
         r = e.search(roots)
         evals = terminal = 0
         for g in range(len(roots)):
@@ -240,16 +241,16 @@ def test_search_hash_trees_bitexact(orc, sims, c_puct, compact):
     assert r.stats.sims - r.stats.terminal_leaves <= r.stats.nn_evals <= r.stats.sims
 
 
-@pytest.mark.parametrize("compact", [0, 1])
+@pytest.mark.parametrize("compact,parts", [(0, 1), (1, 2)])
 @pytest.mark.parametrize("precision", [_abi.FP32, _abi.FP32_SPLIT16])
-def test_search_nn_trees_bitexact_with_gpu_evaluator(orc, precision, compact):
+def test_search_nn_trees_bitexact_with_gpu_evaluator(orc, precision, compact, parts):
     """Real network: the oracle's search is fed the GPU network's outputs (batch-1 calls of
     the same kernel), so both searches see identical evaluations and must agree exactly."""
     roots = random_positions(orc, 4, seed=606)
     w = random_weights(3, 3)
     sims = 48
     with Engine(games=len(roots), sims=sims, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_NN, blocks=3,
-                precision=precision, compact=compact) as e, \
+                precision=precision, compact=compact, parts=parts) as e, \
             Engine(games=4, sims=1, blocks=3, precision=precision) as ev:
         e.load_weights(w)
         ev.load_weights(w)
@@ -384,13 +385,13 @@ def _sorted_rows(a):
     return np.sort(np.frombuffer(a.tobytes(), dtype=np.dtype((np.void, a.dtype.itemsize))))
 
 
-@pytest.mark.parametrize("fixed,max_plies,compact", [(True, 150, 0), (False, 150, 0), (False, 3, 0), (True, 150, 1),
-                                                     (False, 150, 1)])
-def test_selfplay_matches_oracle_games(orc, fixed, max_plies, compact):
+@pytest.mark.parametrize("fixed,max_plies,compact,parts", [(True, 150, 0, 1), (False, 150, 0, 1), (False, 3, 0, 1),
+                                                           (True, 150, 1, 2), (False, 150, 1, 4), (False, 3, 0, 2)])
+def test_selfplay_matches_oracle_games(orc, fixed, max_plies, compact, parts):
     n_games, slots, sims = 24, 8, 12
     deck = [0, 1, 2, 3, 4]
     kw = dict(games=slots, sims=sims, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0,
-              max_plies=max_plies, seed=4242, fixed_deck=int(fixed), deck=deck, compact=compact)
+              max_plies=max_plies, seed=4242, fixed_deck=int(fixed), deck=deck, compact=compact, parts=parts)
     with Engine(**kw) as e:
         got, st = e.selfplay_run(n_games, cap=n_games * (max_plies + 2))
     assert st.games_finished == n_games

@@ -153,8 +153,10 @@ def test_root_noise_host_matches_oracle_and_distribution():
         assert abs(xs.var() / var - 1.0) < 0.2, (K, xs.var(), var)
 
 
-def test_config_compact_out_of_range_is_an_error():
-    """oaz_config.compact is -1, 0 or 1; anything else fails oaz_create before any device work."""
+@pytest.mark.parametrize("kw", [dict(compact=2), dict(compact=-2), dict(parts=3), dict(parts=-1)])
+def test_config_compact_and_parts_out_of_range_are_errors(kw):
+    """oaz_config.compact is -1, 0 or 1 and parts 0, 1, 2 or 4; anything else fails oaz_create
+    before any device work."""
     from onitama_az.engine import Engine
     with pytest.raises(_abi.OazError, match="config out of range"):
-        Engine(games=4, sims=4, compact=2)
+        Engine(games=4, sims=4, **kw)
