@@ -106,7 +106,9 @@ def pmc_traffic(args, cfg):
     if prof is None:
         return None
     plies = args.warmup
-    first, last = plies * cfg["sims"] + 1, (plies + 1) * cfg["sims"]  # 1-based launch index of each kernel
+    parts = sim_parts(cfg["games"])  # launches of each kernel per simulation step
+    per_ply = cfg["sims"] * parts
+    first, last = plies * per_ply + 1, (plies + 1) * per_ply  # 1-based launch index of each kernel
     kb, tree_kb, counts = {}, {"backup_select": {}}, {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         with tempfile.TemporaryDirectory() as d:
@@ -132,19 +134,20 @@ def pmc_traffic(args, cfg):
                 return None
             for k, v in rows.items():  # the last ply's launches only (also if the range was not applied)
                 v.sort()
-                rows[k] = [x for _, x in v[-cfg["sims"]:]]
+                rows[k] = [x for _, x in v[-per_ply:]]
                 counts[k] = len(rows[k])
             kb[ctr] = sum(rows["nn"]) / len(rows["nn"])
             for k in ("backup_select",):
                 if rows[k]:
                     tree_kb[k][ctr] = sum(rows[k]) / len(rows[k])
-    fetch, write = 2.0 * kb["FETCH_SIZE"] * 1024.0, kb["WRITE_SIZE"] * 1024.0
+    # per simulation step: its parts' launches
+    fetch, write = 2.0 * kb["FETCH_SIZE"] * 1024.0 * parts, kb["WRITE_SIZE"] * 1024.0 * parts
     tree = {}
-    for k, v in tree_kb.items():  # per game: every launch covers every game slot
+    for k, v in tree_kb.items():  # per game: a launch covers the game slots of one part
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-            tree[k] = {"fetch_bytes_per_sim": 2.0 * v["FETCH_SIZE"] * 1024.0 / cfg["games"],
-                       "write_bytes_per_sim": v["WRITE_SIZE"] * 1024.0 / cfg["games"]}
-    return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+            tree[k] = {"fetch_bytes_per_sim": 2.0 * v["FETCH_SIZE"] * 1024.0 * parts / cfg["games"],
+                       "write_bytes_per_sim": v["WRITE_SIZE"] * 1024.0 * parts / cfg["games"]}
+    return {"bytes_per_sim_step": fetch + write, "fetch_bytes": fetch, "write_bytes": write, "game_parts": parts,
             "raw_kb": kb, "tree_pmc": tree, "launches_profiled": counts,
             "note": f"rocprofv3 --pmc, separate passes, on the {cfg['sims']} simulation steps of ply {plies + 1} "
                     f"(after {plies} warm-up plies, stagger {args.stagger}); FETCH_SIZE x2 (gfx950 wide-read "
@@ -186,14 +189,17 @@ def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg, pmc=No
     if not kt.backup_select_n:
         return None
     D, K = depth, branching
-    per_launch = sims / max(1, sim_steps)  # games per tree-kernel launch
+    per_launch = sims / max(1, sim_steps) / max(1, kt.parts)  # games per tree-kernel launch (one game part)
     noise = 8.0 * K if cfg.get("noise", True) else 0.0
     sel = 24 + 32 + D * (32 * K + 8 + 4) + noise + 32 + 16 + 1  # + the need flag
     exp = 64 + 4 + 4 + (expansions / max(1, sims)) * (200 + 32 * K + 16) + (D + 1) * (4 + 24)  # + the row
     out = {"bound": "latency (one dependent HBM round trip per tree level; 4 games per wave)",
            "peak_GBps": HBM_PEAK_GBPS, "sims_per_launch": per_launch,
            "kernel": "k_backup_select_seg (expand/backup of simulation s + select of s + 1, one launch per "
-                     "simulation step; the first select and the last expand/backup of a move run alone)"}
+                     "simulation step and game part; the first select and the last expand/backup of a move run "
+                     "alone)",
+           "note": "launch times overlap the other game part's kernels (its NN holds whole CUs), so the rates "
+                   "are lower bounds"}
     for name, ms, n, b in (("backup_select", kt.backup_select_ms, kt.backup_select_n, sel + exp),):
         t = ms / n * 1e-3
         gbps = per_launch * b / t / 1e9
@@ -468,17 +474,44 @@ def pure_mcts_main(args, world, rank, local):
         dist.destroy_process_group()
 
 
-def exact_fp32_leg(args, cfg, device):
-    """The same workload on the exact-fp32 NN kernel (k_nn_sq16: fp32 MFMA products), so the
-    headline's precision trade is visible in the same line: a short run (2 warmup + 2 timed steps,
-    no staggered starts) with the NN kernel timed by HIP events on the engine stream."""
+def sim_parts(games, parts=0):
+    """Game parts (streams) of the engine's simulation loop: oaz_config.parts, or auto = 2 from 2048
+    games (oaz_engine.cpp game_parts); bench.py checks it against kernel_times().parts."""
+    return parts if parts in (1, 2, 4) else (2 if games >= 2048 else 1)
+
+
+def nn_step_rate(kt, evals, sim_steps, blocks):
+    """The NN's rate per simulation step. Each step launches the NN once per game part (kt.parts,
+    one stream each); the parts' launches overlap, so a step's NN time is the union of their
+    intervals (kt.nn_busy_ms over the timed steps), and its positions are all game slots
+    (kt.nn_samples, counted by the engine) or, with leaf compaction, the leaves the playouts use
+    (nn_evals over the region / its simulation steps)."""
+    parts = max(1, kt.parts)
+    steps_timed = max(1, kt.nn_n // parts)
+    positions = kt.nn_samples / steps_timed if kt.nn_samples else evals / max(1, sim_steps)
+    busy = kt.nn_busy_ms / steps_timed
+    flops = FLOP_PER_SIM[blocks] * positions
+    return {"parts": parts, "positions": positions, "busy_ms": busy, "flops": flops,
+            "avg_launch_ms": kt.nn_ms / max(1, kt.nn_n),
+            "achieved": flops / (busy * 1e-3) / 1e12 if kt.nn_n and busy > 0 else 0.0}
+
+
+PREC_ABI = {"bf16": "BF16", "fp32": "FP32", "fp32_split": "FP32_SPLIT", "fp32_split16": "FP32_SPLIT16"}
+
+
+def single_stream_leg(args, cfg, device, precision):
+    """The workload on one stream (oaz_config.parts = 1), a short run (2 warm-up + 2 timed plies, no
+    staggered starts) with HIP events around the NN launches of every 8th simulation step on the
+    engine stream. With the headline's two game parts the parts' NN launches overlap each other
+    and the other part's tree kernels, so per-launch event times there include waiting for CUs;
+    here every launch has the GPU to itself, which is what a kernel roofline needs."""
     from onitama_az import _abi
     from onitama_az.engine import Engine
     from onitama_az.weights import random_weights
     with Engine(device=device, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0,
-                train_noise=0 if args.no_noise else 1, max_plies=150, evaluator=_abi.EVAL_NN, precision=_abi.FP32,
-                fixed_deck=cfg["fixed_deck"], deck=[0, 1, 2, 3, 4], seed=20260101,
-                sample_capacity=cfg["games"] * 8) as e:
+                train_noise=0 if args.no_noise else 1, max_plies=150, evaluator=_abi.EVAL_NN,
+                precision=getattr(_abi, PREC_ABI[precision]), fixed_deck=cfg["fixed_deck"], deck=[0, 1, 2, 3, 4],
+                seed=20260101, sample_capacity=cfg["games"] * 8, parts=1) as e:
         e.load_weights(random_weights(0, cfg["blocks"]))
         e.selfplay_reset()
         e.selfplay_step(2)
@@ -495,18 +528,22 @@ def exact_fp32_leg(args, cfg, device):
         kt = e.kernel_times()
         st1 = e.selfplay_stats()
     sims = st1.search.sims - st0.search.sims
-    nn_ms = kt.nn_ms / max(1, kt.nn_n)
-    # positions per NN launch: all game slots (kt.nn_samples), or with leaf compaction (whose counts
-    # stay on the device) the evaluations the playouts use per simulation step
-    pos = (kt.nn_samples / max(1, kt.nn_n) if kt.nn_samples
-           else (st1.search.nn_evals - st0.search.nn_evals) / max(1, 2 * cfg["sims"]))
-    fl = FLOP_PER_SIM[cfg["blocks"]] * pos
-    tf = fl / (nn_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
-    return {"kernel": NN_KERNEL["fp32"], "value": sims / dt, "unit": "sims/s", "ms_per_step": 1e3 * dt / 2,
-            "steps": 2, "warmup": 2, "nn_avg_launch_ms": nn_ms, "nn_achieved_TFLOPs": tf,
-            "nn_frac_of_fp32_mfma_peak": tf / PEAK_TFLOPS["fp32"],
-            "note": "same workload, exact fp32 MFMA products (no operand splitting); short run without staggered "
-                    "starts (the NN dominates the step)"}
+    nn = nn_step_rate(kt, st1.search.nn_evals - st0.search.nn_evals, 2 * cfg["sims"], cfg["blocks"])
+    nn["nonzero_achieved"] = (nonzero_flop_per_sim(cfg["blocks"]) * nn["positions"] / (nn["avg_launch_ms"] * 1e-3)
+                              / 1e12 if nn["avg_launch_ms"] > 0 else 0.0)
+    nn.update(sims_per_s=sims / dt, ms_per_step=1e3 * dt / 2, launches=kt.nn_n)
+    return nn
+
+
+def exact_fp32_leg(args, cfg, device):
+    """The same workload on the exact-fp32 NN kernel (k_nn_sq16: fp32 MFMA products), so the
+    headline's precision trade is visible in the same line (single_stream_leg)."""
+    nn = single_stream_leg(args, cfg, device, "fp32")
+    return {"kernel": NN_KERNEL["fp32"], "value": nn["sims_per_s"], "unit": "sims/s", "ms_per_step": nn["ms_per_step"],
+            "steps": 2, "warmup": 2, "game_parts": 1, "nn_avg_launch_ms": nn["avg_launch_ms"],
+            "nn_achieved_TFLOPs": nn["achieved"], "nn_frac_of_fp32_mfma_peak": nn["achieved"] / PEAK_TFLOPS["fp32"],
+            "note": "same workload on one stream, exact fp32 MFMA products (no operand splitting); short run "
+                    "without staggered starts (the NN dominates the step)"}
 
 
 def main():
@@ -628,15 +665,11 @@ def main():
 
     if rank == 0:
         sims_steps = cfg["sims"]  # simulation steps (select -> NN -> expand launches) per bench step
-        nn_avg_ms = kt.nn_ms / max(1, kt.nn_n)
-        # every simulation step launches the NN once: on every game slot (nn_samples counted by the
-        # engine), or with leaf compaction on the leaves the playouts use (their count: nn_evals)
-        positions = (kt.nn_samples / max(1, kt.nn_n) if kt.nn_samples else evals / max(1, args.steps * sims_steps))
-        flops_launch = FLOP_PER_SIM[cfg["blocks"]] * positions
-        achieved = flops_launch / (nn_avg_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
-        nz = nonzero_flop_per_sim(cfg["blocks"]) * positions
-        achieved_nz = nz / (nn_avg_ms * 1e-3) / 1e12 if kt.nn_n else 0.0
-        alg_bytes = 0.96e6 + positions * (24 + 204)  # weights once + states in + policy/value out
+        nn = nn_step_rate(kt, evals, args.steps * sims_steps, cfg["blocks"])
+        parts, positions, achieved = nn["parts"], nn["positions"], nn["achieved"]
+        if traffic and parts != sim_parts(cfg["games"]):
+            print(f"bench: PMC passes assumed {sim_parts(cfg['games'])} game parts, the run used {parts}",
+                  file=sys.stderr)
         out = {
             "metric": METRIC, "value": sims_all / T, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * T / args.steps, "higher_is_better": True, "scaling": "weak",
@@ -663,6 +696,7 @@ def main():
             "games_per_s": games_all / T, "plies_per_s": plies_all / T,
             "true_expansions_per_s": exp_all / T, "mean_select_depth": depth, "mean_branching": branching,
             "nn_positions_per_sim": positions * args.steps * sims_steps / max(1, sims),
+            "game_parts": parts,
             "leaf_compaction": not kt.nn_samples,
             "nn_evaluation": "every simulation's leaf is evaluated except a won, terminal-flagged leaf, whose evaluation "
                              "the reference computes and discards (mcts_arena.rs:156-176: no expansion, the reward is "
@@ -673,23 +707,19 @@ def main():
                 "backup_select_fused": kt.backup_select_ms / max(1, kt.backup_select_n) * (sims_steps - 1),
                 "select_first": kt.select_ms / max(1, kt.select_n) if kt.select_n else None,
                 "expand_backup_last": kt.expand_ms / max(1, kt.expand_n) if kt.expand_n else None,
-                "nn": kt.nn_ms / max(1, kt.nn_n) * sims_steps,
+                "nn": nn["busy_ms"] * sims_steps,
                 "leaf_compact": kt.compact_ms / max(1, kt.compact_n) * sims_steps,
                 "move": kt.finalize_ms / args.steps, "root_noise_stream2": kt.noise_ms / args.steps},
             "kernel_timing": "HIP events around the kernels of every %s-th simulation step (per-kernel means x "
-                             "simulation steps per bench step)" % os.environ.get("OAZ_BENCH_TIMING_EVERY", "8"),
-            "roofline": {"bound": "mfma", "kernel": NN_KERNEL[cfg["precision"]],
-                         "achieved": achieved, "peak": PEAK_TFLOPS[cfg["precision"]], "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_TFLOPS[cfg["precision"]],
-                         "traffic": traffic["bytes_per_launch"] if traffic else None,
-                         "flop_per_launch": flops_launch, "avg_launch_ms": nn_avg_ms, "launches": kt.nn_n,
-                         "positions_per_launch": positions, "flop_accounting": "SURVEY 8d dense MACs x2 per sim",
-                         "achieved_nonzero": achieved_nz, "frac_nonzero": achieved_nz / PEAK_TFLOPS[cfg["precision"]],
-                         "algorithmic_bytes_per_launch": alg_bytes, "traffic_detail": traffic,
-                         "peak_note": {"fp32": "F32 MFMA dense peak", "bf16": "BF16 dense MFMA peak",
-                                       "fp32_split": "BF16 dense MFMA peak / 6 products per fp32 MAC",
-                                       "fp32_split16": "FP16 dense MFMA peak / 3 products per fp32 MAC"}[cfg["precision"]],
-                         "frac_of_fp32_mfma_peak": achieved / PEAK_TFLOPS["fp32"]},
+                             "simulation steps per bench step; nn: the union of the game parts' overlapping NN "
+                             "launches per step; the tree kernels' launches overlap the other part's too)"
+                             % os.environ.get("OAZ_BENCH_TIMING_EVERY", "8"),
+            "nn_in_loop": {"game_parts": parts, "busy_ms_per_sim_step": nn["busy_ms"],
+                           "avg_launch_ms": nn["avg_launch_ms"], "positions_per_sim_step": positions,
+                           "achieved_TFLOPs": achieved,
+                           "note": "the game parts' NN launches of a simulation step overlap each other and the "
+                                   "other part's tree kernels; busy = the union of their HIP-event intervals, "
+                                   "which includes waiting for CUs (the roofline below is measured on one stream)"},
             "tree_kernels": tree_roofline(kt, sims, args.steps * sims_steps, expansions, depth, branching, cfg,
                                           traffic.get("tree_pmc") if traffic else None),
             "allgather": allgather,
@@ -697,6 +727,27 @@ def main():
         }
     eng.close()
     if rank == 0:
+        # the dominant kernel's roofline, on one stream (single_stream_leg): per-launch HIP events
+        leg = single_stream_leg(args, cfg, local, cfg["precision"])
+        lp = leg["positions"]
+        out["roofline"] = {
+            "bound": "mfma", "kernel": NN_KERNEL[cfg["precision"]],
+            "achieved": leg["achieved"], "peak": PEAK_TFLOPS[cfg["precision"]], "unit": "TFLOP/s",
+            "frac": leg["achieved"] / PEAK_TFLOPS[cfg["precision"]],
+            "traffic": traffic["bytes_per_sim_step"] if traffic else None,
+            "measured_on": "the same workload on one stream (oaz_config.parts = 1; 2 warm-up + 2 timed plies, no "
+                           "staggered starts), HIP events around the NN launches of every 8th simulation step; "
+                           "rocprofv3 kernel trace of the same launches: tools/trace_steady.py (last dispatches)",
+            "flop_per_launch": leg["flops"], "avg_launch_ms": leg["avg_launch_ms"], "launches": leg["launches"],
+            "positions_per_launch": lp, "flop_accounting": "SURVEY 8d dense MACs x2 per sim",
+            "achieved_nonzero": leg["nonzero_achieved"],
+            "frac_nonzero": leg["nonzero_achieved"] / PEAK_TFLOPS[cfg["precision"]],
+            "algorithmic_bytes_per_launch": 0.96e6 + lp * (24 + 204),  # weights once + states in + outputs
+            "traffic_detail": traffic,
+            "peak_note": {"fp32": "F32 MFMA dense peak", "bf16": "BF16 dense MFMA peak",
+                          "fp32_split": "BF16 dense MFMA peak / 6 products per fp32 MAC",
+                          "fp32_split16": "FP16 dense MFMA peak / 3 products per fp32 MAC"}[cfg["precision"]],
+            "frac_of_fp32_mfma_peak": leg["achieved"] / PEAK_TFLOPS["fp32"]}
         if not args.no_exact and world == 1 and cfg["precision"] in ("fp32_split16", "fp32_split"):
             out["exact_fp32"] = exact_fp32_leg(args, cfg, local)
         if not args.no_cpu_baseline and world == 1:

@@ -203,6 +203,10 @@ typedef struct oaz_kernel_times {
     double backup_select_ms; /* expand/backup of simulation s fused with the select of s + 1 (every
                               * simulation step but the first select and the last expand/backup) */
     uint64_t backup_select_n;
+    double nn_busy_ms;    /* length of the union of the timed nn launches' intervals (the game parts'
+                           * launches of one simulation step overlap; oaz_config.parts) */
+    uint64_t nn_busy_n;   /* disjoint intervals in that union */
+    uint64_t parts;       /* game parts (streams) of the last simulation loop: nn launches per step */
 } oaz_kernel_times;
 
 typedef struct oaz_engine oaz_engine;

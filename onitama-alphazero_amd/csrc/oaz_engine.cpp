@@ -14,6 +14,7 @@
 
 #include <mutex>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/onitama_az.h"
@@ -753,6 +754,39 @@ static void accumulate(oaz_engine* e, const TimedLaunch& p, float ms) {
     if (p.kind == 1) e->times.nn_samples += p.samples;
 }
 
+// Resolve the recorded event pairs: per-kind sums, and the NN's busy time = the length of the union
+// of its launches' intervals (with game parts on several streams the NN launches of a simulation
+// step overlap each other; the union is the time during which any of them ran).
+static int resolve_pending(oaz_engine* e) {
+    std::vector<std::pair<float, float>> nn;
+    hipEvent_t ref = e->pending.empty() ? nullptr : e->pending.front().a;
+    for (auto& p : e->pending) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b));
+        accumulate(e, p, ms);
+        if (p.kind == 1) {
+            float t0 = 0.f;
+            HIP_TRY(hipEventElapsedTime(&t0, ref, p.a));
+            nn.emplace_back(t0, t0 + ms);
+        }
+    }
+    std::sort(nn.begin(), nn.end());
+    for (size_t i = 0; i < nn.size();) {
+        float lo = nn[i].first, hi = nn[i].second;
+        size_t j = i + 1;
+        for (; j < nn.size() && nn[j].first <= hi; ++j) hi = std::max(hi, nn[j].second);
+        e->times.nn_busy_ms += hi - lo;
+        e->times.nn_busy_n += 1;
+        i = j;
+    }
+    for (auto& p : e->pending) {
+        e->pool.push_back(p.a);
+        e->pool.push_back(p.b);
+    }
+    e->pending.clear();
+    return 0;
+}
+
 template <class F>
 static int timed(oaz_engine* e, int kind, uint32_t samples, F&& launch, hipStream_t st = nullptr) {
     if (!st) st = e->stream;
@@ -772,14 +806,8 @@ static int timed(oaz_engine* e, int kind, uint32_t samples, F&& launch, hipStrea
     if (e->pending.size() > 4096) {  // resolve periodically to bound the pool
         HIP_TRY(hipStreamSynchronize(e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream2));
-        for (auto& p : e->pending) {
-            float ms = 0.f;
-            (void)hipEventElapsedTime(&ms, p.a, p.b);
-            accumulate(e, p, ms);
-            e->pool.push_back(p.a);
-            e->pool.push_back(p.b);
-        }
-        e->pending.clear();
+        for (auto s3 : e->stream3) HIP_TRY(hipStreamSynchronize(s3));
+        return resolve_pending(e);
     }
     return 0;
 }
@@ -975,15 +1003,8 @@ extern "C" int oaz_set_timing(oaz_engine* e, int enable) {
 static int resolve_timing(oaz_engine* e) {
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream2));
-    for (auto& p : e->pending) {
-        float ms = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b));
-        accumulate(e, p, ms);
-        e->pool.push_back(p.a);
-        e->pool.push_back(p.b);
-    }
-    e->pending.clear();
-    return 0;
+    for (auto s3 : e->stream3) HIP_TRY(hipStreamSynchronize(s3));
+    return resolve_pending(e);
 }
 
 extern "C" int oaz_kernel_times_get(oaz_engine* e, oaz_kernel_times* out) {
@@ -1129,6 +1150,7 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
     // tree kernels cannot share a CU with it, only fill the CUs it leaves idle).
     const int nh = game_parts(e, t.G);
     const bool split = nh > 1;
+    e->times.parts = (uint64_t)nh;
     const uint32_t Gh = (t.G + (uint32_t)nh - 1) / (uint32_t)nh;
     TreeView tv[kMaxParts];
     hipStream_t sh[kMaxParts] = {e->stream, e->stream3[0], e->stream3[1], e->stream3[2]};

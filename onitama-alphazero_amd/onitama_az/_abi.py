@@ -133,6 +133,9 @@ class oaz_kernel_times(C.Structure):
         ("compact_n", C.c_uint64),
         ("backup_select_ms", C.c_double),
         ("backup_select_n", C.c_uint64),
+        ("nn_busy_ms", C.c_double),
+        ("nn_busy_n", C.c_uint64),
+        ("parts", C.c_uint64),
     ]
 
 

@@ -10,6 +10,7 @@ step bench timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench_
 tail -1 gpurun_out/bench_$TAG.json | cut -c1-600
 step trace timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG/trace -o run -- "$PY" bench.py --steps 2 --no-cpu-baseline --no-allgather --no-pmc --no-exact ${PROF_ARGS:-} > gpurun_out/prof_$TAG/trace.log 2>&1
 find gpurun_out/prof_$TAG -name "*kernel_stats.csv" | head
-# the timed plies only (the --stats summary also averages the staggered warm-up plies)
+# the last 2 plies: bench.py ends with the single-stream roofline leg (2 timed plies, one part), whose
+# NN launches are the roofline's; the --stats summary also averages every earlier launch
 T=$(find gpurun_out/prof_$TAG -name "*kernel_trace.csv" | head -1)
-[ -n "$T" ] && python tools/trace_steady.py "$T" $((2 * ${SIMS:-400})) > gpurun_out/prof_$TAG/steady_kernel_stats.csv
+[ -n "$T" ] && python tools/trace_steady.py "$T" $((2 * ${SIMS:-400})) --union k_nn_ --parts 1 > gpurun_out/prof_$TAG/steady_kernel_stats.csv
