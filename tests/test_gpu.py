@@ -241,6 +241,20 @@ def test_search_hash_trees_bitexact(orc, sims, c_puct, compact, parts):
     assert r.stats.sims - r.stats.terminal_leaves <= r.stats.nn_evals <= r.stats.sims
 
 
+def test_search_uneven_parts_compacted_trees_bitexact(orc):
+    """10 games in 4 parts (3 + 3 + 3 + 1 games, each part its own stream, compaction buckets and
+    rows from its first game) with leaf compaction forced: every tree equals the oracle's."""
+    roots = random_positions(orc, 10, seed=515)
+    with Engine(games=len(roots), sims=96, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0, compact=1,
+                parts=4) as e:
+        r = e.search(roots)
+        for g in range(len(roots)):
+            mv, pi, nodes, st = orc.search(orc.search_cfg(sims=96, c_puct=5.0, evaluator=orc.EVAL_HASH), roots[g])
+            _compare_trees(e, g, nodes)
+            assert np.array_equal(r.pi[g].reshape(-1), pi.reshape(-1))
+            assert _mv(r.moves[g]) == _mv(mv)
+
+
 @pytest.mark.parametrize("compact,parts", [(0, 1), (1, 2)])
 @pytest.mark.parametrize("precision", [_abi.FP32, _abi.FP32_SPLIT16])
 def test_search_nn_trees_bitexact_with_gpu_evaluator(orc, precision, compact, parts):
