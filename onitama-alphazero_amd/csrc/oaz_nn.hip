@@ -2135,7 +2135,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nt = C::STG ? wave >> 1 : wave & 3;
     const int b0 = sp.b0;
-    int* pinfo = reinterpret_cast<int*>(lds + h3::kImageB / 4);
+    int* pinfo = reinterpret_cast<int*>(lds + (C::BF ? h3::kPlaneB : h3::kImageB) / 4);
     const int co = nt * 16 + (lane & 15);
     const int i = lane & 15, kq = lane >> 4;
     int eo[2];
@@ -2336,7 +2336,8 @@ template <class C>
 struct H3Fallback {
     static constexpr bool kOn = !C::BF && C::DBG == 0;
     using X = X6Cfg<C::WAVES, C::WAVES == 4 ? 8 : 4, 1, 0, C::WAVES == 4 ? 0 : 1>;
-    static constexpr int kBase = h3::kLdsFloats + (C::TR && !C::BF ? h3::kLutB / 4 : 0);  // + the first-layer LUT
+    // bf16 mode keeps one piece plane (+ the position info): 52 KB, so two 4-wave workgroups share a CU
+    static constexpr int kBase = C::BF ? h3::kPlaneB / 4 + 256 : h3::kLdsFloats + (C::TR ? h3::kLutB / 4 : 0);
     static constexpr int kLds = kOn && x6::kLdsFloats > kBase ? x6::kLdsFloats : kBase;
 };
 
@@ -3097,8 +3098,11 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
         if (w.bf16_v1 == 4) k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 1>>;  // the previous default (runtime parity)
         if (w.bf16_v1 == 5) k = k_nn_q2<X6Cfg<8, 4, 1, 0, 0, 1, 1, 0, 1, 0, 0, 1, 0, 1, 1>>;  // Q2 (2 N-tiles per wave)
         if (w.bf16_v1 == 6) k = k_nn_q2<X6Cfg<8, 6, 1, 0, 0, 1, 1, 0, 1, 0, 0, 1, 0, 1, 1>>;  // Q2, KH 6
+        if (w.bf16_v1 == 7) k = k_nn_h3<X6Cfg<4, 8, 1, 0, 0, 1, 1, 1, 1, 0, 0, 1>>;  // 4 waves, 2 workgroups / CU
+        if (w.bf16_v1 == 8) k = k_nn_h3<X6Cfg<4, 6, 1, 0, 0, 1, 1, 1, 1, 0, 0, 1>>;  // 4 waves, KH 6
 #endif
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value, nullptr,
+        const int bw = w.bf16_v1 == 7 || w.bf16_v1 == 8 ? 4 : 8;
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * bw), 0, st, s, B, w.blob, w.blocks, policy, value, nullptr,
                            nullptr, w.tm);
     } else {
         hipLaunchKernelGGL(k_nn_sq16<false>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
