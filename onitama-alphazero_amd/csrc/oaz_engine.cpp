@@ -621,7 +621,8 @@ struct oaz_engine {
     int cus = 256;                       // compute units of the device (leaf-compaction threshold)
     hipStream_t stream3[kMaxParts - 1] = {nullptr, nullptr, nullptr};  // A/B build (OAZ_SPLIT_HALVES): parts 1..
     hipEvent_t ev_join = nullptr, ev_part[kMaxParts] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_consumed[2] = {nullptr, nullptr};
+    hipEvent_t ev_ready[2] = {nullptr, nullptr};
+    hipEvent_t ev_consumed[2][kMaxParts] = {};  // noise ring slot done with, per game part
     float* noise = nullptr;              // [2][kNoiseChunk][G][kNoiseStride]
     uint32_t G = 0, cap = 0, pathcap = 0, hcap = 0, out_cap = 0;
     int32_t sims_cap = 0;                // cfg.sims at creation: trees and paths are sized for it
@@ -874,7 +875,10 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         }
     for (int i = 0; i < 2; ++i)
         if (hipEventCreateWithFlags(&e->ev_ready[i], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e->ev_consumed[i], hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&e->ev_consumed[i][0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_consumed[i][1], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_consumed[i][2], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_consumed[i][3], hipEventDisableTiming) != hipSuccess) {
             oaz_set_err(OAZ_ERR_HIP, "event create failed");
             return fail();
         }
@@ -926,7 +930,8 @@ extern "C" void oaz_destroy(oaz_engine* e) {
         if (ev) (void)hipEventDestroy(ev);
     for (int i = 0; i < 2; ++i) {
         if (e->ev_ready[i]) (void)hipEventDestroy(e->ev_ready[i]);
-        if (e->ev_consumed[i]) (void)hipEventDestroy(e->ev_consumed[i]);
+        for (auto ev : e->ev_consumed[i])
+            if (ev) (void)hipEventDestroy(ev);
     }
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     for (auto& p : e->pending) {
@@ -1118,8 +1123,14 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
     const bool noise = e->cfg.train_noise && e->noise;
     const size_t slot_elems = (size_t)kNoiseChunk * t.G * kNoiseStride;
     const uint32_t nchunks = (sims + kNoiseChunk - 1) / kNoiseChunk;
+    // The games in nh parts, each on its own stream: one part's tree kernels, leaf compaction and NN
+    // tail run in the gaps of the others' launches (the NN holds a whole CU per workgroup, so the
+    // tree kernels cannot share a CU with it, only fill the CUs it leaves idle). The parts meet only
+    // through the root-noise ring: chunk c + 2 overwrites chunk c's slot once every part is done with it.
+    const int nh = game_parts(e, t.G);
     auto produce = [&](uint32_t c) -> int {
-        if (c >= 2) HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[c & 1], 0));
+        if (c >= 2)
+            for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[c & 1][h], 0));
         e->timing_skip = false;  // every noise launch is timed (once per chunk)
         const uint32_t s0 = c * kNoiseChunk, n = sims - s0 < kNoiseChunk ? sims - s0 : kNoiseChunk;
         float* buf = e->noise + (c & 1) * slot_elems;
@@ -1131,8 +1142,8 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
         return 0;
     };
     if (noise) {
-        HIP_TRY(hipEventRecord(e->ev_consumed[0], e->stream));  // stream2 starts after prior work
-        HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[0], 0));
+        HIP_TRY(hipEventRecord(e->ev_consumed[0][0], e->stream));  // stream2 starts after prior work
+        HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[0][0], 0));
         if (int rc = produce(0)) return rc;
     }
     TreeView tc = t;  // the compaction arrays, or none (rows = game ids)
@@ -1145,10 +1156,6 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
 #else
     constexpr bool fuse = true;
 #endif
-    // The games in nh parts, each on its own stream: one part's tree kernels, leaf compaction and NN
-    // tail run in the gaps of the others' launches (the NN holds a whole CU per workgroup, so the
-    // tree kernels cannot share a CU with it, only fill the CUs it leaves idle).
-    const int nh = game_parts(e, t.G);
     const bool split = nh > 1;
     e->times.parts = (uint64_t)nh;
     const uint32_t Gh = (t.G + (uint32_t)nh - 1) / (uint32_t)nh;
@@ -1212,9 +1219,8 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
                 }
             }
         }
-        if (split)  // every part is done with this noise slot
-            if (int rc = join()) return rc;
-        if (noise) HIP_TRY(hipEventRecord(e->ev_consumed[c & 1], e->stream));
+        if (noise)  // this part is done with the noise slot (no join: a part may run a chunk ahead)
+            for (int h = 0; h < nh; ++h) HIP_TRY(hipEventRecord(e->ev_consumed[c & 1][h], sh[h]));
     }
     e->timing_skip = false;
     for (int h = 0; h < nh; ++h) {
