@@ -119,7 +119,11 @@ def pmc_traffic(args, cfg):
                    "--sims", str(cfg["sims"]), "--fp32-kernel", args.fp32_kernel]
             try:
                 subprocess.run(cmd, timeout=600, capture_output=True, check=True)
-            except (subprocess.SubprocessError, OSError):
+            except (subprocess.SubprocessError, OSError) as exc:
+                tail = getattr(exc, "stderr", None) or b""
+                tail = tail.decode(errors="replace") if isinstance(tail, bytes) else str(tail)
+                print(f"bench: PMC pass {ctr} failed ({type(exc).__name__}); child stderr:\n{tail[-6000:]}",
+                      file=sys.stderr)
                 return None
             rows = {"nn": [], "backup_select": []}
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -131,6 +135,7 @@ def pmc_traffic(args, cfg):
                     if k:
                         rows[k].append((int(r.get("Dispatch_Id", 0) or 0), float(r["Counter_Value"])))
             if not rows["nn"]:
+                print(f"bench: PMC pass {ctr} collected no k_nn_ rows", file=sys.stderr)
                 return None
             for k, v in rows.items():  # the last ply's launches only (also if the range was not applied)
                 v.sort()
