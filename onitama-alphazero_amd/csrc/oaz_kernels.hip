@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(kCompactThreads) k_eval_compact(TreeView t) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) ls[k] = load_state(&t.leaf_state[g0 + k < t.G ? g0 + k : t.G - 1]);
     uint32_t f = 0;  // need flags of the 4 games, one byte each
-    if (g0 + 4 <= t.G) {
+    if (g0 + 4 <= t.G && (reinterpret_cast<uintptr_t>(t.need + g0) & 3) == 0) {  // (a part may start unaligned)
         f = *reinterpret_cast<const uint32_t*>(t.need + g0);
     } else {
 #pragma unroll
