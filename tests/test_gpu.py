@@ -241,12 +241,14 @@ def test_search_hash_trees_bitexact(orc, sims, c_puct, compact, parts):
     assert r.stats.sims - r.stats.terminal_leaves <= r.stats.nn_evals <= r.stats.sims
 
 
-def test_search_uneven_parts_compacted_trees_bitexact(orc):
-    """10 games in 4 parts (3 + 3 + 3 + 1 games, each part its own stream, compaction buckets and
-    rows from its first game) with leaf compaction forced: every tree equals the oracle's."""
-    roots = random_positions(orc, 10, seed=515)
+@pytest.mark.parametrize("games,parts", [(10, 4), (26, 2)])
+def test_search_uneven_parts_compacted_trees_bitexact(orc, games, parts):
+    """Games in uneven parts (10 in 4: 3 + 3 + 3 + 1; 26 in 2: the second part starts at game 13, an
+    unaligned offset), each part on its own stream with its own compaction buckets and rows, leaf
+    compaction forced: every tree equals the oracle's."""
+    roots = random_positions(orc, games, seed=515)
     with Engine(games=len(roots), sims=96, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0, compact=1,
-                parts=4) as e:
+                parts=parts) as e:
         r = e.search(roots)
         for g in range(len(roots)):
             mv, pi, nodes, st = orc.search(orc.search_cfg(sims=96, c_puct=5.0, evaluator=orc.EVAL_HASH), roots[g])
