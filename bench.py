@@ -516,7 +516,7 @@ def single_stream_leg(args, cfg, device, precision):
     with Engine(device=device, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0,
                 train_noise=0 if args.no_noise else 1, max_plies=150, evaluator=_abi.EVAL_NN,
                 precision=getattr(_abi, PREC_ABI[precision]), fixed_deck=cfg["fixed_deck"], deck=[0, 1, 2, 3, 4],
-                seed=20260101, sample_capacity=cfg["games"] * 8, parts=1) as e:
+                seed=20260101, sample_capacity=cfg["games"] * 8, parts=1, compact=0) as e:
         e.load_weights(random_weights(0, cfg["blocks"]))
         e.selfplay_reset()
         e.selfplay_step(2)
@@ -538,6 +538,41 @@ def single_stream_leg(args, cfg, device, precision):
                               / 1e12 if nn["avg_launch_ms"] > 0 else 0.0)
     nn.update(sims_per_s=sims / dt, ms_per_step=1e3 * dt / 2, launches=kt.nn_n)
     return nn
+
+
+def compaction_leg(args, cfg, device, stagger):
+    """The headline workload with leaf compaction on (oaz_config.compact = 2): the leaves whose
+    evaluation the reference computes and discards (a won, terminal-flagged leaf: no expansion, the
+    reward is backed up, mcts_arena.rs:156-176) do not go to the network. The trees, pi and samples
+    are those of the headline run; the headline itself keeps one NN evaluation per playout (the
+    metric's unit of work). Same warm-up and staggered starts, 2 timed plies."""
+    from onitama_az import _abi
+    from onitama_az.engine import Engine
+    from onitama_az.weights import random_weights
+    with Engine(device=device, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0,
+                train_noise=0 if args.no_noise else 1, max_plies=150, evaluator=_abi.EVAL_NN,
+                precision=getattr(_abi, PREC_ABI[cfg["precision"]]), fixed_deck=cfg["fixed_deck"],
+                deck=[0, 1, 2, 3, 4], seed=20260101, sample_capacity=cfg["games"] * (args.warmup + 4),
+                stagger=stagger, compact=2) as e:
+        e.load_weights(random_weights(0, cfg["blocks"]))
+        e.selfplay_reset()
+        e.selfplay_step(args.warmup)
+        e.sync()
+        st0 = e.selfplay_stats()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e.selfplay_step(2)
+        e.sync()
+        dt = time.perf_counter() - t0
+        st1 = e.selfplay_stats()
+        kt = e.kernel_times()
+    sims = st1.search.sims - st0.search.sims
+    evals = st1.search.nn_evals - st0.search.nn_evals
+    return {"value": sims / dt, "unit": "sims/s", "ms_per_step": 1e3 * dt / 2, "steps": 2, "warmup": args.warmup,
+            "nn_positions_per_sim": evals / max(1, sims), "game_parts": kt.parts,
+            "note": "oaz_config.compact = 2: a won, terminal-flagged leaf's evaluation (computed and discarded by "
+                    "the reference) is not sent to the network; identical trees / pi / samples (GPU parity tests "
+                    "run both settings); not the headline, whose unit of work includes every leaf evaluation"}
 
 
 def exact_fp32_leg(args, cfg, device):
@@ -595,7 +630,8 @@ def main():
                  fixed_deck=cfg["fixed_deck"],
                  deck=[0, 1, 2, 3, 4], seed=20260101, rank=rank, world=world,
                  # every sample of every game that can finish in warmup + steps plies fits (checked below)
-                 sample_capacity=cfg["games"] * (max(args.warmup, args.pmc_plies) + args.steps + 2), stagger=stagger)
+                 sample_capacity=cfg["games"] * (max(args.warmup, args.pmc_plies) + args.steps + 2), stagger=stagger,
+                 compact=0)  # every playout evaluates its leaf: the metric's unit of work
     eng.load_weights(random_weights(0, cfg["blocks"]))  # random-init weights (seed 0), SURVEY.md 8d
     eng.selfplay_reset()
     if args.pmc_child:  # profiled pass: the warm-up plies (not collected), then one collected ply
@@ -702,12 +738,10 @@ def main():
             "true_expansions_per_s": exp_all / T, "mean_select_depth": depth, "mean_branching": branching,
             "nn_positions_per_sim": positions * args.steps * sims_steps / max(1, sims),
             "game_parts": parts,
-            "leaf_compaction": not kt.nn_samples,
-            "nn_evaluation": "every simulation's leaf is evaluated except a won, terminal-flagged leaf, whose evaluation "
-                             "the reference computes and discards (mcts_arena.rs:156-176: no expansion, the reward is "
-                             "backed up); select marks those leaves and, when that saves NN workgroup rounds (games >= "
-                             "12 x 16 x CUs: leaf_compaction), k_eval_compact packs the others per 4096-game bucket; "
-                             "the trees are unchanged and the network runs on nn_positions_per_sim of the leaves",
+            "nn_leaf_evaluations": "every playout" if kt.nn_samples else "compacted",
+            "nn_evaluation": "one NN evaluation per simulation, terminal leaves included (Q2, the metric's unit of "
+                             "work: SURVEY 8d); the leaf_compaction block measures the same workload with the "
+                             "evaluations the reference discards left out (oaz_config.compact)",
             "kernel_ms_per_step": {
                 "backup_select_fused": kt.backup_select_ms / max(1, kt.backup_select_n) * (sims_steps - 1),
                 "select_first": kt.select_ms / max(1, kt.select_n) if kt.select_n else None,
@@ -753,6 +787,8 @@ def main():
                           "fp32_split": "BF16 dense MFMA peak / 6 products per fp32 MAC",
                           "fp32_split16": "FP16 dense MFMA peak / 3 products per fp32 MAC"}[cfg["precision"]],
             "frac_of_fp32_mfma_peak": leg["achieved"] / PEAK_TFLOPS["fp32"]}
+        if world == 1 and not args.no_exact:
+            out["leaf_compaction"] = compaction_leg(args, cfg, local, stagger)
         if not args.no_exact and world == 1 and cfg["precision"] in ("fp32_split16", "fp32_split"):
             out["exact_fp32"] = exact_fp32_leg(args, cfg, local)
         if not args.no_cpu_baseline and world == 1:

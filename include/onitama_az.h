@@ -155,9 +155,11 @@ typedef struct oaz_config {
     int32_t sample_capacity; /* max samples buffered on the device (0: auto) */
     int32_t stagger;         /* self-play: slot g starts playing after g % stagger plies (steady-state
                                 game ages for throughput measurement); 0 = all slots start at once */
-    int32_t compact;         /* leaf compaction (only the leaves whose evaluation the playout uses go to
-                                the evaluator, Q2): 0 = when it saves NN rounds (games >= 12 * 16 * CUs),
-                                1 = always, -1 = never; results are identical either way */
+    int32_t compact;         /* leaf compaction: only the leaves whose evaluation the playout uses go to
+                                the evaluator (a won, terminal-flagged leaf's is computed and discarded by
+                                the reference, Q2). 0 = off: every playout evaluates its leaf, as the
+                                reference (default); 1 = always; 2 = when it saves NN workgroup rounds
+                                (games >= 12 * 16 * CUs). Trees, pi and samples are identical either way */
     int32_t parts;           /* the simulation loop runs the games in this many parts (1, 2 or 4), each
                                 on its own stream so one part's tree kernels fill the others' NN gaps;
                                 0 = auto (2 from 2048 games); results are identical either way */

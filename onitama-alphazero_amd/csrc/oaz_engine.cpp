@@ -823,7 +823,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         return nullptr;
     }
     if (cfg->blocks < 0 || cfg->blocks > 64 || cfg->sims < 1 || cfg->sims > 65535 || cfg->games < 1 ||
-        cfg->max_plies < 0 || cfg->max_plies > 100000 || cfg->compact < -1 || cfg->compact > 1 ||
+        cfg->max_plies < 0 || cfg->max_plies > 100000 || cfg->compact < 0 || cfg->compact > 2 ||
         (cfg->parts != 0 && cfg->parts != 1 && cfg->parts != 2 && cfg->parts != 4)) {
         oaz_set_err(OAZ_ERR_ARG, "create: config out of range");
         return nullptr;
@@ -1078,12 +1078,13 @@ extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* p
     return 0;
 }
 
-// Leaf compaction pays when it can remove whole rounds of NN workgroups (one 16-position tile per
+// Leaf compaction (oaz_config.compact; off by default: every playout evaluates its leaf, Q2) pays
+// when it can remove whole rounds of NN workgroups (one 16-position tile per
 // CU at a time): at C3 the ~8.7 % won leaves are 1.4 of 16 rounds. Below 12 rounds (G < 12 * 16 *
 // CUs, e.g. C2's 4096 games = one round) it would only add its own launch, so the leaves are then
 // evaluated in place. Also off for the A/B-only NN variants without tile maps.
 static bool compact_leaves(const oaz_engine* e, uint32_t G) {
-    if (e->cfg.compact < 0 || (e->cfg.compact == 0 && G < 12u * 16u * (uint32_t)e->cus)) return false;
+    if (e->cfg.compact == 0 || (e->cfg.compact == 2 && G < 12u * 16u * (uint32_t)e->cus)) return false;
 #if OAZ_AB
     if (e->cfg.evaluator == OAZ_EVAL_NN) {
         const char* xv = getenv("OAZ_NN_X6_V");

@@ -218,7 +218,7 @@ def _compare_trees(e, g, nodes_ref):
         assert np.array_equal(a, b), f
 
 
-# compact 0: 12 games evaluate in place, 1: leaf compaction forced; parts: the games on 1 or 2 streams
+# compact 0: every leaf evaluated in place (default), 1: leaf compaction; parts: the games on 1 or 2 streams
 @pytest.mark.parametrize("compact,parts", [(0, 1), (1, 1), (0, 2), (1, 2)])
 @pytest.mark.parametrize("sims,c_puct", [(64, 5.0), (200, 2.0)])
 def test_search_hash_trees_bitexact(orc, sims, c_puct, compact, parts):

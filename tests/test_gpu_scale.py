@@ -115,7 +115,9 @@ def test_c3_search_every_game_vs_oracle(orc):
     node, and the run's statistics are consistent (sims, tree capacity)."""
     G, sims = 65536, 400
     roots = gpu_random_positions(G, seed=303)
-    with Engine(games=G, sims=sims, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=SEED) as e:
+    # leaf compaction on (compact=2: at 65 536 games it removes NN rounds), the C5 test runs it off
+    with Engine(games=G, sims=sims, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=SEED,
+                compact=2) as e:
         r = e.search(roots)
         assert r.stats.sims == sims * G
         assert r.stats.max_nodes <= 1 + 40 * sims

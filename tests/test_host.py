@@ -153,9 +153,9 @@ def test_root_noise_host_matches_oracle_and_distribution():
         assert abs(xs.var() / var - 1.0) < 0.2, (K, xs.var(), var)
 
 
-@pytest.mark.parametrize("kw", [dict(compact=2), dict(compact=-2), dict(parts=3), dict(parts=-1)])
+@pytest.mark.parametrize("kw", [dict(compact=3), dict(compact=-1), dict(parts=3), dict(parts=-1)])
 def test_config_compact_and_parts_out_of_range_are_errors(kw):
-    """oaz_config.compact is -1, 0 or 1 and parts 0, 1, 2 or 4; anything else fails oaz_create
+    """oaz_config.compact is 0, 1 or 2 and parts 0, 1, 2 or 4; anything else fails oaz_create
     before any device work."""
     from onitama_az.engine import Engine
     with pytest.raises(_abi.OazError, match="config out of range"):
