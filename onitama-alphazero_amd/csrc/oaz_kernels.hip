@@ -772,23 +772,42 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
     if (active && active[g] != 1) return;  // uniform over the segment
     oaz_node* T = t.nodes + (size_t)g * t.cap;
     const uint32_t* path = t.path + (size_t)g * t.pathcap;
+    // Two dependent round trips: (1) the leaf record, this lane's first path entry and the node
+    // count; (2) the leaf node, its policy row and value (read whether or not the playout uses them:
+    // the rows are always in bounds) and N / W of this lane's path node. Everything after is stores.
     const oaz_state s = load_state(&t.leaf_state[g]);
     const uint32_t leaf = t.leaf[g], depth = t.depth[g];
-    const uint32_t row = t.slot ? t.slot[g] : g;  // the leaf's evaluation (read only if it was made)
+    const uint32_t row = t.slot ? t.slot[g] : g;  // the leaf's evaluation row
+    const uint32_t pn = (uint32_t)sl < t.pathcap ? path[sl] : 0u;
+    const uint32_t nn0 = t.n_nodes[g];
     const NodeRegs nd = load_node(&T[leaf]);
     uint64_t* st = t.stats + (size_t)g * GS_COUNT;
     const float* pol = policy + (size_t)row * 50;
+    float polr[4];  // lane sl: policy entries sl, 16+sl, 32+sl, 48+sl
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int idx = 16 * c + sl;
+        polr[c] = idx < 50 ? pol[idx] : 0.0f;
+    }
+    const float vrow = value[row];
+    const uint32_t plen = depth < t.pathcap ? depth : t.pathcap - 1;
+    const bool mine = (uint32_t)sl <= plen;  // this lane backs up path node sl
+    uint32_t pN = 0;
+    double pW = 0.0;
+    if (mine) {
+        pN = T[pn].N;
+        pW = T[pn].W;
+    }
+    asm volatile("" ::"v"(polr[0]), "v"(polr[1]), "v"(polr[2]), "v"(polr[3]), "v"(vrow));  // issued in trip 2
 
     if (!(node_flags(nd.misc) & 3)) {
-        // the leaf's 50 policy values in one round trip (lane sl: entries sl, 16+sl, 32+sl, 48+sl),
-        // kept in registers for the renormalisation sums and in LDS for the children's priors
+        // the policy row kept in registers for the renormalisation sums and in LDS for the
+        // children's priors
         __shared__ float spol[kWavesPerBlock * 4][52];
         float* sp = spol[(threadIdx.x >> 4) & 15];
-        float polr[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const int idx = 16 * c + sl;
-            polr[c] = idx < 50 ? pol[idx] : 0.0f;
             if (idx < 50) sp[idx] = polr[c];
         }
         const int color = s.to_move & 1;
@@ -812,7 +831,7 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
         // leaves a non-negative sum unchanged bit for bit (the old loop loaded and waited 50 times).
         double sum0 = 0.0, sum1 = 0.0;
         policy_sums(polr, row0, row1, sum0, sum1, std::make_integer_sequence<int, 25>{});
-        const uint32_t base = t.n_nodes[g];
+        const uint32_t base = nn0;
         uint32_t o = incl - cnt;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -848,10 +867,14 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
         r = reward(res, pc);
         if (sl == 0) st[GS_TERMINAL] += 1;
     } else {
-        r = (double)value[row];
+        r = (double)vrow;
     }
-    const uint32_t plen = depth < t.pathcap ? depth : t.pathcap - 1;
-    for (uint32_t k = (uint32_t)sl; k <= plen; k += kSegLanes) {
+    if (mine) {
+        const double rk = ((depth - (uint32_t)sl) & 1) ? -r : r;
+        T[pn].N = pN + 1;
+        T[pn].W = pW + rk;
+    }
+    for (uint32_t k = (uint32_t)sl + kSegLanes; k <= plen; k += kSegLanes) {  // paths deeper than 16
         const uint32_t n = path[k];
         const double rk = ((depth - k) & 1) ? -r : r;
         T[n].N += 1;
