@@ -619,7 +619,7 @@ struct oaz_engine {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;       // root-noise producer, overlaps the NN kernel
     int cus = 256;                       // compute units of the device (leaf-compaction threshold)
-    hipStream_t stream3[kMaxParts - 1] = {nullptr, nullptr, nullptr};  // A/B build (OAZ_SPLIT_HALVES): parts 1..
+    hipStream_t stream3[kMaxParts - 1] = {nullptr, nullptr, nullptr};  // the streams of game parts 1.. (oaz_config.parts)
     hipEvent_t ev_join = nullptr, ev_part[kMaxParts] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t ev_ready[2] = {nullptr, nullptr};
     hipEvent_t ev_consumed[2][kMaxParts] = {};  // noise ring slot done with, per game part
