@@ -105,9 +105,11 @@ def pmc_traffic(args, cfg):
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None
-    plies = args.warmup
     parts = sim_parts(cfg["games"])  # launches of each kernel per simulation step
     per_ply = cfg["sims"] * parts
+    # the profiled ply follows the bench's warm-up plies, but its first kernel index stays below
+    # ~11 200 (C5's 14 x 1 600 launches made the rocprofv3 counter child crash on the host)
+    plies = min(args.warmup, max(1, 11200 // per_ply))
     first, last = plies * per_ply + 1, (plies + 1) * per_ply  # 1-based launch index of each kernel
     kb, tree_kb, counts = {}, {"backup_select": {}}, {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
