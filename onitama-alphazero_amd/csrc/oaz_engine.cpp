@@ -743,7 +743,10 @@ static hipEvent_t ev_get(oaz_engine* e) {
 }
 
 // Run a launch, bracketed by events on the engine stream when timing is on.
-static constexpr uint32_t kNoiseChunk = 8;  // simulations of root noise produced per launch
+#ifndef OAZ_NOISE_CHUNK  // 50 / 400 measured within noise of 8 at C3 and C2 (DESIGN.md perf log)
+#define OAZ_NOISE_CHUNK 8
+#endif
+static constexpr uint32_t kNoiseChunk = OAZ_NOISE_CHUNK;  // simulations of root noise produced per launch
 
 static void accumulate(oaz_engine* e, const TimedLaunch& p, float ms) {
     double* acc[7] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms,
