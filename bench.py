@@ -695,14 +695,22 @@ def main():
     allgather = None
     if not args.no_allgather:  # C4: RCCL all-gather of (s, pi, z) after the timed region
         from onitama_az.dist import Comm, allgather_samples
-        with _StdoutToStderr():
-            comm = None if rehearse else Comm.create(rank, world, local)
-            t1 = time.perf_counter()
-            got = allgather_samples(eng, world, torch.device("cuda", local), comm=comm)
-            torch.cuda.synchronize()
-        allgather = {"samples_total": int(len(got)), "bytes_per_sample": 228, "seconds": time.perf_counter() - t1,
-                     "backend": "gloo (rehearsal, host copies)" if rehearse else
-                                "oaz_allgather_samples (C ABI: RCCL counts all-gather + grouped broadcasts)"}
+        comm = None
+        # after the timed region: an exchange error is reported in the line (and on stderr) instead
+        # of losing the measured throughput with it
+        try:
+            with _StdoutToStderr():
+                comm = None if rehearse else Comm.create(rank, world, local)
+                t1 = time.perf_counter()
+                got = allgather_samples(eng, world, torch.device("cuda", local), comm=comm)
+                torch.cuda.synchronize()
+            allgather = {"samples_total": int(len(got)), "bytes_per_sample": 228,
+                         "seconds": time.perf_counter() - t1,
+                         "backend": "gloo (rehearsal, host copies)" if rehearse else
+                                    "oaz_allgather_samples (C ABI: RCCL counts all-gather + grouped broadcasts)"}
+        except Exception as ex:  # noqa: BLE001
+            print(f"bench: sample all-gather failed on rank {rank}: {ex!r}", file=sys.stderr, flush=True)
+            allgather = {"error": repr(ex)}
         if comm is not None:
             comm.close()
 
