@@ -5,7 +5,8 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
 TAG=${TAG:-prof}
 mkdir -p gpurun_out/prof_$TAG
 PY=$(command -v python3)  # absolute path after `--` (rocprofv3 must not exec a PATH lookup)
-step() { local name=$1; shift; echo "== $name"; "$@"; local rc=$?; echo "$name rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
+exec 3>&1  # step messages go to the script's stdout, not into a step's redirected output file
+step() { local name=$1; shift; echo "== $name" >&3; "$@"; local rc=$?; echo "$name rc=$rc" >&3; if [ $rc -ne 0 ]; then exit $rc; fi; }
 step bench timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 tail -1 gpurun_out/bench_$TAG.json | cut -c1-600
 step trace timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG/trace -o run -- "$PY" bench.py --steps 2 --no-cpu-baseline --no-allgather --no-pmc --no-exact ${PROF_ARGS:-} > gpurun_out/prof_$TAG/trace.log 2>&1
