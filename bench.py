@@ -85,6 +85,7 @@ def parse():
     ap.add_argument("--no-noise", action="store_true", help=argparse.SUPPRESS)  # experiments only: not C3
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-plies", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-parts", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--mode", default="selfplay", choices=["selfplay", "train", "pure_mcts"],
                     help="train: SGD steps of the training loop (SURVEY 8f #2), not the headline metric")
     ap.add_argument("--train-blocks", type=int, default=5, help="train mode: residual blocks (bin/train.rs:60)")
@@ -110,6 +111,9 @@ def pmc_traffic(args, cfg):
     # the profiled ply follows the bench's warm-up plies, but its first kernel index stays below
     # ~11 200 (C5's 14 x 1 600 launches made the rocprofv3 counter child crash on the host)
     plies = min(args.warmup, max(1, 11200 // per_ply))
+    # with fewer warm-up plies than the timed region follows, the staggered starts are compressed to
+    # them (every slot playing, game ages spread over `plies` plies) so the profiled ply is steady state
+    stagger = min(args.stagger, plies) if args.stagger > 1 else 0
     first, last = plies * per_ply + 1, (plies + 1) * per_ply  # 1-based launch index of each kernel
     kb, tree_kb, counts = {}, {"backup_select": {}}, {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -117,7 +121,7 @@ def pmc_traffic(args, cfg):
             cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "k_nn_|k_backup_select",
                    "--kernel-iteration-range", f"[{first}-{last}]", "--output-format", "csv", "-d", d, "-o", "pmc",
                    "--", sys.executable, str(Path(__file__).resolve()), "--pmc-child", "--pmc-plies", str(plies),
-                   "--stagger", str(args.stagger), "--warmup", str(args.warmup), "--config", args.config, "--games", str(cfg["games"]),
+                   "--stagger", str(stagger), "--warmup", str(plies), "--config", args.config, "--games", str(cfg["games"]),
                    "--sims", str(cfg["sims"]), "--fp32-kernel", args.fp32_kernel]
             try:
                 subprocess.run(cmd, timeout=600, capture_output=True, check=True)
@@ -157,11 +161,63 @@ def pmc_traffic(args, cfg):
     return {"bytes_per_sim_step": fetch + write, "fetch_bytes": fetch, "write_bytes": write, "game_parts": parts,
             "raw_kb": kb, "tree_pmc": tree, "launches_profiled": counts,
             "note": f"rocprofv3 --pmc, separate passes, on the {cfg['sims']} simulation steps of ply {plies + 1} "
-                    f"(after {plies} warm-up plies, stagger {args.stagger}); FETCH_SIZE x2 (gfx950 wide-read "
+                    f"(after {plies} warm-up plies, stagger {stagger}); FETCH_SIZE x2 (gfx950 wide-read "
                     "correction)"}
 
 
+def pmc_clock(args, cfg):
+    """The clock the NN kernel runs at, and its rocprofv3 kernel-trace duration on this box: one child
+    pass `rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace` over the k_nn_ launches of one ply on ONE
+    stream (oaz_config.parts = 1, the single-stream leg's shape) after 2 unprofiled warm-up plies.
+    GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md 'DVFS give-back'): cycles per launch
+    = GRBM_GUI_ACTIVE / 8, clock of a profiled launch = cycles / its traced duration. Cycles barely
+    depend on the clock for an MFMA-bound kernel, so cycles / the un-profiled HIP-event launch time of
+    the single-stream leg is the clock of the measured launches (bench main). Runs before this
+    process touches the GPU."""
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    per_ply, plies = cfg["sims"], 2
+    first, last = plies * per_ply + 1, (plies + 1) * per_ply
+    with tempfile.TemporaryDirectory() as d:
+        cmd = [prof, "--pmc", "GRBM_GUI_ACTIVE", "--kernel-trace", "--kernel-include-regex", "k_nn_",
+               "--kernel-iteration-range", f"[{first}-{last}]", "--output-format", "csv", "-d", d, "-o", "clk",
+               "--", sys.executable, str(Path(__file__).resolve()), "--pmc-child", "--pmc-plies", str(plies),
+               "--pmc-parts", "1", "--stagger", "0", "--warmup", str(plies), "--config", args.config, "--games",
+               str(cfg["games"]), "--sims", str(cfg["sims"]), "--fp32-kernel", args.fp32_kernel]
+        try:
+            subprocess.run(cmd, timeout=600, capture_output=True, check=True)
+        except (subprocess.SubprocessError, OSError) as exc:
+            tail = getattr(exc, "stderr", None) or b""
+            tail = tail.decode(errors="replace") if isinstance(tail, bytes) else str(tail)
+            print(f"bench: PMC clock pass failed ({type(exc).__name__}); child stderr:\n{tail[-4000:]}",
+                  file=sys.stderr)
+            return None
+        grbm, dur = {}, {}
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and "k_nn_" in r["Kernel_Name"]:
+                    grbm[int(r["Dispatch_Id"])] = grbm.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+        for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if "k_nn_" in r["Kernel_Name"]:
+                    dur[int(r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    ids = sorted(set(grbm) & set(dur))[-per_ply:]
+    if not ids:
+        print("bench: PMC clock pass collected no k_nn_ rows", file=sys.stderr)
+        return None
+    cyc = sorted(grbm[i] / 8.0 for i in ids)
+    clk = sorted(grbm[i] / 8.0 / dur[i] / 1e6 for i in ids if dur[i] > 0)
+    ms = [dur[i] * 1e3 for i in ids]
+    return {"cycles_per_launch": cyc[len(cyc) // 2], "profiled_clock_mhz": clk[len(clk) // 2],
+            "profiled_avg_launch_ms": sum(ms) / len(ms), "launches": len(ids),
+            "note": f"rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace, one stream, the {len(ids)} k_nn_ launches of "
+                    f"ply {plies + 1} (median per launch; GRBM_GUI_ACTIVE / 8 XCDs = cycles)"}
+
+
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+NOMINAL_MHZ = 2400.0  # MI355X_MICROARCH.md: max engine clock (the MFMA peaks are quoted at it)
+XGMI_LINK_GBPS = 153.0  # per direction per link (7 links per GPU), the all-gather's reference rate
 
 
 class _StdoutToStderr:
@@ -621,9 +677,10 @@ def main():
         cfg["sims"] = args.sims
     # staggered starts must be over before the timed region (every slot playing)
     stagger = min(args.stagger, args.warmup) if args.stagger > 1 else 0
-    traffic = None
+    traffic = clock = None
     if not args.pmc_child and not args.no_pmc and world == 1:
         traffic = pmc_traffic(args, cfg)  # child processes; this process has not touched the GPU yet
+        clock = pmc_clock(args, cfg)
     eng = Engine(device=local, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0,
                  train_noise=0 if args.no_noise else 1,
                  max_plies=150, evaluator=_abi.EVAL_NN,
@@ -633,7 +690,8 @@ def main():
                  deck=[0, 1, 2, 3, 4], seed=20260101, rank=rank, world=world,
                  # every sample of every game that can finish in warmup + steps plies fits (checked below)
                  sample_capacity=cfg["games"] * (max(args.warmup, args.pmc_plies) + args.steps + 2), stagger=stagger,
-                 compact=0)  # every playout evaluates its leaf: the metric's unit of work
+                 compact=0,  # every playout evaluates its leaf: the metric's unit of work
+                 parts=args.pmc_parts if args.pmc_child else 0)
     eng.load_weights(random_weights(0, cfg["blocks"]))  # random-init weights (seed 0), SURVEY.md 8d
     eng.selfplay_reset()
     if args.pmc_child:  # profiled pass: the warm-up plies (not collected), then one collected ply
@@ -692,27 +750,66 @@ def main():
               "nn_fp16_range_fallback_tiles": int(fallbacks_all),
               "ok": bool(dropped_all == 0 and max_nodes_all <= cap_nodes and sims_all > 0)}
 
+    # per-rank view of the timed region for the line: every rank's simulations and time (rank order)
+    per_rank = torch.tensor([float(st1.search.sims - st0.search.sims), elapsed], dtype=torch.float64, device=cdev)
+    if world > 1:
+        gathered = [torch.zeros_like(per_rank) for _ in range(world)]
+        dist.all_gather(gathered, per_rank)
+    else:
+        gathered = [per_rank]
+    rank_sims = [float(t[0]) for t in gathered]
+    rank_s = [float(t[1]) for t in gathered]
+
     allgather = None
     if not args.no_allgather:  # C4: RCCL all-gather of (s, pi, z) after the timed region
-        from onitama_az.dist import Comm, allgather_samples
+        from onitama_az.dist import Comm, allgather_sample_bytes, allgather_samples_device
         comm = None
         # after the timed region: an exchange error is reported in the line (and on stderr) instead
         # of losing the measured throughput with it
         try:
-            with _StdoutToStderr():
-                comm = None if rehearse else Comm.create(rank, world, local)
+            if rehearse:  # gloo over host copies (one-GPU rehearsal of the multi-rank script)
                 t1 = time.perf_counter()
-                got = allgather_samples(eng, world, torch.device("cuda", local), comm=comm)
-                torch.cuda.synchronize()
-            allgather = {"samples_total": int(len(got)), "bytes_per_sample": 228,
-                         "seconds": time.perf_counter() - t1,
-                         "backend": "gloo (rehearsal, host copies)" if rehearse else
-                                    "oaz_allgather_samples (C ABI: RCCL counts all-gather + grouped broadcasts)"}
+                mine = eng.samples_fetch(int(eng.selfplay_stats().samples_ready))
+                own = len(mine)
+                raw = allgather_sample_bytes(torch.from_numpy(mine.view("uint8").copy()), world)
+                total, counts = raw.numel() // 228, None
+                allgather = {"backend": "gloo (rehearsal, host copies)", "seconds": time.perf_counter() - t1}
+            else:
+                with _StdoutToStderr():
+                    comm = Comm.create(rank, world, local)
+                    raw, total, counts = allgather_samples_device(eng, world, torch.device("cuda", local), comm)
+                    torch.cuda.synchronize()
+                cs = comm.stats()
+                own = int(cs.own_records)
+                recv = (total - own) * 228  # bytes this rank received over the links
+                allgather = {"backend": "oaz_allgather_samples (C ABI: RCCL counts all-gather + grouped broadcasts)",
+                             "rccl_ranks": int(cs.ranks), "counts": counts, "collective_ms": cs.allgather_ms,
+                             "counts_ms": cs.counts_ms, "bytes_received": recv,
+                             "GBps_received": recv / (cs.allgather_ms * 1e-3) / 1e9 if cs.allgather_ms > 0 else None,
+                             "xgmi_note": f"xGMI: {XGMI_LINK_GBPS:.0f} GB/s per link and direction, 7 links per GPU; "
+                                          "collective_ms = HIP events on the communicator stream around the grouped "
+                                          "broadcasts only (no host copies)"}
+            # every rank: the gathered total is the sum of the ranks' own contributions
+            chk = torch.tensor([float(own), float(total)], dtype=torch.float64, device=cdev)
+            if world > 1:
+                dist.all_reduce(chk[:1])
+            ok = int(chk[0].item()) == total and (counts is None or sum(counts) == total)
+            if world > 1:
+                okt = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=cdev)
+                dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+                ok = bool(okt.item() == 1.0)
+            allgather.update(samples_total=int(total), bytes_per_sample=228, totals_consistent=ok)
+            if not ok:
+                print(f"bench: all-gather totals inconsistent on rank {rank}", file=sys.stderr, flush=True)
         except Exception as ex:  # noqa: BLE001
             print(f"bench: sample all-gather failed on rank {rank}: {ex!r}", file=sys.stderr, flush=True)
             allgather = {"error": repr(ex)}
         if comm is not None:
             comm.close()
+        if world > 1 and allgather is not None and "collective_ms" in allgather:
+            ms = torch.tensor([allgather["collective_ms"]], dtype=torch.float64, device=cdev)
+            dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+            allgather["collective_ms_max_over_ranks"] = float(ms.item())
 
     if rank == 0:
         sims_steps = cfg["sims"]  # simulation steps (select -> NN -> expand launches) per bench step
@@ -772,6 +869,9 @@ def main():
             "tree_kernels": tree_roofline(kt, sims, args.steps * sims_steps, expansions, depth, branching, cfg,
                                           traffic.get("tree_pmc") if traffic else None),
             "allgather": allgather,
+            "ranks": {"world": world, "sims_per_rank": rank_sims, "seconds_per_rank": rank_s,
+                      "min_rank_s": min(rank_s), "max_rank_s": max(rank_s),
+                      "note": "value = all ranks' simulations / the max rank time (barrier + synchronize on both sides)"},
             "checks": checks,
         }
     eng.close()
@@ -797,12 +897,28 @@ def main():
                           "fp32_split": "BF16 dense MFMA peak / 6 products per fp32 MAC",
                           "fp32_split16": "FP16 dense MFMA peak / 3 products per fp32 MAC"}[cfg["precision"]],
             "frac_of_fp32_mfma_peak": leg["achieved"] / PEAK_TFLOPS["fp32"]}
+        if clock:
+            # the clock of the measured launches: the kernel's cycles per launch (PMC pass) over the
+            # un-profiled HIP-event launch time above; the peak scaled to that clock (2400 MHz nominal)
+            mhz = clock["cycles_per_launch"] / (leg["avg_launch_ms"] * 1e-3) / 1e6
+            out["roofline"].update(
+                sclk_mhz=mhz, peak_at_measured_clock=PEAK_TFLOPS[cfg["precision"]] * mhz / NOMINAL_MHZ,
+                frac_at_measured_clock=out["roofline"]["frac"] * NOMINAL_MHZ / mhz,
+                frac_nonzero_at_measured_clock=out["roofline"]["frac_nonzero"] * NOMINAL_MHZ / mhz,
+                rocprof_avg_launch_ms=clock["profiled_avg_launch_ms"], clock_detail=clock,
+                clock_note="sclk = GRBM_GUI_ACTIVE/8 cycles per k_nn_ launch (rocprofv3 pass on this box, one stream) "
+                           "/ the HIP-event launch time above; rocprof_avg_launch_ms = the same pass's kernel-trace "
+                           "duration of those launches (profiled launches run at profiled_clock_mhz)")
         if world == 1 and not args.no_exact:
             out["leaf_compaction"] = compaction_leg(args, cfg, local, stagger)
         if not args.no_exact and world == 1 and cfg["precision"] in ("fp32_split16", "fp32_split"):
             out["exact_fp32"] = exact_fp32_leg(args, cfg, local)
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads)
+            try:  # after the timed region: a baseline failure must not lose the measured line
+                out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads)
+            except Exception as ex:  # noqa: BLE001
+                print(f"bench: cpu_baseline failed: {ex!r}", file=sys.stderr, flush=True)
+                out["cpu_baseline"] = {"error": repr(ex)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define OAZ_ABI_VERSION 3
+#define OAZ_ABI_VERSION 4
 
 /* ---- enums mirroring the reference --------------------------------------- */
 enum { OAZ_RED = 0, OAZ_BLUE = 1 };                 /* PlayerColor, player_color.rs:7-10 */
@@ -163,7 +163,13 @@ typedef struct oaz_config {
     int32_t parts;           /* the simulation loop runs the games in this many parts (1, 2 or 4), each
                                 on its own stream so one part's tree kernels fill the others' NN gaps;
                                 0 = auto (2 from 2048 games); results are identical either way */
-    int32_t reserved[4];
+    int64_t search_time_ns;  /* Q7, AlphaZeroMctsConfig.search_time (mcts_arena.rs:78: playouts run while
+                                `playouts < max_playouts && elapsed < search_time`). 0 = off (default, the
+                                parity mode: exactly `sims` playouts). > 0: a search (or self-play ply) stops
+                                after the first simulation step that ends at or past this wall-clock budget
+                                from its start; all games of the batch run the same number of playouts
+                                (>= 1, <= sims) and pi / the move come from those visits (oaz_last_sims) */
+    int32_t reserved[2];
 } oaz_config;
 
 typedef struct oaz_search_stats {
@@ -264,8 +270,37 @@ int oaz_get_config(const oaz_engine* eng, oaz_config* out);
  * agents with different configs can share one engine as the reference's agents share one
  * Arc<Mutex<ConvResNet>> (mod.rs:84,124). */
 int oaz_set_search_params(oaz_engine* eng, int sims, double c_puct, int train_noise);
+/* Q7 wall-clock budget per search (AlphaZeroMctsConfig.search_time, alphazero_mcts/mod.rs:26-43;
+ * the reference's default agent: 400 ms / 5000 playouts, its tournament: 1 s / 5000,
+ * bin/tournament.rs:121-129) for the following searches / plies: oaz_config.search_time_ns. 0 = off. */
+int oaz_set_search_time(oaz_engine* eng, int64_t search_time_ns);
+/* Simulations per game run by the last search / self-play ply (= sims unless a search_time_ns budget
+ * stopped it earlier). */
+int oaz_last_sims(oaz_engine* eng, int* sims);
 /* Weights in canonical order (n == oaz_weight_count). BN is folded on the host. */
 int oaz_load_weights(oaz_engine* eng, const float* blob, size_t n);
+
+/* ---- model loading by name (AlphaZeroMcts::from_model_file: `vs.load(model_path)` on the
+ * ConvResNet of net.rs:101-213, alphazero_mcts/mod.rs:89-105) ----------------------------------
+ * The canonical tensor table = the VarStore variables net.rs creates, in creation order (the blob
+ * layout of oaz_load_weights): names joined with '|' as in the .ot files ('.' — tch's in-memory
+ * separator — is accepted everywhere a name is taken). Host-only helpers (no GPU). */
+size_t oaz_weight_tensor_count(int blocks);
+int oaz_weight_tensor_info(int blocks, size_t i, char* name, size_t name_cap, size_t* numel);
+/* n named fp32 tensors (any order, e.g. tch's `vs.variables()` HashMap: name, data pointer, numel)
+ * -> the canonical blob (out_n >= oaz_weight_count). A missing, duplicate, unknown or wrongly sized
+ * tensor is OAZ_ERR_WEIGHTS naming it (the reference silently keeps random weights, Q13). */
+int oaz_weights_from_named(int blocks, const char* const* names, const float* const* data, const size_t* sizes,
+                           size_t n, float* out, size_t out_n);
+/* The same, straight into an engine (blocks = the engine's). */
+int oaz_load_weights_named(oaz_engine* eng, const char* const* names, const float* const* data,
+                           const size_t* sizes, size_t n);
+/* A VarStore::save .ot archive (train.rs:414-430; TorchScript zip with stored members) -> canonical
+ * blob; *blocks_out = residual blocks found in it. data.pkl is read by a restricted pickle machine
+ * that builds plain values only (nothing is imported or executed). out may be NULL to size. */
+int oaz_ot_read(const char* path, float* out, size_t cap, size_t* n_out, int* blocks_out);
+/* oaz_ot_read + oaz_load_weights; the file must hold a network of the engine's block count. */
+int oaz_load_ot(oaz_engine* eng, const char* path);
 int oaz_sync(oaz_engine* eng);
 /* enable: 0 off, 1 HIP events around every launch, N > 1 around the kernels of every N-th
  * simulation step only (the events cost ~2 % of a C3 step when every launch is timed). */
@@ -333,6 +368,19 @@ int oaz_comm_allreduce_sum_f32(oaz_comm* comm, float* dev, size_t n, void* strea
 int oaz_comm_broadcast(oaz_comm* comm, void* dev, size_t bytes, int root, void* stream);
 /* Waits for the communicator's own stream. */
 int oaz_comm_sync(oaz_comm* comm);
+/* What RCCL itself reports for the communicator, and the last oaz_allgather_samples timed by HIP events
+ * on the communicator's stream (host copies and any caller-side post-processing excluded). */
+typedef struct oaz_comm_stats {
+    int32_t ranks;              /* ncclCommCount(): ranks in the RCCL communicator */
+    int32_t rank;
+    uint64_t allgather_calls;
+    double counts_ms;           /* last all-gather: the uint64 counts all-gather (+ its 8-byte host copies) */
+    double allgather_ms;        /* last all-gather: the grouped per-rank broadcasts of the 228-byte records */
+    uint64_t allgather_records; /* records every rank received in the last all-gather (sum of the counts) */
+    uint64_t allgather_bytes;   /* = allgather_records * sizeof(oaz_sample) */
+    uint64_t own_records;       /* this rank's contribution to the last all-gather */
+} oaz_comm_stats;
+int oaz_comm_stats_get(oaz_comm* comm, oaz_comm_stats* out);
 
 /* ---- training step ---------------------------------
  * One trainer = one GPU. Parameters live on the device in the canonical blob

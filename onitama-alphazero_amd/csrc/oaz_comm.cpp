@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "../../include/onitama_az.h"
@@ -31,6 +32,7 @@ struct Rccl {
     ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
     ncclResult_t (*group_start)(void);
     ncclResult_t (*group_end)(void);
+    ncclResult_t (*comm_count)(const ncclComm_t, int*);
     const char* (*error_string)(ncclResult_t);
 };
 Rccl g_rccl;
@@ -54,6 +56,7 @@ int rccl_load() {
            sym(h, "ncclCommDestroy", r.comm_destroy) && sym(h, "ncclAllGather", r.all_gather) &&
            sym(h, "ncclBroadcast", r.broadcast) && sym(h, "ncclAllReduce", r.all_reduce) &&
            sym(h, "ncclGroupStart", r.group_start) && sym(h, "ncclGroupEnd", r.group_end) &&
+           sym(h, "ncclCommCount", r.comm_count) &&
            sym(h, "ncclGetErrorString", r.error_string);
     if (!r.ok) return oaz_set_err(OAZ_ERR_COMM, "librccl.so.1 lacks an expected symbol");
     return 0;
@@ -73,6 +76,8 @@ struct oaz_comm {
     int rank = 0, world = 1, device = 0;
     hipStream_t stream = nullptr;
     uint64_t* d_counts = nullptr;  // [world] all-gathered sample counts
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // last all-gather: start, counts done, records done
+    oaz_comm_stats st{};
 };
 
 extern "C" int oaz_comm_unique_id(oaz_comm_id* out) {
@@ -90,6 +95,8 @@ extern "C" void oaz_comm_destroy(oaz_comm* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->nc) (void)g_rccl.comm_destroy(c->nc);
     if (c->d_counts) (void)hipFree(c->d_counts);
+    for (auto ev : c->ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -108,9 +115,15 @@ static int comm_init(const oaz_comm_id* id, int rank, int world, int device, oaz
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(hipMalloc((void**)&c->d_counts, (size_t)world * sizeof(uint64_t)));
+    for (auto& ev : c->ev) HIP_TRY(hipEventCreate(&ev));
     ncclUniqueId uid;
     memcpy(uid.internal, id->internal, sizeof(uid.internal));
     NCCL_TRY(g_rccl.comm_init_rank(&c->nc, world, uid, rank));
+    int n = 0;
+    NCCL_TRY(g_rccl.comm_count(c->nc, &n));
+    if (n != world) return oaz_set_err(OAZ_ERR_COMM, "comm_init: RCCL communicator holds %d ranks, expected %d", n, world);
+    c->st.ranks = n;
+    c->st.rank = rank;
     return 0;
 }
 
@@ -131,24 +144,51 @@ extern "C" int oaz_comm_sync(oaz_comm* c) {
     return 0;
 }
 
+extern "C" int oaz_comm_stats_get(oaz_comm* c, oaz_comm_stats* out) {
+    if (!c || !out) return oaz_set_err(OAZ_ERR_ARG, "comm_stats: null");
+    int n = 0;
+    NCCL_TRY(g_rccl.comm_count(c->nc, &n));
+    c->st.ranks = n;
+    *out = c->st;
+    return 0;
+}
+
+// A rank whose own part fails before the exchange (bad engine / device, the sample peek) still joins
+// the counts all-gather with this count, so every rank sees the failure and returns an error instead
+// of the others blocking in the collective.
+static constexpr uint64_t kLocalFailure = UINT64_MAX;
+
 extern "C" int oaz_allgather_samples(oaz_engine* eng, oaz_comm* c, oaz_sample* dev_out, size_t cap, size_t* n_total,
                                      uint64_t* counts_out) {
-    if (!eng || !c || (!dev_out && cap)) return oaz_set_err(OAZ_ERR_ARG, "allgather_samples: bad arguments");
+    if (!c) return oaz_set_err(OAZ_ERR_ARG, "allgather_samples: null communicator");
     const oaz_sample* src = nullptr;
     size_t n = 0;
-    int dev = 0;
-    if (int rc = oaz_engine_samples_peek(eng, &src, &n, &dev)) return rc;
-    if (dev != c->device) return oaz_set_err(OAZ_ERR_ARG, "allgather_samples: engine on GPU %d, comm on GPU %d", dev, c->device);
+    int dev = c->device, rc_local = 0;
+    std::string why;
+    if (!eng || (!dev_out && cap)) {
+        rc_local = oaz_set_err(OAZ_ERR_ARG, "allgather_samples: bad arguments");
+    } else if ((rc_local = oaz_engine_samples_peek(eng, &src, &n, &dev)) == 0 && dev != c->device) {
+        rc_local = oaz_set_err(OAZ_ERR_ARG, "allgather_samples: engine on GPU %d, comm on GPU %d", dev, c->device);
+    }
+    if (rc_local) why = oaz_last_error();
     HIP_TRY(hipSetDevice(c->device));
-    // 1. counts
-    const uint64_t mine = (uint64_t)n;
+    // 1. counts (every rank joins, also after a local failure)
+    const uint64_t mine = rc_local ? kLocalFailure : (uint64_t)n;
+    HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_counts + c->rank, &mine, sizeof(mine), hipMemcpyHostToDevice, c->stream));
     NCCL_TRY(g_rccl.all_gather(c->d_counts + c->rank, c->d_counts, 1, ncclUint64, c->nc, c->stream));
     std::vector<uint64_t> counts((size_t)c->world);
     HIP_TRY(hipMemcpyAsync(counts.data(), c->d_counts, counts.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (rc_local) return oaz_set_err(rc_local, "%s", why.c_str());
     uint64_t total = 0;
-    for (uint64_t k : counts) total += k;
+    for (int r = 0; r < c->world; ++r) {
+        if (counts[r] == kLocalFailure)  // every rank sees the same counts: all fail alike, nothing consumed
+            return oaz_set_err(OAZ_ERR_COMM, "allgather_samples: rank %d failed before the exchange", r);
+        total += counts[r];
+    }
+    if (counts[c->rank] != mine) return oaz_set_err(OAZ_ERR_COMM, "allgather_samples: own count not gathered");
     if (counts_out) memcpy(counts_out, counts.data(), counts.size() * sizeof(uint64_t));
     if (n_total) *n_total = (size_t)total;
     if (total > cap)  // every rank sees the same counts: all fail alike, nothing consumed
@@ -170,7 +210,17 @@ extern "C" int oaz_allgather_samples(oaz_engine* eng, oaz_comm* c, oaz_sample* d
         off += counts[r];
     }
     NCCL_TRY(g_rccl.group_end());
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    float ms_counts = 0.f, ms_data = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms_counts, c->ev[0], c->ev[1]));
+    HIP_TRY(hipEventElapsedTime(&ms_data, c->ev[1], c->ev[2]));
+    c->st.allgather_calls += 1;
+    c->st.counts_ms = ms_counts;
+    c->st.allgather_ms = ms_data;
+    c->st.allgather_records = total;
+    c->st.allgather_bytes = total * sizeof(oaz_sample);
+    c->st.own_records = mine;
     return oaz_engine_samples_consume(eng, n);
 }
 

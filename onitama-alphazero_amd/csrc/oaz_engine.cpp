@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stddef.h>
+#include <time.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -23,6 +25,8 @@
 #include "oaz_kernels.h"
 
 using namespace oaz;
+
+static_assert(offsetof(oaz_config, search_time_ns) == 104 && sizeof(oaz_config) == 120, "oaz_config layout (ABI 4)");
 
 // ---- errors ---------------------------------------------------------------------------------
 static thread_local std::string g_err;
@@ -647,6 +651,7 @@ struct oaz_engine {
     float* s_rootv = nullptr;
     float* s_rootp = nullptr;
     uint32_t search_calls = 0;
+    uint32_t last_sims = 0;  // simulations per game of the last run_sims (Q7 budget: may be < cfg.sims)
     uint32_t* s_ply = nullptr;
     // self-play
     oaz_state* root = nullptr;
@@ -826,7 +831,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         return nullptr;
     }
     if (cfg->blocks < 0 || cfg->blocks > 64 || cfg->sims < 1 || cfg->sims > 65535 || cfg->games < 1 ||
-        cfg->max_plies < 0 || cfg->max_plies > 100000 || cfg->compact < 0 || cfg->compact > 2 ||
+        cfg->max_plies < 0 || cfg->max_plies > 100000 || cfg->compact < 0 || cfg->compact > 2 || cfg->search_time_ns < 0 ||
         (cfg->parts != 0 && cfg->parts != 1 && cfg->parts != 2 && cfg->parts != 4)) {
         oaz_set_err(OAZ_ERR_ARG, "create: config out of range");
         return nullptr;
@@ -972,6 +977,19 @@ extern "C" int oaz_set_search_params(oaz_engine* e, int sims, double c_puct, int
     return 0;
 }
 
+extern "C" int oaz_set_search_time(oaz_engine* e, int64_t search_time_ns) {
+    if (!e) return oaz_set_err(OAZ_ERR_ARG, "set_search_time: null");
+    if (search_time_ns < 0) return oaz_set_err(OAZ_ERR_ARG, "set_search_time: negative budget");
+    e->cfg.search_time_ns = search_time_ns;
+    return 0;
+}
+
+extern "C" int oaz_last_sims(oaz_engine* e, int* sims) {
+    if (!e || !sims) return oaz_set_err(OAZ_ERR_ARG, "last_sims: null");
+    *sims = (int)e->last_sims;
+    return 0;
+}
+
 extern "C" int oaz_get_config(const oaz_engine* e, oaz_config* out) {
     if (!e || !out) return oaz_set_err(OAZ_ERR_ARG, "get_config: null");
     *out = e->cfg;
@@ -995,8 +1013,10 @@ extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
 
 extern "C" int oaz_sync(oaz_engine* e) {
     if (!e) return oaz_set_err(OAZ_ERR_ARG, "sync: null");
+    HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream2));
+    for (auto s3 : e->stream3) HIP_TRY(hipStreamSynchronize(s3));
     return 0;
 }
 
@@ -1116,14 +1136,57 @@ static int game_parts(const oaz_engine* e, uint32_t G) {
     if (const char* v = getenv("OAZ_SPLIT_HALVES")) p = atoi(v);
 #endif
     if (p != 2 && p != 4) p = 1;
-    while (p > 1 && (uint32_t)p > G) p /= 2;
+    // every part non-empty: part h starts at h * ceil(G / p), so the last one needs (p - 1) * ceil(G / p) < G
+    // (G = 5, p = 4 would give parts of 2, 2, 1 and an empty fourth)
+    while (p > 1 && (uint32_t)(p - 1) * ((G + (uint32_t)p - 1) / (uint32_t)p) >= G) p /= 2;
     return p;
 }
 
+// Game range [g0, g0 + n) of part h of nh over G games (clamped: no part extends past G).
+static void part_range(uint32_t G, int nh, int h, uint32_t* g0, uint32_t* n) {
+    const uint32_t Gh = (G + (uint32_t)nh - 1) / (uint32_t)nh;
+    const uint32_t s = std::min((uint32_t)h * Gh, G);
+    *g0 = s;
+    *n = std::min(Gh, G - s);
+}
+
+static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* roots, const uint8_t* active,
+                         const uint64_t* gids, const uint32_t* plies);
+
+// run_sims_body, and on an error the game parts' streams are joined into the engine stream anyway
+// (its early returns skip the join), so oaz_sync and buffer reuse after an error wait for them.
 static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, const uint8_t* active,
                     const uint64_t* gids, const uint32_t* plies) {
+    const int rc = run_sims_body(e, t, roots, active, gids, plies);
+    if (rc) {
+        const std::string msg = g_err;
+        for (int h = 1; h < kMaxParts; ++h)
+            if (hipEventRecord(e->ev_part[h], e->stream3[h - 1]) == hipSuccess)
+                (void)hipStreamWaitEvent(e->stream, e->ev_part[h], 0);
+        e->timing_skip = false;
+        g_err = msg;
+    }
+    return rc;
+}
+
+static double now_ns() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e9 + (double)ts.tv_nsec;
+}
+
+static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* roots, const uint8_t* active,
+                         const uint64_t* gids, const uint32_t* plies) {
     const SearchParams prm = search_params(e);
     const uint32_t sims = (uint32_t)e->cfg.sims;
+    // Q7 (opt-in, oaz_config.search_time_ns): the reference's loop runs playouts while
+    // `playouts < max_playouts && elapsed < search_time` (mcts_arena.rs:78). Here all games advance
+    // together, so the clock is read between simulation steps (after the streams drained) and the
+    // search stops after the first step that ends at or past the budget: every game of the batch then
+    // has run the same number of playouts (>= 1), and pi / the move come from those visits.
+    const double budget_ns = (double)e->cfg.search_time_ns;
+    const double t_start = budget_ns > 0 ? now_ns() : 0.0;
+    e->last_sims = 0;
     const bool noise = e->cfg.train_noise && e->noise;
     const size_t slot_elems = (size_t)kNoiseChunk * t.G * kNoiseStride;
     const uint32_t nchunks = (sims + kNoiseChunk - 1) / kNoiseChunk;
@@ -1162,13 +1225,16 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
 #endif
     const bool split = nh > 1;
     e->times.parts = (uint64_t)nh;
-    const uint32_t Gh = (t.G + (uint32_t)nh - 1) / (uint32_t)nh;
     TreeView tv[kMaxParts];
+    uint32_t gstart[kMaxParts] = {0, 0, 0, 0};
     hipStream_t sh[kMaxParts] = {e->stream, e->stream3[0], e->stream3[1], e->stream3[2]};
-    for (int h = 0; h < nh; ++h)
-        tv[h] = split ? slice_view(tc, (uint32_t)h * Gh, (uint32_t)h * Gh + Gh <= t.G ? Gh : t.G - (uint32_t)h * Gh,
-                                   h * buckets_of(Gh))
-                      : tc;
+    int b0 = 0;  // a part's compaction bucket counters follow the previous parts'
+    for (int h = 0; h < nh; ++h) {
+        uint32_t n = t.G;
+        part_range(t.G, nh, h, &gstart[h], &n);
+        tv[h] = split ? slice_view(tc, gstart[h], n, b0) : tc;
+        b0 += buckets_of(n);
+    }
     if (split) {
         HIP_TRY(hipEventRecord(e->ev_join, e->stream));  // the other streams start after prior work
         for (int h = 1; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(sh[h], e->ev_join, 0));
@@ -1180,7 +1246,8 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
         }
         return 0;
     };
-    for (uint32_t c = 0; c < nchunks; ++c) {
+    bool out_of_time = false;
+    for (uint32_t c = 0; c < nchunks && !out_of_time; ++c) {
         if (noise) {
             if (c + 1 < nchunks)
                 if (int rc = produce(c + 1)) return rc;
@@ -1188,11 +1255,19 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
         }
         const uint32_t s0 = c * kNoiseChunk, s1 = s0 + kNoiseChunk < sims ? s0 + kNoiseChunk : sims;
         for (uint32_t s = s0; s < s1; ++s) {
+            if (budget_ns > 0 && s > 0) {  // Q7: is the budget spent after simulation s - 1?
+                for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamSynchronize(sh[h]));
+                if (now_ns() - t_start >= budget_ns) {
+                    out_of_time = true;
+                    break;
+                }
+            }
+            e->last_sims = s + 1;
             // sampled steps sit mid-chunk: a chunk's first select also waits for its noise
             e->timing_skip = e->timing_every > 1 && s % (uint32_t)e->timing_every != (uint32_t)e->timing_every / 2;
             for (int h = 0; h < nh; ++h) {
                 const TreeView& th = tv[h];
-                const size_t go = (size_t)h * Gh;
+                const size_t go = gstart[h];
                 if (th.G == 0) continue;
                 const hipStream_t st = sh[h];
                 const oaz_state* rh = roots + go;
@@ -1215,7 +1290,9 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
                     return rc;
                 }
                 if (th.need) {
-                    const TileMap tm{th.bcnt, buckets_of(th.G), (int32_t)th.G + 16};
+                    // row loads clamped to the part's own rows (the next part's compaction writes its
+                    // rows on another stream)
+                    const TileMap tm{th.bcnt, buckets_of(th.G), (int32_t)th.G};
                     if (int rc = timed(e, 5, th.G, [&] { return launch_eval_compact(th, st); }, st)) return rc;
                     if (int rc = evaluate(e, th.cstate, th.G, pol, val, st, &tm)) return rc;
                 } else if (int rc = evaluate(e, th.leaf_state, th.G, pol, val, st)) {
@@ -1228,7 +1305,7 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
     }
     e->timing_skip = false;
     for (int h = 0; h < nh; ++h) {
-        const size_t go = (size_t)h * Gh;
+        const size_t go = gstart[h];
         if (tv[h].G == 0) continue;
         if (int rc = timed(e, 2, tv[h].G, [&] {
                 return launch_expand_backup(tv[h], roots + go, active ? active + go : nullptr, e->policy + go * 50,

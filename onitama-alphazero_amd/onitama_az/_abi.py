@@ -22,7 +22,7 @@ FP32, BF16, FP32_SPLIT, FP32_SPLIT16 = 0, 1, 2, 3  # OAZ_FP32 / OAZ_BF16 / OAZ_F
 ERR_RANGE = -7  # OAZ_ERR_RANGE (ABI 1 only; ABI 2 recomputes fp16-range tiles, oaz_nn_fallbacks)
 ERR_CAPACITY = -4
 ERR_COMM = -8
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_MOVES = 40
 
 
@@ -85,7 +85,8 @@ class oaz_config(C.Structure):
         ("stagger", C.c_int32),
         ("compact", C.c_int32),
         ("parts", C.c_int32),
-        ("reserved", C.c_int32 * 4),
+        ("search_time_ns", C.c_int64),
+        ("reserved", C.c_int32 * 2),
     ]
 
 
@@ -174,10 +175,24 @@ class oaz_comm_id(C.Structure):
     _fields_ = [("internal", C.c_char * 128)]
 
 
+class oaz_comm_stats(C.Structure):
+    _fields_ = [
+        ("ranks", C.c_int32),
+        ("rank", C.c_int32),
+        ("allgather_calls", C.c_uint64),
+        ("counts_ms", C.c_double),
+        ("allgather_ms", C.c_double),
+        ("allgather_records", C.c_uint64),
+        ("allgather_bytes", C.c_uint64),
+        ("own_records", C.c_uint64),
+    ]
+
+
 assert C.sizeof(oaz_state) == 24
 assert C.sizeof(oaz_move) == 4
 assert C.sizeof(oaz_node) == 32
 assert C.sizeof(oaz_sample) == 228
+assert C.sizeof(oaz_config) == 120 and oaz_config.search_time_ns.offset == 104
 
 STATE_DTYPE = np.dtype(
     [("kings", "<u4", 2), ("pawns", "<u4", 2), ("cards", "u1", 5), ("to_move", "u1"), ("pad", "u1", 2)]
@@ -216,7 +231,15 @@ _PROTOS = {
     "oaz_destroy": (None, [_VOIDP]),
     "oaz_get_config": (C.c_int, [_VOIDP, _P(oaz_config)]),
     "oaz_set_search_params": (C.c_int, [_VOIDP, C.c_int, C.c_double, C.c_int]),
+    "oaz_set_search_time": (C.c_int, [_VOIDP, C.c_int64]),
+    "oaz_last_sims": (C.c_int, [_VOIDP, _P(C.c_int)]),
     "oaz_load_weights": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
+    "oaz_weight_tensor_count": (C.c_size_t, [C.c_int]),
+    "oaz_weight_tensor_info": (C.c_int, [C.c_int, C.c_size_t, C.c_char_p, C.c_size_t, _P(C.c_size_t)]),
+    "oaz_weights_from_named": (C.c_int, [C.c_int, _VOIDP, _VOIDP, _VOIDP, C.c_size_t, _VOIDP, C.c_size_t]),
+    "oaz_load_weights_named": (C.c_int, [_VOIDP, _VOIDP, _VOIDP, _VOIDP, C.c_size_t]),
+    "oaz_ot_read": (C.c_int, [C.c_char_p, _VOIDP, C.c_size_t, _P(C.c_size_t), _P(C.c_int)]),
+    "oaz_load_ot": (C.c_int, [_VOIDP, C.c_char_p]),
     "oaz_sync": (C.c_int, [_VOIDP]),
     "oaz_set_timing": (C.c_int, [_VOIDP, C.c_int]),
     "oaz_kernel_times_get": (C.c_int, [_VOIDP, _P(oaz_kernel_times)]),
@@ -238,6 +261,7 @@ _PROTOS = {
     "oaz_comm_allreduce_sum_f32": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t, _VOIDP]),
     "oaz_comm_broadcast": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t, C.c_int, _VOIDP]),
     "oaz_comm_sync": (C.c_int, [_VOIDP]),
+    "oaz_comm_stats_get": (C.c_int, [_VOIDP, _P(oaz_comm_stats)]),
     "oaz_pure_mcts_config_default": (None, [_P(oaz_pure_mcts_config)]),
     "oaz_pure_mcts_tree_capacity": (C.c_size_t, [_P(oaz_pure_mcts_config)]),
     "oaz_pure_mcts_search": (C.c_int, [_VOIDP, C.c_int, _P(oaz_pure_mcts_config), _VOIDP, _VOIDP,

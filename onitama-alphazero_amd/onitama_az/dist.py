@@ -87,6 +87,12 @@ class Comm:
                                                     out.numel() // SAMPLE_BYTES, C.byref(n), _abi.ptr(counts)))
         return int(n.value), [int(c) for c in counts]
 
+    def stats(self) -> _abi.oaz_comm_stats:
+        """ncclCommCount ranks and the HIP-event times of the last all-gather on the comm stream."""
+        st = _abi.oaz_comm_stats()
+        _abi.check(self._lib.oaz_comm_stats_get(self._h, C.byref(st)))
+        return st
+
     def allreduce_sum_(self, t: torch.Tensor, stream: Optional[int] = None) -> None:
         assert t.dtype == torch.float32 and t.is_cuda and t.is_contiguous()
         _abi.check(self._lib.oaz_comm_allreduce_sum_f32(self._h, C.c_void_p(t.data_ptr()), t.numel(),
@@ -124,19 +130,26 @@ def as_samples(raw: torch.Tensor) -> np.ndarray:
     return np.frombuffer(raw.cpu().numpy().tobytes(), dtype=_abi.SAMPLE_DTYPE).copy()
 
 
+def allgather_samples_device(eng, world: int, device: torch.device, comm: Comm) -> Tuple[torch.Tensor, int, List[int]]:
+    """The RCCL exchange alone: every rank's buffered samples as raw 228-byte records in one uint8
+    tensor on this rank's GPU (rank order), the total and the per-rank counts. No host copy."""
+    st = eng.selfplay_stats()
+    # capacity for the largest possible total: a counts pre-pass is inside the C call
+    n_local = torch.tensor([int(st.samples_ready)], dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(n_local)
+    out = torch.empty(max(1, int(n_local.item())) * SAMPLE_BYTES, dtype=torch.uint8, device=device)
+    total, counts = comm.allgather_samples(eng, out)
+    return out[: total * SAMPLE_BYTES], total, counts
+
+
 def allgather_samples(eng, world: int, device: torch.device, comm: Optional[Comm] = None) -> np.ndarray:
     """Every rank's buffered samples (oaz_sample records, rank order) on every rank. With an RCCL
     `comm` the exchange is device to device through the C ABI; without one (gloo / CPU tests) the
     samples are fetched to the host and gathered over the default process group."""
     if comm is not None:
-        st = eng.selfplay_stats()
-        # capacity for the largest possible total: a counts pre-pass is inside the C call
-        n_local = torch.tensor([int(st.samples_ready)], dtype=torch.int64, device=device)
-        if world > 1:
-            dist.all_reduce(n_local)
-        out = torch.empty(max(1, int(n_local.item())) * SAMPLE_BYTES, dtype=torch.uint8, device=device)
-        total, _ = comm.allgather_samples(eng, out)
-        return as_samples(out[: total * SAMPLE_BYTES])
+        raw, _, _ = allgather_samples_device(eng, world, device, comm)
+        return as_samples(raw)
     local = eng.samples_fetch(int(eng.selfplay_stats().samples_ready))
     raw = torch.from_numpy(local.view(np.uint8).copy())
     return as_samples(allgather_sample_bytes(raw, world))

@@ -69,6 +69,17 @@ class Engine:
         """Per-agent AlphaZeroMctsConfig for the next searches (sims <= the creation budget)."""
         _abi.check(self._lib.oaz_set_search_params(self._h, int(sims), float(c_puct), int(bool(train_noise))))
 
+    def set_search_time(self, seconds: float) -> None:
+        """Q7 wall-clock budget per search / ply (AlphaZeroMctsConfig.search_time); 0 = off (exactly
+        `sims` playouts, the parity mode)."""
+        _abi.check(self._lib.oaz_set_search_time(self._h, int(round(float(seconds) * 1e9))))
+
+    def last_sims(self) -> int:
+        """Simulations per game of the last search / ply (< sims when a search_time budget stopped it)."""
+        n = C.c_int(0)
+        _abi.check(self._lib.oaz_last_sims(self._h, C.byref(n)))
+        return int(n.value)
+
     def sync(self) -> None:
         _abi.check(self._lib.oaz_sync(self._h))
 

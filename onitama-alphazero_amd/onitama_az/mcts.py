@@ -15,15 +15,19 @@ import numpy as np
 from . import _abi
 from .engine import Engine
 from .game import DoneMove, GameState, MoveResult, PlayerColor, State
-from .weights import random_weights, read_ot, blob_from_named, blocks_from_names
+from .weights import ot_blob, random_weights
 
 
 @dataclass
 class AlphaZeroMctsConfig:  # alphazero_mcts/mod.rs:26-43
-    search_time: float = 0.4          # seconds; NOT used: searches run exactly max_playouts (Q7)
+    search_time: float = 0.4          # seconds; honoured only with enforce_search_time (Q7)
     exploration_c: float = math.sqrt(2.0)
     max_playouts: int = 5000
     train: bool = False
+    # Q7: False (default, the parity mode) runs exactly max_playouts playouts per search; True stops a
+    # search at the first simulation step that ends past search_time, as the reference's loop
+    # `while playouts < max_playouts && elapsed < search_time` (mcts_arena.rs:78) does
+    enforce_search_time: bool = False
 
 
 def reward(move_result: MoveResult, reward_color: PlayerColor) -> float:  # mod.rs:45-53
@@ -66,9 +70,8 @@ class ConvResNet:
     def from_model_file(path: str, options: Options = None) -> "ConvResNet":
         """alphazero_mcts/mod.rs:89-105, but a load error raises instead of keeping random
         weights (Q13)."""
-        named = read_ot(path)
-        b = blocks_from_names(named)
-        return ConvResNet(ConvResNetConfig(resnet_block_amnt=b), options, blob_from_named(named, b))
+        blob, b = ot_blob(path)  # the C ABI's reader (oaz_ot_read), as a Rust host would load it
+        return ConvResNet(ConvResNetConfig(resnet_block_amnt=b), options, blob)
 
     def save(self, path: str) -> None:
         """VarStore::save of the model's variables (train.rs:414-430)."""
@@ -111,6 +114,7 @@ def _search_engine(cache: dict, config: AlphaZeroMctsConfig, model: ConvResNet, 
         eng.load_weights(model.weights)
         shared.update(engine=eng, key=key, games=g, sims=n)
     eng.set_search_params(config.max_playouts, config.exploration_c, config.train)
+    eng.set_search_time(config.search_time if config.enforce_search_time else 0.0)
     return eng
 
 

@@ -97,7 +97,41 @@ def blocks_from_names(names) -> int:
     return (max(idx) + 1) if idx else 0
 
 
-# ---- safe .ot reader -------------------------------------------------------------------------
+# ---- through the C ABI (the product path of model loading) ---------------------------------------
+def ot_blob(path: str) -> Tuple[np.ndarray, int]:
+    """(canonical blob, blocks) of a VarStore .ot archive, read by the library's C reader
+    (oaz_ot_read: restricted pickle machine, nothing executed)."""
+    lib = _abi.load()
+    n, blocks = C.c_size_t(0), C.c_int(0)
+    _abi.check(lib.oaz_ot_read(str(path).encode(), None, 0, C.byref(n), C.byref(blocks)))
+    out = np.zeros(n.value, dtype=np.float32)
+    _abi.check(lib.oaz_ot_read(str(path).encode(), _abi.ptr(out), out.size, C.byref(n), C.byref(blocks)))
+    return out, int(blocks.value)
+
+
+def tensor_table(blocks: int) -> List[Tuple[str, int]]:
+    """The library's canonical (name, numel) table (oaz_weight_tensor_info)."""
+    lib = _abi.load()
+    out = []
+    for i in range(lib.oaz_weight_tensor_count(blocks)):
+        name, n = C.create_string_buffer(128), C.c_size_t(0)
+        _abi.check(lib.oaz_weight_tensor_info(blocks, i, name, 128, C.byref(n)))
+        out.append((name.value.decode(), int(n.value)))
+    return out
+
+
+def blob_from_named_c(named: Dict[str, np.ndarray], blocks: int) -> np.ndarray:
+    """oaz_weights_from_named: tensors placed by name (either '|' or '.' separators)."""
+    keep = [np.ascontiguousarray(v, dtype=np.float32).reshape(-1) for v in named.values()]
+    names = (C.c_char_p * len(keep))(*[k.encode() for k in named])
+    data = (C.c_void_p * len(keep))(*[a.ctypes.data for a in keep])
+    sizes = (C.c_size_t * len(keep))(*[a.size for a in keep])
+    out = np.zeros(weight_count(blocks), dtype=np.float32)
+    _abi.check(_abi.load().oaz_weights_from_named(blocks, names, data, sizes, len(keep), _abi.ptr(out), out.size))
+    return out
+
+
+# ---- safe .ot reader (Python restatement, a cross-check of the C reader) -----------------------------
 class _Sym:
     """Symbolic stand-in for a pickle GLOBAL/REDUCE result (never resolved or called)."""
 

@@ -1,7 +1,13 @@
 /* abi_smoke.c — the C ABI used from plain C, as a Rust/C host would bind it.
  * Built by tests/test_c_abi.py with gcc against include/onitama_az.h and libonitama_az.so.
  * Without a GPU it checks the host-side entry points and the loud no-device errors; with one it
- * runs a batched search, a self-play game batch and the pure-MCTS agent. Prints "OK ..." lines. */
+ * runs a batched search, a self-play game batch and the pure-MCTS agent. Prints "OK ..." lines.
+ *   abi_smoke [model.ot golden.bin]: also loads the model the way AlphaZeroMcts::from_model_file
+ *   does (alphazero_mcts/mod.rs:89-105) — by path (oaz_load_ot) and by name (oaz_load_weights_named,
+ *   the tensors in shuffled order with tch's '.' separator, as `vs.variables()` hands them over) —
+ *   and compares oaz_nn_forward with the golden policy/value (golden.bin: n, then n states, n x 50
+ *   policy and n values). */
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -22,7 +28,110 @@ int hipMemcpy(void* dst, const void* src, size_t bytes, int kind); /* kind 2 = d
         }                                                                          \
     } while (0)
 
-int main(void) {
+/* The model file by path and by name (host side: no GPU). Fills *blob (canonical order). */
+static int model_host(const char* ot, float** blob, size_t* nblob) {
+    size_t n = 0;
+    int blocks = -1;
+    CHECK(oaz_ot_read(ot, NULL, 0, &n, &blocks) == 0 && blocks == 3 && n == oaz_weight_count(3, 64, 21));
+    float* w = (float*)malloc(n * sizeof(float));
+    CHECK(oaz_ot_read(ot, w, n, &n, &blocks) == 0);
+    /* by name: the canonical table, tensors handed over in a shuffled order with '.' separators */
+    const size_t nt = oaz_weight_tensor_count(3);
+    CHECK(nt == 60);
+    char(*names)[96] = malloc(nt * sizeof(*names));
+    const char** np = malloc(nt * sizeof(char*));
+    const float** dp = malloc(nt * sizeof(float*));
+    size_t* sz = malloc(nt * sizeof(size_t));
+    size_t off = 0;
+    for (size_t i = 0; i < nt; ++i) {
+        const size_t j = (i * 37) % nt; /* 37 is coprime with 60: a permutation */
+        size_t numel = 0;
+        CHECK(oaz_weight_tensor_info(3, i, names[j], sizeof(names[j]), &numel) == 0);
+        for (char* c = names[j]; *c; ++c)
+            if (*c == '|') *c = '.';
+        np[j] = names[j];
+        dp[j] = w + off;
+        sz[j] = numel;
+        off += numel;
+    }
+    CHECK(off == n);
+    float* w2 = (float*)malloc(n * sizeof(float));
+    CHECK(oaz_weights_from_named(3, np, dp, sz, nt, w2, n) == 0 && memcmp(w, w2, n * sizeof(float)) == 0);
+    sz[5] += 1; /* a wrongly sized tensor is refused, naming it */
+    CHECK(oaz_weights_from_named(3, np, dp, sz, nt, w2, n) == OAZ_ERR_WEIGHTS && strstr(oaz_last_error(), "elements"));
+    sz[5] -= 1;
+    CHECK(oaz_weights_from_named(3, np, dp, sz, nt - 1, w2, n) == OAZ_ERR_WEIGHTS && strstr(oaz_last_error(), "missing"));
+    CHECK(oaz_weights_from_named(2, np, dp, sz, nt, w2, n) == OAZ_ERR_WEIGHTS); /* resnet_2 is not in 2 blocks */
+    free(w2);
+    free(names);
+    free(np);
+    free(dp);
+    free(sz);
+    *blob = w;
+    *nblob = n;
+    return 0;
+}
+
+/* On the GPU: load by path and by name, forward the golden positions, compare. */
+static int model_gpu(const char* ot, const char* golden, const float* w, size_t nw) {
+    FILE* f = fopen(golden, "rb");
+    CHECK(f != NULL);
+    int32_t n = 0;
+    CHECK(fread(&n, 4, 1, f) == 1 && n > 0 && n <= 4096);
+    oaz_state* st = malloc(n * sizeof(oaz_state));
+    float *gp = malloc(n * 50 * sizeof(float)), *gv = malloc(n * sizeof(float));
+    float *p = malloc(n * 50 * sizeof(float)), *v = malloc(n * sizeof(float));
+    float *p2 = malloc(n * 50 * sizeof(float)), *v2 = malloc(n * sizeof(float));
+    CHECK(fread(st, sizeof(oaz_state), n, f) == (size_t)n && fread(gp, 4, n * 50, f) == (size_t)n * 50 &&
+          fread(gv, 4, n, f) == (size_t)n);
+    fclose(f);
+    oaz_config cfg;
+    oaz_config_default(&cfg);
+    cfg.blocks = 3;
+    cfg.sims = 1;
+    cfg.games = n;
+    cfg.precision = OAZ_FP32_SPLIT16;
+    oaz_engine* e = oaz_create(&cfg, 0);
+    CHECK(e != NULL);
+    CHECK(oaz_load_ot(e, ot) == 0 && oaz_nn_forward(e, st, n, p, v) == 0);
+    double err = 0;
+    for (int i = 0; i < n * 50; ++i) err = fabs(p[i] - gp[i]) > err ? fabs(p[i] - gp[i]) : err;
+    for (int i = 0; i < n; ++i) err = fabs(v[i] - gv[i]) > err ? fabs(v[i] - gv[i]) : err;
+    CHECK(err < 1e-5);
+    /* by name: the same tensors from host memory, bit-identical forward */
+    const size_t nt = oaz_weight_tensor_count(3);
+    char(*names)[96] = malloc(nt * sizeof(*names));
+    const char** np = malloc(nt * sizeof(char*));
+    const float** dp = malloc(nt * sizeof(float*));
+    size_t* sz = malloc(nt * sizeof(size_t));
+    size_t off = 0;
+    for (size_t i = 0; i < nt; ++i) {
+        CHECK(oaz_weight_tensor_info(3, i, names[i], sizeof(names[i]), &sz[i]) == 0);
+        np[i] = names[i];
+        dp[i] = w + off;
+        off += sz[i];
+    }
+    CHECK(off == nw);
+    CHECK(oaz_load_weights_named(e, np, dp, sz, nt) == 0 && oaz_nn_forward(e, st, n, p2, v2) == 0);
+    CHECK(memcmp(p, p2, n * 50 * sizeof(float)) == 0 && memcmp(v, v2, n * sizeof(float)) == 0);
+    CHECK(oaz_load_weights_named(e, np, dp, sz, nt - 2) == OAZ_ERR_WEIGHTS);
+    oaz_destroy(e);
+    printf("OK model %d positions max err %.2e\n", n, err);
+    free(names);
+    free(np);
+    free(dp);
+    free(sz);
+    free(st);
+    free(gp);
+    free(gv);
+    free(p);
+    free(v);
+    free(p2);
+    free(v2);
+    return 0;
+}
+
+int main(int argc, char** argv) {
     CHECK(oaz_abi_version() == OAZ_ABI_VERSION);
     oaz_config cfg;
     oaz_config_default(&cfg);
@@ -35,6 +144,12 @@ int main(void) {
     oaz_initial_state(deck, &s);
     CHECK(s.kings[0] == 0x200u && s.kings[1] == 0x20000000u && s.to_move == 1); /* Crab neutral: Blue starts */
     printf("OK host\n");
+    float* model = NULL;
+    size_t nmodel = 0;
+    if (argc >= 3) {
+        if (model_host(argv[1], &model, &nmodel)) return 1;
+        printf("OK model-host\n");
+    }
     int ndev = 0;
     oaz_device_count(&ndev);
     if (ndev == 0) {
@@ -43,6 +158,7 @@ int main(void) {
         printf("OK no-device\n");
         return 0;
     }
+    if (model && model_gpu(argv[1], argv[2], model, nmodel)) return 1;
     /* rules */
     oaz_move moves[40];
     uint8_t count = 0;
@@ -103,6 +219,9 @@ int main(void) {
         CHECK(sum > 0.999f && sum < 1.001f && (hs[i].z == 0.0f || hs[i].z == 1.0f || hs[i].z == -1.0f));
     }
     CHECK(oaz_selfplay_stats_get(e, &sp) == 0 && sp.samples_ready == 0); /* consumed */
+    oaz_comm_stats cs;
+    CHECK(oaz_comm_stats_get(comm, &cs) == 0 && cs.ranks == 1 && cs.rank == 0 && cs.allgather_calls == 1 &&
+          cs.allgather_records == ready && cs.allgather_bytes == ready * sizeof(oaz_sample) && cs.allgather_ms >= 0.0);
     CHECK(oaz_comm_allreduce_sum_f32(comm, (float*)dev, 16, NULL) == 0 && oaz_comm_sync(comm) == 0);
     CHECK(oaz_comm_broadcast(comm, dev, 64, 0, NULL) == 0 && oaz_comm_sync(comm) == 0);
     oaz_comm_destroy(comm);
@@ -135,5 +254,6 @@ int main(void) {
     oaz_destroy(e);
     free(buf);
     free(w);
+    free(model);
     return 0;
 }

@@ -241,11 +241,12 @@ def test_search_hash_trees_bitexact(orc, sims, c_puct, compact, parts):
     assert r.stats.sims - r.stats.terminal_leaves <= r.stats.nn_evals <= r.stats.sims
 
 
-@pytest.mark.parametrize("games,parts", [(10, 4), (26, 2)])
+@pytest.mark.parametrize("games,parts", [(10, 4), (26, 2), (5, 4), (3, 4), (2, 4)])
 def test_search_uneven_parts_compacted_trees_bitexact(orc, games, parts):
     """Games in uneven parts (10 in 4: 3 + 3 + 3 + 1; 26 in 2: the second part starts at game 13, an
-    unaligned offset), each part on its own stream with its own compaction buckets and rows, leaf
-    compaction forced: every tree equals the oracle's."""
+    unaligned offset; 5 in 4 would leave the fourth part empty, so it runs as 3 + 2), each part on its
+    own stream with its own compaction buckets and rows, leaf compaction forced: every tree equals the
+    oracle's."""
     roots = random_positions(orc, games, seed=515)
     with Engine(games=len(roots), sims=96, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0, compact=1,
                 parts=parts) as e:
@@ -402,9 +403,12 @@ def _sorted_rows(a):
 
 
 @pytest.mark.parametrize("fixed,max_plies,compact,parts", [(True, 150, 0, 1), (False, 150, 0, 1), (False, 3, 0, 1),
-                                                           (True, 150, 1, 2), (False, 150, 1, 4), (False, 3, 0, 2)])
+                                                           (True, 150, 1, 2), (False, 150, 1, 4), (False, 3, 0, 2),
+                                                           (False, 150, 1, 5)])
 def test_selfplay_matches_oracle_games(orc, fixed, max_plies, compact, parts):
     n_games, slots, sims = 24, 8, 12
+    if parts == 5:  # 5 slots in 4 parts (the fourth would be empty: runs as 3 + 2)
+        slots, parts = 5, 4
     deck = [0, 1, 2, 3, 4]
     kw = dict(games=slots, sims=sims, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0,
               max_plies=max_plies, seed=4242, fixed_deck=int(fixed), deck=deck, compact=compact, parts=parts)
@@ -518,3 +522,43 @@ def test_set_search_params_per_agent_config(orc):
             assert _mv(r.moves[g]) == _mv(mv)
         with pytest.raises(_abi.OazError):
             e.set_search_params(65, 2.0, False)  # beyond the creation budget
+
+
+# ---- Q7: the wall-clock search budget (opt-in) -------------------------------------------------
+def test_search_time_budget_stops_early_and_matches_oracle_at_that_budget(orc):
+    """oaz_config.search_time_ns (mcts_arena.rs:78: `while playouts < max_playouts && elapsed <
+    search_time`): a 25 ms budget on a 20 000-playout search stops early; every game ran the same
+    number of playouts, and trees, pi and moves equal the oracle's search with that many playouts."""
+    roots = random_positions(orc, 8, seed=1313)
+    with Engine(games=8, sims=20000, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0,
+                parts=2) as e:
+        e.set_search_time(0.025)
+        r = e.search(roots)
+        n = e.last_sims()
+        assert 1 <= n < 20000, n
+        assert r.stats.sims == 8 * n
+        for g in range(8):
+            mv, pi, nodes, _ = orc.search(orc.search_cfg(sims=n, c_puct=5.0, evaluator=orc.EVAL_HASH), roots[g])
+            _compare_trees(e, g, nodes)
+            assert np.array_equal(r.pi[g].reshape(-1), pi.reshape(-1)) and _mv(r.moves[g]) == _mv(mv)
+        e.set_search_time(0.0)  # off again: exactly `sims` playouts (the parity mode)
+        e.set_search_params(64, 5.0, False)
+        r = e.search(roots)
+        assert e.last_sims() == 64 and r.stats.sims == 8 * 64
+
+
+def test_search_time_through_agent_config():
+    """AlphaZeroMctsConfig.enforce_search_time applies search_time to the engine; without it the
+    search runs max_playouts exactly (Q7 default)."""
+    from onitama_az.mcts import AlphaZeroMcts, AlphaZeroMctsConfig, ConvResNet, ConvResNetConfig
+    model = ConvResNet(ConvResNetConfig(resnet_block_amnt=3), seed=0)
+    gs = GameState.with_deck(Deck([ORIGINAL_CARDS[i] for i in range(5)]))
+    timed = AlphaZeroMcts(AlphaZeroMctsConfig(search_time=0.02, exploration_c=5.0, max_playouts=20000,
+                                              enforce_search_time=True), model)
+    mv, _ = timed.generate_move(gs)
+    eng = model.__dict__["_search"]["engine"]
+    assert 1 <= eng.last_sims() < 20000
+    assert (mv.used_card_idx, mv.mov) in gs.state.generate_all_legal_moves(gs.curr_player_color)
+    plain = AlphaZeroMcts(AlphaZeroMctsConfig(search_time=0.02, exploration_c=5.0, max_playouts=300), model)
+    plain.generate_move(gs)
+    assert eng.last_sims() == 300

@@ -30,8 +30,9 @@ def test_header_functions_exported(lib):
 
 
 def test_abi_version_and_structs(lib):
-    assert lib.oaz_abi_version() == _abi.ABI_VERSION == 3
-    assert C.sizeof(_abi.oaz_config) == 112 or C.sizeof(_abi.oaz_config) > 0
+    assert lib.oaz_abi_version() == _abi.ABI_VERSION == 4
+    assert C.sizeof(_abi.oaz_config) == 120 and _abi.oaz_config.search_time_ns.offset == 104
+    assert C.sizeof(_abi.oaz_comm_stats) == 56
 
 
 def test_default_config_matches_reference_train_bin():  # bin/train.rs:50-78
@@ -87,6 +88,48 @@ def test_ot_reader_matches_committed_fixture(trained3):
     named = W.read_ot("/root/reference/models/model_5e-3_3_resnet.ot")
     assert W.blocks_from_names(named) == 3 and len(named) == 60
     assert np.array_equal(W.blob_from_named(named, 3), trained3)
+
+
+REF_MODELS = sorted(Path("/root/reference/models").glob("*.ot")) if Path("/root/reference/models").exists() else []
+
+
+@pytest.mark.skipif(not REF_MODELS, reason="reference not mounted")
+@pytest.mark.parametrize("path", REF_MODELS, ids=lambda p: p.name)
+def test_c_ot_reader_on_reference_archives(path):
+    """The library's C reader (oaz_ot_read, the product path of from_model_file) reads every .ot the
+    reference ships (libtorch-written archives: BINPUT memo, NEWOBJ module, FB-padded members)
+    exactly as the Python restatement does."""
+    blob, blocks = W.ot_blob(str(path))
+    named = W.read_ot(str(path))
+    assert blocks == W.blocks_from_names(named)
+    assert np.array_equal(blob, W.blob_from_named(named, blocks))
+
+
+def test_c_ot_reader_and_named_loader(trained3, tmp_path):
+    """oaz_ot_read on an archive written with the tensors in a non-canonical order; the named loader
+    (oaz_weights_from_named) with tch's '.' separator and shuffled order; its refusals (Q13)."""
+    named = W.named_from_blob(trained3, 3)
+    p = tmp_path / "m.ot"
+    W.write_ot(str(p), {k: named[k] for k in sorted(named, reverse=True)})
+    blob, blocks = W.ot_blob(str(p))
+    assert blocks == 3 and np.array_equal(blob, trained3)
+    table = W.tensor_table(3)
+    assert [(n, int(np.prod(s))) for n, s in W.canonical_layout(3)] == table
+    rng = np.random.default_rng(0)
+    keys = list(named)
+    rng.shuffle(keys)
+    dotted = {k.replace("|", "."): named[k] for k in keys}
+    assert np.array_equal(W.blob_from_named_c(dotted, 3), trained3)
+    for bad, msg in ((dict(list(dotted.items())[1:]), "missing"),
+                     (dict(dotted, **{"extra|weight": np.zeros(3, np.float32)}), "not part of"),
+                     (dict(dotted, **{"bn1.weight": np.zeros(65, np.float32)}), "elements")):
+        with pytest.raises(_abi.OazError, match=msg):
+            W.blob_from_named_c(bad, 3)
+    with pytest.raises(_abi.OazError, match="cannot open"):
+        W.ot_blob(str(tmp_path / "absent.ot"))
+    (tmp_path / "junk.ot").write_bytes(b"not a zip archive at all" * 10)
+    with pytest.raises(_abi.OazError, match="zip"):
+        W.ot_blob(str(tmp_path / "junk.ot"))
 
 
 def test_ot_writer_round_trip(trained3, tmp_path):
