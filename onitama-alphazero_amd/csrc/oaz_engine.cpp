@@ -1061,15 +1061,9 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
     w.blob = e->weights;
     w.blocks = e->cfg.blocks;
     w.precision = e->cfg.precision;
-    w.bf16_v1 = 0;
     w.x6_variant = 0;
-#if OAZ_AB  // A/B build only: kernel alternatives by environment variable
-    {
-        const char* v1 = getenv("OAZ_NN_BF16_V1");
-        w.bf16_v1 = v1 ? atoi(v1) : 0;  // 0: k_nn_h3 in bf16 mode, 1: k_nn_sq16<bf16>, 2: k_nn_bf16g<4>, 3: k_nn_bf16g<2>, 4: k_nn_h3 bf16 without EP
-        const char* xv = getenv("OAZ_NN_X6_V");
-        w.x6_variant = xv ? atoi(xv) : 0;
-    }
+#if OAZ_AB  // A/B build only: the diagnostic builds of k_nn_h3 by environment variable
+    if (const char* xv = getenv("OAZ_NN_X6_V")) w.x6_variant = atoi(xv);
 #endif
     w.blob_x6 = e->cfg.precision == OAZ_FP32_SPLIT16 ? e->weights + nn_packed_floats(e->cfg.blocks, OAZ_FP32_SPLIT16)
                                                      : nullptr;
@@ -1105,17 +1099,9 @@ extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* p
 // when it can remove whole rounds of NN workgroups (one 16-position tile per
 // CU at a time): at C3 the ~8.7 % won leaves are 1.4 of 16 rounds. Below 12 rounds (G < 12 * 16 *
 // CUs, e.g. C2's 4096 games = one round) it would only add its own launch, so the leaves are then
-// evaluated in place. Also off for the A/B-only NN variants without tile maps.
+// evaluated in place.
 static bool compact_leaves(const oaz_engine* e, uint32_t G) {
-    if (e->cfg.compact == 0 || (e->cfg.compact == 2 && G < 12u * 16u * (uint32_t)e->cus)) return false;
-#if OAZ_AB
-    if (e->cfg.evaluator == OAZ_EVAL_NN) {
-        const char* xv = getenv("OAZ_NN_X6_V");
-        const char* v1 = getenv("OAZ_NN_BF16_V1");
-        if ((xv && atoi(xv) == 20) || (v1 && (atoi(v1) == 2 || atoi(v1) == 3))) return false;  // k_nn_p8, k_nn_bf16g
-    }
-#endif
-    return true;
+    return e->cfg.compact == 1 || (e->cfg.compact == 2 && G >= 12u * 16u * (uint32_t)e->cus);
 }
 
 // All cfg.sims simulations of one move for every game, in lock step: select -> leaf compaction ->

@@ -95,8 +95,7 @@ struct NNView {
     int32_t blocks;
     int32_t precision;  // OAZ_FP32 (exact fp32 MFMA), OAZ_BF16 (bf16 inputs), OAZ_FP32_SPLIT (bf16x6 split),
                         // OAZ_FP32_SPLIT16 (fp16x3 split)
-    int32_t x6_variant; // A/B build only (OAZ_NN_X6_V): split kernel variant
-    int32_t bf16_v1;    // A/B build only (OAZ_NN_BF16_V1): 1 k_nn_sq16<bf16>, 2 k_nn_bf16g<4>, 3 k_nn_bf16g<2>
+    int32_t x6_variant; // A/B build only (OAZ_NN_X6_V): a diagnostic build of k_nn_h3 (timing only)
     const float* blob_x6;             // OAZ_FP32_SPLIT16: the OAZ_FP32_SPLIT blob of the same weights
     unsigned long long* fallback;     // OAZ_FP32_SPLIT16: tiles recomputed by the k_nn_x6 body (fp16 range)
     TileMap tm;                       // compacted leaves (tm.bcnt null: rows [0, B))

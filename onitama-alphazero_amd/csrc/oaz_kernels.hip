@@ -728,19 +728,12 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
     }
 }
 
-// register budgets: 80 VGPRs = 6 waves/SIMD (default), 72 = 7 waves/SIMD (a few dwords spilled)
+// register budget: 80 VGPRs = 6 waves/SIMD (7 waves spill and measured 10 % slower)
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6)))
 k_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
              const float* __restrict__ noise, SearchParams prm) {
     select_seg_body(t, roots, active, noise, prm);
 }
-#if OAZ_AB
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7)))
-k_select_seg7(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
-              const float* __restrict__ noise, SearchParams prm) {
-    select_seg_body(t, roots, active, noise, prm);
-}
-#endif
 
 template <int N>
 __device__ __forceinline__ float bcast_f32(float v) {
@@ -1132,14 +1125,6 @@ static bool tree_seg() {
 }
 hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                          const float* noise, SearchParams p, hipStream_t st) {
-#if OAZ_AB  // A/B build only: 7 waves/SIMD (spills; measured 10 % slower)
-    static const bool w7 = getenv("OAZ_SELECT_W7") && getenv("OAZ_SELECT_W7")[0] == '1';
-    if (tree_seg() && w7) {
-        hipLaunchKernelGGL(k_select_seg7, dim3(wave_grid((t.G + 3) / 4)), dim3(kBlock), 0, st, t, roots, active, noise,
-                           p);
-        return hipGetLastError();
-    }
-#endif
     if (tree_seg())
         hipLaunchKernelGGL(k_select_seg, dim3(wave_grid((t.G + 3) / 4)), dim3(kBlock), 0, st, t, roots, active, noise,
                            p);

@@ -1,11 +1,16 @@
 // oaz_nn.hip — ConvResNet policy-value forward (alphazero-training/src/net.rs:101-232), fused
 // into one kernel: encoder -> conv3x3(21->64)+BN+ReLU -> blocks x [conv3x3+BN+ReLU ->
 // conv3x3+BN -> +skip -> ReLU] -> value head (1x1 conv, MLP, tanh) -> policy head (1x1 conv,
-// linear, softmax over 50).
+// linear, softmax over 50). One kernel per oaz_config.precision:
+//   k_nn_h3   OAZ_FP32_SPLIT16 (the benches' fp32 kernel): fp32 operands split into hi + lo fp16
+//             terms, three products on v_mfma_f32_16x16x32_f16; fp16-range tiles recomputed in the
+//             same launch with the k_nn_x6 body. With H3Cfg<1> the same structure in OAZ_BF16 (C5).
+//   k_nn_x6   OAZ_FP32_SPLIT: an exact three-term bf16 split, six products on 16x16x32 bf16 MFMA.
+//   k_nn_sq16 OAZ_FP32: exact fp32 products on v_mfma_f32_16x16x4_f32.
+// DESIGN.md section 5 describes each; below, k_nn_sq16's geometry, which the others refine.
 //
 // Geometry (k_nn_sq16)
-//   * A workgroup evaluates 16 positions. The 3x3 convs are implicit GEMMs on
-//     v_mfma_f32_16x16x4_f32 (exact fp32 MFMA; gfx950 has no xf32) whose 400 rows are ordered
+//   * A workgroup evaluates 16 positions. The 3x3 convs are implicit GEMMs whose 400 rows are ordered
 //     SQUARE-MAJOR (row = square*16 + position): an M-tile is one board square of all 16
 //     positions. For a tap, a tile's neighbour square is on the board for the whole tile or off
 //     it for the whole tile, so off-board products are skipped instead of multiplied by zero
@@ -21,14 +26,7 @@
 //   * First layer: of the 21 input planes (common.rs:26-80) only the 4 bitboards vary across
 //     the board; the 16 card planes and the side-to-move plane are constant over all squares,
 //     so their contribution is the host-precomputed table T[square][card][channel] (sum of the
-//     folded weights over the on-board taps) added in the epilogue. The MFMA part of the first
-//     layer is therefore one k-step (4 bitboards) per (square, tap), with A values taken
-//     straight from the state's bits: the 21 planes are never materialised.
-//   * bf16 variant (OAZ_BF16, BASELINE C5): activations are stored in LDS as bf16 (row stride
-//     80 elements = 160 B: with the natural channel order the 16-lane ds_read_b128 groups hit
-//     16 distinct bank slots), 64->64 convs use v_mfma_f32_16x16x32_bf16 (K = 32: two MFMAs per
-//     (square, tap, N-tile) instead of sixteen), accumulation, skip, bias and heads stay fp32;
-//     the first layer keeps the exact fp32 MFMA on 0/1 inputs.
+//     folded weights over the on-board taps). The 21 planes are never materialised.
 #include <hip/hip_runtime.h>
 
 #include <utility>
@@ -59,28 +57,11 @@ constexpr size_t kL1Table = 25 * 17 * kCh;
 constexpr size_t kW64 = 9 * 4 * 4 * 64 * 4;
 constexpr size_t kValueF = 64 + 4 + 64 * 25 + 64 + 64 + 4;
 constexpr size_t kPolicyF = 128 + 4 + 2500 + 52;
-// bf16 variant: 64->64 conv B fragments are bf16 [9 taps][2 K-halves][4 N-tiles][64 lanes][8],
-// stored in the float blob as 9*2*4*64*4 floats; LDS rows hold 80 bf16 (64 + 16 pad)
-constexpr size_t kW64h = 9 * 2 * 4 * 64 * 4;
-constexpr int kRSh = 80;
-constexpr int kLdsFloatsH = kSB * 25 * kRSh / 2 + kWaves * kScratch;  // 17024 floats = 68,096 B
 
-// Element type of the LDS activation image.
-template <bool BF16> struct Act;
-template <> struct Act<false> {
-    using T = float;
-    static constexpr int kRS = nn::kRS;
-    static constexpr size_t kW = nn::kW64;
-    static __device__ __forceinline__ float load(const T* p) { return *p; }
-    static __device__ __forceinline__ void store(T* p, float v) { *p = v; }
-};
-template <> struct Act<true> {
-    using T = __bf16;
-    static constexpr int kRS = nn::kRSh;
-    static constexpr size_t kW = nn::kW64h;
-    static __device__ __forceinline__ float load(const T* p) { return (float)*p; }
-    static __device__ __forceinline__ void store(T* p, float v) { *p = (__bf16)v; }
-};
+// OAZ_BF16 (k_nn_h3 in bf16 mode): 64->64 conv B fragments are bf16 [9 taps][2 K-halves][4 N-tiles]
+// [64 lanes][8], stored in the float blob as 9*2*4*64*4 floats
+constexpr size_t kW64h = 9 * 2 * 4 * 64 * 4;
+
 }  // namespace nn
 
 // Rows of this workgroup: [b0, b0 + kSB) below `end`; row loads are clamped to `cap` rows. Plain
@@ -252,36 +233,10 @@ __device__ __forceinline__ void conv_l1_const(f32x4 (&acc)[nn::kTPW], const floa
         }
 }
 
-// bf16: acc[j] += conv3x3 over 64 channels with v_mfma_f32_16x16x32_bf16. For K-half m, lane
-// l supplies A[row l&15][k = 8(l>>4) + e] = channel 32m + 8(l>>4) + e (natural order).
-__device__ __forceinline__ void conv64_bf16(f32x4 (&acc)[nn::kTPW], const __bf16* act, const bf16x8* W,
-                                            const int (&sq)[nn::kTPW], int lane, int nt, int ntiles) {
-    const int i = lane & 15, kq = lane >> 4;
-    const __bf16* base = act + i * nn::kRSh + 8 * kq;
-    for (int t = 0; t < 9; ++t) {
-        const bf16x8 b0 = W[((t * 2 + 0) * 4 + nt) * 64 + lane];
-        const bf16x8 b1 = W[((t * 2 + 1) * 4 + nt) * 64 + lane];
-#pragma unroll
-        for (int j = 0; j < nn::kTPW; ++j) {
-            const int nb = nbr_index(sq[j], t);
-            if (j < ntiles && nb < 25) {
-                const __bf16* a = base + nb * nn::kSB * nn::kRSh;
-                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(a);
-                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(a + 32);
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc[j], 0, 0, 0);
-            }
-        }
-    }
-}
-
 // C/D of v_mfma_f32_16x16x4_f32: reg r of lane l = (row (l>>4)*4 + r, col l&15) of the tile,
 // i.e. position (l>>4)*4 + r at square sq[j]; LDS row = square*16 + position.
-template <bool BF16>
-__device__ __forceinline__ void epilogue(const f32x4 (&acc)[nn::kTPW], typename nn::Act<BF16>::T* act,
-                                         const float* bias, const f32x4* skip, const int (&sq)[nn::kTPW],
-                                         int lane, int nt, int ntiles) {
-    using A = nn::Act<BF16>;
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[nn::kTPW], float* act, const float* bias, const f32x4* skip,
+                                         const int (&sq)[nn::kTPW], int lane, int nt, int ntiles) {
     const int co = nt * 16 + (lane & 15);
     const float bb = bias[co];
 #pragma unroll
@@ -292,42 +247,18 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[nn::kTPW], typename 
                 const int row = sq[j] * nn::kSB + (lane >> 4) * 4 + r;
                 float v = acc[j][r] + bb;
                 if (skip) v += skip[j][r];
-                A::store(act + row * A::kRS + co, v > 0.0f ? v : 0.0f);
+                act[row * nn::kRS + co] = v > 0.0f ? v : 0.0f;
             }
 }
 
-// First-layer epilogue: bias + constant-plane table (the mover's two cards, blue-to-move).
-template <bool BF16>
-__device__ __forceinline__ void epilogue_l1(const f32x4 (&acc)[nn::kTPW], typename nn::Act<BF16>::T* act,
-                                            const float* bias, const float* table, const int* pinfo,
-                                            const int (&sq)[nn::kTPW], int lane, int nt, int ntiles) {
-    using A = nn::Act<BF16>;
-    const int co = nt * 16 + (lane & 15);
-    const float bb = bias[co];
-#pragma unroll
-    for (int j = 0; j < nn::kTPW; ++j)
-        if (j < ntiles)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int pos = (lane >> 4) * 4 + r;
-                const int info = pinfo[pos];
-                const float* ts = table + (size_t)sq[j] * 17 * nn::kCh + co;
-                float v = acc[j][r] + bb + ts[(info & 15) * nn::kCh] + ts[((info >> 4) & 15) * nn::kCh];
-                if (info & 0x100) v += ts[16 * nn::kCh];
-                A::store(act + (sq[j] * nn::kSB + pos) * A::kRS + co, v > 0.0f ? v : 0.0f);
-            }
-}
-
-template <bool BF16>
-__device__ __forceinline__ void read_skip(f32x4 (&skip)[nn::kTPW], const typename nn::Act<BF16>::T* act,
-                                          const int (&sq)[nn::kTPW], int lane, int nt, int ntiles) {
-    using A = nn::Act<BF16>;
+__device__ __forceinline__ void read_skip(f32x4 (&skip)[nn::kTPW], const float* act, const int (&sq)[nn::kTPW], int lane,
+                                          int nt, int ntiles) {
     const int co = nt * 16 + (lane & 15);
 #pragma unroll
     for (int j = 0; j < nn::kTPW; ++j)
         if (j < ntiles)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) skip[j][r] = A::load(act + (sq[j] * nn::kSB + (lane >> 4) * 4 + r) * A::kRS + co);
+            for (int r = 0; r < 4; ++r) skip[j][r] = act[(sq[j] * nn::kSB + (lane >> 4) * 4 + r) * nn::kRS + co];
 }
 
 // value + policy heads (net.rs:152-213) for position `s` of the workgroup (one wave). ld(row, c)
@@ -450,63 +381,6 @@ __device__ __forceinline__ float wave_max_dpp(float v) {
     return fmaxf(fmaxf(readlane_f(v, 0), readlane_f(v, 16)), fmaxf(readlane_f(v, 32), readlane_f(v, 48)));
 }
 
-// heads_mlp with the MLP weights requested up front (HeadRegs, issued before the head 1x1 convs, so
-// their latency hides behind those MFMAs and barriers) and the features read as float4s; the same
-// arithmetic in the same order as heads_mlp.
-struct HeadRegs {
-    float w1[25], wp[50], b1, bp, w2, b2;
-};
-__device__ __forceinline__ void heads_fetch(HeadRegs& R, const float* p, int lane) {
-    const float* l1w = p + 68;
-    const float* l1b = l1w + 64 * 25;
-    const float* l2w = l1b + 64;
-    const float* pp = p + nn::kValueF;
-    const float* plw = pp + 132;
-    const float* plb = plw + 2500;
-    const int pl = lane < 50 ? lane : 0;  // lanes >= 50 carry no logit (masked below)
-#pragma unroll
-    for (int k = 0; k < 25; ++k) R.w1[k] = l1w[k * 64 + lane];
-#pragma unroll
-    for (int f = 0; f < 50; ++f) R.wp[f] = plw[f * 50 + pl];
-    R.b1 = l1b[lane];
-    R.bp = plb[pl];
-    R.w2 = l2w[lane];
-    R.b2 = l2w[64];
-}
-template <int NP>
-__device__ __forceinline__ void heads_mlp_r(const HeadRegs& R, const float* const (&feat)[NP], const int (&bs)[NP],
-                                            int lane, int B, float* policy, float* value) {
-    const bool pl = lane < 50;
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-        float f[76];
-#pragma unroll
-        for (int k = 0; k < 19; ++k) {  // features 0..75 (75: pad, unused)
-            const float4 v = *reinterpret_cast<const float4*>(feat[q] + 4 * k);
-            f[4 * k] = v.x;
-            f[4 * k + 1] = v.y;
-            f[4 * k + 2] = v.z;
-            f[4 * k + 3] = v.w;
-        }
-        float hj = R.b1, lg = pl ? R.bp : -INFINITY;
-#pragma unroll
-        for (int k = 0; k < 25; ++k) hj += R.w1[k] * f[k];
-        if (pl) {
-#pragma unroll
-            for (int k = 0; k < 50; ++k) lg += R.wp[k] * f[25 + k];
-        }
-        const float h = hj > 0.0f ? hj : 0.0f;
-        const float vsum = wave_sum_dpp(R.w2 * h);
-        const float mx = wave_max_dpp(lg);
-        const float e = pl ? expf(lg - mx) : 0.0f;
-        const float den = wave_sum_dpp(e);
-        if (bs[q] < B) {
-            if (pl) policy[(size_t)bs[q] * 50 + lane] = e / den;
-            if (lane == 0) value[bs[q]] = tanhf(vsum + R.b2);
-        }
-    }
-}
-
 // Heads MLPs as exact-fp32 MFMAs over the workgroup's 16 positions (8 waves): waves 0-3 the value
 // hidden layer (K = 25 features, 16 units each), waves 4-7 the policy logits (K = 50, 16 logits
 // each; logits 50..63 and K padding have zero weights). Each wave fetches only its B fragments
@@ -576,23 +450,18 @@ __device__ __forceinline__ void heads_mm(const HeadMM& R, const float* feat, flo
     }
 }
 
-template <bool BF16>
-__device__ __forceinline__ void heads(const typename nn::Act<BF16>::T* act, float* scratch, int s, const float* p,
-                                      int lane, int b, int B, float* policy, float* value) {
-    using A = nn::Act<BF16>;
-    heads_g([&](int row, int c) { return A::load(act + row * A::kRS + c); }, scratch, s, p, lane, b, B, policy,
-            value);
+__device__ __forceinline__ void heads(const float* act, float* scratch, int s, const float* p, int lane, int b, int B,
+                                      float* policy, float* value) {
+    heads_g([&](int row, int c) { return act[row * nn::kRS + c]; }, scratch, s, p, lane, b, B, policy, value);
 }
 
-template <bool BF16>
 __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __restrict__ states, int B,
                                                              const float* __restrict__ blob, int blocks,
                                                              float* __restrict__ policy,
                                                              float* __restrict__ value, TileMap tm) {
-    using A = nn::Act<BF16>;
-    constexpr int kImageFloats = BF16 ? nn::kSB * 25 * nn::kRSh / 2 : nn::kSB * 25 * nn::kRS;
-    __shared__ __attribute__((aligned(16))) float lds[BF16 ? nn::kLdsFloatsH : nn::kLdsFloats];
-    typename A::T* act = reinterpret_cast<typename A::T*>(lds);
+    constexpr int kImageFloats = nn::kSB * 25 * nn::kRS;
+    __shared__ __attribute__((aligned(16))) float lds[nn::kLdsFloats];
+    float* act = lds;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nt = wave & 3, grp = wave >> 2;
     const int ntiles = grp == 0 ? nn::kTPW : 25 - nn::kTPW;
@@ -626,7 +495,7 @@ __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __
         for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
         conv_l1(acc, bb, blob, sq, lane, nt, ntiles);
         conv_l1_const(acc, blob + nn::kL1B + nn::kCh, pinfo[lane & 15], sq, lane, nt, ntiles);
-        epilogue<BF16>(acc, act, blob + nn::kL1B, nullptr, sq, lane, nt, ntiles);
+        epilogue(acc, act, blob + nn::kL1B, nullptr, sq, lane, nt, ntiles);
         __syncthreads();
     }
 
@@ -636,235 +505,26 @@ __global__ void __launch_bounds__(64 * nn::kWaves) k_nn_sq16(const oaz_state* __
     auto conv = [&](const float* w) {
 #pragma unroll
         for (int j = 0; j < nn::kTPW; ++j) acc[j] = f32x4{};
-        if constexpr (BF16)
-            conv64_bf16(acc, act, reinterpret_cast<const bf16x8*>(w), sq, lane, nt, ntiles);
-        else
-            conv64(acc, act, reinterpret_cast<const float4*>(w), sq, lane, nt, ntiles);
+        conv64(acc, act, reinterpret_cast<const float4*>(w), sq, lane, nt, ntiles);
     };
     for (int blk = 0; blk < blocks; ++blk) {
-        read_skip<BF16>(skip, act, sq, lane, nt, ntiles);
+        read_skip(skip, act, sq, lane, nt, ntiles);
         conv(p);  // small block 1: conv + BN + ReLU
-        p += A::kW;
+        p += nn::kW64;
         __syncthreads();
-        epilogue<BF16>(acc, act, p, nullptr, sq, lane, nt, ntiles);
+        epilogue(acc, act, p, nullptr, sq, lane, nt, ntiles);
         p += nn::kCh;
         __syncthreads();
         conv(p);  // small block 2: conv + BN, + skip, ReLU
-        p += A::kW;
+        p += nn::kW64;
         __syncthreads();
-        epilogue<BF16>(acc, act, p, skip, sq, lane, nt, ntiles);
+        epilogue(acc, act, p, skip, sq, lane, nt, ntiles);
         p += nn::kCh;
         __syncthreads();
     }
     float* scratch = lds + kImageFloats + wave * nn::kScratch;
-    for (int s = wave; s < nn::kSB; s += nn::kWaves) heads<BF16>(act, scratch, s, p, lane, b0 + s, B, policy, value);
+    for (int s = wave; s < nn::kSB; s += nn::kWaves) heads(act, scratch, s, p, lane, b0 + s, B, policy, value);
 }
-
-#if OAZ_AB  // A/B build only (make AB=1): the earlier C5 kernels, superseded by k_nn_h3 in bf16 mode
-// ---- bf16, 4 waves x 4 N-tiles ------------------------------------------------------------------
-// Each wave owns all 64 output channels (4 N-tiles) of one square group, so every A fragment read
-// from LDS (one (square, tap) of 16 positions x 64 channels) feeds 8 MFMAs instead of 2: LDS
-// traffic per MFMA drops 4x, which is what bounds the 8-wave bf16 variant. Groups (corner, edges,
-// interior squares; on-board taps 40 / 40 / 46 / 43):
-namespace nn4 {
-constexpr int kTPW = 7;
-constexpr int lds_floats(int waves) { return nn::kSB * 25 * nn::kRSh / 2 + waves * nn::kScratch; }
-}
-__constant__ int8_t c_sq4[4][nn4::kTPW] = {{0, 1, 2, 3, 6, 7, 0}, {4, 9, 14, 19, 8, 13, 0},
-                                           {20, 5, 10, 15, 21, 11, 16}, {24, 22, 23, 12, 17, 18, 0}};
-__constant__ int8_t c_sq4_n[4] = {6, 6, 7, 6};
-
-// NPW = N-tiles per wave: 4 -> 4 waves (one per square group), 2 -> 8 waves (2 per group).
-template <int NPW>
-__global__ void __launch_bounds__(64 * 16 / NPW) k_nn_bf16g(const oaz_state* __restrict__ states, int B,
-                                                           const float* __restrict__ blob, int blocks,
-                                                           float* __restrict__ policy, float* __restrict__ value) {
-    constexpr int kWaves = 16 / NPW, kSplit = 4 / NPW;
-    constexpr int kImageFloats = nn::kSB * 25 * nn::kRSh / 2;
-    constexpr int T = nn4::kTPW;
-    __shared__ __attribute__((aligned(16))) float lds[nn4::lds_floats(kWaves)];
-    __bf16* act = reinterpret_cast<__bf16*>(lds);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int i = lane & 15, kq = lane >> 4;
-    const int grp = wave / kSplit, n0 = (wave % kSplit) * NPW;
-    const int ntiles = c_sq4_n[grp];
-    int sq[T];
-#pragma unroll
-    for (int j = 0; j < T; ++j) sq[j] = c_sq4[grp][j];
-    const int b0 = blockIdx.x * nn::kSB;
-    int* pinfo = reinterpret_cast<int*>(lds + kImageFloats);
-    f32x4 acc[T][NPW];
-
-    // first layer: 4 bitboards through the fp32 MFMA + the constant-plane table (see k_nn_sq16)
-    {
-        const int b = b0 + i < B ? b0 + i : b0;
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
-        const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
-        if (tid < nn::kSB) {
-            const oaz_state st = states[b];
-            const int blue = st.to_move & 1;
-            const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
-            pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < T; ++j)
-#pragma unroll
-            for (int n = 0; n < NPW; ++n) acc[j][n] = f32x4{};
-        for (int t = 0; t < 9; ++t) {
-            float bw[NPW];
-#pragma unroll
-            for (int n = 0; n < NPW; ++n) bw[n] = blob[(t * 4 + n0 + n) * 64 + lane];
-#pragma unroll
-            for (int j = 0; j < T; ++j) {
-                const int nb = nbr_index(sq[j], t);
-                if (j < ntiles && nb < 25) {
-                    const float a = (float)((bb >> (31 - nb)) & 1u);
-#pragma unroll
-                    for (int n = 0; n < NPW; ++n) acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bw[n], acc[j][n], 0, 0, 0);
-                }
-            }
-        }
-        {  // constant planes (cards, colour) as 5 MFMA k-steps per (square, N-tile), see conv_l1_const
-            const float* table = blob + nn::kL1B + nn::kCh;
-            const int cinfo = pinfo[i];
-            const int c0 = cinfo & 15, c1 = (cinfo >> 4) & 15, blue = (cinfo >> 8) & 1;
-            float a[5];
-#pragma unroll
-            for (int st = 0; st < 5; ++st) {
-                const int k = 4 * st + kq;
-                a[st] = k < 16 ? ((k == c0 || k == c1) ? 1.0f : 0.0f) : (k == 16 ? (float)blue : 0.0f);
-            }
-#pragma unroll
-            for (int j = 0; j < T; ++j)
-                if (j < ntiles)
-#pragma unroll
-                    for (int n = 0; n < NPW; ++n) {
-                        const float* ts = table + (size_t)sq[j] * 17 * nn::kCh + (n0 + n) * 16 + i;
-#pragma unroll
-                        for (int st = 0; st < 5; ++st) {
-                            const int k = 4 * st + kq;
-                            const float b = k < 17 ? ts[k * nn::kCh] : 0.0f;
-                            acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], b, acc[j][n], 0, 0, 0);
-                        }
-                    }
-        }
-        const float* bias = blob + nn::kL1B;
-#pragma unroll
-        for (int n = 0; n < NPW; ++n) {
-            const int co = (n0 + n) * 16 + i;
-            const float bbias = bias[co];
-#pragma unroll
-            for (int j = 0; j < T; ++j)
-                if (j < ntiles)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float v = acc[j][n][r] + bbias;
-                        act[(sq[j] * nn::kSB + kq * 4 + r) * nn::kRSh + co] = (__bf16)(v > 0.0f ? v : 0.0f);
-                    }
-        }
-        __syncthreads();
-    }
-
-    const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
-    // residual input kept as packed bf16 pairs (exact: the LDS image is bf16)
-    uint32_t skip[T][NPW][2];
-    const __bf16* abase = act + i * nn::kRSh + 8 * kq;
-    auto conv = [&](const bf16x8* W) {
-#pragma unroll
-        for (int j = 0; j < T; ++j)
-#pragma unroll
-            for (int n = 0; n < NPW; ++n) acc[j][n] = f32x4{};
-        for (int t = 0; t < 9; ++t) {
-            bf16x8 bw[2][NPW];
-#pragma unroll
-            for (int m = 0; m < 2; ++m)
-#pragma unroll
-                for (int n = 0; n < NPW; ++n) bw[m][n] = W[((t * 2 + m) * 4 + n0 + n) * 64 + lane];
-            // scalar offsets / on-board mask; A fragments of a batch requested before its MFMAs
-            int off[T];
-            uint32_t vm = 0;
-#pragma unroll
-            for (int j = 0; j < T; ++j) {
-                const int nb = nbr_index(sq[j], t);
-                const bool ok = j < ntiles && nb < 25;
-                off[j] = __builtin_amdgcn_readfirstlane((ok ? nb : sq[j]) * nn::kSB * nn::kRSh);
-                vm |= (ok ? 1u : 0u) << j;
-            }
-            vm = __builtin_amdgcn_readfirstlane(vm);
-            constexpr int kH = (T + 1) / 2;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                bf16x8 a0[kH], a1[kH];
-#pragma unroll
-                for (int q = 0; q < kH; ++q) {
-                    const int j = h * kH + q;
-                    if (j < T) {
-                        a0[q] = *reinterpret_cast<const bf16x8*>(abase + off[j]);
-                        a1[q] = *reinterpret_cast<const bf16x8*>(abase + off[j] + 32);
-                    }
-                }
-#pragma unroll
-                for (int q = 0; q < kH; ++q) {
-                    const int j = h * kH + q;
-                    if (j < T && (vm & (1u << j)))
-#pragma unroll
-                        for (int n = 0; n < NPW; ++n) {
-                            acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[q], bw[0][n], acc[j][n], 0, 0, 0);
-                            acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[q], bw[1][n], acc[j][n], 0, 0, 0);
-                        }
-                }
-            }
-        }
-    };
-    auto epilogue = [&](const float* bias, bool with_skip) {
-#pragma unroll
-        for (int n = 0; n < NPW; ++n) {
-            const int co = (n0 + n) * 16 + i;
-            const float bb = bias[co];
-#pragma unroll
-            for (int j = 0; j < T; ++j)
-                if (j < ntiles)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float v = acc[j][n][r] + bb;
-                        if (with_skip) {
-                            const uint32_t w = skip[j][n][r >> 1];
-                            v += __uint_as_float((r & 1) ? (w & 0xFFFF0000u) : (w << 16));
-                        }
-                        act[(sq[j] * nn::kSB + kq * 4 + r) * nn::kRSh + co] = (__bf16)(v > 0.0f ? v : 0.0f);
-                    }
-        }
-    };
-    for (int blk = 0; blk < blocks; ++blk) {
-#pragma unroll
-        for (int n = 0; n < NPW; ++n)
-#pragma unroll
-            for (int j = 0; j < T; ++j)
-                if (j < ntiles)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const unsigned short* q = reinterpret_cast<const unsigned short*>(
-                            act + (sq[j] * nn::kSB + kq * 4 + 2 * h) * nn::kRSh + (n0 + n) * 16 + i);
-                        skip[j][n][h] = (uint32_t)q[0] | ((uint32_t)q[nn::kRSh] << 16);
-                    }
-        conv(reinterpret_cast<const bf16x8*>(p));  // small block 1: conv + BN + ReLU
-        p += nn::kW64h;
-        __syncthreads();
-        epilogue(p, false);
-        p += nn::kCh;
-        __syncthreads();
-        conv(reinterpret_cast<const bf16x8*>(p));  // small block 2: conv + BN, + skip, ReLU
-        p += nn::kW64h;
-        __syncthreads();
-        epilogue(p, true);
-        p += nn::kCh;
-        __syncthreads();
-    }
-    float* scratch = lds + kImageFloats + wave * nn::kScratch;
-    for (int s = wave; s < nn::kSB; s += kWaves) heads<true>(act, scratch, s, p, lane, b0 + s, B, policy, value);
-}
-#endif  // OAZ_AB
 
 // ---- fp32 split (OAZ_FP32_SPLIT): bf16x6 MFMA with fp32-level error ------------------------------
 // Every fp32 operand x (activation or folded weight) is split EXACTLY into three bf16 terms,
@@ -917,31 +577,16 @@ __device__ __forceinline__ float load_at(const char* img, int o) {  // h + m + l
 __device__ __forceinline__ float load(const char* img, int row, int c) { return load_at(img, elem_off(row, c)); }
 }  // namespace x6
 
-// Square groups (compile-time): GRP 0 / 1 are the two halves of the 8-wave kernel (waves 0-3 /
-// 4-7; 4 corners + 4 edges + 5 interior | 8 edges + 4 interior = 85 / 84 on-board taps), GRP 2 is
-// the whole board (4-wave kernel: one wave per SIMD, all 25 squares of one N-tile).
-constexpr int8_t kSqOrder[25] = {0, 4, 20, 24, 1, 3, 21, 23, 6, 8, 12, 16, 18,
-                                 2, 5, 10, 15, 9, 14, 19, 22, 7, 11, 13, 17};
-// GRP 3 / 4: an uneven split for the two waves of a SIMD (interior + corners + 2 edges = 109
-// on-board taps | the other 10 edges = 60): the older wave wins MFMA arbitration and runs ahead,
-// the younger fills its gaps, so equal halves leave the younger finishing alone.
+// Square groups (compile-time) of the split kernels: the two waves of a SIMD (waves w and w + 4)
+// own N-tile w & 3 of two disjoint square groups, cut unevenly from kSqOrderU (interior, corners,
+// then edges): the older wave wins MFMA arbitration and runs ahead, the younger fills its gaps, so
+// equal halves leave the younger finishing alone. GRP 3 / 4: 15 / 10 squares (109 / 60 on-board
+// taps; k_nn_x6), GRP 7 / 8: 17 / 8 (k_nn_h3; measured 1-2 % faster than 15 / 10 there).
 constexpr int8_t kSqOrderU[25] = {6, 7, 8, 11, 12, 13, 16, 17, 18, 0, 4, 20, 24, 2, 22,
                                   1, 3, 5, 10, 9, 14, 15, 19, 21, 23};
-// GRP 5 / 6: 16 / 9 squares (115 / 54 taps), same order with one more edge in the first group;
-// GRP 7 / 8: 17 / 8 (the default, measured 1-2 % faster than 15 / 10), GRP 9 / 10: 18 / 7.
-// GRP 11-14: the four groups of k_nn_q2 (3 interior + 2 edges + 1 corner = 43 on-board taps |
-// 2 interior + 4 edges = 42 | 2 + 4 = 42 | 2 interior + 2 edges + 3 corners = 42)
-constexpr int8_t kSqOrderQ[25] = {0, 1, 2, 6, 7, 8, 3, 5, 10, 11, 12, 15, 9, 13, 14, 16, 19, 21,
-                                  4, 17, 18, 20, 22, 23, 24};
-constexpr int grp_n(int grp) {
-    return grp >= 11 ? (grp == 14 ? 7 : 6) : grp == 0 ? nn::kTPW : grp == 1 ? 25 - nn::kTPW : grp == 3 ? 15 : grp == 4 ? 10 : grp == 5 ? 16 : grp == 6 ? 9
-         : grp == 7 ? 17 : grp == 8 ? 8 : grp == 9 ? 18 : grp == 10 ? 7 : 25;
-}
-constexpr int grp_sq(int grp, int j) {
-    return grp >= 11 ? kSqOrderQ[(grp - 11) * 6 + j] : grp == 2 ? j : grp >= 9 ? kSqOrderU[(grp - 9) * 18 + j] : grp >= 7 ? kSqOrderU[(grp - 7) * 17 + j]
-         : grp >= 5 ? kSqOrderU[(grp - 5) * 16 + j]
-         : grp >= 3 ? kSqOrderU[(grp - 3) * 15 + j] : kSqOrder[grp * nn::kTPW + j];
-}
+constexpr int grp_n(int grp) { return grp == 3 ? 15 : grp == 4 ? 10 : grp == 7 ? 17 : 8; }
+constexpr int grp_first(int grp) { return grp == 4 ? 15 : grp == 8 ? 17 : 0; }
+constexpr int grp_sq(int grp, int j) { return kSqOrderU[grp_first(grp) + j]; }
 
 // On-board squares of group GRP for tap T: the conv is straight-line code per (group, tap), with no
 // per-MFMA on-board tests.
@@ -1000,110 +645,64 @@ struct X6PlanOf {
     static constexpr X6Plan P = x6_plan(GRP, KH);
 };
 
-// k_nn_h3 plan: the group's squares in NPH phases (consecutive slices of the square list), each
-// phase a full pass over the 18 (tap, K-half) steps cut into batches of <= KH squares. A batch
-// also carries the squares of the previous phase whose epilogue (pack) it runs between its MFMAs,
-// so only the last phase's packs remain after the conv. first: the batch starts a step run (its
-// B pieces were prefetched); nstep: the step of the next run (its B pieces are prefetched now).
+// k_nn_h3 plan: the 18 (tap, K-half) steps of the group cut into batches of <= KH squares. first:
+// the batch starts a step run (its B pieces were prefetched); nstep: the step of the next run (its B
+// pieces are prefetched now).
 struct H3Batch {
-    int t, m, n, first, nstep, ne, nnstep;  // nnstep: the step of the run after next (BD 2)
-    int8_t j[16], nb[16], e[16];
+    int t, m, n, first, nstep;
+    int8_t j[16], nb[16];
 };
 struct H3Plan {
-    int nbat, tail;  // tail: first square index packed after the conv
-    H3Batch b[160];
+    int nbat;
+    H3Batch b[96];
 };
-// khf 0: the 18 (tap, K-half) steps interleaved; khf 1 / 2: only the 9 taps of K-half 0 / 1 (the
-// staggered kernel runs each K-half of a conv in its own barrier interval).
-constexpr H3Plan h3_plan(int grp, int kh, int nph, int khf = 0) {
+constexpr H3Plan h3_plan(int grp, int kh) {
     H3Plan P{};
-    const int n = grp_n(grp);
-    for (int ph = 0; ph < nph; ++ph) {
-        const int lo = ph * n / nph, hi = (ph + 1) * n / nph;
-        const int b0 = P.nbat;
-        for (int s0 = 0; s0 < (khf ? 9 : 18); ++s0) {
-            const int s = khf ? s0 * 2 + (khf - 1) : s0;  // step = tap * 2 + K-half
-            const TapList L0 = tap_list(grp, s / 2);
-            TapList L{};
-            for (int q = 0; q < L0.n; ++q)
-                if (L0.j[q] >= lo && L0.j[q] < hi) {
-                    L.j[L.n] = L0.j[q];
-                    L.nb[L.n] = L0.nb[q];
-                    ++L.n;
-                }
-            const int nb = (L.n + kh - 1) / kh;
-            int q = 0;
-            for (int k = 0; k < nb; ++k) {
-                const int m = (L.n - q) / (nb - k);
-                H3Batch B{};
-                B.t = s / 2;
-                B.m = s % 2;
-                B.n = m;
-                B.first = k == 0;
-                B.nstep = -1;
-                for (int i = 0; i < m; ++i) {
-                    B.j[i] = L.j[q + i];
-                    B.nb[i] = L.nb[q + i];
-                }
-                q += m;
-                P.b[P.nbat++] = B;
+    for (int s = 0; s < 18; ++s) {  // step = tap * 2 + K-half
+        const TapList L = tap_list(grp, s / 2);
+        const int nb = (L.n + kh - 1) / kh;
+        int q = 0;
+        for (int k = 0; k < nb; ++k) {
+            const int m = (L.n - q) / (nb - k);  // near-equal split, larger batches last
+            H3Batch B{};
+            B.t = s / 2;
+            B.m = s % 2;
+            B.n = m;
+            B.first = k == 0;
+            B.nstep = -1;
+            for (int i = 0; i < m; ++i) {
+                B.j[i] = L.j[q + i];
+                B.nb[i] = L.nb[q + i];
             }
+            q += m;
+            P.b[P.nbat++] = B;
         }
-        if (ph > 0) {  // spread the previous phase's packs over this phase's batches
-            const int plo = (ph - 1) * n / nph, cnt = lo - plo, nbt = P.nbat - b0;
-            for (int i = 0; i < cnt; ++i) {
-                H3Batch& B = P.b[b0 + (i * nbt) / cnt];
-                B.e[B.ne++] = (int8_t)(plo + i);
-            }
-        }
-        P.tail = lo;
     }
-    int next = -1, next2 = -1;
-    for (int k = P.nbat - 1; k >= 0; --k) {
+    int next = -1;
+    for (int k = P.nbat - 1; k >= 0; --k)
         if (P.b[k].first) {
             P.b[k].nstep = next;
-            P.b[k].nnstep = next2;
-            next2 = next;
             next = P.b[k].t * 2 + P.b[k].m;
         }
-    }
     return P;
 }
-template <int GRP, int KH, int NPH, int KHF = 0>
+template <int GRP, int KH>
 struct H3PlanOf {
-    static constexpr H3Plan P = h3_plan(GRP, KH, NPH, KHF);
+    static constexpr H3Plan P = h3_plan(GRP, KH);
 };
 
-// Kernel configuration. WAVES 8: two waves per SIMD (square groups 0/1 x 4 N-tiles, <= 256 VGPRs);
-// WAVES 4: one wave per SIMD owning one N-tile of all 25 squares (up to 512 VGPRs). KH: squares per
-// batch. PIPE 1: two A-piece buffers (the m pieces of batch k+1 load during batch k's last
-// products); PIPE 2: three buffers (m, h, l each loaded one batch ahead). DBG 2 (timing only,
-// wrong results): per-wave s_memtime phase sums over the first policy rows (tools/nn_phases.py).
-// UNEVEN (8 waves): square groups 3 / 4 (15 / 10 squares) instead of 0 / 1, the bigger group at
-// s_setprio 1.
-template <int WAVES_, int KH_, int PIPE_, int DBG_ = 0, int UNEVEN_ = 0, int TR_ = 0, int PH_ = 1, int HV_ = 0,
-          int BF_ = 0, int PF_ = 0, int STG_ = 0, int EP_ = 0, int PHA_ = 0, int BD_ = 1, int Q2_ = 0>
-struct X6Cfg {
-    // h3 + TR, 8 waves, even 13 / 12 split: waves 0-3 (N-tiles 0, 1) and 4-7 (N-tiles 2, 3) run each
-    // conv's two K-halves and their epilogue in three barrier intervals, waves 4-7 one interval
-    // behind, so one wave's epilogue runs beside its SIMD partner's MFMAs (nn_h3_body). 2: + s_setprio 1
-    // for waves 4-7.
-    static constexpr int STG = STG_;
-    static constexpr int BD = BD_;  // h3: B pieces loaded BD step runs ahead (1 or 2)
-    static constexpr int Q2 = Q2_;  // k_nn_q2: two N-tiles per wave over four square groups (GRP 11-14)
-    static constexpr int EP = EP_;    // h3 + TR: convs in pairs, the residual parity at compile time
-    static constexpr int PHA = PHA_;  // h3 + TR, UNEVEN 3: the first (17-square) group in PHA phases
-    static constexpr int PF = PF_;  // h3 + TR: the next conv's first B pieces load during this conv's last steps
-    static constexpr int BF = BF_;  // h3 + TR: OAZ_BF16 mode (one bf16 piece, one product; C5)
-    static constexpr int HV = HV_;  // h3 heads: 0 MLPs on MFMA (8 waves), 1 per-position VALU MLPs
-    static constexpr int TR = TR_;
-    static constexpr int PH = PH_;  // h3 + TR: square phases of the second (younger) group
-    static constexpr int WAVES = WAVES_;
-    static constexpr int UNEVEN = UNEVEN_;
-    static constexpr int NS = Q2_ ? 7 : WAVES_ == 8 ? (UNEVEN_ == 4 ? 18 : UNEVEN_ == 3 ? 17 : UNEVEN_ == 2 ? 16 : UNEVEN_ ? 15 : nn::kTPW) : 25;  // tiles per wave
-    static constexpr int KH = KH_;
-    static constexpr int PIPE = PIPE_;
-    static constexpr int DBG = DBG_;
+// Kernel configurations (8 waves: two per SIMD, square groups GRP0 / GRP1 x 4 N-tiles, <= 256 VGPRs;
+// KH: squares per batch of A fragments). DBG (diagnostic builds only, `make AB=1`; timing only, wrong
+// results): 2 per-wave s_memtime phase sums written over the first policy rows (tools/nn_phases.py),
+// 3 no conv A reads, 4 no conv B loads (ablations), 5 workgroup start / end stamps
+// (tools/nn_timeline.py).
+template <int DBG_ = 0>
+struct X6Cfg {  // k_nn_x6 (OAZ_FP32_SPLIT, and k_nn_h3's fp16-range recompute): 15 / 10 squares
+    static constexpr int WAVES = 8, KH = 4, NS = 15, GRP0 = 3, GRP1 = 4, TR = 0, DBG = DBG_;
+};
+template <int BF_, int DBG_ = 0>
+struct H3Cfg {  // k_nn_h3: 17 / 8 squares; BF: OAZ_BF16 mode (one bf16 piece, one product; C5)
+    static constexpr int WAVES = 8, KH = 4, NS = 17, GRP0 = 7, GRP1 = 8, TR = 1, BF = BF_, DBG = DBG_;
 };
 
 // A-fragment loads / MFMAs of batch K (compile-time: the LDS address is one of six per-lane bases
@@ -1181,27 +780,6 @@ __device__ __forceinline__ void conv_x6_batch(f32x4 (&acc)[C::NS], const char* i
     __builtin_amdgcn_sched_barrier(0);      // bound the live ranges: no loads hoisted across batches
 }
 
-// PIPE 2, batch K: three buffers, each piece loaded one batch ahead of its use
-//   load BL = l | m*Bh, m*Bm | load BM = next m | h*Bh, h*Bm, h*Bl | load BH = next h | l*Bh
-template <class C, int GRP, int K>
-__device__ __forceinline__ void conv_x6_batch3(f32x4 (&acc)[C::NS], const char* img, const X6W& W,
-                                               bf16x8 (&b)[3], bf16x8 (&bn)[3], bf16x8 (&BM)[C::KH],
-                                               bf16x8 (&BH)[C::KH], bf16x8 (&BL)[C::KH], const int (&ab)[2][3]) {
-    constexpr int KH = C::KH, NS = C::NS;
-    constexpr bool more = K + 1 < X6PlanOf<GRP, KH>::P.nbat;
-    x6_step_b<C, GRP, K>(W, b, bn);
-    x6_load<GRP, KH, K>(BL, img, ab, 2);
-    x6_mfma<GRP, KH, K, NS>(acc, BM, b[0]);  // mh
-    x6_mfma<GRP, KH, K, NS>(acc, BM, b[1]);  // mm
-    if constexpr (more) x6_load<GRP, KH, K + 1>(BM, img, ab, 1);
-    x6_mfma<GRP, KH, K, NS>(acc, BH, b[0]);  // hh
-    x6_mfma<GRP, KH, K, NS>(acc, BH, b[1]);  // hm
-    x6_mfma<GRP, KH, K, NS>(acc, BH, b[2]);  // hl
-    if constexpr (more) x6_load<GRP, KH, K + 1>(BH, img, ab, 0);
-    x6_mfma<GRP, KH, K, NS>(acc, BL, b[0]);  // lh
-    __builtin_amdgcn_sched_barrier(0);
-}
-
 template <class C, int GRP, int... K>
 __device__ __forceinline__ void conv_x6_run(f32x4 (&acc)[C::NS], const char* img, const X6W& W, const int (&lo)[2],
                                             std::integer_sequence<int, K...>) {
@@ -1213,18 +791,11 @@ __device__ __forceinline__ void conv_x6_run(f32x4 (&acc)[C::NS], const char* img
     bf16x8 b[3], bn[3];
 #pragma unroll
     for (int pc = 0; pc < 3; ++pc) b[pc] = x6_ldb(W, pc * 4);
-    if constexpr (C::PIPE == 2) {
-        bf16x8 BM[C::KH], BH[C::KH], BL[C::KH];
-        x6_load<GRP, C::KH, 0>(BM, img, ab, 1);
-        x6_load<GRP, C::KH, 0>(BH, img, ab, 0);
-        (conv_x6_batch3<C, GRP, K>(acc, img, W, b, bn, BM, BH, BL, ab), ...);
-    } else {
-        bf16x8 X[C::KH], Y[C::KH];
-        x6_load<GRP, C::KH, 0>(X, img, ab, 1);
-        ((K % 2 == 0 ? conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab)
-                     : conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, Y, X, ab)),
-         ...);
-    }
+    bf16x8 X[C::KH], Y[C::KH];
+    x6_load<GRP, C::KH, 0>(X, img, ab, 1);
+    ((K % 2 == 0 ? conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab)
+                 : conv_x6_batch<C, GRP, K>(acc, img, W, b, bn, Y, X, ab)),
+     ...);
 }
 
 // bias (+ residual), ReLU, split into the three LDS planes; C/D layout as in epilogue<>. Lanes co
@@ -1504,20 +1075,12 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_x6(const oaz_state* __rest
                                                         TileMap tm) {
     __shared__ __attribute__((aligned(16))) float lds[x6::kLdsFloats];
     const TileSpan sp = tile_span(tm, B);
-    if constexpr (C::WAVES == 4) {
-        nn_x6_body<C, 2>(states, sp, blob, blocks, policy, value, lds);
-    } else if constexpr (C::UNEVEN) {
-        constexpr int g0 = C::UNEVEN == 4 ? 9 : C::UNEVEN == 3 ? 7 : C::UNEVEN == 2 ? 5 : 3;
-        if ((threadIdx.x >> 8) == 0) {
-            __builtin_amdgcn_s_setprio(1);
-            nn_x6_body<C, g0>(states, sp, blob, blocks, policy, value, lds);
-        } else {
-            nn_x6_body<C, g0 + 1>(states, sp, blob, blocks, policy, value, lds);
-        }
-    } else if ((threadIdx.x >> 8) == 0)  // waves 0-3: square group 0, waves 4-7: group 1
-        nn_x6_body<C, 0>(states, sp, blob, blocks, policy, value, lds);
-    else
-        nn_x6_body<C, 1>(states, sp, blob, blocks, policy, value, lds);
+    if ((threadIdx.x >> 8) == 0) {  // waves 0-3: the bigger square group, ahead in MFMA arbitration
+        __builtin_amdgcn_s_setprio(1);
+        nn_x6_body<C, C::GRP0>(states, sp, blob, blocks, policy, value, lds);
+    } else {
+        nn_x6_body<C, C::GRP1>(states, sp, blob, blocks, policy, value, lds);
+    }
 }
 
 // ---- fp32 split over fp16 (OAZ_FP32_SPLIT16): three f16 MFMA products per fp32 MAC -----------------
@@ -1547,15 +1110,8 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-// Phases of group GRP's squares (C::PH for the second group of the TR kernel, else 1).
 template <class C, int GRP>
-constexpr int h3_nph() {
-    return (C::TR && (GRP == 1 || GRP == 4 || GRP == 6)) ? C::PH : (C::PHA && GRP == 7) ? C::PHA : 1;
-}
-// GRP may carry a K-half filter in bits 5-6 (h3_khalf): the plan functions below then run one K-half.
-template <class C, int GRP>
-using H3P = H3PlanOf<GRP & 31, C::KH, h3_nph<C, GRP & 31>(), (GRP >> 5)>;
-constexpr int h3_khalf(int grp, int m) { return grp | ((m + 1) << 5); }
+using H3P = H3PlanOf<GRP, C::KH>;
 
 // A-fragment loads / MFMAs of batch K; the LDS address is one of four per-lane bases
 // ab[m][seg] = lo[m] + seg * 64 KiB plus an immediate offset < 64 KiB (piece 1 = + kPlaneB)
@@ -1571,9 +1127,9 @@ __device__ __forceinline__ void h3_load(f16x8 (&a)[N], const char* img, const in
         }
 }
 
-// TR: the operands swapped (weights as A, positions as B), so the C/D tile is transposed: lane =
-// (position lane & 15, channels 4 * (lane >> 4) + r of the N-tile) -- the A/B fragment layouts of
-// 16x16x32 are symmetric, so the same registers serve either order.
+// Transposed C/D tiles: the operands swapped (weights as A, positions as B), so a lane holds the
+// position lane & 15 and the channels 4 * (lane >> 4) + r of the N-tile -- the A/B fragment layouts
+// of 16x16x32 are symmetric, so the same registers serve either order.
 template <class C, int GRP, int K, int N>
 __device__ __forceinline__ void h3_mfma(f32x4 (&acc)[C::NS], const f16x8 (&a)[N], const f16x8& bv) {
     constexpr H3Batch B = H3P<C, GRP>::P.b[K];
@@ -1583,15 +1139,7 @@ __device__ __forceinline__ void h3_mfma(f32x4 (&acc)[C::NS], const f16x8 (&a)[N]
             acc[B.j[q]] = C::BF ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bv),
                                                                           __builtin_bit_cast(bf16x8, a[q]), acc[B.j[q]],
                                                                           0, 0, 0)
-                          : C::TR ? __builtin_amdgcn_mfma_f32_16x16x32_f16(bv, a[q], acc[B.j[q]], 0, 0, 0)
-                                  : __builtin_amdgcn_mfma_f32_16x16x32_f16(a[q], bv, acc[B.j[q]], 0, 0, 0);
-}
-
-// the packs of earlier-phase squares that batch K runs (compile-time list)
-template <class C, int GRP, int K, class E, int... I>
-__device__ __forceinline__ void h3_epi(E& epi, std::integer_sequence<int, I...>) {
-    constexpr H3Batch B = H3P<C, GRP>::P.b[K];
-    ((I < B.ne ? epi(std::integral_constant<int, B.e[I < B.ne ? I : 0]>{}) : void()), ...);
+                                : __builtin_amdgcn_mfma_f32_16x16x32_f16(bv, a[q], acc[B.j[q]], 0, 0, 0);
 }
 
 // B pieces of (tap, K-half) step S for N-tile nt: [step][piece][N-tile][lane] f16x8, buffer loads
@@ -1604,32 +1152,22 @@ __device__ __forceinline__ X6W h3_w(const float* p, int lane, int nt, int bytes 
 __device__ __forceinline__ f16x8 h3_ldb(const X6W& w, int entry) {  // entry = (step * 2 + piece) * 4
     return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(w.r, w.voff, entry * 64 * 16, 0));
 }
-__device__ __forceinline__ f16x8 h3_ldb_at(const X6W& w, int bytes) {
-    return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(w.r, w.voff, bytes, 0));
-}
 
-// B pieces: b = the current step run's, bn[0..1] = the next run's, bn[2..3] = the run after next
-// (BD 2: loads issued two step runs ahead; BD 1: one)
+// B pieces: b = the current step run's, bn = the next run's (loaded one step run ahead)
 template <class C, int GRP, int K>
-__device__ __forceinline__ void h3_step_b(const X6W& W, f16x8 (&b)[2], f16x8 (&bn)[4]) {
+__device__ __forceinline__ void h3_step_b(const X6W& W, f16x8 (&b)[2], f16x8 (&bn)[2]) {
     constexpr H3Batch B = H3P<C, GRP>::P.b[K];
     if constexpr (B.first && K > 0) {
         b[0] = bn[0];
         b[1] = bn[1];
-        if constexpr (C::BD == 2) {
-            bn[0] = bn[2];
-            bn[1] = bn[3];
-        }
     }
-    constexpr int ld = C::BD == 2 ? B.nnstep : B.nstep;
-    constexpr int o = C::BD == 2 ? 2 : 0;
-    if constexpr (B.first && ld >= 0 && C::DBG != 4) {  // prefetch a later step run's B pieces
-                                                         // (DBG 4: ablation, no B loads)
+    if constexpr (B.first && B.nstep >= 0 && C::DBG != 4) {  // prefetch the next step run's B pieces
+                                                              // (DBG 4: ablation, no B loads)
         if constexpr (C::BF) {  // BF: [step][N-tile][lane] bf16x8, one piece
-            bn[o] = h3_ldb(W, ld * 4);
+            bn[0] = h3_ldb(W, B.nstep * 4);
         } else {
-            bn[o] = h3_ldb(W, (ld * 2 + 0) * 4);
-            bn[o + 1] = h3_ldb(W, (ld * 2 + 1) * 4);
+            bn[0] = h3_ldb(W, (B.nstep * 2 + 0) * 4);
+            bn[1] = h3_ldb(W, (B.nstep * 2 + 1) * 4);
         }
     }
 }
@@ -1638,7 +1176,7 @@ __device__ __forceinline__ void h3_step_b(const X6W& W, f16x8 (&b)[2], f16x8 (&b
 // (two buffers, roles swap with K's parity)
 template <class C, int GRP, int K>
 __device__ __forceinline__ void conv_h1_batch(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
-                                              f16x8 (&bn)[4], f16x8 (&X)[C::KH], f16x8 (&Xn)[C::KH],
+                                              f16x8 (&bn)[2], f16x8 (&X)[C::KH], f16x8 (&Xn)[C::KH],
                                               const int (&ab)[2][2]) {
     h3_step_b<C, GRP, K>(W, b, bn);
     if constexpr (K + 1 < H3P<C, GRP>::P.nbat) h3_load<C, GRP, K + 1>(Xn, img, ab, 0);
@@ -1646,67 +1184,31 @@ __device__ __forceinline__ void conv_h1_batch(f32x4 (&acc)[C::NS], const char* i
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// PIPE 1, batch K (X holds its lo pieces on entry and the next batch's on exit):
-//   load Y = hi | lo*Bhi | load X = next lo | hi*Bhi, hi*Blo | earlier-phase packs
-template <class C, int GRP, int K, class E>
+// fp16x3 batch K (X holds its lo pieces on entry and the next batch's on exit):
+//   load Y = hi | lo*Bhi | load X = next lo | hi*Bhi, hi*Blo
+template <class C, int GRP, int K>
 __device__ __forceinline__ void conv_h3_batch(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
-                                              f16x8 (&bn)[4], f16x8 (&X)[C::KH], f16x8 (&Y)[C::KH],
-                                              const int (&ab)[2][2], E& epi, f16x8 (*carry)[2] = nullptr) {
+                                              f16x8 (&bn)[2], f16x8 (&X)[C::KH], f16x8 (&Y)[C::KH],
+                                              const int (&ab)[2][2]) {
     h3_step_b<C, GRP, K>(W, b, bn);
-    if constexpr (C::PF) {  // the last step run: prefetch the next conv's first pieces (one conv further on)
-        constexpr H3Batch B = H3P<C, GRP>::P.b[K];
-        constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
-        if constexpr (B.first && B.nstep < 0) {
-            constexpr int next = (int)((h3::kW + 2 * nn::kCh) * 4);  // bytes per conv
-            (*carry)[0] = h3_ldb_at(W, next + ((B0.t * 2 + B0.m) * 2 + 0) * 4 * 64 * 16);
-            (*carry)[1] = h3_ldb_at(W, next + ((B0.t * 2 + B0.m) * 2 + 1) * 4 * 64 * 16);
-        }
-    }
     h3_load<C, GRP, K>(Y, img, ab, 0);
     h3_mfma<C, GRP, K>(acc, X, b[0]);  // lo*hi
     if constexpr (K + 1 < H3P<C, GRP>::P.nbat) h3_load<C, GRP, K + 1>(X, img, ab, 1);
     h3_mfma<C, GRP, K>(acc, Y, b[0]);  // hi*hi
     h3_mfma<C, GRP, K>(acc, Y, b[1]);  // hi*lo
-    h3_epi<C, GRP, K>(epi, std::make_integer_sequence<int, 16>{});
     __builtin_amdgcn_sched_barrier(0);  // bound the live ranges: no loads hoisted across batches
 }
 
-// PIPE 2, batch K: both pieces of batch K+1 load during batch K (four buffers, roles swap with K's
-// parity):  lo*Bhi | load next lo | hi*Bhi | load next hi | hi*Blo
-template <class C, int GRP, int K, class E>
-__device__ __forceinline__ void conv_h3_batch2(f32x4 (&acc)[C::NS], const char* img, const X6W& W, f16x8 (&b)[2],
-                                               f16x8 (&bn)[4], f16x8 (&L)[C::KH], f16x8 (&H)[C::KH],
-                                               f16x8 (&Ln)[C::KH], f16x8 (&Hn)[C::KH], const int (&ab)[2][2],
-                                               E& epi) {
-    constexpr bool more = K + 1 < H3P<C, GRP>::P.nbat;
-    h3_step_b<C, GRP, K>(W, b, bn);
-    h3_mfma<C, GRP, K>(acc, L, b[0]);  // lo*hi
-    if constexpr (more) h3_load<C, GRP, K + 1>(Ln, img, ab, 1);
-    h3_mfma<C, GRP, K>(acc, H, b[0]);  // hi*hi
-    if constexpr (more) h3_load<C, GRP, K + 1>(Hn, img, ab, 0);
-    h3_mfma<C, GRP, K>(acc, H, b[1]);  // hi*lo
-    h3_epi<C, GRP, K>(epi, std::make_integer_sequence<int, 16>{});
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-template <class C, int GRP, class E, int... K>
+template <class C, int GRP, int... K>
 __device__ __forceinline__ void conv_h3_run(f32x4 (&acc)[C::NS], const char* img, const X6W& W, const int (&lo)[2],
-                                            E& epi, std::integer_sequence<int, K...>, f16x8 (*carry)[2] = nullptr) {
+                                            std::integer_sequence<int, K...>) {
     int ab[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int sg = 0; sg < 2; ++sg) ab[m][sg] = lo[m] + sg * 65536;
     constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
-    f16x8 b[2], bn[4];
-    if constexpr (C::BD == 2 && B0.nstep >= 0) {  // the second run's pieces, before the first's are used
-        if constexpr (C::BF) {
-            bn[0] = h3_ldb(W, B0.nstep * 4);
-        } else {
-            bn[0] = h3_ldb(W, (B0.nstep * 2 + 0) * 4);
-            bn[1] = h3_ldb(W, (B0.nstep * 2 + 1) * 4);
-        }
-    }
+    f16x8 b[2], bn[2];
     if constexpr (C::BF) {
         b[0] = h3_ldb(W, (B0.t * 2 + B0.m) * 4);
         f16x8 X[C::KH], X2[C::KH];
@@ -1714,75 +1216,16 @@ __device__ __forceinline__ void conv_h3_run(f32x4 (&acc)[C::NS], const char* img
         ((K % 2 == 0 ? conv_h1_batch<C, GRP, K>(acc, img, W, b, bn, X, X2, ab)
                      : conv_h1_batch<C, GRP, K>(acc, img, W, b, bn, X2, X, ab)),
          ...);
-        (void)epi;
-        return;
-    }
-    if constexpr (C::PF) {  // this conv's first pieces were loaded during the previous conv
-        b[0] = (*carry)[0];
-        b[1] = (*carry)[1];
     } else {
         b[0] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 0) * 4);
         b[1] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 1) * 4);
-    }
-    if constexpr (C::PIPE == 2) {
-        f16x8 L[C::KH], H[C::KH], L2[C::KH], H2[C::KH];
-        h3_load<C, GRP, 0>(L, img, ab, 1);
-        h3_load<C, GRP, 0>(H, img, ab, 0);
-        ((K % 2 == 0 ? conv_h3_batch2<C, GRP, K>(acc, img, W, b, bn, L, H, L2, H2, ab, epi)
-                     : conv_h3_batch2<C, GRP, K>(acc, img, W, b, bn, L2, H2, L, H, ab, epi)),
-         ...);
-    } else {
         f16x8 X[C::KH], Y[C::KH];
         h3_load<C, GRP, 0>(X, img, ab, 1);
-        (conv_h3_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab, epi, carry), ...);
+        (conv_h3_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab), ...);
     }
 }
 
-// acc * (1/s) + bias (+ residual), ReLU, split into the two LDS planes; lane pairing, DPP exchange
-// and ADD / KEEP as epilogue_x6_pack. vmax: the largest activation this lane has split.
-template <class C, int GRP>
-__device__ __forceinline__ void epilogue_h3_pack(const f32x4 (&acc)[C::NS], uint32_t (&pk)[C::NS][2][2], float bb,
-                                                 float sc, f32x4 (&skip)[C::NS], int co, bool add, bool keep,
-                                                 float& vmax) {
-    const bool odd = co & 1;
-    const float addf = add ? 1.0f : 0.0f;  // fma(skip, addf, v) = v + skip or v, exactly
-#pragma unroll
-    for (int j = 0; j < grp_n(GRP); ++j) {
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            v[r] = __builtin_fmaf(skip[j][r], addf, __builtin_fmaf(acc[j][r], sc, bb));
-            v[r] = v[r] > 0.0f ? v[r] : 0.0f;
-            if (keep) skip[j][r] = v[r];
-        }
-        vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const float keep_ = odd ? v[2 * k + 1] : v[2 * k];  // stays in this lane
-            const float send = odd ? v[2 * k] : v[2 * k + 1];   // goes to the partner
-            const float got = __int_as_float(
-                __builtin_amdgcn_update_dpp(0, __float_as_int(send), 0xB1, 0xF, 0xF, false));
-            const float e0 = odd ? got : keep_, e1 = odd ? keep_ : got;  // (even, odd) channel
-            const _Float16 h0 = (_Float16)e0, h1 = (_Float16)e1;
-            const _Float16 l0 = (_Float16)(e0 - (float)h0), l1 = (_Float16)(e1 - (float)h1);
-            pk[j][k][0] = __builtin_bit_cast(uint32_t, f16x2{h0, h1});
-            pk[j][k][1] = __builtin_bit_cast(uint32_t, f16x2{l0, l1});
-        }
-    }
-}
-template <class C, int GRP>
-__device__ __forceinline__ void epilogue_h3_store(const uint32_t (&pk)[C::NS][2][2], char* img, const int (&eo)[2]) {
-#pragma unroll
-    for (int j = 0; j < grp_n(GRP); ++j)
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            char* d = img + grp_sq(GRP, j) * (nn::kSB * h3::kRowB) + eo[k];
-            *reinterpret_cast<uint32_t*>(d) = pk[j][k][0];
-            *reinterpret_cast<uint32_t*>(d + h3::kPlaneB) = pk[j][k][1];
-        }
-}
-
-// TR epilogue: the lane holds 4 consecutive channels (4 * kq + r of the N-tile) of one position,
+// Epilogue: the lane holds 4 consecutive channels (4 * kq + r of the N-tile) of one position,
 // so no lane exchange is needed: bias / scale per register, the pair splits are packed
 // conversions (v_cvt_pk_f16_f32, RNE), lo = fp16(fma(hi, -1, v)) (x - hi is exact in fp32, one
 // rounding: v_fma_mix), and each piece is one 8-byte store per square.
@@ -1799,26 +1242,23 @@ __device__ __forceinline__ uint32_t h3_lo_pair(uint32_t hi, float v0, float v1) 
 }
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-// FIRST (the first layer): no residual, keep the result. Convs: res = the block's second conv (add
-// the residual, keep the result for the next block). (A compile-time parity branch instead of the
-// selects makes the allocator spill.)
-// vmax: the largest hi bit pattern (v >= 0 after ReLU, so the u16 order is the value order; an
+// FIRST (the first layer): no residual, keep the result (the first block's skip). RES (the convs,
+// in pairs: the block parity is compile-time): 0 = small block 1 (conv + BN + ReLU), 1 = small block
+// 2 (conv + BN, + the residual, ReLU; the result is the next block's skip).
+// hmax: the largest hi bit pattern (v >= 0 after ReLU, so the u16 order is the value order; an
 // overflowed hi is +inf = 0x7C00).
-// RESC 0 / 1: res known at compile time (the EP kernel's conv pairs): no selects, no multiply by 0.
-template <bool FIRST, bool BF = false, int RESC = -1>
+template <bool FIRST, bool BF, int RES>
 __device__ __forceinline__ void h3t_pack_one(const f32x4& acc, uint32_t (&pk)[2][2], const f32x4& bb, const f32x4& sc,
-                                             f32x4& skip, bool res_, uint32_t& hmax) {
-    const bool res = RESC < 0 ? res_ : RESC == 1;
-    const f32x2 rf = {res ? 1.0f : 0.0f, res ? 1.0f : 0.0f};  // fma(skip, rf, v) = v + skip or v, exactly
+                                             f32x4& skip, uint32_t& hmax) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const f32x2 a2 = {acc[2 * k], acc[2 * k + 1]}, s2 = {sc[2 * k], sc[2 * k + 1]};
         const f32x2 b2 = {bb[2 * k], bb[2 * k + 1]};
         f32x2 v = __builtin_elementwise_fma(a2, s2, b2);
-        if constexpr (!FIRST && RESC != 0) v = __builtin_elementwise_fma(f32x2{skip[2 * k], skip[2 * k + 1]}, rf, v);
+        if constexpr (!FIRST && RES == 1) v += f32x2{skip[2 * k], skip[2 * k + 1]};
         v[0] = v[0] > 0.0f ? v[0] : 0.0f;
         v[1] = v[1] > 0.0f ? v[1] : 0.0f;
-        if (FIRST || res) {
+        if constexpr (FIRST || RES == 1) {
             skip[2 * k] = v[0];
             skip[2 * k + 1] = v[1];
         }
@@ -1835,13 +1275,12 @@ __device__ __forceinline__ void h3t_pack_one(const f32x4& acc, uint32_t (&pk)[2]
         }
     }
 }
-template <class C, int GRP, bool FIRST, int RESC = -1>
+template <class C, int GRP, bool FIRST, int RES>
 __device__ __forceinline__ void epilogue_h3t_pack(const f32x4 (&acc)[C::NS], uint32_t (&pk)[C::NS][2][2],
-                                                  const f32x4& bb, const f32x4& sc, f32x4 (&skip)[C::NS], bool res,
-                                                  uint32_t& hmax, int from = 0) {
+                                                  const f32x4& bb, const f32x4& sc, f32x4 (&skip)[C::NS],
+                                                  uint32_t& hmax) {
 #pragma unroll
-    for (int j = 0; j < grp_n(GRP); ++j)
-        if (j >= from) h3t_pack_one<FIRST, (bool)C::BF, RESC>(acc[j], pk[j], bb, sc, skip[j], res, hmax);
+    for (int j = 0; j < grp_n(GRP); ++j) h3t_pack_one<FIRST, (bool)C::BF, RES>(acc[j], pk[j], bb, sc, skip[j], hmax);
 }
 template <class C, int GRP>
 __device__ __forceinline__ void epilogue_h3t_store(const uint32_t (&pk)[C::NS][2][2], char* img, int eo) {
@@ -1850,65 +1289,6 @@ __device__ __forceinline__ void epilogue_h3t_store(const uint32_t (&pk)[C::NS][2
         char* d = img + grp_sq(GRP, j) * (nn::kSB * h3::kRowB) + eo;
         *reinterpret_cast<uint2*>(d) = uint2{pk[j][0][0], pk[j][0][1]};
         if constexpr (!C::BF) *reinterpret_cast<uint2*>(d + h3::kPlaneB) = uint2{pk[j][1][0], pk[j][1][1]};
-    }
-}
-
-// k_nn_h3 (TR) first layer: the bitboard part as k_nn_x6 (exact fp32 16x16x4 MFMAs, weights scaled
-// by s per output channel: exact), the 17 constant planes as ONE fp16 K-step per square: A = the
-// scaled table T[sq] split hi / lo (two 16x16x32 MFMAs), B = the position's 0/1 plane indicators
-// (exact in fp16, the same for every square). 2 x 16 instead of 5 x 32 MFMA cycles per square.
-template <class C, int GRP>
-__device__ __forceinline__ void first_layer_h3t(f32x4 (&acc)[C::NS], const L1Regs<GRP>& R, const float* l1c,
-                                                uint32_t bb, int cinfo, int lane, int nt) {
-    constexpr int n = grp_n(GRP), kB = 4;  // squares per batch of A-fragment loads
-    const int kq = lane >> 4;
-    X6W A;
-    A.r = __builtin_amdgcn_make_buffer_rsrc((void*)l1c, (short)0, (int)(25 * 2 * 4 * 64 * 16), 0x00020000);
-    A.voff = (nt * 64 + lane) * 16;
-    auto ld = [&](int sq, int pc) {  // fragment [sq][pc][nt][lane]
-        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(A.r, A.voff, (sq * 2 + pc) * 4 * 64 * 16, 0));
-    };
-    f16x8 fa[2][kB][2];
-#pragma unroll
-    for (int q = 0; q < kB; ++q)
-        if (q < n) {
-            fa[0][q][0] = ld(grp_sq(GRP, q), 0);
-            fa[0][q][1] = ld(grp_sq(GRP, q), 1);
-        }
-    const float s = l1c[25 * 2 * 4 * 64 * 4 + nt * 16 + (lane & 15)];
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int j = 0; j < n; ++j) {
-            const int sq = grp_sq(GRP, j);
-            const int r = sq / 5 + t / 3 - 1, c = sq % 5 + t % 3 - 1;
-            if (r >= 0 && r < 5 && c >= 0 && c < 5) {
-                const float a = (float)((bb >> (31 - (r * 5 + c))) & 1u);
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(R.w[t] * s, a, acc[j], 0, 0, 0);
-            }
-        }
-    const int c0 = cinfo & 15, c1 = (cinfo >> 4) & 15, blue = (cinfo >> 8) & 1;
-    f16x8 bc;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int k = 8 * kq + e;
-        bc[e] = (_Float16)(k < 16 ? ((k == c0 || k == c1) ? 1.0f : 0.0f) : (k == 16 ? (float)blue : 0.0f));
-    }
-#pragma unroll
-    for (int j0 = 0, b = 0; j0 < n; j0 += kB, b ^= 1) {
-        if (j0 + kB < n)
-#pragma unroll
-            for (int q = 0; q < kB; ++q)
-                if (j0 + kB + q < n) {
-                    fa[b ^ 1][q][0] = ld(grp_sq(GRP, j0 + kB + q), 0);
-                    fa[b ^ 1][q][1] = ld(grp_sq(GRP, j0 + kB + q), 1);
-                }
-#pragma unroll
-        for (int q = 0; q < kB; ++q)
-            if (j0 + q < n) {
-                acc[j0 + q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[b][q][0], bc, acc[j0 + q], 0, 0, 0);
-                acc[j0 + q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[b][q][1], bc, acc[j0 + q], 0, 0, 0);
-            }
     }
 }
 
@@ -2046,9 +1426,7 @@ __device__ __forceinline__ void first_layer_h3f(f32x4 (&acc)[C::NS], const L1H<G
     (sq_mfma(std::integral_constant<int, J>{}), ...);
 }
 
-// Returns true in a lane that split an activation beyond the fp16 range (an fp16 hi term that
-// overflowed, or would have): the tile's results are then invalid and k_nn_h3 recomputes them.
-// heads (k_nn_h3, k_nn_q2): the value / policy 1x1 convs as split MFMAs on the LDS image (one 16x16
+// heads (k_nn_h3): the value / policy 1x1 convs as split MFMAs on the LDS image (one 16x16
 // tile per square: rows = positions, columns 0 / 1 / 2 = value, policy planes 0 / 1, each scaled by a
 // power of two), then the MLPs per position from a feature table in LDS. p: the head parameters
 // (after the convs).
@@ -2066,12 +1444,8 @@ __device__ __forceinline__ void h3_heads(const float* p, char* img, const int (&
             for (int pc = 0; pc < 2; ++pc) hb[m][pc] = HB[(C::BF ? m : m * 2 + pc) * 64 + lane];  // BF: [m][lane]
         const float hs = C::BF ? 1.0f : hp[2 * 2 * 64 * 4 + (i < 3 ? i : 0)];
         // MLP weights in flight during the head convs (after hb: vmcnt is in order)
-        HeadRegs hr;
         HeadMM hm;
-        if constexpr (C::WAVES == 8 && C::HV == 0)
-            heads_mm_fetch(hm, p, wave, lane);
-        else
-            heads_fetch(hr, p, lane);
+        heads_mm_fetch(hm, p, wave, lane);
         constexpr int kSqPerWave = (25 + C::WAVES - 1) / C::WAVES;
         f32x4 hacc[kSqPerWave];
 #pragma unroll
@@ -2109,22 +1483,13 @@ __device__ __forceinline__ void h3_heads(const float* p, char* img, const int (&
                 }
         }
         __syncthreads();
-        if constexpr (C::WAVES == 8 && C::HV == 0) {
-            heads_mm(hm, feat, feat + nn::kSB * 80, wave, lane, b0, B, policy, value);
-        } else {
-            constexpr int NP = nn::kSB / C::WAVES;  // positions per wave
-            const float* fq[NP];
-            int bq[NP];
-#pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                fq[q] = feat + (wave + q * C::WAVES) * 80;
-                bq[q] = b0 + wave + q * C::WAVES;
-            }
-            heads_mlp_r<NP>(hr, fq, bq, lane, B, policy, value);
-        }
+        heads_mm(hm, feat, feat + nn::kSB * 80, wave, lane, b0, B, policy, value);
     }
 }
 
+// The whole forward for the waves of square group GRP. Returns true in a lane that split an
+// activation beyond the fp16 range (an fp16 hi term that overflowed, or would have): the tile's
+// results are then invalid and k_nn_h3 recomputes them.
 template <class C, int GRP>
 __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states, const TileSpan sp,
                                            const float* __restrict__ blob, int blocks, float* __restrict__ policy,
@@ -2133,22 +1498,17 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
     constexpr int NS = C::NS;
     char* img = reinterpret_cast<char*>(lds);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int nt = C::STG ? wave >> 1 : wave & 3;
+    const int nt = wave & 3;
     const int b0 = sp.b0;
     int* pinfo = reinterpret_cast<int*>(lds + (C::BF ? h3::kPlaneB : h3::kImageB) / 4);
-    const int co = nt * 16 + (lane & 15);
     const int i = lane & 15, kq = lane >> 4;
-    int eo[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) eo[k] = h3::elem_off(kq * 4 + 2 * k + (co & 1), co & ~1);
     const int lo[2] = {h3::chunk_off(i, kq), h3::chunk_off(i, 4 + kq)};
-    const int cq = nt * 16 + 4 * kq;  // TR: this lane's 4 channels cq .. cq + 3 of position i
+    const int cq = nt * 16 + 4 * kq;  // this lane's 4 channels cq .. cq + 3 of position i
     const int eot = h3::chunk_off(i, cq >> 3) + (cq & 7) * 2;
 
     f32x4 acc[NS];
     f32x4 skip[NS];
-    float vmax = 0.0f;
-    uint32_t hmax = 0;  // TR: largest hi bit patterns (two u16 halves)
+    uint32_t hmax = 0;  // largest hi bit patterns (two u16 halves)
     // DBG 2: first layer (MFMA tail + epilogue), conv, barrier 1, epilogue, barrier 2, heads, kernel start (state,
     // LUT, barrier), first-layer MFMAs (incl. their operand loads)
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -2160,14 +1520,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
             tm = t;
         }
     };
-    f16x8 carry[2];  // PF: the first B pieces of the next conv (conv 0's load under the first layer)
-    if constexpr (C::PF && !C::BF) {
-        constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
-        const X6W W0 = h3_w(blob + nn::kL1B + nn::kCh + nn::kL1Table, lane, nt);
-        carry[0] = h3_ldb(W0, ((B0.t * 2 + B0.m) * 2 + 0) * 4);
-        carry[1] = h3_ldb(W0, ((B0.t * 2 + B0.m) * 2 + 1) * 4);
-    }
-    {  // encoder + first layer (exact fp32 MFMA on the 0/1 inputs, as k_nn_x6)
+    {  // encoder + first layer
         L1Regs<GRP> l1;
         L1H<GRP> l1h;
         const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
@@ -2179,7 +1532,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
         oaz_state st{};
         if (tid < nn::kSB) st = states[b];
-        if constexpr (C::TR && !C::BF)
+        if constexpr (!C::BF)
             first_layer_h3f_fetch<GRP>(l1h, l1c, lane, nt);
         else
             first_layer_x6_fetch<GRP>(l1, blob, lane, nt);
@@ -2188,19 +1541,18 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
             const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
             pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
         }
-        if constexpr (C::TR && !C::BF)
+        if constexpr (!C::BF)
             for (int t = tid; t < 512; t += 64 * C::WAVES) l1_lut_build(img, t);
-        const float bias1 = blob[nn::kL1B + co];
         const f32x4 bias1t = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
         if (b0 >= B) return false;  // an empty tile of a compacted bucket (uniform over the workgroup)
         __syncthreads();
         stamp(6);
 #pragma unroll
-        for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};  // skip: finite for the fma in the epilogue
-        if constexpr (C::TR && !C::BF)
+        for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};
+        if constexpr (!C::BF)  // fp16 MFMA on the 0/1 inputs
             first_layer_h3f<C, GRP>(acc, l1h, bb, pinfo[i], lane, reinterpret_cast<const char*>(lds),
                                     std::make_integer_sequence<int, grp_n(GRP)>{});
-        else
+        else  // exact fp32 MFMA on the 0/1 inputs, as k_nn_x6
             first_layer_x6<C, GRP>(acc, l1, blob + nn::kL1B + nn::kCh, bb, pinfo[i], lane, nt);
         if constexpr (C::DBG == 2) {  // the MFMA results, so the stamp follows the MFMAs
             float z = 0.0f;
@@ -2210,110 +1562,40 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         }
         stamp(7);
         uint32_t pk[NS][2][2];
-        if constexpr (C::TR) {
-            const f32x4 inv1 = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f}
-                                     : *reinterpret_cast<const f32x4*>(l1c + 26 * h3::kL1Frag + cq);
-            epilogue_h3t_pack<C, GRP, true>(acc, pk, bias1t, inv1, skip, false, hmax);
-            epilogue_h3t_store<C, GRP>(pk, img, eot);
-        } else {
-            epilogue_h3_pack<C, GRP>(acc, pk, bias1, 1.0f, skip, co, false, true, vmax);
-            epilogue_h3_store<C, GRP>(pk, img, eo);
-        }
+        const f32x4 inv1 = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f}
+                                 : *reinterpret_cast<const f32x4*>(l1c + 26 * h3::kL1Frag + cq);
+        epilogue_h3t_pack<C, GRP, true, 0>(acc, pk, bias1t, inv1, skip, hmax);
+        epilogue_h3t_store<C, GRP>(pk, img, eot);
         __syncthreads();
     }
-    // 2 * blocks convs through one call site (small block 1: conv + BN + ReLU; small block 2:
-    // conv + BN, + skip, ReLU)
+    // the 2 * blocks convs in pairs, so the residual's role is compile-time (small block 1: conv + BN +
+    // ReLU; small block 2: conv + BN, + skip, ReLU, the result kept as the next skip)
     stamp(0);
     const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
-    if constexpr (C::STG) {
-        // Staggered convs. Conv c reads the image by K-half (channels 0-31 = the output of waves 0-3,
-        // 32-63 = waves 4-7) and overwrites it in place. A wave's program is h0(c) | h1(c) | E(c)
-        // (K-half 0 MFMAs, K-half 1 MFMAs, epilogue), one barrier interval each; waves 4-7 run it
-        // one interval behind waves 0-3, so each interval pairs one wave's epilogue or K-half with its
-        // SIMD partner's MFMAs:
-        //   interval 3c:     0-3 h0(c)   4-7 E(c-1)   (writes K-half 1: nobody reads it now)
-        //   interval 3c + 1: 0-3 h1(c)   4-7 h0(c)
-        //   interval 3c + 2: 0-3 E(c)    4-7 h1(c)    (0-3 write K-half 0: both h0(c) are done)
-        // Every read of a K-half of conv c's input precedes, by a barrier, the epilogue that overwrites
-        // it, and every epilogue precedes, by a barrier, the first read of what it wrote.
-        static_assert(!C::BF && C::TR && C::WAVES == 8 && !C::UNEVEN, "STG: fp16x3, transposed tiles, 8 waves, 13 / 12");
-        constexpr int kStride = (int)(h3::kW + 2 * nn::kCh);
-        const int nconv = 2 * blocks;
-        const int lag = __builtin_amdgcn_readfirstlane(wave) >> 2;  // 0: waves 0-3, 1: waves 4-7
-        if constexpr (C::STG == 2)
-            if (lag) __builtin_amdgcn_s_setprio(1);
-        f32x4 bbt{}, sct{};
-        auto noepi = [](auto) {};
-        for (int k = 0; k < 3 * nconv + 1; ++k) {
-            const int v = k - lag;  // this wave's interval
-            if (v >= 0 && v < 3 * nconv) {
-                const int c = v / 3, a = v - 3 * c;
-                const float* pc = p + (size_t)c * kStride;
-                const X6W W = h3_w(pc, lane, nt, (int)(h3::kW * 4));
-                if (a == 0) {
-                    bbt = *reinterpret_cast<const f32x4*>(pc + h3::kW + cq);  // in flight during the conv
-                    sct = *reinterpret_cast<const f32x4*>(pc + h3::kW + nn::kCh + cq);
-#pragma unroll
-                    for (int j = 0; j < NS; ++j) acc[j] = f32x4{};
-                    conv_h3_run<C, h3_khalf(GRP, 0)>(acc, img, W, lo, noepi,
-                                                     std::make_integer_sequence<int, H3P<C, h3_khalf(GRP, 0)>::P.nbat>{});
-                    stamp(1);
-                } else if (a == 1) {
-                    conv_h3_run<C, h3_khalf(GRP, 1)>(acc, img, W, lo, noepi,
-                                                     std::make_integer_sequence<int, H3P<C, h3_khalf(GRP, 1)>::P.nbat>{});
-                    stamp(1);
-                } else {
-                    uint32_t pk[NS][2][2];
-                    epilogue_h3t_pack<C, GRP, false>(acc, pk, bbt, sct, skip, c & 1, hmax);
-                    epilogue_h3t_store<C, GRP>(pk, img, eot);
-                    stamp(3);
-                }
-            }
-            __syncthreads();
-            stamp(2);
-        }
-        p += (size_t)nconv * kStride;
-    }
-    auto conv_one = [&](int c, auto resc) {  // RESC: -1 runtime parity, 0 / 1 compile-time (EP)
-        constexpr int RESC = decltype(resc)::value;
-        const float bb = p[h3::kW + co], sc = p[h3::kW + nn::kCh + co];  // in flight during the conv
+    auto conv_one = [&](auto res) {
+        constexpr int RES = decltype(res)::value;
         constexpr size_t kWc = C::BF ? nn::kW64h : h3::kW;  // B fragments of one conv
-        const f32x4 bbt = *reinterpret_cast<const f32x4*>(p + kWc + cq);
+        const f32x4 bbt = *reinterpret_cast<const f32x4*>(p + kWc + cq);  // in flight during the conv
         const f32x4 sct = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f} : *reinterpret_cast<const f32x4*>(p + kWc + nn::kCh + cq);
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = f32x4{};
-        uint32_t pk[NS][2][2];
-        const bool res = c & 1;
-        auto epi = [&](auto jc) {  // an earlier phase's square: its pack runs between MFMAs
-            constexpr int j = decltype(jc)::value;
-            h3t_pack_one<false, false, RESC>(acc[j], pk[j], bbt, sct, skip[j], res, hmax);
-        };
-        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt, (int)(C::PF ? 2 * (h3::kW + 2 * nn::kCh) * 4 : kWc * 4)), lo,
-                            epi, std::make_integer_sequence<int, H3P<C, GRP>::P.nbat>{}, &carry);
+        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt, (int)(kWc * 4)), lo,
+                            std::make_integer_sequence<int, H3P<C, GRP>::P.nbat>{});
         stamp(1);
         p += C::BF ? nn::kW64h + nn::kCh : h3::kW + 2 * nn::kCh;
-        if constexpr (C::TR) {
-            epilogue_h3t_pack<C, GRP, false, RESC>(acc, pk, bbt, sct, skip, res, hmax, H3P<C, GRP>::P.tail);
-        } else
-            epilogue_h3_pack<C, GRP>(acc, pk, bb, sc, skip, co, c & 1, c & 1, vmax);
-        stamp(3);
-        __syncthreads();
+        uint32_t pk[NS][2][2];
+        epilogue_h3t_pack<C, GRP, false, RES>(acc, pk, bbt, sct, skip, hmax);  // before the barrier: a
+        stamp(3);                                                             // wave done early packs
+        __syncthreads();                                                      // beside its partner's MFMAs
         stamp(2);
-        if constexpr (C::TR)
-            epilogue_h3t_store<C, GRP>(pk, img, eot);
-        else
-            epilogue_h3_store<C, GRP>(pk, img, eo);
+        epilogue_h3t_store<C, GRP>(pk, img, eot);
         stamp(3);
         __syncthreads();
         stamp(4);
     };
-    if constexpr (C::EP) {  // conv pairs: the residual parity at compile time
-        for (int c = 0; c < (C::STG ? 0 : 2 * blocks); c += 2) {
-            conv_one(c, std::integral_constant<int, 0>{});
-            conv_one(c + 1, std::integral_constant<int, 1>{});
-        }
-    } else {
-        for (int c = 0; c < (C::STG ? 0 : 2 * blocks); ++c) conv_one(c, std::integral_constant<int, -1>{});
+    for (int c = 0; c < blocks; ++c) {
+        conv_one(std::integral_constant<int, 0>{});
+        conv_one(std::integral_constant<int, 1>{});
     }
     h3_heads<C>(p, img, lo, wave, lane, b0, B, policy, value);
     if constexpr (C::DBG == 2) {
@@ -2322,7 +1604,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         if (lane < 8 && b0 + nn::kSB <= B) policy[(size_t)b0 * 50 + wave * 8 + lane] = (float)ph[lane];
     }
     if constexpr (C::BF) return false;  // bf16 pieces have fp32's exponent range
-    return vmax >= 65504.0f || (C::TR && ((hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u));  // hi = inf
+    return (hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u;  // hi = inf
 }
 
 // fp16-range fallback: a workgroup in which any lane split an activation beyond the fp16 range
@@ -2335,9 +1617,10 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
 template <class C>
 struct H3Fallback {
     static constexpr bool kOn = !C::BF && C::DBG == 0;
-    using X = X6Cfg<C::WAVES, C::WAVES == 4 ? 8 : 4, 1, 0, C::WAVES == 4 ? 0 : 1>;
-    // bf16 mode keeps one piece plane (+ the position info): 52 KB, so two 4-wave workgroups share a CU
-    static constexpr int kBase = C::BF ? h3::kPlaneB / 4 + 256 : h3::kLdsFloats + (C::TR ? h3::kLutB / 4 : 0);
+    using X = X6Cfg<>;
+    // bf16 mode keeps one piece plane (+ the position info): 52 KB, and 194 VGPRs, so a tree-kernel
+    // wave fits beside the two NN waves of a SIMD
+    static constexpr int kBase = C::BF ? h3::kPlaneB / 4 + 256 : h3::kLdsFloats + h3::kLutB / 4;
     static constexpr int kLds = kOn && x6::kLdsFloats > kBase ? x6::kLdsFloats : kBase;
 };
 
@@ -2362,35 +1645,20 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __rest
     const uint64_t rt0 = C::DBG == 5 ? __builtin_amdgcn_s_memrealtime() : 0;
     const TileSpan sp = tile_span(tm, B);
     bool ovf;
-    const bool g0 = (threadIdx.x >> 8) == 0;  // 8 waves: waves 0-3 square group A, waves 4-7 group B
-    if constexpr (C::WAVES == 4) {
-        ovf = nn_h3_body<C, 2>(states, sp, blob, blocks, policy, value, lds);
-    } else if constexpr (C::UNEVEN) {
-        constexpr int ga = C::UNEVEN == 4 ? 9 : C::UNEVEN == 3 ? 7 : C::UNEVEN == 2 ? 5 : 3;
-        if (g0) {
-            __builtin_amdgcn_s_setprio(1);
-            ovf = nn_h3_body<C, ga>(states, sp, blob, blocks, policy, value, lds);
-        } else {
-            ovf = nn_h3_body<C, ga + 1>(states, sp, blob, blocks, policy, value, lds);
-        }
-    } else if constexpr (C::STG) {  // square group = wave parity (the SIMD partners w, w + 4 share it)
-        if (((threadIdx.x >> 6) & 1) == 0)
-            ovf = nn_h3_body<C, 0>(states, sp, blob, blocks, policy, value, lds);
-        else
-            ovf = nn_h3_body<C, 1>(states, sp, blob, blocks, policy, value, lds);
-    } else if (g0)
-        ovf = nn_h3_body<C, 0>(states, sp, blob, blocks, policy, value, lds);
-    else
-        ovf = nn_h3_body<C, 1>(states, sp, blob, blocks, policy, value, lds);
+    const bool g0 = (threadIdx.x >> 8) == 0;  // waves 0-3: square group GRP0 (17 squares), 4-7: GRP1 (8)
+    if (g0) {
+        __builtin_amdgcn_s_setprio(1);
+        ovf = nn_h3_body<C, C::GRP0>(states, sp, blob, blocks, policy, value, lds);
+    } else {
+        ovf = nn_h3_body<C, C::GRP1>(states, sp, blob, blocks, policy, value, lds);
+    }
     if constexpr (H3Fallback<C>::kOn) {
         using X = typename H3Fallback<C>::X;
         if (__syncthreads_or(ovf)) {  // uniform over the workgroup; also the barrier before LDS reuse
-            if constexpr (C::WAVES == 4)
-                nn_h3_fallback<X, 2>(states, sp, xblob, blocks, policy, value, lds);
-            else if (g0)
-                nn_h3_fallback<X, 3>(states, sp, xblob, blocks, policy, value, lds);
+            if (g0)
+                nn_h3_fallback<X, X::GRP0>(states, sp, xblob, blocks, policy, value, lds);
             else
-                nn_h3_fallback<X, 4>(states, sp, xblob, blocks, policy, value, lds);
+                nn_h3_fallback<X, X::GRP1>(states, sp, xblob, blocks, policy, value, lds);
             if (threadIdx.x == 0) atomicAdd(fallback, 1ull);
         }
     }
@@ -2411,587 +1679,8 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __rest
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// k_nn_q2: the k_nn_h3 arithmetic (fp16x3 split, or one bf16 piece in BF mode; transposed C/D tiles,
-// compile-time batch plans, convs in pairs, in-kernel fp16-range recompute) with TWO N-tiles per
-// wave: 8 waves = 4 square groups (GRP 11-14, 43 / 42 / 42 / 42 on-board taps) x 2 N-tile pairs;
-// waves w and w + 4 share a SIMD and a square group. Every A fragment read from LDS feeds the MFMAs
-// of both N-tiles, so the conv reads half the A bytes of k_nn_h3 (whose four N-tile waves each read
-// the same fragments), at twice the B-piece loads per wave (L2).
-template <class C, int GRP, int K, int N>
-__device__ __forceinline__ void q2_mfma(f32x4 (&acc)[2 * C::NS], const f16x8 (&a)[N], const f16x8& b0v,
-                                        const f16x8& b1v) {
-    constexpr H3Batch B = H3P<C, GRP>::P.b[K];
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int q = 0; q < N; ++q)
-            if (q < B.n) {
-                f32x4& d = acc[n * C::NS + B.j[q]];
-                const f16x8& bv = n ? b1v : b0v;
-                d = C::BF ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bv),
-                                                                    __builtin_bit_cast(bf16x8, a[q]), d, 0, 0, 0)
-                          : __builtin_amdgcn_mfma_f32_16x16x32_f16(bv, a[q], d, 0, 0, 0);
-            }
-}
-// B pieces b[n * 2 + piece] of N-tile nt0 + n (the next N-tile is the next 1 KiB entry)
-template <class C, int GRP, int K>
-__device__ __forceinline__ void q2_step_b(const X6W& W, f16x8 (&b)[4], f16x8 (&bn)[4]) {
-    constexpr H3Batch B = H3P<C, GRP>::P.b[K];
-    if constexpr (B.first && K > 0) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) b[k] = bn[k];
-    }
-    if constexpr (B.first && B.nstep >= 0) {
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-            if constexpr (C::BF) {
-                bn[n * 2] = h3_ldb(W, B.nstep * 4 + n);
-            } else {
-                bn[n * 2] = h3_ldb(W, (B.nstep * 2 + 0) * 4 + n);
-                bn[n * 2 + 1] = h3_ldb(W, (B.nstep * 2 + 1) * 4 + n);
-            }
-        }
-    }
-}
-// batch K (X holds its lo pieces on entry and the next batch's on exit; BF: its only piece):
-//   load Y = hi | lo*Bhi (both tiles) | load X = next lo | hi*Bhi, hi*Blo (both tiles)
-template <class C, int GRP, int K>
-__device__ __forceinline__ void q2_batch(f32x4 (&acc)[2 * C::NS], const char* img, const X6W& W, f16x8 (&b)[4],
-                                         f16x8 (&bn)[4], f16x8 (&X)[C::KH], f16x8 (&Y)[C::KH], const int (&ab)[2][2]) {
-    q2_step_b<C, GRP, K>(W, b, bn);
-    if constexpr (C::BF) {  // one piece: X = this batch, Y = the next (roles swap with K's parity)
-        if constexpr (K + 1 < H3P<C, GRP>::P.nbat) h3_load<C, GRP, K + 1>(Y, img, ab, 0);
-        q2_mfma<C, GRP, K>(acc, X, b[0], b[2]);
-    } else {
-        h3_load<C, GRP, K>(Y, img, ab, 0);
-        q2_mfma<C, GRP, K>(acc, X, b[0], b[2]);  // lo*hi
-        if constexpr (K + 1 < H3P<C, GRP>::P.nbat) h3_load<C, GRP, K + 1>(X, img, ab, 1);
-        q2_mfma<C, GRP, K>(acc, Y, b[0], b[2]);  // hi*hi
-        q2_mfma<C, GRP, K>(acc, Y, b[1], b[3]);  // hi*lo
-    }
-    __builtin_amdgcn_sched_barrier(0);
-}
-template <class C, int GRP, int... K>
-__device__ __forceinline__ void q2_run(f32x4 (&acc)[2 * C::NS], const char* img, const X6W& W, const int (&lo)[2],
-                                       std::integer_sequence<int, K...>) {
-    int ab[2][2];
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int sg = 0; sg < 2; ++sg) ab[m][sg] = lo[m] + sg * 65536;
-    constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
-    f16x8 b[4], bn[4];
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-        if constexpr (C::BF) {
-            b[n * 2] = h3_ldb(W, (B0.t * 2 + B0.m) * 4 + n);
-        } else {
-            b[n * 2] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 0) * 4 + n);
-            b[n * 2 + 1] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 1) * 4 + n);
-        }
-    }
-    f16x8 X[C::KH], Y[C::KH];
-    h3_load<C, GRP, 0>(X, img, ab, C::BF ? 0 : 1);
-    if constexpr (C::BF)
-        ((K % 2 == 0 ? q2_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab) : q2_batch<C, GRP, K>(acc, img, W, b, bn, Y, X, ab)),
-         ...);
-    else
-        (q2_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab), ...);
-}
-template <class C>
-using Acc1 = f32x4[C::NS];
-template <class C>
-__device__ __forceinline__ Acc1<C>& q2_tile(f32x4 (&a)[2 * C::NS], int n) {  // N-tile n's accumulators
-    return *reinterpret_cast<Acc1<C>*>(&a[n * C::NS]);
-}
-
-template <class C, int GRP>
-__device__ __forceinline__ bool nn_q2_body(const oaz_state* __restrict__ states, const TileSpan sp,
-                                           const float* __restrict__ blob, int blocks, float* __restrict__ policy,
-                                           float* __restrict__ value, float* lds) {
-    const int B = sp.end;
-    constexpr int NS = C::NS;
-    char* img = reinterpret_cast<char*>(lds);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int nt0 = (wave >> 2) * 2;  // N-tiles nt0, nt0 + 1
-    const int b0 = sp.b0;
-    int* pinfo = reinterpret_cast<int*>(lds + h3::kImageB / 4);
-    const int i = lane & 15, kq = lane >> 4;
-    const int lo[2] = {h3::chunk_off(i, kq), h3::chunk_off(i, 4 + kq)};
-    int cq[2], eot[2];
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-        cq[n] = (nt0 + n) * 16 + 4 * kq;  // this lane's 4 channels of position i in N-tile nt0 + n
-        eot[n] = h3::chunk_off(i, cq[n] >> 3) + (cq[n] & 7) * 2;
-    }
-    f32x4 acc[2 * NS], skip[2 * NS];
-    uint32_t hmax = 0;
-    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // DBG 2: as nn_h3_body
-    uint64_t tm = C::DBG == 2 ? __builtin_amdgcn_s_memtime() : 0;
-    auto stamp = [&](int k) {
-        if constexpr (C::DBG == 2) {
-            const uint64_t t = __builtin_amdgcn_s_memtime();
-            ph[k] += t - tm;
-            tm = t;
-        }
-    };
-    {  // encoder + first layer
-        const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
-                           nn::kValueF + nn::kPolicyF + h3::kHeadB;
-        const int b = min(b0 + i, sp.cap - 1);  // an empty tile of a bucket starts past cap
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(&states[b]);
-        const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
-        oaz_state st{};
-        if (tid < nn::kSB) st = states[b];
-        L1H<GRP> l1h[C::BF ? 1 : 2];
-        L1Regs<GRP> l1[C::BF ? 2 : 1];
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-            if constexpr (C::BF)
-                first_layer_x6_fetch<GRP>(l1[n], blob, lane, nt0 + n);
-            else
-                first_layer_h3f_fetch<GRP>(l1h[n], l1c, lane, nt0 + n);
-        }
-        if (tid < nn::kSB) {
-            const int blue = st.to_move & 1;
-            const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
-            pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
-        }
-        if constexpr (!C::BF)
-            for (int t = tid; t < 512; t += 64 * C::WAVES) l1_lut_build(img, t);
-        f32x4 bias1t[2], inv1[2];
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-            bias1t[n] = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq[n]);
-            inv1[n] = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f} : *reinterpret_cast<const f32x4*>(l1c + 26 * h3::kL1Frag + cq[n]);
-        }
-        if (b0 >= B) return false;  // an empty tile of a compacted bucket (uniform over the workgroup)
-        __syncthreads();
-        stamp(6);
-#pragma unroll
-        for (int j = 0; j < 2 * NS; ++j) acc[j] = skip[j] = f32x4{};
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-            if constexpr (C::BF)
-                first_layer_x6<C, GRP>(q2_tile<C>(acc, n), l1[n], blob + nn::kL1B + nn::kCh, bb, pinfo[i], lane, nt0 + n);
-            else
-                first_layer_h3f<C, GRP>(q2_tile<C>(acc, n), l1h[n], bb, pinfo[i], lane, reinterpret_cast<const char*>(lds),
-                                        std::make_integer_sequence<int, grp_n(GRP)>{});
-        }
-        stamp(7);
-        uint32_t pk[2][NS][2][2];
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-            epilogue_h3t_pack<C, GRP, true>(q2_tile<C>(acc, n), pk[n], bias1t[n], inv1[n], q2_tile<C>(skip, n), false,
-                                            hmax);
-            epilogue_h3t_store<C, GRP>(pk[n], img, eot[n]);
-        }
-        __syncthreads();
-    }
-    stamp(0);
-    const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
-    constexpr size_t kWc = C::BF ? nn::kW64h : h3::kW;  // B fragments of one conv
-    auto conv_one = [&](auto resc) {  // RESC 0 / 1: the block's first / second conv
-        constexpr int RESC = decltype(resc)::value;
-        f32x4 bbt[2], sct[2];
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-            bbt[n] = *reinterpret_cast<const f32x4*>(p + kWc + cq[n]);  // in flight during the conv
-            sct[n] = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f} : *reinterpret_cast<const f32x4*>(p + kWc + nn::kCh + cq[n]);
-        }
-#pragma unroll
-        for (int j = 0; j < 2 * NS; ++j) acc[j] = f32x4{};
-        q2_run<C, GRP>(acc, img, h3_w(p, lane, nt0, (int)(kWc * 4)), lo,
-                       std::make_integer_sequence<int, H3P<C, GRP>::P.nbat>{});
-        stamp(1);
-        p += kWc + 2 * nn::kCh - (C::BF ? nn::kCh : 0);
-        uint32_t pk[2][NS][2][2];
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-            epilogue_h3t_pack<C, GRP, false, RESC>(q2_tile<C>(acc, n), pk[n], bbt[n], sct[n], q2_tile<C>(skip, n),
-                                                   RESC == 1, hmax);
-        stamp(3);
-        __syncthreads();
-        stamp(2);
-#pragma unroll
-        for (int n = 0; n < 2; ++n) epilogue_h3t_store<C, GRP>(pk[n], img, eot[n]);
-        stamp(3);
-        __syncthreads();
-        stamp(4);
-    };
-    for (int c = 0; c < 2 * blocks; c += 2) {
-        conv_one(std::integral_constant<int, 0>{});
-        conv_one(std::integral_constant<int, 1>{});
-    }
-    h3_heads<C>(p, img, lo, wave, lane, b0, B, policy, value);
-    if constexpr (C::DBG == 2) {
-        stamp(5);
-        __syncthreads();
-        if (lane < 8 && b0 + nn::kSB <= B) policy[(size_t)b0 * 50 + wave * 8 + lane] = (float)ph[lane];
-    }
-    if constexpr (C::BF) return false;
-    return (hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u;  // an fp16 hi = inf
-}
-
-template <class C>
-__global__ void __launch_bounds__(64 * C::WAVES) k_nn_q2(const oaz_state* __restrict__ states, int B,
-                                                        const float* __restrict__ blob, int blocks,
-                                                        float* __restrict__ policy, float* __restrict__ value,
-                                                        const float* __restrict__ xblob,
-                                                        unsigned long long* __restrict__ fallback, TileMap tm) {
-    static_assert(C::Q2 && C::WAVES == 8 && C::TR && C::EP, "k_nn_q2: 8 waves, transposed tiles, conv pairs");
-    __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
-    const TileSpan sp = tile_span(tm, B);
-    bool ovf;
-    switch ((threadIdx.x >> 6) & 3) {  // square group; waves w and w + 4 (one SIMD) share it
-        case 0: ovf = nn_q2_body<C, 11>(states, sp, blob, blocks, policy, value, lds); break;
-        case 1: ovf = nn_q2_body<C, 12>(states, sp, blob, blocks, policy, value, lds); break;
-        case 2: ovf = nn_q2_body<C, 13>(states, sp, blob, blocks, policy, value, lds); break;
-        default: ovf = nn_q2_body<C, 14>(states, sp, blob, blocks, policy, value, lds); break;
-    }
-    if constexpr (H3Fallback<C>::kOn) {
-        using X = typename H3Fallback<C>::X;
-        const bool g0 = (threadIdx.x >> 8) == 0;
-        if (__syncthreads_or(ovf)) {  // uniform over the workgroup; also the barrier before LDS reuse
-            if (g0)
-                nn_h3_fallback<X, 3>(states, sp, xblob, blocks, policy, value, lds);
-            else
-                nn_h3_fallback<X, 4>(states, sp, xblob, blocks, policy, value, lds);
-            if (threadIdx.x == 0) atomicAdd(fallback, 1ull);
-        }
-    }
-}
-
-#if OAZ_AB
-// ---------------------------------------------------------------------------------------------
-// k_nn_p8 (OAZ_FP32_SPLIT16, OAZ_NN_X6_V=20): the k_nn_h3 arithmetic (fp16 hi/lo split, 3 products,
-// transposed C/D tiles, per-channel weight scales, range guard) on 8 positions per workgroup, so
-// that two workgroups share a CU (53 KB of LDS each) and one's epilogues, barriers, first layer
-// and heads run beside the other's conv MFMAs. A 16-row MFMA tile is two squares x 8 positions;
-// the 13 tiles pair squares whose on-board tap sets nest (interior / edge pairs: equal sets; a
-// corner with an edge square that contains its set; square 18 with the zero slot), so a tile's
-// (tap) list is the union and only the half whose neighbour is off the board reads the zero slot:
-// 93 tile-taps per conv instead of the ideal 84.5. 4 waves, wave = N-tile over all 13 tiles.
-namespace p8 {
-constexpr int kP = 8;
-constexpr int kZ = 9;                       // zero slot (tile 4, half 1), never written non-zero
-constexpr int kSlotB = kP * 128;            // 8 rows of 64 f16
-constexpr int kPlaneB = 26 * kSlotB;        // 26,624 B
-constexpr int kImageB = 2 * kPlaneB;        // 53,248 B
-constexpr int8_t kTileSq[13][2] = {{6, 7},  {11, 12}, {16, 17}, {8, 13},  {18, 25}, {1, 2},  {21, 22},
-                                   {5, 10}, {9, 14},  {4, 3},   {24, 19}, {20, 23}, {0, 15}};
-constexpr int slot_of(int sq) {
-    for (int k = 0; k < 13; ++k)
-        for (int h = 0; h < 2; ++h)
-            if (kTileSq[k][h] == sq) return 2 * k + h;
-    return kZ;
-}
-constexpr int nb_sq(int sq, int t) {
-    if (sq >= 25) return -1;
-    const int r = sq / 5 + t / 3 - 1, c = sq % 5 + t % 3 - 1;
-    return (r >= 0 && r < 5 && c >= 0 && c < 5) ? r * 5 + c : -1;
-}
-struct Batch {
-    int t, m, n, first, nstep;
-    int8_t j[8], sa[8], sb[8];  // tile, neighbour slot of half 0 / half 1 (kZ when off the board)
-};
-struct Plan {
-    int nbat;
-    Batch b[96];
-};
-constexpr Plan make_plan(int kh) {
-    Plan P{};
-    for (int s = 0; s < 18; ++s) {
-        const int t = s / 2;
-        int tl[13] = {}, nt = 0;
-        for (int k = 0; k < 13; ++k)
-            if (nb_sq(kTileSq[k][0], t) >= 0 || nb_sq(kTileSq[k][1], t) >= 0) tl[nt++] = k;
-        const int nb = (nt + kh - 1) / kh;
-        int q = 0;
-        for (int i = 0; i < nb; ++i) {
-            const int m = (nt - q) / (nb - i);
-            Batch B{};
-            B.t = t;
-            B.m = s % 2;
-            B.n = m;
-            B.first = i == 0;
-            B.nstep = -1;
-            for (int e = 0; e < m; ++e) {
-                const int k = tl[q + e];
-                const int na = nb_sq(kTileSq[k][0], t), nbb = nb_sq(kTileSq[k][1], t);
-                B.j[e] = (int8_t)k;
-                B.sa[e] = (int8_t)(na >= 0 ? slot_of(na) : kZ);
-                B.sb[e] = (int8_t)(nbb >= 0 ? slot_of(nbb) : kZ);
-            }
-            q += m;
-            P.b[P.nbat++] = B;
-        }
-    }
-    int next = -1;
-    for (int k = P.nbat - 1; k >= 0; --k)
-        if (P.b[k].first) {
-            P.b[k].nstep = next;
-            next = P.b[k].t * 2 + P.b[k].m;
-        }
-    return P;
-}
-template <int KH>
-struct PlanOf {
-    static constexpr Plan P = make_plan(KH);
-};
-}  // namespace p8
-
-// image fragment loads of batch K: lane (half h, position p, k-group kq) reads its half's neighbour
-// slot: base lb[m] + h * (sb - sa) * 1 KiB, immediate sa * 1 KiB + piece plane
-template <int KH, int K>
-__device__ __forceinline__ void p8_load(f16x8 (&a)[KH], const char* img, const int (&lb)[2], bool h, int piece) {
-    constexpr p8::Batch B = p8::PlanOf<KH>::P.b[K];
-#pragma unroll
-    for (int q = 0; q < KH; ++q)
-        if (q < B.n) {
-            const int d = h ? (B.sb[q] - B.sa[q]) * p8::kSlotB : 0;
-            a[q] = *reinterpret_cast<const f16x8*>(img + lb[B.m] + d + B.sa[q] * p8::kSlotB + piece * p8::kPlaneB);
-        }
-}
-template <int KH, int K>
-__device__ __forceinline__ void p8_mfma(f32x4 (&acc)[13], const f16x8 (&a)[KH], const f16x8& w) {
-    constexpr p8::Batch B = p8::PlanOf<KH>::P.b[K];
-#pragma unroll
-    for (int q = 0; q < KH; ++q)
-        if (q < B.n) acc[B.j[q]] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w, a[q], acc[B.j[q]], 0, 0, 0);
-}
-template <int KH, int K>
-__device__ __forceinline__ void p8_batch(f32x4 (&acc)[13], const char* img, const X6W& W, f16x8 (&b)[2],
-                                         f16x8 (&bn)[2], f16x8 (&X)[KH], f16x8 (&Y)[KH], const int (&lb)[2], bool h) {
-    constexpr p8::Plan P = p8::PlanOf<KH>::P;
-    constexpr p8::Batch B = P.b[K];
-    if constexpr (B.first && K > 0) {
-        b[0] = bn[0];
-        b[1] = bn[1];
-    }
-    if constexpr (B.first && B.nstep >= 0) {
-        bn[0] = h3_ldb(W, (B.nstep * 2 + 0) * 4);
-        bn[1] = h3_ldb(W, (B.nstep * 2 + 1) * 4);
-    }
-    p8_load<KH, K>(Y, img, lb, h, 0);
-    p8_mfma<KH, K>(acc, X, b[0]);  // lo * Bhi
-    if constexpr (K + 1 < P.nbat) p8_load<KH, K + 1>(X, img, lb, h, 1);
-    p8_mfma<KH, K>(acc, Y, b[0]);  // hi * Bhi
-    p8_mfma<KH, K>(acc, Y, b[1]);  // hi * Blo
-    __builtin_amdgcn_sched_barrier(0);
-}
-// PIPE 2: both pieces of batch K+1 load during batch K (four buffers, roles swap with K's parity)
-template <int KH, int K>
-__device__ __forceinline__ void p8_batch2(f32x4 (&acc)[13], const char* img, const X6W& W, f16x8 (&b)[2],
-                                          f16x8 (&bn)[2], f16x8 (&L)[KH], f16x8 (&H)[KH], f16x8 (&Ln)[KH],
-                                          f16x8 (&Hn)[KH], const int (&lb)[2], bool h) {
-    constexpr p8::Plan P = p8::PlanOf<KH>::P;
-    constexpr p8::Batch B = P.b[K];
-    constexpr bool more = K + 1 < P.nbat;
-    if constexpr (B.first && K > 0) {
-        b[0] = bn[0];
-        b[1] = bn[1];
-    }
-    if constexpr (B.first && B.nstep >= 0) {
-        bn[0] = h3_ldb(W, (B.nstep * 2 + 0) * 4);
-        bn[1] = h3_ldb(W, (B.nstep * 2 + 1) * 4);
-    }
-    p8_mfma<KH, K>(acc, L, b[0]);  // lo * Bhi
-    if constexpr (more) p8_load<KH, K + 1>(Ln, img, lb, h, 1);
-    p8_mfma<KH, K>(acc, H, b[0]);  // hi * Bhi
-    if constexpr (more) p8_load<KH, K + 1>(Hn, img, lb, h, 0);
-    p8_mfma<KH, K>(acc, H, b[1]);  // hi * Blo
-    __builtin_amdgcn_sched_barrier(0);
-}
-template <int KH, int PIPE, int... K>
-__device__ __forceinline__ void p8_conv(f32x4 (&acc)[13], const char* img, const X6W& W, const int (&lb)[2], bool h,
-                                        std::integer_sequence<int, K...>) {
-    constexpr p8::Batch B0 = p8::PlanOf<KH>::P.b[0];
-    f16x8 b[2], bn[2];
-    b[0] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 0) * 4);
-    b[1] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 1) * 4);
-    if constexpr (PIPE == 2) {
-        f16x8 L[KH], H[KH], L2[KH], H2[KH];
-        p8_load<KH, 0>(L, img, lb, h, 1);
-        p8_load<KH, 0>(H, img, lb, h, 0);
-        ((K % 2 == 0 ? p8_batch2<KH, K>(acc, img, W, b, bn, L, H, L2, H2, lb, h)
-                     : p8_batch2<KH, K>(acc, img, W, b, bn, L2, H2, L, H, lb, h)),
-         ...);
-    } else {
-        f16x8 X[KH], Y[KH];
-        p8_load<KH, 0>(X, img, lb, h, 1);
-        (p8_batch<KH, K>(acc, img, W, b, bn, X, Y, lb, h), ...);
-    }
-}
-// the pack of tile 4's half 1 (the zero slot) is forced to 0
-__device__ __forceinline__ void p8_store(uint32_t (&pk)[13][2][2], char* img, int est, bool h) {
-    if (h) pk[4][0][0] = pk[4][0][1] = pk[4][1][0] = pk[4][1][1] = 0u;
-#pragma unroll
-    for (int k = 0; k < 13; ++k) {
-        char* d = img + k * 2 * p8::kSlotB + est;
-        *reinterpret_cast<uint2*>(d) = uint2{pk[k][0][0], pk[k][0][1]};
-        *reinterpret_cast<uint2*>(d + p8::kPlaneB) = uint2{pk[k][1][0], pk[k][1][1]};
-    }
-}
-
-template <int KH, int PIPE>
-__global__ void __launch_bounds__(256) k_nn_p8(const oaz_state* __restrict__ states, int B,
-                                               const float* __restrict__ blob, int blocks,
-                                               float* __restrict__ policy, float* __restrict__ value,
-                                               unsigned long long* __restrict__ range_flag) {
-    __shared__ __attribute__((aligned(16))) char img[p8::kImageB];
-    __shared__ int pinfo[p8::kP];
-    const int tid = threadIdx.x, nt = tid >> 6, lane = tid & 63;
-    const int n = lane & 15, pp = n & 7, kq = lane >> 4;
-    const bool h = n >= 8;
-    const int b0 = blockIdx.x * p8::kP;
-    const int cq = nt * 16 + 4 * kq;  // this lane's 4 output channels (TR C/D tiles), position (h, pp)
-    int lb[2];
-#pragma unroll
-    for (int m = 0; m < 2; ++m) lb[m] = pp * 128 + (((kq + 4 * m) ^ pp) << 4);
-    const int est = (h ? p8::kSlotB : 0) + pp * 128 + (((cq >> 3) ^ pp) << 4) + (cq & 7) * 2;
-    f32x4 acc[13], skip[13];
-    uint32_t hmax = 0;
-    {  // encoder + first layer: exact fp32 MFMA (0/1 inputs); K = the 4 bitboards per tap, then the
-       // constant planes as K = (half, plane) over the two squares' table rows (9 k-steps)
-        float w1[9];
-#pragma unroll
-        for (int t = 0; t < 9; ++t) w1[t] = blob[(t * 4 + nt) * 64 + lane];
-        const int b = b0 + pp < B ? b0 + pp : b0;
-        const uint32_t* sw = reinterpret_cast<const uint32_t*>(&states[b]);
-        const uint32_t bb = kq == 0 ? sw[2] : kq == 1 ? sw[0] : kq == 2 ? sw[3] : sw[1];
-        if (tid < p8::kP) {
-            const oaz_state st = states[b0 + tid < B ? b0 + tid : b0];
-            const int blue = st.to_move & 1;
-            const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
-            pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
-        }
-        const f32x4 bias1 = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
-        const float* table = blob + nn::kL1B + nn::kCh;
-        const int ch = nt * 16 + n;  // A-operand row (output channel) of this lane
-        float tb[2][9];
-        auto fetch = [&](float (&d)[9], int k) {  // table rows of tile k: k-step kk, lane k-group kq
-#pragma unroll
-            for (int kk = 0; kk < 9; ++kk) {
-                const int kx = 4 * kk + kq, hh = kx >= 17, pl = kx - 17 * hh;
-                const int sq = p8::kTileSq[k][hh];  // (compile-time per (k, kk) up to the lane's hh)
-                d[kk] = (kx < 34 && sq < 25) ? table[(size_t)sq * 17 * nn::kCh + pl * nn::kCh + ch] : 0.0f;
-            }
-        };
-        fetch(tb[0], 0);
-        __syncthreads();
-        const int ci = pinfo[pp];
-        const int c0 = ci & 15, c1 = (ci >> 4) & 15, blue = (ci >> 8) & 1;
-        float ac[9];
-#pragma unroll
-        for (int kk = 0; kk < 9; ++kk) {
-            const int kx = 4 * kk + kq, hh = kx >= 17, pl = kx - 17 * hh;
-            const float v = pl < 16 ? ((pl == c0 || pl == c1) ? 1.0f : 0.0f) : (float)blue;
-            ac[kk] = (kx < 34 && hh == (int)h) ? v : 0.0f;
-        }
-#pragma unroll
-        for (int k = 0; k < 13; ++k) {
-            acc[k] = skip[k] = f32x4{};
-            if (k + 1 < 13) fetch(tb[(k + 1) & 1], k + 1);
-#pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                const int na = p8::nb_sq(p8::kTileSq[k][0], t), nbq = p8::nb_sq(p8::kTileSq[k][1], t);
-                if (na >= 0 || nbq >= 0) {
-                    const int sh = h ? (nbq >= 0 ? 31 - nbq : 0) : (na >= 0 ? 31 - na : 0);  // bit 0 is never set
-                    const float a = (float)((bb >> sh) & 1u);
-                    acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[t], a, acc[k], 0, 0, 0);
-                }
-            }
-#pragma unroll
-            for (int kk = 0; kk < 9; ++kk)
-                acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[k & 1][kk], ac[kk], acc[k], 0, 0, 0);
-        }
-        uint32_t pk[13][2][2];
-#pragma unroll
-        for (int k = 0; k < 13; ++k)
-            h3t_pack_one<true>(acc[k], pk[k], bias1, f32x4{1.0f, 1.0f, 1.0f, 1.0f}, skip[k], false, hmax);
-        p8_store(pk, img, est, h);
-        __syncthreads();
-    }
-    const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
-    for (int c = 0; c < 2 * blocks; ++c) {
-        const f32x4 bbt = *reinterpret_cast<const f32x4*>(p + h3::kW + cq);
-        const f32x4 sct = *reinterpret_cast<const f32x4*>(p + h3::kW + nn::kCh + cq);
-#pragma unroll
-        for (int k = 0; k < 13; ++k) acc[k] = f32x4{};
-        // opaque per iteration: the ~90 per-(tile, tap) half-select addresses must not be hoisted out of
-        // the conv loop as loop invariants (they would stay live in registers)
-        int hv = h, lb2[2] = {lb[0], lb[1]};
-        asm volatile("" : "+v"(hv), "+v"(lb2[0]), "+v"(lb2[1]));
-        p8_conv<KH, PIPE>(acc, img, h3_w(p, lane, nt), lb2, hv != 0,
-                    std::make_integer_sequence<int, p8::PlanOf<KH>::P.nbat>{});
-        p += h3::kW + 2 * nn::kCh;
-        uint32_t pk[13][2][2];
-        const bool res = c & 1;
-#pragma unroll
-        for (int k = 0; k < 13; ++k) h3t_pack_one<false>(acc[k], pk[k], bbt, sct, skip[k], res, hmax);
-        __syncthreads();
-        p8_store(pk, img, est, h);
-        __syncthreads();
-    }
-    {  // heads: 1x1 convs as split MFMAs per tile (rows = (half, position), columns = value, policy
-       // planes 0 / 1), feature table [8][80] in LDS, then the MLPs (2 positions per wave)
-        const float* hp = p + nn::kValueF + nn::kPolicyF;
-        const f16x8* HB = reinterpret_cast<const f16x8*>(hp);
-        f16x8 hb[2][2];
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int pc = 0; pc < 2; ++pc) hb[m][pc] = HB[(m * 2 + pc) * 64 + lane];
-        const float hs = hp[2 * 2 * 64 * 4 + (n < 3 ? n : 0)];
-        HeadRegs hr;
-        heads_fetch(hr, p, lane);
-        f32x4 hacc[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            hacc[q] = f32x4{};
-            const int k = nt + 4 * q;
-            if (k < 13) {
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    // A operand: rows (half, position) = lane & 15 -> own half's slot of tile k
-                    const char* a = img + k * 2 * p8::kSlotB + (h ? p8::kSlotB : 0) + lb[m];
-                    const f16x8 ah = *reinterpret_cast<const f16x8*>(a);
-                    const f16x8 al = *reinterpret_cast<const f16x8*>(a + p8::kPlaneB);
-                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, hb[m][0], hacc[q], 0, 0, 0);
-                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][0], hacc[q], 0, 0, 0);
-                    hacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][1], hacc[q], 0, 0, 0);
-                }
-            }
-        }
-        __syncthreads();  // the image is no longer read: its first 2.5 KB become the feature table
-        float* feat = reinterpret_cast<float*>(img);  // [8 positions][80]
-        const float hbias = n == 0 ? p[64] : n == 1 ? p[nn::kValueF + 128] : p[nn::kValueF + 129];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int k = nt + 4 * q;
-            if (k < 13 && n < 3)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = kq * 4 + r, sq = p8::kTileSq[k][row >> 3];  // C/D row = (half, position)
-                    const float v = __builtin_fmaf(hacc[q][r], hs, hbias);
-                    if (sq < 25) feat[(row & 7) * 80 + n * 25 + sq] = v > 0.0f ? v : 0.0f;
-                }
-        }
-        __syncthreads();
-        const float* fq[2] = {feat + nt * 80, feat + (nt + 4) * 80};
-        const int bq[2] = {b0 + nt, b0 + nt + 4};
-        heads_mlp_r<2>(hr, fq, bq, lane, B, policy, value);
-    }
-    // A/B-only kernel: no recompute; the counter records the overflow (the tile's results are invalid)
-    if ((hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u) atomicAdd(range_flag, 1ull);  // an fp16 hi = inf
-}
-#endif  // OAZ_AB
-
-// One kernel per precision in the product build. The A/B build (make AB=1, -DOAZ_AB=1) adds the
-// measured alternatives of the DESIGN.md perf log, selected by OAZ_NN_X6_V / OAZ_NN_BF16_V1; the
-// product build ignores those variables.
+// One kernel per precision. The A/B build (make AB=1, -DOAZ_AB=1) adds the diagnostic builds of
+// k_nn_h3, selected by OAZ_NN_X6_V (timing only, wrong results); the product build ignores it.
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy, float* value,
                              hipStream_t st) {
     if (B <= 0) return hipSuccess;
@@ -2999,114 +1688,32 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
     // exit early); plain: ceil(B / 16)
     const int per_bucket = ((B < (int)kBucket ? B : (int)kBucket) + nn::kSB - 1) / nn::kSB;
     const unsigned grid = w.tm.bcnt ? (unsigned)(w.tm.nb * per_bucket) : (unsigned)((B + nn::kSB - 1) / nn::kSB);
+    const dim3 block(64 * nn::kWaves);
     if (w.precision == OAZ_FP32_SPLIT16) {
         if (!w.fallback || !w.blob_x6) return hipErrorInvalidValue;
         // 8 waves, uneven 17 / 8 square split, batches of <= 4 squares, transposed C/D tiles, convs in
-        // pairs (compile-time residual parity), in-kernel k_nn_x6 recompute of fp16-range tiles
-        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 0, 0, 1>>;
-        int waves = 8;
+        // pairs (compile-time residual), in-kernel k_nn_x6 recompute of fp16-range tiles
+        auto k = k_nn_h3<H3Cfg<0>>;
 #if OAZ_AB
         switch (w.x6_variant) {
-            case 1: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 1, 1>>; break;  // both pieces one batch ahead
-            case 2: k = k_nn_h3<X6Cfg<8, 6, 1, 0, 1, 1>>; break;
-            case 3: k = k_nn_h3<X6Cfg<8, 6, 2, 0, 1, 1>>; break;
-            case 4: k = k_nn_h3<X6Cfg<8, 5, 1, 0, 1, 1>>; break;
-            case 5: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 0, 1>>; break;  // even 13 / 12 split
-            case 6: k = k_nn_h3<X6Cfg<8, 8, 1, 0, 1, 1>>; break;
-            case 7: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 2, 1>>; break;  // 16 / 9 split
-            case 8: k = k_nn_h3<X6Cfg<4, 8, 1, 0, 0, 1>>; waves = 4; break;  // one 512-VGPR wave per SIMD
-            case 10: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 3, 1>>; break;  // timing only: phase stamps
-            case 11: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1>>; break;  // lane-per-channel C/D tiles (DPP pair stores)
-            case 12: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1>>; break;     // timing only: phase stamps, variant 11
-            case 13: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1, 2>>; break;  // younger group in 2 phases (slower)
-            case 17: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1, 1, 1>>; break;  // heads MLPs on the VALU
-            case 18: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1>>; break;  // 15 / 10 split (the previous default)
-            case 19: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 4, 1>>; break;  // 18 / 7 split
-            case 14: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 1, 1, 2>>; break;  // timing only: phase stamps
-            case 21: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 1>>; break;  // PF: cross-conv B prefetch
-            case 22: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 3, 1, 1, 0, 0, 1>>; break;  // timing only: PF phase stamps
-            case 23: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 0, 1, 1, 0, 0, 0, 1>>; break;  // STG: staggered K-halves
-            case 24: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 0, 1, 1, 0, 0, 0, 2>>; break;  // STG + waves 4-7 at prio 1
-            case 25: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 0, 1, 1, 0, 0, 0, 1>>; break;  // STG, PIPE 2
-            case 26: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 0, 1, 1, 0, 0, 0, 1>>; break;  // timing only: STG phase stamps
-            case 27: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1>>; break;  // the previous default (runtime parity selects)
-            case 28: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 0, 0, 0, 2>>; break;  // PHA 2
-            case 29: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 0, 0, 1, 2>>; break;  // EP + PHA 2
-            case 30: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 0, 0, 0, 3>>; break;  // PHA 3
-            case 31: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 3, 1, 1, 0, 0, 0, 0, 1, 2>>; break;  // timing only: EP + PHA 2
-            case 32: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, PIPE 2
-            case 33: k = k_nn_h3<X6Cfg<8, 5, 1, 0, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, KH 5
-            case 34: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 2, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, 16 / 9
-            case 35: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 4, 1, 1, 0, 0, 0, 0, 1>>; break;  // EP, 18 / 7
-            case 36: k = k_nn_h3<X6Cfg<8, 4, 1, 2, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // timing only: EP phase stamps
-            case 60: k = k_nn_h3<X6Cfg<8, 4, 1, 5, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // timing only: WG timeline
-            case 42: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 0, 0, 0, 1, 0, 2>>; break;  // EP + BD 2
-            case 43: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 1, 1, 1, 0, 0, 0, 0, 1, 0, 2>>; break;  // EP + BD 2, 15 / 10
-            case 44: k = k_nn_h3<X6Cfg<8, 4, 2, 0, 0, 1, 1, 0, 0, 0, 0, 1, 0, 2>>; break;  // EP + BD 2, 13 / 12, PIPE 2
-            case 45: k = k_nn_h3<X6Cfg<8, 4, 1, 0, 0, 1, 1, 0, 0, 0, 0, 1, 0, 2>>; break;  // EP + BD 2, 13 / 12
-            case 50: k = k_nn_q2<X6Cfg<8, 4, 1, 0, 0, 1, 1, 0, 0, 0, 0, 1, 0, 1, 1>>; break;  // Q2: 2 N-tiles per wave
-            case 51: k = k_nn_q2<X6Cfg<8, 3, 1, 0, 0, 1, 1, 0, 0, 0, 0, 1, 0, 1, 1>>; break;  // Q2, KH 3
-            case 52: k = k_nn_q2<X6Cfg<8, 4, 1, 2, 0, 1, 1, 0, 0, 0, 0, 1, 0, 1, 1>>; break;  // timing only: Q2 stamps
-            case 40: k = k_nn_h3<X6Cfg<8, 4, 1, 3, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // ablation: no conv A reads
-            case 41: k = k_nn_h3<X6Cfg<8, 4, 1, 4, 3, 1, 1, 0, 0, 0, 0, 1>>; break;  // ablation: no conv B loads
-            case 20: {  // 8 positions per workgroup, 2 workgroups per CU (measured 1.40 vs 1.25 ms)
-                if (w.tm.bcnt) return hipErrorInvalidValue;  // plain tiles only (the engine does not compact)
-                const unsigned g8 = (unsigned)((B + p8::kP - 1) / p8::kP);
-                hipLaunchKernelGGL((k_nn_p8<4, 1>), dim3(g8), dim3(256), 0, st, s, B, w.blob, w.blocks, policy, value,
-                                   w.fallback);
-                return hipGetLastError();
-            }
+            case 36: k = k_nn_h3<H3Cfg<0, 2>>; break;  // phase stamps (tools/nn_phases.py)
+            case 40: k = k_nn_h3<H3Cfg<0, 3>>; break;  // ablation: no conv A reads
+            case 41: k = k_nn_h3<H3Cfg<0, 4>>; break;  // ablation: no conv B loads
+            case 60: k = k_nn_h3<H3Cfg<0, 5>>; break;  // workgroup timeline (tools/nn_timeline.py)
             default: break;
         }
 #endif
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value, w.blob_x6,
-                           w.fallback, w.tm);
+        hipLaunchKernelGGL(k, dim3(grid), block, 0, st, s, B, w.blob, w.blocks, policy, value, w.blob_x6, w.fallback,
+                           w.tm);
     } else if (w.precision == OAZ_FP32_SPLIT) {
         // 8 waves, uneven 15 / 10 square split, pipelined batches of <= 4 squares
-        auto k = k_nn_x6<X6Cfg<8, 4, 1, 0, 1>>;
-        int waves = 8;
-#if OAZ_AB
-        switch (w.x6_variant) {
-            case 1: k = k_nn_x6<X6Cfg<4, 8, 1>>; waves = 4; break;  // one 512-VGPR wave per SIMD
-            case 2: k = k_nn_x6<X6Cfg<4, 8, 2>>; waves = 4; break;  // + three piece buffers
-            case 10: k = k_nn_x6<X6Cfg<8, 5, 1, 2>>; break;             // timing only: phase stamps
-            case 5: k = k_nn_x6<X6Cfg<8, 7, 1>>; break;
-            case 6: k = k_nn_x6<X6Cfg<8, 5, 1, 0, 1>>; break;
-            case 7: k = k_nn_x6<X6Cfg<8, 5, 1>>; break;  // even 13 / 12 split
-            case 9: k = k_nn_x6<X6Cfg<8, 3, 1, 0, 1>>; break;
-            case 13: k = k_nn_x6<X6Cfg<8, 4, 1, 2, 1>>; break;  // timing only: phase stamps
-            default: break;
-        }
-#endif
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 0, st, s, B, w.blob, w.blocks, policy, value, w.tm);
+        hipLaunchKernelGGL(k_nn_x6<X6Cfg<>>, dim3(grid), block, 0, st, s, B, w.blob, w.blocks, policy, value, w.tm);
     } else if (w.precision == OAZ_BF16) {
-#if OAZ_AB
-        if (w.bf16_v1 == 1)
-            hipLaunchKernelGGL(k_nn_sq16<true>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks,
-                               policy, value, w.tm);
-        else if ((w.bf16_v1 == 2 || w.bf16_v1 == 3) && w.tm.bcnt)
-            return hipErrorInvalidValue;  // plain tiles only (the engine does not compact)
-        else if (w.bf16_v1 == 2)
-            hipLaunchKernelGGL(k_nn_bf16g<4>, dim3(grid), dim3(64 * 4), 0, st, s, B, w.blob, w.blocks, policy, value);
-        else if (w.bf16_v1 == 3)
-            hipLaunchKernelGGL(k_nn_bf16g<2>, dim3(grid), dim3(64 * 8), 0, st, s, B, w.blob, w.blocks, policy, value);
-        if (w.bf16_v1 >= 1 && w.bf16_v1 <= 3) return hipGetLastError();
-#endif
-        // the k_nn_h3 structure with one bf16 piece and one product (k_nn_h1), convs in pairs
-        auto k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 1, 0, 0, 1>>;
-#if OAZ_AB
-        if (w.bf16_v1 == 4) k = k_nn_h3<X6Cfg<8, 4, 1, 0, 3, 1, 1, 0, 1>>;  // the previous default (runtime parity)
-        if (w.bf16_v1 == 5) k = k_nn_q2<X6Cfg<8, 4, 1, 0, 0, 1, 1, 0, 1, 0, 0, 1, 0, 1, 1>>;  // Q2 (2 N-tiles per wave)
-        if (w.bf16_v1 == 6) k = k_nn_q2<X6Cfg<8, 6, 1, 0, 0, 1, 1, 0, 1, 0, 0, 1, 0, 1, 1>>;  // Q2, KH 6
-        if (w.bf16_v1 == 7) k = k_nn_h3<X6Cfg<4, 8, 1, 0, 0, 1, 1, 1, 1, 0, 0, 1>>;  // 4 waves, 2 workgroups / CU
-        if (w.bf16_v1 == 8) k = k_nn_h3<X6Cfg<4, 6, 1, 0, 0, 1, 1, 1, 1, 0, 0, 1>>;  // 4 waves, KH 6
-#endif
-        const int bw = w.bf16_v1 == 7 || w.bf16_v1 == 8 ? 4 : 8;
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * bw), 0, st, s, B, w.blob, w.blocks, policy, value, nullptr,
+        // the k_nn_h3 structure with one bf16 piece and one product, convs in pairs
+        hipLaunchKernelGGL(k_nn_h3<H3Cfg<1>>, dim3(grid), block, 0, st, s, B, w.blob, w.blocks, policy, value, nullptr,
                            nullptr, w.tm);
     } else {
-        hipLaunchKernelGGL(k_nn_sq16<false>, dim3(grid), dim3(64 * nn::kWaves), 0, st, s, B, w.blob, w.blocks, policy,
-                           value, w.tm);
+        hipLaunchKernelGGL(k_nn_sq16, dim3(grid), block, 0, st, s, B, w.blob, w.blocks, policy, value, w.tm);
     }
     return hipGetLastError();
 }
