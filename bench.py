@@ -107,9 +107,13 @@ def pmc_traffic(args, cfg):
     if prof is None:
         return None
     parts = sim_parts(cfg["games"])  # launches of each kernel per simulation step
+    # the profiled ply follows the bench's warm-up plies, but its first kernel index stays at most
+    # ~11 200 (C5's 14 x 1 600 launches made the rocprofv3 counter child crash on the host): where the
+    # game parts would push it past that, the child runs one part (half the launches per ply, the same
+    # positions and trees per simulation step), so C5 is also profiled after all 14 warm-up plies
+    if args.warmup * cfg["sims"] * parts > 11200:
+        parts = 1
     per_ply = cfg["sims"] * parts
-    # the profiled ply follows the bench's warm-up plies, but its first kernel index stays below
-    # ~11 200 (C5's 14 x 1 600 launches made the rocprofv3 counter child crash on the host)
     plies = min(args.warmup, max(1, 11200 // per_ply))
     # with fewer warm-up plies than the timed region follows, the staggered starts are compressed to
     # them (every slot playing, game ages spread over `plies` plies) so the profiled ply is steady state
@@ -122,7 +126,7 @@ def pmc_traffic(args, cfg):
                    "--kernel-iteration-range", f"[{first}-{last}]", "--output-format", "csv", "-d", d, "-o", "pmc",
                    "--", sys.executable, str(Path(__file__).resolve()), "--pmc-child", "--pmc-plies", str(plies),
                    "--stagger", str(stagger), "--warmup", str(plies), "--config", args.config, "--games", str(cfg["games"]),
-                   "--sims", str(cfg["sims"]), "--fp32-kernel", args.fp32_kernel]
+                   "--sims", str(cfg["sims"]), "--fp32-kernel", args.fp32_kernel, "--pmc-parts", str(parts)]
             try:
                 subprocess.run(cmd, timeout=600, capture_output=True, check=True)
             except (subprocess.SubprocessError, OSError) as exc:

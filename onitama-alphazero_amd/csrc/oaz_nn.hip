@@ -581,11 +581,25 @@ __device__ __forceinline__ float load(const char* img, int row, int c) { return 
 // own N-tile w & 3 of two disjoint square groups, cut unevenly from kSqOrderU (interior, corners,
 // then edges): the older wave wins MFMA arbitration and runs ahead, the younger fills its gaps, so
 // equal halves leave the younger finishing alone. GRP 3 / 4: 15 / 10 squares (109 / 60 on-board
-// taps; k_nn_x6), GRP 7 / 8: 17 / 8 (k_nn_h3; measured 1-2 % faster than 15 / 10 there).
+// taps; k_nn_x6), GRP 7 / 8 and 9 / 10: k_nn_h3's (below).
 constexpr int8_t kSqOrderU[25] = {6, 7, 8, 11, 12, 13, 16, 17, 18, 0, 4, 20, 24, 2, 22,
                                   1, 3, 5, 10, 9, 14, 15, 19, 21, 23};
-constexpr int grp_n(int grp) { return grp == 3 ? 15 : grp == 4 ? 10 : grp == 7 ? 17 : 8; }
-constexpr int grp_first(int grp) { return grp == 4 ? 15 : grp == 8 ? 17 : 0; }
+// k_nn_h3's split: 17 / 8 in fp16x3 mode (GRP 7 / 8), 14 / 11 in bf16 mode (GRP 9 / 10). Same-box A/B
+// (tools/ab_libs.sh; profiles/r03_nn_split_ab.log, r03_nn_h1split_ab.log): fp16x3 16 / 9 within noise
+// of 17 / 8, 18 / 7 +1.2 %, 15 / 10 +0.2 %; bf16 6-block against 17 / 8: 16 / 9 -1.8 %, 15 / 10 -2.2 %,
+// 14 / 11 -3.0 %, 13 / 12 -2.4 % (its single product leaves the partner wave less to fill).
+#ifndef OAZ_H3_SPLIT
+#define OAZ_H3_SPLIT 17
+#endif
+#ifndef OAZ_H1_SPLIT
+#define OAZ_H1_SPLIT 14
+#endif
+constexpr int kH3Split = OAZ_H3_SPLIT, kH1Split = OAZ_H1_SPLIT;
+constexpr int grp_n(int grp) {
+    return grp == 3 ? 15 : grp == 4 ? 10 : grp == 7 ? kH3Split : grp == 8 ? 25 - kH3Split : grp == 9 ? kH1Split
+                                                                                                  : 25 - kH1Split;
+}
+constexpr int grp_first(int grp) { return grp == 4 ? 15 : grp == 8 ? kH3Split : grp == 10 ? kH1Split : 0; }
 constexpr int grp_sq(int grp, int j) { return kSqOrderU[grp_first(grp) + j]; }
 
 // On-board squares of group GRP for tap T: the conv is straight-line code per (group, tap), with no
@@ -701,8 +715,10 @@ struct X6Cfg {  // k_nn_x6 (OAZ_FP32_SPLIT, and k_nn_h3's fp16-range recompute):
     static constexpr int WAVES = 8, KH = 4, NS = 15, GRP0 = 3, GRP1 = 4, TR = 0, DBG = DBG_;
 };
 template <int BF_, int DBG_ = 0>
-struct H3Cfg {  // k_nn_h3: 17 / 8 squares; BF: OAZ_BF16 mode (one bf16 piece, one product; C5)
-    static constexpr int WAVES = 8, KH = 4, NS = 17, GRP0 = 7, GRP1 = 8, TR = 1, BF = BF_, DBG = DBG_;
+struct H3Cfg {  // k_nn_h3: 17 / 8 squares (bf16: 14 / 11); BF: OAZ_BF16 mode (one bf16 piece, one product; C5)
+    static constexpr int kSplit = BF_ ? kH1Split : kH3Split;
+    static constexpr int WAVES = 8, KH = 4, NS = kSplit > 12 ? kSplit : 25 - kSplit, GRP0 = BF_ ? 9 : 7,
+                         GRP1 = BF_ ? 10 : 8, TR = 1, BF = BF_, DBG = DBG_;
 };
 
 // A-fragment loads / MFMAs of batch K (compile-time: the LDS address is one of six per-lane bases
@@ -1098,6 +1114,14 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_x6(const oaz_state* __rest
 // [piece][row][64 channels] (row = square*16 + position, 128 B); the 16-byte chunk c of row r sits
 // at c ^ key(r), an XOR-linear key on the row bits found by exhaustive search
 // (tools/h3_swizzle.py): conflict-free A-fragment ds_read_b128s and epilogue ds_write_b32s.
+// PF: the B pieces of each conv's first step run are requested during the previous phase's
+// epilogue (h3_first_b); same-box A/B -0.6 % (fp16x3) / -1.4 % (bf16 6-block) per launch. The
+// phase-stamp build (DBG 2) keeps the old order: with both, its stamps make the allocator spill.
+#ifndef OAZ_H3_PF
+#define OAZ_H3_PF 1
+#endif
+template <class C>
+constexpr bool h3_pf() { return OAZ_H3_PF && C::DBG != 2; }
 namespace h3 {
 __device__ __forceinline__ int key(int r) {
     return ((r & 1) << 1) ^ ((r >> 1) & 1) ^ (((r >> 2) & 1) << 2) ^ (((r >> 3) & 1) << 1);
@@ -1199,26 +1223,37 @@ __device__ __forceinline__ void conv_h3_batch(f32x4 (&acc)[C::NS], const char* i
     __builtin_amdgcn_sched_barrier(0);  // bound the live ranges: no loads hoisted across batches
 }
 
+// The B pieces of a conv's first step run, requested before the previous phase's epilogue and
+// barriers (their L2 latency would otherwise stall both waves of the SIMD at every conv's start).
+template <class C, int GRP>
+__device__ __forceinline__ void h3_first_b(f16x8 (&b)[2], const X6W& W) {
+    constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
+    if constexpr (C::BF) {
+        b[0] = h3_ldb(W, (B0.t * 2 + B0.m) * 4);
+        b[1] = b[0];
+    } else {
+        b[0] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 0) * 4);
+        b[1] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 1) * 4);
+    }
+}
+
 template <class C, int GRP, int... K>
 __device__ __forceinline__ void conv_h3_run(f32x4 (&acc)[C::NS], const char* img, const X6W& W, const int (&lo)[2],
-                                            std::integer_sequence<int, K...>) {
+                                            const f16x8 (&bfirst)[2], std::integer_sequence<int, K...>) {
     int ab[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int sg = 0; sg < 2; ++sg) ab[m][sg] = lo[m] + sg * 65536;
-    constexpr H3Batch B0 = H3P<C, GRP>::P.b[0];
-    f16x8 b[2], bn[2];
+    f16x8 b[2] = {bfirst[0], bfirst[1]}, bn[2];
+    if constexpr (!h3_pf<C>()) h3_first_b<C, GRP>(b, W);
     if constexpr (C::BF) {
-        b[0] = h3_ldb(W, (B0.t * 2 + B0.m) * 4);
         f16x8 X[C::KH], X2[C::KH];
         h3_load<C, GRP, 0>(X, img, ab, 0);
         ((K % 2 == 0 ? conv_h1_batch<C, GRP, K>(acc, img, W, b, bn, X, X2, ab)
                      : conv_h1_batch<C, GRP, K>(acc, img, W, b, bn, X2, X, ab)),
          ...);
     } else {
-        b[0] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 0) * 4);
-        b[1] = h3_ldb(W, ((B0.t * 2 + B0.m) * 2 + 1) * 4);
         f16x8 X[C::KH], Y[C::KH];
         h3_load<C, GRP, 0>(X, img, ab, 1);
         (conv_h3_batch<C, GRP, K>(acc, img, W, b, bn, X, Y, ab), ...);
@@ -1508,6 +1543,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
 
     f32x4 acc[NS];
     f32x4 skip[NS];
+    f16x8 bpre[2];  // the next conv's first B pieces (h3_first_b)
     uint32_t hmax = 0;  // largest hi bit patterns (two u16 halves)
     // DBG 2: first layer (MFMA tail + epilogue), conv, barrier 1, epilogue, barrier 2, heads, kernel start (state,
     // LUT, barrier), first-layer MFMAs (incl. their operand loads)
@@ -1565,6 +1601,10 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         const f32x4 inv1 = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f}
                                  : *reinterpret_cast<const f32x4*>(l1c + 26 * h3::kL1Frag + cq);
         epilogue_h3t_pack<C, GRP, true, 0>(acc, pk, bias1t, inv1, skip, hmax);
+        if constexpr (h3_pf<C>()) {
+            constexpr size_t kWc = C::BF ? nn::kW64h : h3::kW;
+            h3_first_b<C, GRP>(bpre, h3_w(blob + nn::kL1B + nn::kCh + nn::kL1Table, lane, nt, (int)(kWc * 4)));
+        }
         epilogue_h3t_store<C, GRP>(pk, img, eot);
         __syncthreads();
     }
@@ -1572,19 +1612,22 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
     // ReLU; small block 2: conv + BN, + skip, ReLU, the result kept as the next skip)
     stamp(0);
     const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;
-    auto conv_one = [&](auto res) {
+    auto conv_one = [&](auto res, bool more) {
         constexpr int RES = decltype(res)::value;
         constexpr size_t kWc = C::BF ? nn::kW64h : h3::kW;  // B fragments of one conv
         const f32x4 bbt = *reinterpret_cast<const f32x4*>(p + kWc + cq);  // in flight during the conv
         const f32x4 sct = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f} : *reinterpret_cast<const f32x4*>(p + kWc + nn::kCh + cq);
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = f32x4{};
-        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt, (int)(kWc * 4)), lo,
+        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt, (int)(kWc * 4)), lo, bpre,
                             std::make_integer_sequence<int, H3P<C, GRP>::P.nbat>{});
         stamp(1);
+        const float* pc = p;
         p += C::BF ? nn::kW64h + nn::kCh : h3::kW + 2 * nn::kCh;
         uint32_t pk[NS][2][2];
         epilogue_h3t_pack<C, GRP, false, RES>(acc, pk, bbt, sct, skip, hmax);  // before the barrier: a
+        // (unconditional, so that the old pieces are dead during the conv; the last conv reloads its own)
+        if constexpr (h3_pf<C>()) h3_first_b<C, GRP>(bpre, h3_w(more ? p : pc, lane, nt, (int)(kWc * 4)));
         stamp(3);                                                             // wave done early packs
         __syncthreads();                                                      // beside its partner's MFMAs
         stamp(2);
@@ -1594,14 +1637,17 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         stamp(4);
     };
     for (int c = 0; c < blocks; ++c) {
-        conv_one(std::integral_constant<int, 0>{});
-        conv_one(std::integral_constant<int, 1>{});
+        conv_one(std::integral_constant<int, 0>{}, true);
+        conv_one(std::integral_constant<int, 1>{}, c + 1 < blocks);
     }
     h3_heads<C>(p, img, lo, wave, lane, b0, B, policy, value);
     if constexpr (C::DBG == 2) {
         stamp(5);
         __syncthreads();
-        if (lane < 8 && b0 + nn::kSB <= B) policy[(size_t)b0 * 50 + wave * 8 + lane] = (float)ph[lane];
+        float v = 0.0f;  // (compile-time indices: the sums stay in scalar registers)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v = lane == k ? (float)ph[k] : v;
+        if (lane < 8 && b0 + nn::kSB <= B) policy[(size_t)b0 * 50 + wave * 8 + lane] = v;
     }
     if constexpr (C::BF) return false;  // bf16 pieces have fp32's exponent range
     return (hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u;  // hi = inf
@@ -1645,9 +1691,9 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __rest
     const uint64_t rt0 = C::DBG == 5 ? __builtin_amdgcn_s_memrealtime() : 0;
     const TileSpan sp = tile_span(tm, B);
     bool ovf;
-    const bool g0 = (threadIdx.x >> 8) == 0;  // waves 0-3: square group GRP0 (17 squares), 4-7: GRP1 (8)
+    const bool g0 = (threadIdx.x >> 8) == 0;  // waves 0-3: square group GRP0 (17 / 15 squares), 4-7: GRP1
     if (g0) {
-        __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(1);  // (priority to the smaller group measured 6 % slower)
         ovf = nn_h3_body<C, C::GRP0>(states, sp, blob, blocks, policy, value, lds);
     } else {
         ovf = nn_h3_body<C, C::GRP1>(states, sp, blob, blocks, policy, value, lds);
