@@ -708,7 +708,8 @@ struct H3PlanOf {
 // Kernel configurations (8 waves: two per SIMD, square groups GRP0 / GRP1 x 4 N-tiles, <= 256 VGPRs;
 // KH: squares per batch of A fragments). DBG (diagnostic builds only, `make AB=1`; timing only, wrong
 // results): 2 per-wave s_memtime phase sums written over the first policy rows (tools/nn_phases.py),
-// 3 no conv A reads, 4 no conv B loads (ablations), 5 workgroup start / end stamps
+// 3 no conv A reads, 4 no conv B loads, 7 conv B loads of one step, 9 conv A reads discarded (ablations),
+// 5 workgroup start / end stamps
 // (tools/nn_timeline.py).
 template <int DBG_ = 0>
 struct X6Cfg {  // k_nn_x6 (OAZ_FP32_SPLIT, and k_nn_h3's fp16-range recompute): 15 / 10 squares
@@ -1147,7 +1148,11 @@ __device__ __forceinline__ void h3_load(f16x8 (&a)[N], const char* img, const in
     for (int q = 0; q < N; ++q)
         if (q < B.n) {
             const int off = B.nb[q] * (nn::kSB * h3::kRowB) + piece * h3::kPlaneB;  // folds to a constant
-            a[q] = *reinterpret_cast<const f16x8*>(img + ab[B.m][off >> 16] + (off & 0xffff));
+            const f16x8 v = *reinterpret_cast<const f16x8*>(img + ab[B.m][off >> 16] + (off & 0xffff));
+            if constexpr (C::DBG == 9 && K > 1)  // ablation: the A reads happen, the MFMAs keep stale operands
+                asm volatile("" ::"v"(v));
+            else
+                a[q] = v;
         }
 }
 
@@ -1187,11 +1192,12 @@ __device__ __forceinline__ void h3_step_b(const X6W& W, f16x8 (&b)[2], f16x8 (&b
     }
     if constexpr (B.first && B.nstep >= 0 && C::DBG != 4) {  // prefetch the next step run's B pieces
                                                               // (DBG 4: ablation, no B loads)
+        constexpr int ns = C::DBG == 7 ? 0 : B.nstep;  // ablation 7: every step reads step 0's pieces (L1 hits)
         if constexpr (C::BF) {  // BF: [step][N-tile][lane] bf16x8, one piece
-            bn[0] = h3_ldb(W, B.nstep * 4);
+            bn[0] = h3_ldb(W, ns * 4);
         } else {
-            bn[0] = h3_ldb(W, (B.nstep * 2 + 0) * 4);
-            bn[1] = h3_ldb(W, (B.nstep * 2 + 1) * 4);
+            bn[0] = h3_ldb(W, (ns * 2 + 0) * 4);
+            bn[1] = h3_ldb(W, (ns * 2 + 1) * 4);
         }
     }
 }
@@ -1745,6 +1751,8 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
             case 36: k = k_nn_h3<H3Cfg<0, 2>>; break;  // phase stamps (tools/nn_phases.py)
             case 40: k = k_nn_h3<H3Cfg<0, 3>>; break;  // ablation: no conv A reads
             case 41: k = k_nn_h3<H3Cfg<0, 4>>; break;  // ablation: no conv B loads
+            case 47: k = k_nn_h3<H3Cfg<0, 7>>; break;  // ablation: conv B loads from one step (L1 hits)
+            case 49: k = k_nn_h3<H3Cfg<0, 9>>; break;  // ablation: conv A reads discarded (stale operands)
             case 60: k = k_nn_h3<H3Cfg<0, 5>>; break;  // workgroup timeline (tools/nn_timeline.py)
             default: break;
         }
