@@ -86,10 +86,11 @@ def parse():
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-plies", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--pmc-parts", type=int, default=0, help=argparse.SUPPRESS)
-    ap.add_argument("--mode", default="selfplay", choices=["selfplay", "train", "pure_mcts"],
+    ap.add_argument("--mode", default="selfplay", choices=["selfplay", "train", "pure_mcts", "arena"],
                     help="train: SGD steps of the training loop (SURVEY 8f #2), not the headline metric")
     ap.add_argument("--train-blocks", type=int, default=5, help="train mode: residual blocks (bin/train.rs:60)")
     ap.add_argument("--pm-games", type=int, default=262144, help="pure_mcts mode: searches per launch")
+    ap.add_argument("--arena-games", type=int, default=4096, help="arena mode: games per fight per GPU")
     ap.add_argument("--pm-playouts", type=int, default=400, help="pure_mcts mode: playouts per search")
     ap.add_argument("--train-batch", type=int, default=512, help="train mode: global batch (train.rs:142)")
     return ap.parse_args()
@@ -541,6 +542,74 @@ def pure_mcts_main(args, world, rank, local):
         dist.destroy_process_group()
 
 
+ARENA_METRIC = "arena fight games/sec (AlphaZero vs AlphaZero, evaluator.rs fight, 400 sims/move, train=false)"
+
+
+def arena_main(args, world, rank, local):
+    """one step = one whole fight (evaluator.rs:355-399) of arena_games games between
+    two AlphaZero agents (3-block random-init weights, seeds 0 and 1; AlphaZeroMctsConfig of the pit,
+    evaluator.rs:198-204, with the playout budget and no time cutoff), the games played in parallel
+    (onitama_az/evaluator.py fight: every ply, each agent searches all of its games in one batched
+    oaz_search). Games are sharded over ranks (each rank its own deals); nothing is exchanged."""
+    from onitama_az import _abi
+    from onitama_az.evaluator import AlphaZeroAgent, EvaluatorConfig, fight
+    from onitama_az.mcts import AlphaZeroMctsConfig, ConvResNet, ConvResNetConfig, Options
+    n, sims = args.arena_games, args.sims or 400
+    opts = Options(precision=_abi.FP32_SPLIT16, device=local)
+    net = ConvResNetConfig(resnet_block_amnt=3)
+    new, best = ConvResNet(net, opts, seed=0), ConvResNet(net, opts, seed=1)
+    cfg = AlphaZeroMctsConfig(search_time=0.4, exploration_c=5.0, max_playouts=sims, train=False)
+    agent, opponent = AlphaZeroAgent(cfg, new), AlphaZeroAgent(cfg, best)
+    fight(EvaluatorConfig(game_amnt=n, max_plies=1, seed=20260101 + rank), agent, opponent)  # warm-up: 3 plies
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    plies = games = 0
+    wins = [0, 0, 0]
+    for k in range(args.steps):
+        st = fight(EvaluatorConfig(game_amnt=n, seed=20260101 + (k + 1) * world + rank), agent, opponent)
+        plies += sum(st.plies)
+        games += n
+        wins[0] += st.general.wins
+        wins[1] += st.general.loses
+        wins[2] += st.general.draws
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed, float(plies), float(games)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        tm = t[:1].clone()
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t[0] = tm[0]
+    T, plies_all, games_all = (float(x) for x in t.tolist())
+    if rank == 0:
+        out = {"metric": ARENA_METRIC, "value": games_all / T, "unit": "games/s", "n_gpus": world, "steps": args.steps,
+               "warmup": 1, "ms_per_step": 1e3 * T / args.steps, "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "fp32 (fp16x3 split)",
+               "data": "synthetic (random-init weights seeds 0 / 1, seeded 5-of-16 deals)",
+               "config": {"workload": f"arena: {n} games/GPU per fight, {sims} sims/move, 3-block, c 5, train=false, "
+                                      "152-ply cut", "parallelism": f"games sharded x{world}"},
+               "sims_per_s": plies_all * sims / T, "plies_per_s": plies_all / T,
+               "mean_plies_per_game": plies_all / max(1.0, games_all),
+               "rank0_results": {"wins": wins[0], "loses": wins[1], "draws": wins[2]},
+               "note": "a fight runs until its last game ends (or the 152-ply cut), so its tail searches few games"}
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cb = cpu_baseline({"blocks": 3, "sims": sims, "fixed_deck": 0}, args.cpu_seconds, args.cpu_threads)
+                mpg = out["mean_plies_per_game"]
+                out["cpu_baseline"] = {"value": cb["value"] / (sims * mpg), "unit": "games/s", "cores": cb["cores"],
+                                       "kind": "port", "sims_per_s": cb["value"],
+                                       "sample": cb["sample"] + f"; games/s = sims/s / ({sims} sims x {mpg:.1f} plies "
+                                                 "per game of this fight); the reference's arena runs the same "
+                                                 "searches without root noise (train=false)"}
+            except Exception as ex:  # noqa: BLE001
+                out["cpu_baseline"] = {"error": repr(ex)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def sim_parts(games, parts=0):
     """Game parts (streams) of the engine's simulation loop: oaz_config.parts, or auto = 2 from 2048
     games (oaz_engine.cpp game_parts); bench.py checks it against kernel_times().parts."""
@@ -668,6 +737,8 @@ def main():
         return train_main(args, world, rank, local)
     if args.mode == "pure_mcts":
         return pure_mcts_main(args, world, rank, local)
+    if args.mode == "arena":
+        return arena_main(args, world, rank, local)
     from onitama_az import _abi
     from onitama_az.engine import Engine
     from onitama_az.weights import random_weights

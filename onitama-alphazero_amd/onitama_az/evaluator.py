@@ -9,6 +9,7 @@ reference's; only the order in which the games' moves are computed differs.
 """
 from __future__ import annotations
 
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
@@ -118,6 +119,11 @@ class BatchedAgent:
     def name(self) -> str:
         raise NotImplementedError
 
+    def device_key(self):
+        """What this agent's searches run on (None: the host). Two agents with different GPU keys can
+        search their games of a ply at the same time (fight)."""
+        return None
+
 
 class AlphaZeroAgent(BatchedAgent):
     """AlphaZeroMcts (alphazero_mcts/mod.rs:122-161) answering a batch of positions with one
@@ -137,6 +143,9 @@ class AlphaZeroAgent(BatchedAgent):
 
     def name(self) -> str:
         return self.mcts.name()
+
+    def device_key(self):  # the model's shared search engine (one search at a time per engine)
+        return ("engine", id(self.mcts.model))
 
 
 class RandomAgent(BatchedAgent):
@@ -200,20 +209,29 @@ def fight(config: EvaluatorConfig, agent: BatchedAgent, opponent: BatchedAgent, 
     agent_red = np.arange(n) % 2 == 0  # agents = [agent, opponent], swapped after every game
     agent.reserve(n)
     opponent.reserve(n)
+    ka, kb = (getattr(a, "device_key", lambda: None)() for a in (agent, opponent))  # (duck-typed agents)
+    # two agents on different GPU engines search their games of a ply at the same time (the games
+    # are disjoint, so the order of the two searches does not matter); the C ABI calls release the GIL
+    pool = ThreadPoolExecutor(max_workers=2) if ka is not None and kb is not None and ka != kb else None
     while active.any():
         red_to_move = states["to_move"] == 0
         agent_moves = active & (red_to_move == agent_red)
-        for who, ag in ((agent_moves, agent), (active & ~agent_moves, opponent)):
-            idx = np.where(who)[0]
-            if len(idx) == 0:
-                continue
-            mv = ag.generate_moves_np(np.ascontiguousarray(states[idx]))
+        turns = [(np.where(who)[0], ag) for who, ag in ((agent_moves, agent), (active & ~agent_moves, opponent))]
+        turns = [(idx, ag) for idx, ag in turns if len(idx)]
+        if pool is not None and len(turns) == 2:
+            futs = [pool.submit(ag.generate_moves_np, np.ascontiguousarray(states[idx])) for idx, ag in turns]
+            moves = [f.result() for f in futs]
+        else:
+            moves = [ag.generate_moves_np(np.ascontiguousarray(states[idx])) for idx, ag in turns]
+        for (idx, _), mv in zip(turns, moves):
             progress[idx] = _apply(states, idx, mv)
         plies[active] += 1
         won = (progress == _abi.RED_WIN) | (progress == _abi.BLUE_WIN)
         cut = active & ~won & (budget < 0)  # train/evaluator loop: `if max_plies < 0 { break }`
         budget[active] -= 1
         active &= ~won & ~cut
+    if pool is not None:
+        pool.shutdown()
     stats = FightStatistics(agent_rating, opponent_rating)
     for k in range(n):  # Elo in game order, as the sequential reference loop
         stats.update(MoveResult(int(progress[k])), PlayerColor.Red if agent_red[k] else PlayerColor.Blue)

@@ -77,6 +77,9 @@ class Mcts:  # ai/mcts/mod.rs:13-30 (search_time is not used: searches run exact
     def reserve(self, n: int) -> None:
         pass
 
+    def device_key(self):  # a stateless GPU search (its own buffers per call): may run beside an engine's
+        return ("pure_mcts", id(self))
+
     def name(self) -> str:
         return "MCTS AI"
 

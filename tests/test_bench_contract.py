@@ -83,3 +83,13 @@ def test_sim_parts_mirrors_engine(bench, games, parts, expect):
     # oaz_engine.cpp game_parts: auto = 2 from 2048 games; 1, 2 or 4 when set (the engine itself
     # rejects other values, test_host.py)
     assert bench.sim_parts(games, parts) == expect
+
+
+def test_extra_modes_parse(bench, monkeypatch):
+    # the SURVEY 8f rows with their own measurement: train (#2), pure_mcts (#4), arena (#1)
+    for mode in ("train", "pure_mcts", "arena"):
+        monkeypatch.setattr(sys, "argv", ["bench.py", "--mode", mode])
+        assert bench.parse().mode == mode
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--mode", "arena", "--arena-games", "128"])
+    assert bench.parse().arena_games == 128
+    assert "games/sec" in bench.ARENA_METRIC
