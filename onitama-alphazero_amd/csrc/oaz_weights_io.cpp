@@ -147,20 +147,25 @@ int zip_index(const std::vector<uint8_t>& f, std::map<std::string, Member>& out)
     uint64_t entries = rd16(&f[eocd + 10]), cd_off = rd32(&f[eocd + 16]);
     if ((entries == 0xFFFF || cd_off == 0xFFFFFFFFu) && eocd >= 20 && rd32(&f[eocd - 20]) == 0x07064b50u) {
         const uint64_t z64 = rd64(&f[eocd - 20 + 8]);  // zip64 end-of-central-directory record
-        if (z64 + 56 > n || rd32(&f[z64]) != 0x06064b50u) return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: bad zip64 record");
+        if (z64 > n || n - z64 < 56 || rd32(&f[z64]) != 0x06064b50u)
+            return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: bad zip64 record");
         entries = rd64(&f[z64 + 32]);
         cd_off = rd64(&f[z64 + 48]);
     }
     uint64_t p = cd_off;
     for (uint64_t k = 0; k < entries; ++k) {
-        if (p + 46 > n || rd32(&f[p]) != 0x02014b50u) return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: bad central directory");
+        // (every bound is checked by subtraction: offsets and sizes come from the file and may be near 2^64)
+        if (p > n || n - p < 46 || rd32(&f[p]) != 0x02014b50u)
+            return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: bad central directory");
         const uint32_t method = rd16(&f[p + 10]);
         uint64_t size = rd32(&f[p + 24]), local = rd32(&f[p + 42]);
         const uint32_t nl = rd16(&f[p + 28]), xl = rd16(&f[p + 30]), cl = rd16(&f[p + 32]);
-        if (p + 46 + nl + xl + cl > n) return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: truncated central directory");
+        if (n - p - 46 < (uint64_t)nl + xl + cl) return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: truncated central directory");
         std::string name((const char*)&f[p + 46], nl);
-        for (uint64_t x = p + 46 + nl; x + 4 <= p + 46 + nl + xl;) {  // zip64 extra: sizes / offset
+        const uint64_t xend = p + 46 + nl + xl;
+        for (uint64_t x = p + 46 + nl; x + 4 <= xend;) {  // zip64 extra: sizes / offset
             const uint32_t id = rd16(&f[x]), len = rd16(&f[x + 2]);
+            if (x + 4 + len > xend) return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: bad zip extra field");
             if (id == 0x0001) {
                 uint64_t q = x + 4;
                 if (size == 0xFFFFFFFFu && q + 8 <= x + 4 + len) size = rd64(&f[q]), q += 8;  // uncompressed
@@ -169,9 +174,11 @@ int zip_index(const std::vector<uint8_t>& f, std::map<std::string, Member>& out)
             }
             x += 4 + len;
         }
-        if (local + 30 > n || rd32(&f[local]) != 0x04034b50u) return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: bad local header");
+        if (local > n || n - local < 30 || rd32(&f[local]) != 0x04034b50u)
+            return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: bad local header");
         const uint64_t data = local + 30 + rd16(&f[local + 26]) + rd16(&f[local + 28]);
-        if (method == 0 && data + size > n) return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: member '%s' truncated", name.c_str());
+        if (method == 0 && (data > n || n - data < size))
+            return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: member '%s' truncated", name.c_str());
         out[name] = Member{data, size, method};
         p += 46 + nl + xl + cl;
     }
@@ -452,9 +459,13 @@ int read_ot(const char* path, int* blocks_out, std::vector<float>* blob) {
         const size_t avail = (size_t)(it->second.size / 4);
         const uint8_t* base = &f[it->second.data_off];
         size_t numel = 1;
-        for (int64_t d : r.shape) {
-            if (d < 0) return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: tensor '%s': negative size", kv.first.c_str());
-            numel *= (size_t)d;
+        for (size_t d = 0; d < r.shape.size(); ++d) {
+            const int64_t sz = r.shape[d], sd = r.stride[d];
+            if (sz < 0 || sd < 0 || (uint64_t)sd > avail)
+                return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: tensor '%s': bad size or stride", kv.first.c_str());
+            if (sz > 0 && numel > avail / (size_t)sz)  // a parameter holds at most its storage's elements
+                return oaz_set_err(OAZ_ERR_WEIGHTS, "ot: tensor '%s' is larger than its storage", kv.first.c_str());
+            numel *= (size_t)sz;
         }
         std::vector<float> out(numel);
         std::vector<int64_t> idx(r.shape.size(), 0);

@@ -132,6 +132,36 @@ def test_c_ot_reader_and_named_loader(trained3, tmp_path):
         W.ot_blob(str(tmp_path / "junk.ot"))
 
 
+def test_c_ot_reader_survives_corrupt_archives(trained3, tmp_path):
+    """The C reader takes an untrusted file: truncations and byte mutations of a valid archive
+    (offsets, sizes, pickle opcodes, shapes) must end in OAZ_ERR_WEIGHTS or a correct read, never a
+    crash (this process would die) or a silently different blob."""
+    p = tmp_path / "m.ot"
+    W.write_ot(str(p), W.named_from_blob(trained3, 3))
+    good = p.read_bytes()
+    rng = np.random.default_rng(7)
+    q = tmp_path / "bad.ot"
+    cases = [good[:k] for k in (0, 21, 22, 100, len(good) // 2, len(good) - 23, len(good) - 1)]
+    for _ in range(300):
+        b = bytearray(good)
+        for _ in range(int(rng.integers(1, 4))):
+            i = int(rng.integers(0, len(b)))
+            if rng.random() < 0.5:  # near the directory / pickle (most structure lives there)
+                i = len(b) - 1 - int(rng.integers(0, min(len(b), 4096)))
+            b[i] = int(rng.integers(0, 256))
+        cases.append(bytes(b))
+    ok = 0
+    for data in cases:
+        q.write_bytes(data)
+        try:
+            blob, blocks = W.ot_blob(str(q))
+        except _abi.OazError:
+            continue
+        ok += 1  # a mutation inside tensor bytes reads fine; anything else must still be the network
+        assert blocks == 3 and blob.shape == trained3.shape
+    assert ok < len(cases)
+
+
 def test_ot_writer_round_trip(trained3, tmp_path):
     """save_vs format (train.rs:414-430): read back by the safe reader and by TorchScript's own
     loader (the loader tch's VarStore::load drives), tensors stored 64-byte aligned."""
