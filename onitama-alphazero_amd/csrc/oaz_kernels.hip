@@ -560,6 +560,19 @@ __device__ __forceinline__ T pick3(int c, const T& a, const T& b, const T& d) {
     return c == 0 ? a : c == 1 ? b : d;
 }
 
+// Per-game statistics from the segmented tree kernels: relaxed atomics whose result is unused
+// (no-return global atomics), so the update costs no load round trip at the end of a walk; each game's
+// counters have one writer at a time, the atomic form only drops the read.
+#ifndef OAZ_STAT_ATOMICS
+#define OAZ_STAT_ATOMICS 1
+#endif
+__device__ __forceinline__ void stat_add(uint64_t* p, uint64_t v) {
+    (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stat_max(uint64_t* p, uint64_t v) {
+    (void)__hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // lane n of every 16-lane row, to the whole row (DPP row_newbcast)
 template <int N>
 __device__ __forceinline__ double bcast_f64(double v) {
@@ -719,10 +732,17 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
         t.depth[g] = depth;
         if (t.need) t.need[g] = need;
         uint64_t* st = t.stats + (size_t)g * GS_COUNT;
+#if OAZ_STAT_ATOMICS
+        stat_add(&st[GS_SIMS], 1);
+        stat_add(&st[GS_DEPTH], depth);
+        stat_add(&st[GS_EVALS], need);
+        if (stuck) stat_add(&st[GS_STUCK], 1);
+#else
         st[GS_SIMS] += 1;
         st[GS_DEPTH] += depth;
         st[GS_EVALS] += need;
         if (stuck) st[GS_STUCK] += 1;
+#endif
     } else if (!on && g < t.G && sl == 0 && t.need) {
         t.need[g] = 0;  // an idle slot: nothing to evaluate
     }
@@ -847,9 +867,15 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
             T[leaf].first = base;
             T[leaf].nch = (uint8_t)K;
             T[leaf].flags = 1;
+#if OAZ_STAT_ATOMICS
+            stat_add(&st[GS_EXPANSIONS], 1);
+            stat_add(&st[GS_CHILDREN], K);
+            stat_max(&st[GS_MAXNODES], base + K);
+#else
             st[GS_EXPANSIONS] += 1;
             st[GS_CHILDREN] += K;
             if (base + K > st[GS_MAXNODES]) st[GS_MAXNODES] = base + K;
+#endif
         }
     }
     const int res = current_state(s);
@@ -858,7 +884,11 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
         const int root_color = roots[g].to_move & 1;
         const int pc = depth == 0 ? root_color : (root_color ^ (int)((depth - 1) & 1));
         r = reward(res, pc);
+#if OAZ_STAT_ATOMICS
+        if (sl == 0) stat_add(&st[GS_TERMINAL], 1);
+#else
         if (sl == 0) st[GS_TERMINAL] += 1;
+#endif
     } else {
         r = (double)vrow;
     }
