@@ -918,6 +918,7 @@ def main():
             "sims_per_s_per_gpu": sims_all / T / world, "stagger": stagger,
             "games_per_s": games_all / T, "plies_per_s": plies_all / T,
             "true_expansions_per_s": exp_all / T, "mean_select_depth": depth, "mean_branching": branching,
+            "plies_per_game": plies_all / max(1.0, games_all),  # steady state: plies played per game finished
             "nn_positions_per_sim": positions * args.steps * sims_steps / max(1, sims),
             "game_parts": parts,
             "nn_leaf_evaluations": "every playout" if kt.nn_samples else "compacted",
