@@ -1,0 +1,33 @@
+"""Agent-API latency: one oaz_search (one move for each of G positions) at `sims` playouts, 3-block
+fp16x3 network, train=false, for small G (the GUI / tournament / arena-tail case). Experiment tool.
+usage: python tools/search_latency.py [sims] [reps]"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "onitama-alphazero_amd"))
+import numpy as np  # noqa: E402
+
+from onitama_az import _abi  # noqa: E402
+from onitama_az.engine import Engine  # noqa: E402
+from onitama_az.game import initial_state_np  # noqa: E402
+from onitama_az.weights import random_weights  # noqa: E402
+
+sims = int(sys.argv[1]) if len(sys.argv) > 1 else 400
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+out = {}
+for G in (1, 16, 256, 2048):
+    roots = np.concatenate([initial_state_np([0, 1, 2, 3, 4]) for _ in range(G)])
+    with Engine(games=G, sims=sims, blocks=3, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_NN,
+                precision=_abi.FP32_SPLIT16) as e:
+        e.load_weights(random_weights(0, 3))
+        e.search(roots)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            e.search(roots)
+            ts.append(time.perf_counter() - t0)
+    out[G] = {"ms_median": 1e3 * float(np.median(ts)), "ms_min": 1e3 * min(ts),
+              "us_per_sim_step": 1e6 * float(np.median(ts)) / sims}
+print(json.dumps(out, indent=1))
