@@ -212,26 +212,25 @@ def fight(config: EvaluatorConfig, agent: BatchedAgent, opponent: BatchedAgent, 
     ka, kb = (getattr(a, "device_key", lambda: None)() for a in (agent, opponent))  # (duck-typed agents)
     # two agents on different GPU engines search their games of a ply at the same time (the games
     # are disjoint, so the order of the two searches does not matter); the C ABI calls release the GIL
-    pool = ThreadPoolExecutor(max_workers=2) if ka is not None and kb is not None and ka != kb else None
-    while active.any():
-        red_to_move = states["to_move"] == 0
-        agent_moves = active & (red_to_move == agent_red)
-        turns = [(np.where(who)[0], ag) for who, ag in ((agent_moves, agent), (active & ~agent_moves, opponent))]
-        turns = [(idx, ag) for idx, ag in turns if len(idx)]
-        if pool is not None and len(turns) == 2:
-            futs = [pool.submit(ag.generate_moves_np, np.ascontiguousarray(states[idx])) for idx, ag in turns]
-            moves = [f.result() for f in futs]
-        else:
-            moves = [ag.generate_moves_np(np.ascontiguousarray(states[idx])) for idx, ag in turns]
-        for (idx, _), mv in zip(turns, moves):
-            progress[idx] = _apply(states, idx, mv)
-        plies[active] += 1
-        won = (progress == _abi.RED_WIN) | (progress == _abi.BLUE_WIN)
-        cut = active & ~won & (budget < 0)  # train/evaluator loop: `if max_plies < 0 { break }`
-        budget[active] -= 1
-        active &= ~won & ~cut
-    if pool is not None:
-        pool.shutdown()
+    concurrent = ka is not None and kb is not None and ka != kb
+    with ThreadPoolExecutor(max_workers=2 if concurrent else 1) as pool:  # (joined on any exit)
+        while active.any():
+            red_to_move = states["to_move"] == 0
+            agent_moves = active & (red_to_move == agent_red)
+            turns = [(np.where(who)[0], ag) for who, ag in ((agent_moves, agent), (active & ~agent_moves, opponent))]
+            turns = [(idx, ag) for idx, ag in turns if len(idx)]
+            if concurrent and len(turns) == 2:
+                futs = [pool.submit(ag.generate_moves_np, np.ascontiguousarray(states[idx])) for idx, ag in turns]
+                moves = [f.result() for f in futs]
+            else:
+                moves = [ag.generate_moves_np(np.ascontiguousarray(states[idx])) for idx, ag in turns]
+            for (idx, _), mv in zip(turns, moves):
+                progress[idx] = _apply(states, idx, mv)
+            plies[active] += 1
+            won = (progress == _abi.RED_WIN) | (progress == _abi.BLUE_WIN)
+            cut = active & ~won & (budget < 0)  # train/evaluator loop: `if max_plies < 0 { break }`
+            budget[active] -= 1
+            active &= ~won & ~cut
     stats = FightStatistics(agent_rating, opponent_rating)
     for k in range(n):  # Elo in game order, as the sequential reference loop
         stats.update(MoveResult(int(progress[k])), PlayerColor.Red if agent_red[k] else PlayerColor.Blue)
