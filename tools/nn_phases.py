@@ -1,6 +1,7 @@
-"""Per-wave phase breakdown of k_nn_x6 / k_nn_h3 (timing build OAZ_NN_X6_V=10 (default layout; 12: variant 11): s_memtime sums per
-phase, written over each workgroup's first policy rows). Output: mean cycles per wave per phase.
-Usage: python tools/nn_phases.py [B] [blocks] [x6|h3]"""
+"""Per-wave phase breakdown of k_nn_h3 from its phase-stamp build (the A/B library, `make AB=1`,
+OAZ_NN_X6_V=36): s_memtime sums per phase, written over each workgroup's first policy rows.
+Output: mean cycles per wave per phase.
+Usage: OAZ_LIB=.../libonitama_az_ab.so python tools/nn_phases.py [B] [blocks] h3"""
 import json
 import os
 import sys
@@ -10,7 +11,7 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "onitama-alphazero_amd"))
-os.environ["OAZ_NN_X6_V"] = os.environ.get("OAZ_NN_X6_V", "10")  # (A/B build: OAZ_LIB)
+os.environ["OAZ_NN_X6_V"] = os.environ.get("OAZ_NN_X6_V", "36")  # (A/B build: OAZ_LIB)
 from onitama_az import _abi  # noqa: E402
 from onitama_az.engine import Engine  # noqa: E402
 from onitama_az.weights import random_weights  # noqa: E402
