@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of k_nn_h3 variants in the A/B build (make AB=1): per-launch time (nn_ab.py, interleaved rounds)
 # and, for timing-build variants, the per-phase cycle breakdown (nn_phases.py).
-# VARIANTS="0 21" PHASES="10 22" tools/nn_variants.sh
+# VARIANTS="0 40 41" PHASES="36" tools/nn_variants.sh  (the diagnostic variants: oaz_nn.hip launch_nn_forward)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
 export OAZ_LIB=$PWD/onitama-alphazero_amd/onitama_az/libonitama_az_ab.so
 mkdir -p gpurun_out/ab
