@@ -576,7 +576,8 @@ def arena_main(args, world, rank, local):
         wins[2] += st.general.draws
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed, float(plies), float(games)], dtype=torch.float64, device="cuda")
+    cdev = "cpu" if os.environ.get("OAZ_BENCH_REHEARSE") == "1" else "cuda"  # (gloo rehearsal: host tensors)
+    t = torch.tensor([elapsed, float(plies), float(games)], dtype=torch.float64, device=cdev)
     if world > 1:
         tm = t[:1].clone()
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
