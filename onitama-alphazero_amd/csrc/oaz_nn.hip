@@ -1282,15 +1282,12 @@ __device__ __forceinline__ uint32_t h3_lo_pair(uint32_t hi, float v0, float v1) 
     return d;
 }
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 // FIRST (the first layer): no residual, keep the result (the first block's skip). RES (the convs,
 // in pairs: the block parity is compile-time): 0 = small block 1 (conv + BN + ReLU), 1 = small block
 // 2 (conv + BN, + the residual, ReLU; the result is the next block's skip).
-// hmax: the largest hi bit pattern (v >= 0 after ReLU, so the u16 order is the value order; an
-// overflowed hi is +inf = 0x7C00).
 template <bool FIRST, bool BF, int RES>
 __device__ __forceinline__ void h3t_pack_one(const f32x4& acc, uint32_t (&pk)[2][2], const f32x4& bb, const f32x4& sc,
-                                             f32x4& skip, uint32_t& hmax) {
+                                             f32x4& skip) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const f32x2 a2 = {acc[2 * k], acc[2 * k + 1]}, s2 = {sc[2 * k], sc[2 * k + 1]};
@@ -1309,8 +1306,6 @@ __device__ __forceinline__ void h3t_pack_one(const f32x4& acc, uint32_t (&pk)[2]
         } else {
             uint32_t hi;  // (RNE; one packed conversion)
             asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(hi) : "v"(v[0]), "v"(v[1]));
-            hmax = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, hmax),
-                                                                          __builtin_bit_cast(u16x2, hi)));
             pk[0][k] = hi;
             pk[1][k] = h3_lo_pair(hi, v[0], v[1]);
         }
@@ -1321,7 +1316,16 @@ __device__ __forceinline__ void epilogue_h3t_pack(const f32x4 (&acc)[C::NS], uin
                                                   const f32x4& bb, const f32x4& sc, f32x4 (&skip)[C::NS],
                                                   uint32_t& hmax) {
 #pragma unroll
-    for (int j = 0; j < grp_n(GRP); ++j) h3t_pack_one<FIRST, (bool)C::BF, RES>(acc[j], pk[j], bb, sc, skip[j], hmax);
+    for (int j = 0; j < grp_n(GRP); ++j) {
+        h3t_pack_one<FIRST, (bool)C::BF, RES>(acc[j], pk[j], bb, sc, skip[j]);
+        // the range guard: both hi pairs of the square in one v_pk_maximum3_f16 (IEEE maximum: an
+        // overflowed hi is +inf = 0x7C00, a NaN stays NaN; hi >= +0 after ReLU)
+        if constexpr (!C::BF)
+            hmax = __builtin_bit_cast(
+                uint32_t, __builtin_elementwise_maximum(
+                              __builtin_elementwise_maximum(__builtin_bit_cast(f16x2, hmax), __builtin_bit_cast(f16x2, pk[j][0][0])),
+                              __builtin_bit_cast(f16x2, pk[j][0][1])));
+    }
 }
 template <class C, int GRP>
 __device__ __forceinline__ void epilogue_h3t_store(const uint32_t (&pk)[C::NS][2][2], char* img, int eo) {
