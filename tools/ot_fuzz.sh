@@ -23,6 +23,8 @@ W.write_ot(f"{d}/trained3.ot", W.named_from_blob(np.load("tests/golden/weights_3
 for b in (0, 1):
     W.write_ot(f"{d}/random{b}.ot", W.named_from_blob(W.random_weights(b, b), b))
 EOF
+# (libFuzzer writes its per-worker fuzz-<n>.log into the working directory)
+cd "$OUT"
 ASAN_OPTIONS=detect_leaks=1:abort_on_error=1:detect_odr_violation=0 UBSAN_OPTIONS=print_stacktrace=1 \
     "$OUT/ot_fuzz" "$OUT/corpus" "$OUT/seed" -max_total_time="$SECS" -jobs="$JOBS" -workers="$JOBS" \
     -max_len=400000 -rss_limit_mb=4096 -artifact_prefix="$OUT/" 2>&1 | tail -n 30
