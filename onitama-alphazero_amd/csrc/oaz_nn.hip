@@ -591,6 +591,9 @@ constexpr int8_t kSqOrderU[25] = {6, 7, 8, 11, 12, 13, 16, 17, 18, 0, 4, 20, 24,
 #ifndef OAZ_H3_SPLIT
 #define OAZ_H3_SPLIT 17
 #endif
+#ifndef OAZ_H3_KH
+#define OAZ_H3_KH 4  // squares per batch (A fragments in flight per step run)
+#endif
 #ifndef OAZ_H1_SPLIT
 #define OAZ_H1_SPLIT 14
 #endif
@@ -713,12 +716,12 @@ struct H3PlanOf {
 // (tools/nn_timeline.py).
 template <int DBG_ = 0>
 struct X6Cfg {  // k_nn_x6 (OAZ_FP32_SPLIT, and k_nn_h3's fp16-range recompute): 15 / 10 squares
-    static constexpr int WAVES = 8, KH = 4, NS = 15, GRP0 = 3, GRP1 = 4, TR = 0, DBG = DBG_;
+    static constexpr int WAVES = 8, KH = OAZ_H3_KH, NS = 15, GRP0 = 3, GRP1 = 4, TR = 0, DBG = DBG_;
 };
 template <int BF_, int DBG_ = 0>
 struct H3Cfg {  // k_nn_h3: 17 / 8 squares (bf16: 14 / 11); BF: OAZ_BF16 mode (one bf16 piece, one product; C5)
     static constexpr int kSplit = BF_ ? kH1Split : kH3Split;
-    static constexpr int WAVES = 8, KH = 4, NS = kSplit > 12 ? kSplit : 25 - kSplit, GRP0 = BF_ ? 9 : 7,
+    static constexpr int WAVES = 8, KH = OAZ_H3_KH, NS = kSplit > 12 ? kSplit : 25 - kSplit, GRP0 = BF_ ? 9 : 7,
                          GRP1 = BF_ ? 10 : 8, TR = 1, BF = BF_, DBG = DBG_;
 };
 
