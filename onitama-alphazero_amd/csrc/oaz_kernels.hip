@@ -23,7 +23,10 @@ namespace oaz {
 __constant__ AttackTable c_attack = make_attack_table();
 
 constexpr int kWave = 64;
-constexpr int kWavesPerBlock = 4;
+#ifndef OAZ_TREE_WPB
+#define OAZ_TREE_WPB 4
+#endif
+constexpr int kWavesPerBlock = OAZ_TREE_WPB;  // waves per workgroup of the tree kernels
 constexpr int kBlock = kWave * kWavesPerBlock;
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -817,7 +820,7 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
         // the policy row kept in registers for the renormalisation sums and in LDS for the
         // children's priors
         __shared__ float spol[kWavesPerBlock * 4][52];
-        float* sp = spol[(threadIdx.x >> 4) & 15];
+        float* sp = spol[threadIdx.x >> 4];  // this segment's row
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const int idx = 16 * c + sl;
