@@ -547,6 +547,33 @@ def test_search_time_budget_stops_early_and_matches_oracle_at_that_budget(orc):
         assert e.last_sims() == 64 and r.stats.sims == 8 * 64
 
 
+def test_search_time_budget_with_root_noise_then_full_search(orc):
+    """Q7 with root noise: the budget stops the search wherever the clock says, usually inside a
+    noise chunk whose successor's draws are already requested on the noise stream. The trees equal
+    the oracle's noisy search with the playouts that ran, and the engine's next search (ply 1, no
+    budget, its noise ring restarted) equals the oracle's as well (mcts_arena.rs:75-81, 183-223)."""
+    roots = random_positions(orc, 8, seed=1414)
+    with Engine(games=8, sims=20000, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=77,
+                parts=2) as e:
+        e.set_search_time(0.02)
+        e.search(roots)
+        n = e.last_sims()
+        assert 1 <= n < 20000, n
+        for g in range(8):
+            cfg = orc.search_cfg(sims=n, c_puct=5.0, evaluator=orc.EVAL_HASH, train_noise=1, seed=77, game_id=g, ply=0)
+            _, _, nodes, _ = orc.search(cfg, roots[g])
+            _compare_trees(e, g, nodes)
+        e.set_search_time(0.0)
+        e.set_search_params(48, 5.0, True)
+        r = e.search(roots)
+        assert e.last_sims() == 48 and r.stats.sims == 8 * 48
+        for g in range(8):
+            cfg = orc.search_cfg(sims=48, c_puct=5.0, evaluator=orc.EVAL_HASH, train_noise=1, seed=77, game_id=g, ply=1)
+            mv, pi, nodes, _ = orc.search(cfg, roots[g])
+            _compare_trees(e, g, nodes)
+            assert np.array_equal(r.pi[g].reshape(-1), pi.reshape(-1)) and _mv(r.moves[g]) == _mv(mv)
+
+
 def test_search_time_through_agent_config():
     """AlphaZeroMctsConfig.enforce_search_time applies search_time to the engine; without it the
     search runs max_playouts exactly (Q7 default)."""
