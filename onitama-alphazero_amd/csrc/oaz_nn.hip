@@ -594,6 +594,9 @@ constexpr int8_t kSqOrderU[25] = {6, 7, 8, 11, 12, 13, 16, 17, 18, 0, 4, 20, 24,
 #ifndef OAZ_H3_KH
 #define OAZ_H3_KH 4  // squares per batch (A fragments in flight per step run)
 #endif
+#ifndef OAZ_H1_PP
+#define OAZ_H1_PP 1  // bf16 mode: two image buffers, the convs alternate (one barrier per conv)
+#endif
 #ifndef OAZ_H1_SPLIT
 #define OAZ_H1_SPLIT 14
 #endif
@@ -1548,7 +1551,8 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nt = wave & 3;
     const int b0 = sp.b0;
-    int* pinfo = reinterpret_cast<int*>(lds + (C::BF ? h3::kPlaneB : h3::kImageB) / 4);
+    // (bf16 mode with two image buffers: one piece plane each, so the image area is kImageB as well)
+    int* pinfo = reinterpret_cast<int*>(lds + (C::BF && !OAZ_H1_PP ? h3::kPlaneB : h3::kImageB) / 4);
     const int i = lane & 15, kq = lane >> 4;
     const int lo[2] = {h3::chunk_off(i, kq), h3::chunk_off(i, 4 + kq)};
     const int cq = nt * 16 + 4 * kq;  // this lane's 4 channels cq .. cq + 3 of position i
@@ -1632,7 +1636,14 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         const f32x4 sct = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f} : *reinterpret_cast<const f32x4*>(p + kWc + nn::kCh + cq);
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = f32x4{};
-        conv_h3_run<C, GRP>(acc, img, h3_w(p, lane, nt, (int)(kWc * 4)), lo, bpre,
+        // bf16 mode, two buffers: the pair's first conv reads buffer 0 and writes buffer 1, the second
+        // reads 1 and writes 0 (the first layer and the heads use buffer 0). Every wave has finished
+        // reading the buffer a conv writes before the previous conv's closing barrier, so the
+        // in-place barrier between the MFMAs and the stores is not needed.
+        constexpr bool kPP = C::BF && OAZ_H1_PP;
+        char* const rd = kPP && RES == 1 ? img + h3::kPlaneB : img;
+        char* const wr = kPP && RES == 0 ? img + h3::kPlaneB : img;
+        conv_h3_run<C, GRP>(acc, rd, h3_w(p, lane, nt, (int)(kWc * 4)), lo, bpre,
                             std::make_integer_sequence<int, H3P<C, GRP>::P.nbat>{});
         stamp(1);
         const float* pc = p;
@@ -1642,9 +1653,9 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         // (unconditional, so that the old pieces are dead during the conv; the last conv reloads its own)
         if constexpr (h3_pf<C>()) h3_first_b<C, GRP>(bpre, h3_w(more ? p : pc, lane, nt, (int)(kWc * 4)));
         stamp(3);                                                             // wave done early packs
-        __syncthreads();                                                      // beside its partner's MFMAs
+        if constexpr (!kPP) __syncthreads();                                  // beside its partner's MFMAs
         stamp(2);
-        epilogue_h3t_store<C, GRP>(pk, img, eot);
+        epilogue_h3t_store<C, GRP>(pk, wr, eot);
         stamp(3);
         __syncthreads();
         stamp(4);
@@ -1677,9 +1688,9 @@ template <class C>
 struct H3Fallback {
     static constexpr bool kOn = !C::BF && C::DBG == 0;
     using X = X6Cfg<>;
-    // bf16 mode keeps one piece plane (+ the position info): 52 KB, and 194 VGPRs, so a tree-kernel
-    // wave fits beside the two NN waves of a SIMD
-    static constexpr int kBase = C::BF ? h3::kPlaneB / 4 + 256 : h3::kLdsFloats + h3::kLutB / 4;
+    // bf16 mode keeps two buffers of one piece plane (+ the position info): 103 KB, and 168 VGPRs, so
+    // two tree-kernel waves (80 VGPRs, 15.6 KB per workgroup) fit beside the two NN waves of a SIMD
+    static constexpr int kBase = C::BF ? (OAZ_H1_PP ? h3::kImageB : h3::kPlaneB) / 4 + 256 : h3::kLdsFloats + h3::kLutB / 4;
     static constexpr int kLds = kOn && x6::kLdsFloats > kBase ? x6::kLdsFloats : kBase;
 };
 
