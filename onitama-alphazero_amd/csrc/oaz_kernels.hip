@@ -23,6 +23,9 @@ namespace oaz {
 __constant__ AttackTable c_attack = make_attack_table();
 
 constexpr int kWave = 64;
+#ifndef OAZ_TREE_WPE
+#define OAZ_TREE_WPE 6  // waves per SIMD the segmented tree kernels are register-budgeted for (80 VGPRs)
+#endif
 #ifndef OAZ_TREE_WPB
 #define OAZ_TREE_WPB 4
 #endif
@@ -752,7 +755,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
 }
 
 // register budget: 80 VGPRs = 6 waves/SIMD (7 waves spill and measured 10 % slower)
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OAZ_TREE_WPE)))
 k_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
              const float* __restrict__ noise, SearchParams prm) {
     select_seg_body(t, roots, active, noise, prm);
@@ -919,7 +922,7 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const 
 // a game's next walk needs only its own backup (the wave's own writes, ordered by a workgroup-scope
 // fence), so every segment goes straight on to its next select instead of waiting for the whole
 // grid; one launch and one grid ramp per simulation step fewer.
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OAZ_TREE_WPE)))
 k_backup_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
                     const float* __restrict__ policy, const float* __restrict__ value, const float* __restrict__ noise,
                     SearchParams prm) {
