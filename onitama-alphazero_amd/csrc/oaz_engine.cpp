@@ -748,8 +748,8 @@ static hipEvent_t ev_get(oaz_engine* e) {
 }
 
 // Run a launch, bracketed by events on the engine stream when timing is on.
-#ifndef OAZ_NOISE_CHUNK  // 50 / 400 measured within noise of 8 at C3 and C2 (DESIGN.md perf log)
-#define OAZ_NOISE_CHUNK 8
+#ifndef OAZ_NOISE_CHUNK  // 16: C3 +0.3 % over 8 in a 4-round same-box A/B (50: +0.4 %, 3x the ring); DESIGN.md perf log
+#define OAZ_NOISE_CHUNK 16
 #endif
 static constexpr uint32_t kNoiseChunk = OAZ_NOISE_CHUNK;  // simulations of root noise produced per launch
 
