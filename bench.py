@@ -156,6 +156,33 @@ def pmc_traffic(args, cfg):
             for k in ("backup_select",):
                 if rows[k]:
                     tree_kb[k][ctr] = sum(rows[k]) / len(rows[k])
+    # the tree kernel's VALU work (one more pass, SQ block): instructions per wave and per simulation
+    sq = {}
+    with tempfile.TemporaryDirectory() as d:
+        cmd = [prof, "--pmc", "SQ_INSTS_VALU", "SQ_WAVES", "--kernel-include-regex", "k_backup_select",
+               "--kernel-iteration-range", f"[{first}-{last}]", "--output-format", "csv", "-d", d, "-o", "pmc",
+               "--", sys.executable, str(Path(__file__).resolve()), "--pmc-child", "--pmc-plies", str(plies),
+               "--stagger", str(stagger), "--warmup", str(plies), "--config", args.config, "--games", str(cfg["games"]),
+               "--sims", str(cfg["sims"]), "--fp32-kernel", args.fp32_kernel, "--pmc-parts", str(parts)]
+        try:
+            subprocess.run(cmd, timeout=600, capture_output=True, check=True)
+            per = {}
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                for r in csv.DictReader(open(f)):
+                    if "k_backup_select" in r["Kernel_Name"]:
+                        key = (int(r.get("Dispatch_Id", 0) or 0), r["Counter_Name"])
+                        per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+            ids = sorted({i for i, _ in per})[-per_ply:]
+            valu = [per.get((i, "SQ_INSTS_VALU"), 0.0) for i in ids]
+            waves = [per.get((i, "SQ_WAVES"), 0.0) for i in ids]
+            if ids and sum(waves) > 0:
+                games_per_launch = cfg["games"] / parts
+                sq = {"valu_instructions_per_wave": sum(valu) / sum(waves),
+                      "valu_instructions_per_sim": sum(valu) / len(ids) / games_per_launch,
+                      "valu_cycles_per_simd_per_launch": 4.0 * sum(valu) / len(ids) / SIMDS,
+                      "launches": len(ids)}
+        except (subprocess.SubprocessError, OSError) as exc:
+            print(f"bench: PMC pass SQ_INSTS_VALU failed ({type(exc).__name__})", file=sys.stderr)
     # per simulation step: its parts' launches
     fetch, write = 2.0 * kb["FETCH_SIZE"] * 1024.0 * parts, kb["WRITE_SIZE"] * 1024.0 * parts
     tree = {}
@@ -163,6 +190,8 @@ def pmc_traffic(args, cfg):
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
             tree[k] = {"fetch_bytes_per_sim": 2.0 * v["FETCH_SIZE"] * 1024.0 * parts / cfg["games"],
                        "write_bytes_per_sim": v["WRITE_SIZE"] * 1024.0 * parts / cfg["games"]}
+    if sq and "backup_select" in tree:
+        tree["backup_select"]["sq"] = sq
     return {"bytes_per_sim_step": fetch + write, "fetch_bytes": fetch, "write_bytes": write, "game_parts": parts,
             "raw_kb": kb, "tree_pmc": tree, "launches_profiled": counts,
             "note": f"rocprofv3 --pmc, separate passes, on the {cfg['sims']} simulation steps of ply {plies + 1} "
@@ -221,6 +250,7 @@ def pmc_clock(args, cfg):
 
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+SIMDS = 1024  # 256 CUs x 4 SIMDs (a wave64 VALU instruction occupies its SIMD for 4 cycles)
 NOMINAL_MHZ = 2400.0  # MI355X_MICROARCH.md: max engine clock (the MFMA peaks are quoted at it)
 XGMI_LINK_GBPS = 153.0  # per direction per link (7 links per GPU), the all-gather's reference rate
 
@@ -261,7 +291,8 @@ def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg, pmc=No
     noise = 8.0 * K if cfg.get("noise", True) else 0.0
     sel = 24 + 32 + D * (32 * K + 8 + 4) + noise + 32 + 16 + 1  # + the need flag
     exp = 64 + 4 + 4 + (expansions / max(1, sims)) * (200 + 32 * K + 16) + (D + 1) * (4 + 24)  # + the row
-    out = {"bound": "latency (one dependent HBM round trip per tree level; 4 games per wave)",
+    out = {"bound": "latency and VALU issue (one dependent HBM round trip per tree level, 4 games per wave; "
+                    "pmc.sq: the VALU work per launch against its time)",
            "peak_GBps": HBM_PEAK_GBPS, "sims_per_launch": per_launch,
            "kernel": "k_backup_select_seg (expand/backup of simulation s + select of s + 1, one launch per "
                      "simulation step and game part; the first select and the last expand/backup of a move run "
@@ -277,6 +308,15 @@ def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg, pmc=No
             out[name]["pmc"] = dict(pmc[name], note="rocprofv3 FETCH/WRITE_SIZE per simulation over the launches "
                                     "of one steady-state ply (after the warm-up plies); writes are small scattered "
                                     "records (leaf record, counters, path entries), each a whole write transaction")
+            sq = out[name]["pmc"].get("sq")
+            if sq:  # the launch time the VALU work alone would take, every SIMD issuing VALU every cycle
+                sq = dict(sq)
+                sq["valu_floor_us_at_nominal_clock"] = sq["valu_cycles_per_simd_per_launch"] / NOMINAL_MHZ
+                sq["valu_floor_frac_of_launch"] = sq["valu_floor_us_at_nominal_clock"] / (t * 1e6)
+                sq["note"] = ("SQ_INSTS_VALU / SQ_WAVES over the same ply; a wave64 VALU instruction holds its SIMD 4 "
+                              "cycles, so valu_cycles_per_simd_per_launch / clock is the launch's VALU-issue floor "
+                              "(the launch time here overlaps the other part's kernels)")
+                out[name]["pmc"]["sq"] = sq
     return out
 
 
@@ -668,7 +708,8 @@ def single_stream_leg(args, cfg, device, precision):
     nn = nn_step_rate(kt, st1.search.nn_evals - st0.search.nn_evals, 2 * cfg["sims"], cfg["blocks"])
     nn["nonzero_achieved"] = (nonzero_flop_per_sim(cfg["blocks"]) * nn["positions"] / (nn["avg_launch_ms"] * 1e-3)
                               / 1e12 if nn["avg_launch_ms"] > 0 else 0.0)
-    nn.update(sims_per_s=sims / dt, ms_per_step=1e3 * dt / 2, launches=kt.nn_n)
+    nn.update(sims_per_s=sims / dt, ms_per_step=1e3 * dt / 2, launches=kt.nn_n,
+              tree_launch_us=1e3 * kt.backup_select_ms / kt.backup_select_n if kt.backup_select_n else None)
     return nn
 
 
@@ -986,6 +1027,16 @@ def main():
                 clock_note="sclk = GRBM_GUI_ACTIVE/8 cycles per k_nn_ launch (rocprofv3 pass on this box, one stream) "
                            "/ the HIP-event launch time above; rocprof_avg_launch_ms = the same pass's kernel-trace "
                            "duration of those launches (profiled launches run at profiled_clock_mhz)")
+        bs = (out.get("tree_kernels") or {}).get("backup_select") or {}
+        sq = (bs.get("pmc") or {}).get("sq")
+        if leg.get("tree_launch_us"):
+            bs["single_stream_launch_us"] = leg["tree_launch_us"]  # all games in one launch, nothing beside it
+            if sq:
+                mhz = out["roofline"].get("sclk_mhz") or NOMINAL_MHZ
+                parts = max(1, (traffic or {}).get("game_parts", 1))
+                floor_us = sq["valu_cycles_per_simd_per_launch"] * parts / mhz
+                sq["valu_floor_frac_single_stream"] = floor_us / leg["tree_launch_us"]
+                sq["clock_mhz_used"] = mhz
         if world == 1 and not args.no_exact:
             out["leaf_compaction"] = compaction_leg(args, cfg, local, stagger)
         if not args.no_exact and world == 1 and cfg["precision"] in ("fp32_split16", "fp32_split"):
