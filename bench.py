@@ -179,7 +179,7 @@ def pmc_traffic(args, cfg):
                 games_per_launch = cfg["games"] / parts
                 sq = {"valu_instructions_per_wave": sum(valu) / sum(waves),
                       "valu_instructions_per_sim": sum(valu) / len(ids) / games_per_launch,
-                      "valu_cycles_per_simd_per_launch": 4.0 * sum(valu) / len(ids) / SIMDS,
+                      "valu_cycles_per_simd_per_launch": VALU_CYC * sum(valu) / len(ids) / SIMDS,
                       "launches": len(ids)}
         except (subprocess.SubprocessError, OSError) as exc:
             print(f"bench: PMC pass SQ_INSTS_VALU failed ({type(exc).__name__})", file=sys.stderr)
@@ -250,7 +250,8 @@ def pmc_clock(args, cfg):
 
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
-SIMDS = 1024  # 256 CUs x 4 SIMDs (a wave64 VALU instruction occupies its SIMD for 4 cycles)
+SIMDS = 1024  # 256 CUs x 4 SIMDs
+VALU_CYC = 2  # issue throughput of a wave64 32-bit VALU instruction on a SIMD-32 (MI355X_MICROARCH.md; f64 ops take more)
 NOMINAL_MHZ = 2400.0  # MI355X_MICROARCH.md: max engine clock (the MFMA peaks are quoted at it)
 XGMI_LINK_GBPS = 153.0  # per direction per link (7 links per GPU), the all-gather's reference rate
 
@@ -291,8 +292,8 @@ def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg, pmc=No
     noise = 8.0 * K if cfg.get("noise", True) else 0.0
     sel = 24 + 32 + D * (32 * K + 8 + 4) + noise + 32 + 16 + 1  # + the need flag
     exp = 64 + 4 + 4 + (expansions / max(1, sims)) * (200 + 32 * K + 16) + (D + 1) * (4 + 24)  # + the row
-    out = {"bound": "latency and VALU issue (one dependent HBM round trip per tree level, 4 games per wave; "
-                    "pmc.sq: the VALU work per launch against its time)",
+    out = {"bound": "latency (one dependent HBM round trip per tree level, 4 games per wave; pmc.sq: the VALU "
+                    "work per launch against its time)",
            "peak_GBps": HBM_PEAK_GBPS, "sims_per_launch": per_launch,
            "kernel": "k_backup_select_seg (expand/backup of simulation s + select of s + 1, one launch per "
                      "simulation step and game part; the first select and the last expand/backup of a move run "
@@ -313,9 +314,10 @@ def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg, pmc=No
                 sq = dict(sq)
                 sq["valu_floor_us_at_nominal_clock"] = sq["valu_cycles_per_simd_per_launch"] / NOMINAL_MHZ
                 sq["valu_floor_frac_of_launch"] = sq["valu_floor_us_at_nominal_clock"] / (t * 1e6)
-                sq["note"] = ("SQ_INSTS_VALU / SQ_WAVES over the same ply; a wave64 VALU instruction holds its SIMD 4 "
-                              "cycles, so valu_cycles_per_simd_per_launch / clock is the launch's VALU-issue floor "
-                              "(the launch time here overlaps the other part's kernels)")
+                sq["note"] = ("SQ_INSTS_VALU / SQ_WAVES over the same ply; at 2 issue cycles per wave64 VALU "
+                              "instruction (SIMD-32; f64 ops take more) valu_cycles_per_simd_per_launch / clock is a "
+                              "lower bound of the launch's VALU time; far below the launch time = latency-bound (the "
+                              "launch time here overlaps the other part's kernels, single_stream_launch_us does not)")
                 out[name]["pmc"]["sq"] = sq
     return out
 

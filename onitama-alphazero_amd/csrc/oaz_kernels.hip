@@ -583,8 +583,10 @@ __device__ __forceinline__ void stat_max(uint64_t* p, uint64_t v) {
 template <int N>
 __device__ __forceinline__ double bcast_f64(double v) {
     const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x150 + N, 0xF, 0xF, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x150 + N, 0xF, 0xF, false);
+    // (every lane of a row is a valid source for row_newbcast, so bound_ctrl changes nothing but lets
+    // the compiler drop the zero it would otherwise write into the destination first)
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x150 + N, 0xF, 0xF, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x150 + N, 0xF, 0xF, true);
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 // Root fold operands of this lane's child in one chunk: q, base = P (1 - eps), sq = sqrt(N_parent)
@@ -765,18 +767,18 @@ template <int N>
 __device__ __forceinline__ float bcast_f32(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + N, 0xF, 0xF, false));
 }
+// polm: the lane's policy entries with the squares no child moves to already zeroed (+0.0), so each
+// term is one broadcast-convert and one add
 template <int SQ>
-__device__ __forceinline__ void policy_sum_step(const float (&polr)[4], uint32_t row0, uint32_t row1, double& sum0,
-                                                double& sum1) {
+__device__ __forceinline__ void policy_sum_step(const float (&polm)[4], double& sum0, double& sum1) {
     constexpr int i0 = SQ, i1 = 25 + SQ;
-    const float v0 = bcast_f32<(i0 & 15)>(polr[i0 >> 4]), v1 = bcast_f32<(i1 & 15)>(polr[i1 >> 4]);
-    sum0 += (row0 & sq_bit(SQ)) ? (double)v0 : 0.0;
-    sum1 += (row1 & sq_bit(SQ)) ? (double)v1 : 0.0;
+    sum0 += (double)bcast_f32<(i0 & 15)>(polm[i0 >> 4]);
+    sum1 += (double)bcast_f32<(i1 & 15)>(polm[i1 >> 4]);
 }
 template <int... SQ>
-__device__ __forceinline__ void policy_sums(const float (&polr)[4], uint32_t row0, uint32_t row1, double& sum0,
-                                            double& sum1, std::integer_sequence<int, SQ...>) {
-    (policy_sum_step<SQ>(polr, row0, row1, sum0, sum1), ...);
+__device__ __forceinline__ void policy_sums(const float (&polm)[4], double& sum0, double& sum1,
+                                            std::integer_sequence<int, SQ...>) {
+    (policy_sum_step<SQ>(polm, sum0, sum1), ...);
 }
 
 // k_expand_backup with 16 lanes per game: lane sl generates the moves of (card, from) combos
@@ -849,7 +851,13 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
         // Entry idx comes from lane idx & 15 by DPP row_newbcast; an unset square adds +0.0, which
         // leaves a non-negative sum unchanged bit for bit (the old loop loaded and waited 50 times).
         double sum0 = 0.0, sum1 = 0.0;
-        policy_sums(polr, row0, row1, sum0, sum1, std::make_integer_sequence<int, 25>{});
+        float polm[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int idx = 16 * c + sl, k = idx >= 25 ? 1 : 0, sq = idx - 25 * k;
+            polm[c] = idx < 50 && ((k ? row1 : row0) & sq_bit(sq)) ? polr[c] : 0.0f;
+        }
+        policy_sums(polm, sum0, sum1, std::make_integer_sequence<int, 25>{});
         const uint32_t base = nn0;
         uint32_t o = incl - cnt;
 #pragma unroll
