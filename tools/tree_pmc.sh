@@ -7,9 +7,12 @@ PY=$(command -v python3)
 SIMS=${SIMS:-400}
 R="[$((2 * SIMS + 1))-$((3 * SIMS - 1))]"
 i=0
-for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM" \
+DEFAULT_SETS=("SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM" \
            "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_WAVES SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE" \
-           "FETCH_SIZE" "WRITE_SIZE" "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum" ; do
+           "FETCH_SIZE" "WRITE_SIZE" "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum" )
+if [ -n "${SETS:-}" ]; then IFS=';' read -r -a SETLIST <<< "$SETS"; else SETLIST=("${DEFAULT_SETS[@]}"); fi
+# SETS="A B;C D" overrides the counter sets (one rocprofv3 pass per ';'-separated set)
+for set in "${SETLIST[@]}"; do
   i=$((i+1))
   timeout -s KILL 180 rocprofv3 --pmc $set --kernel-include-regex k_backup_select_seg --kernel-iteration-range "$R" \
       --output-format csv -d $OUT/p$i -o run -- "$PY" tools/tree_prof.py 65536 $SIMS 3 > $OUT/p$i.log 2>&1
