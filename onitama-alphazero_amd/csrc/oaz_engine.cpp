@@ -427,8 +427,10 @@ static int pack_weights(const float* raw, int blocks, int precision, std::vector
         out.resize(base + h.size() / 2);
         memcpy(out.data() + base, h.data(), h.size() * sizeof(uint16_t));
         for (int k = 0; k < 4; ++k) out.push_back(inv[k]);
-        // k_nn_h3 first layer on fp16 MFMA: K block 0 = [piece][N-tile][lane] f16x8, lane l supplying
-        // A[row co = 16nt + (l&15)][k = 8q + e] (q = l>>4) = piece of s_co W[co][bitboard plane q][tap e];
+    }
+    if (precision == OAZ_FP32_SPLIT16 || precision == OAZ_BF16) {
+        // k_nn_h3 first layer on fp16 MFMA (both modes): K block 0 = [piece][N-tile][lane] f16x8, lane
+        // l supplying A[row co = 16nt + (l&15)][k = 8q + e] (q = l>>4) = piece of s_co W[co][plane q][tap e];
         // K block 1 per square = [square][piece][N-tile][lane] f16x8 with k = 8q + e: e = 0 tap 8 of
         // plane q, e >= 1 the table T[sq][c = 7q + e - 1][co] (c < 17: the 16 card planes and the
         // colour plane summed over the square's on-board taps); then 1/s[64]. s = 2^k per output

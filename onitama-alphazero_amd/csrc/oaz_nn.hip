@@ -112,7 +112,7 @@ size_t nn_packed_floats(int blocks, int precision) {
                nn::kPolicyF + h3::kHeadB + h3::kL1C;
     const size_t w = precision == OAZ_BF16 ? nn::kW64h : precision == OAZ_FP32_SPLIT ? x6::kW : nn::kW64;
     return nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (w + nn::kCh) + nn::kValueF + nn::kPolicyF +
-           (precision == OAZ_FP32_SPLIT ? x6::kHeadB : 0) + (precision == OAZ_BF16 ? 2 * 64 * 4 : 0);
+           (precision == OAZ_FP32_SPLIT ? x6::kHeadB : 0) + (precision == OAZ_BF16 ? 2 * 64 * 4 + h3::kL1C : 0);
 }
 
 // Square groups: 4 corners + 4 edges + 5 interior (85 on-board taps) | 8 edges + 4 interior (84).
@@ -596,6 +596,9 @@ constexpr int8_t kSqOrderU[25] = {6, 7, 8, 11, 12, 13, 16, 17, 18, 0, 4, 20, 24,
 #endif
 #ifndef OAZ_H1_PP
 #define OAZ_H1_PP 1  // bf16 mode: two image buffers, the convs alternate (one barrier per conv)
+#endif
+#ifndef OAZ_H1_L1F16
+#define OAZ_H1_L1F16 1  // bf16 mode: the first layer on fp16 MFMA (the fp16x3 mode's), not exact fp32 MFMA
 #endif
 #ifndef OAZ_H1_SPLIT
 #define OAZ_H1_SPLIT 14
@@ -1576,8 +1579,12 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
     {  // encoder + first layer
         L1Regs<GRP> l1;
         L1H<GRP> l1h;
-        const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
-                           nn::kValueF + nn::kPolicyF + h3::kHeadB;
+        // the fp16 first layer's fragments and inverse scales (after the heads; bf16 mode: same section)
+        constexpr bool kF16 = !C::BF || OAZ_H1_L1F16;
+        const float* l1c = C::BF ? blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (nn::kW64h + nn::kCh) +
+                                       nn::kValueF + nn::kPolicyF + 2 * 64 * 4
+                                 : blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
+                                       nn::kValueF + nn::kPolicyF + h3::kHeadB;
         // the state loads first: vmcnt retires in issue order, so the pinfo / LUT work before the
         // barrier then waits for these and not for the first-layer operands issued after them
         const int b = min(b0 + i, sp.cap - 1);  // an empty tile of a bucket starts past cap
@@ -1585,7 +1592,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         const uint32_t bb = kq == 0 ? w[2] : kq == 1 ? w[0] : kq == 2 ? w[3] : w[1];
         oaz_state st{};
         if (tid < nn::kSB) st = states[b];
-        if constexpr (!C::BF)
+        if constexpr (kF16)
             first_layer_h3f_fetch<GRP>(l1h, l1c, lane, nt);
         else
             first_layer_x6_fetch<GRP>(l1, blob, lane, nt);
@@ -1594,7 +1601,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
             const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
             pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
         }
-        if constexpr (!C::BF)
+        if constexpr (kF16)
             for (int t = tid; t < 512; t += 64 * C::WAVES) l1_lut_build(img, t);
         const f32x4 bias1t = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
         if (b0 >= B) return false;  // an empty tile of a compacted bucket (uniform over the workgroup)
@@ -1602,7 +1609,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         stamp(6);
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[j] = skip[j] = f32x4{};
-        if constexpr (!C::BF)  // fp16 MFMA on the 0/1 inputs
+        if constexpr (kF16)  // fp16 MFMA on the 0/1 inputs
             first_layer_h3f<C, GRP>(acc, l1h, bb, pinfo[i], lane, reinterpret_cast<const char*>(lds),
                                     std::make_integer_sequence<int, grp_n(GRP)>{});
         else  // exact fp32 MFMA on the 0/1 inputs, as k_nn_x6
@@ -1615,7 +1622,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
         }
         stamp(7);
         uint32_t pk[NS][2][2];
-        const f32x4 inv1 = C::BF ? f32x4{1.0f, 1.0f, 1.0f, 1.0f}
+        const f32x4 inv1 = !kF16 ? f32x4{1.0f, 1.0f, 1.0f, 1.0f}
                                  : *reinterpret_cast<const f32x4*>(l1c + 26 * h3::kL1Frag + cq);
         epilogue_h3t_pack<C, GRP, true, 0>(acc, pk, bias1t, inv1, skip, hmax);
         if constexpr (h3_pf<C>()) {
@@ -1690,7 +1697,8 @@ struct H3Fallback {
     using X = X6Cfg<>;
     // bf16 mode keeps two buffers of one piece plane (+ the position info): 103 KB, and 168 VGPRs, so
     // two tree-kernel waves (80 VGPRs, 15.6 KB per workgroup) fit beside the two NN waves of a SIMD
-    static constexpr int kBase = C::BF ? (OAZ_H1_PP ? h3::kImageB : h3::kPlaneB) / 4 + 256 : h3::kLdsFloats + h3::kLutB / 4;
+    static constexpr int kBase = C::BF && !OAZ_H1_L1F16 ? (OAZ_H1_PP ? h3::kImageB : h3::kPlaneB) / 4 + 256
+                                                        : h3::kLdsFloats + h3::kLutB / 4;
     static constexpr int kLds = kOn && x6::kLdsFloats > kBase ? x6::kLdsFloats : kBase;
 };
 
