@@ -601,7 +601,7 @@ constexpr int8_t kSqOrderU[25] = {6, 7, 8, 11, 12, 13, 16, 17, 18, 0, 4, 20, 24,
 #define OAZ_H1_L1F16 1  // bf16 mode: the first layer on fp16 MFMA (the fp16x3 mode's), not exact fp32 MFMA
 #endif
 #ifndef OAZ_H1_SPLIT
-#define OAZ_H1_SPLIT 14
+#define OAZ_H1_SPLIT 13
 #endif
 constexpr int kH3Split = OAZ_H3_SPLIT, kH1Split = OAZ_H1_SPLIT;
 constexpr int grp_n(int grp) {
@@ -725,7 +725,7 @@ struct X6Cfg {  // k_nn_x6 (OAZ_FP32_SPLIT, and k_nn_h3's fp16-range recompute):
     static constexpr int WAVES = 8, KH = OAZ_H3_KH, NS = 15, GRP0 = 3, GRP1 = 4, TR = 0, DBG = DBG_;
 };
 template <int BF_, int DBG_ = 0>
-struct H3Cfg {  // k_nn_h3: 17 / 8 squares (bf16: 14 / 11); BF: OAZ_BF16 mode (one bf16 piece, one product; C5)
+struct H3Cfg {  // k_nn_h3: 17 / 8 squares (bf16: 13 / 12); BF: OAZ_BF16 mode (one bf16 piece, one product; C5)
     static constexpr int kSplit = BF_ ? kH1Split : kH3Split;
     static constexpr int WAVES = 8, KH = OAZ_H3_KH, NS = kSplit > 12 ? kSplit : 25 - kSplit, GRP0 = BF_ ? 9 : 7,
                          GRP1 = BF_ ? 10 : 8, TR = 1, BF = BF_, DBG = DBG_;
