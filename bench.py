@@ -90,7 +90,9 @@ def parse():
                     help="train: SGD steps of the training loop (SURVEY 8f #2), not the headline metric")
     ap.add_argument("--train-blocks", type=int, default=5, help="train mode: residual blocks (bin/train.rs:60)")
     ap.add_argument("--pm-games", type=int, default=262144, help="pure_mcts mode: searches per launch")
-    ap.add_argument("--arena-games", type=int, default=4096, help="arena mode: games per fight per GPU")
+    ap.add_argument("--arena-games", type=int, default=65536,
+                    help="arena mode: games per fight per GPU (the self-play headline's 65 536 slots: a fight lasts as "
+                         "long as its longest game, so small fights are tail-bound)")
     ap.add_argument("--pm-playouts", type=int, default=400, help="pure_mcts mode: playouts per search")
     ap.add_argument("--train-batch", type=int, default=512, help="train mode: global batch (train.rs:142)")
     return ap.parse_args()
