@@ -244,15 +244,39 @@ class Evaluator:  # evaluator.rs:139-193
                  ratings: Sequence[Tuple[float, float]] = ((800.0, 800.0), (800.0, 800.0), (800.0, 800.0))):
         self.config, self.best, self.new, self.ratings = config, best, new, ratings
 
-    def pit(self, sims: int = 400) -> Tuple[PitStatistics, bool]:
+    def pit(self, sims: int = 400, concurrent: bool = True) -> Tuple[PitStatistics, bool]:
+        """evaluator.rs:169-193. The reference starts the fights on threads of their own, each with
+        its own copy of the networks (`VarStore::copy`, evaluator.rs:206-231); here each fight gets
+        weight copies too, so every fight searches on engines of its own and the fights run at the
+        same time (concurrent=True: a fight is tail-bound by its longest game's small late batches,
+        so three tails overlap on one GPU). The fights share nothing, so their statistics equal the
+        one-after-the-other run (concurrent=False)."""
         cfg = AlphaZeroMctsConfig(search_time=0.4, max_playouts=sims, train=False)  # evaluator.rs:198-204
-        self_fight = fight(self.config, AlphaZeroAgent(cfg, self.new), AlphaZeroAgent(cfg, self.best),
-                           *self.ratings[0])
-        random_fight = fight(self.config, AlphaZeroAgent(cfg, self.new), RandomAgent(self.config.seed),
-                             *self.ratings[1])
         from .pure_mcts import Mcts  # evaluator.rs:314-353: Mcts{400 ms, min visits 5, c 1.41, 400 playouts}
-        mcts_fight = fight(self.config, AlphaZeroAgent(cfg, self.new),
-                           Mcts(search_time=0.4, min_node_visits=5, exploration_c=1.41, max_playouts=sims,
-                                seed=self.config.seed), *self.ratings[2])
+
+        def copy(m: ConvResNet) -> ConvResNet:  # train_vs.copy(self.new_nn_vs)
+            return ConvResNet(m.config, m.options, weights=np.array(m.weights, copy=True))
+
+        models = [copy(self.new), copy(self.best), copy(self.new), copy(self.new)]
+        fights = [
+            lambda: fight(self.config, AlphaZeroAgent(cfg, models[0]), AlphaZeroAgent(cfg, models[1]),
+                          *self.ratings[0]),
+            lambda: fight(self.config, AlphaZeroAgent(cfg, models[2]), RandomAgent(self.config.seed),
+                          *self.ratings[1]),
+            lambda: fight(self.config, AlphaZeroAgent(cfg, models[3]),
+                          Mcts(search_time=0.4, min_node_visits=5, exploration_c=1.41, max_playouts=sims,
+                               seed=self.config.seed), *self.ratings[2]),
+        ]
+        try:
+            if concurrent:
+                with ThreadPoolExecutor(max_workers=len(fights)) as pool:  # handles joined in order
+                    self_fight, random_fight, mcts_fight = [f.result() for f in [pool.submit(f) for f in fights]]
+            else:
+                self_fight, random_fight, mcts_fight = [f() for f in fights]
+        finally:
+            for m in models:  # the copies' engines (the reference drops each fight's VarStores)
+                eng = m.__dict__.get("_search", {}).get("engine")
+                if eng is not None:
+                    eng.close()
         return (PitStatistics(self_fight, random_fight, mcts_fight),
                 self_fight.winrate > self.config.winrate_percent)

@@ -178,3 +178,20 @@ def test_evaluator_pit():
     assert promote == (pit.self_fight.winrate > 0.55)
     assert pit.random_fight is not None and len(pit.random_fight.results) == 4
     assert pit.mcts_fight is not None and len(pit.mcts_fight.results) == 4
+
+
+@pytest.mark.gpu
+def test_evaluator_pit_concurrent_equals_sequential():
+    """The three fights on threads of their own (evaluator.rs:169-193, each on its own weight copies)
+    give the same games and ratings as the fights run one after the other."""
+    best = ConvResNet(ConvResNetConfig(resnet_block_amnt=3), seed=31)
+    new = ConvResNet(ConvResNetConfig(resnet_block_amnt=3), seed=32)
+    ev = Evaluator(EvaluatorConfig(game_amnt=24, max_plies=80, seed=10), best, new)
+    par, promote_par = ev.pit(sims=24, concurrent=True)
+    seq, promote_seq = ev.pit(sims=24, concurrent=False)
+    assert promote_par == promote_seq
+    for a, b in ((par.self_fight, seq.self_fight), (par.random_fight, seq.random_fight),
+                 (par.mcts_fight, seq.mcts_fight)):
+        assert a.results == b.results and a.plies == b.plies
+        assert (a.rating_a, a.rating_b, a.general, a.winrate) == (b.rating_a, b.rating_b, b.general, b.winrate)
+        assert a.rating_change_history == b.rating_change_history
