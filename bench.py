@@ -512,7 +512,12 @@ def train_main(args, world, rank, local):
                             "frac": achieved / PEAK_TFLOPS["fp32"], "traffic": None,
                             "flop_per_step_per_gpu": fl}}
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = train_cpu_baseline(blocks, B, args.cpu_seconds, args.cpu_threads or min(16, os.cpu_count() or 1))
+            try:  # after the timed region: a baseline failure must not lose the measured line
+                out["cpu_baseline"] = train_cpu_baseline(blocks, B, args.cpu_seconds,
+                                                         args.cpu_threads or min(16, os.cpu_count() or 1))
+            except Exception as ex:  # noqa: BLE001
+                print(f"bench: cpu_baseline failed: {ex!r}", file=sys.stderr, flush=True)
+                out["cpu_baseline"] = {"error": repr(ex)}
         print(json.dumps(out), flush=True)
     tr.close()
     if world > 1:
@@ -569,18 +574,22 @@ def pure_mcts_main(args, world, rank, local):
                "searches_per_s": G * args.steps * world / T,
                "mean_rollout_plies": plies / max(1, G * P * args.steps)}
         if not args.no_cpu_baseline and world == 1:
-            sys.path.insert(0, str(ROOT / "tests"))
-            import oracle_ffi as orc
-            from onitama_az.pure_mcts import default_config
-            cfg = default_config()
-            cfg.max_playouts, cfg.min_node_visits, cfg.exploration_c = P, 5, 1.41
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            t1 = time.perf_counter()
-            po, ns = orc.pure_mcts_bench(cfg, threads, args.cpu_seconds)
-            dt = time.perf_counter() - t1
-            out["cpu_baseline"] = {"value": po / dt, "unit": "playouts/s", "cores": threads, "kind": "port",
-                                   "sample": f"{ns} searches x {P} playouts in {dt:.1f}s on {threads} host threads "
-                                             f"(oracle C restatement of mcts_arena.rs)"}
+            try:  # after the timed region: a baseline failure must not lose the measured line
+                sys.path.insert(0, str(ROOT / "tests"))
+                import oracle_ffi as orc
+                from onitama_az.pure_mcts import default_config
+                cfg = default_config()
+                cfg.max_playouts, cfg.min_node_visits, cfg.exploration_c = P, 5, 1.41
+                threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+                t1 = time.perf_counter()
+                po, ns = orc.pure_mcts_bench(cfg, threads, args.cpu_seconds)
+                dt = time.perf_counter() - t1
+                out["cpu_baseline"] = {"value": po / dt, "unit": "playouts/s", "cores": threads, "kind": "port",
+                                       "sample": f"{ns} searches x {P} playouts in {dt:.1f}s on {threads} host "
+                                                 f"threads (oracle C restatement of mcts_arena.rs)"}
+            except Exception as ex:  # noqa: BLE001
+                print(f"bench: cpu_baseline failed: {ex!r}", file=sys.stderr, flush=True)
+                out["cpu_baseline"] = {"error": repr(ex)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
