@@ -27,7 +27,7 @@ constexpr int kWave = 64;
 #define OAZ_TREE_WPE 6  // waves per SIMD the segmented tree kernels are register-budgeted for (80 VGPRs)
 #endif
 #ifndef OAZ_TREE_WPB
-#define OAZ_TREE_WPB 4
+#define OAZ_TREE_WPB 8
 #endif
 constexpr int kWavesPerBlock = OAZ_TREE_WPB;  // waves per workgroup of the tree kernels
 constexpr int kBlock = kWave * kWavesPerBlock;
