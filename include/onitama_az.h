@@ -301,6 +301,16 @@ int oaz_load_weights_named(oaz_engine* eng, const char* const* names, const floa
 int oaz_ot_read(const char* path, float* out, size_t cap, size_t* n_out, int* blocks_out);
 /* oaz_ot_read + oaz_load_weights; the file must hold a network of the engine's block count. */
 int oaz_load_ot(oaz_engine* eng, const char* path);
+/* ---- checkpoints (save_vs, alphazero-training/src/train.rs:414-430: `vs.save(&path)`) ---------
+ * A canonical blob (n == oaz_weight_count(blocks, 64, 21)) -> a VarStore .ot archive at `path`: the
+ * TorchScript zip layout VarStore::load, oaz_ot_read and torch.jit.load read (stored members under
+ * "<file stem>/", '|' names, 64-byte aligned fp32 storages). Written to "<path>.tmp" and renamed
+ * over `path`. Host only. */
+int oaz_ot_write(const char* path, const float* blob, size_t n, int blocks);
+/* save_vs naming: "<folder>/[best_]model_<iteration>_<stamp>.ot", stamp NULL = the local time as
+ * "%Y%m%d_%H%M%S" (chrono Local::now()). OAZ_ERR_CAPACITY if out[cap] is too small. */
+int oaz_checkpoint_path(const char* folder, int64_t iteration, int is_best, const char* stamp, char* out,
+                        size_t cap);
 int oaz_sync(oaz_engine* eng);
 /* enable: 0 off, 1 HIP events around every launch, N > 1 around the kernels of every N-th
  * simulation step only (the events cost ~2 % of a C3 step when every launch is timed). */
@@ -413,6 +423,9 @@ int oaz_trainer_set_stream(oaz_trainer* t, void* stream);
  * set_weights also clears the momentum buffers (a fresh nn::Sgd). */
 int oaz_trainer_set_weights(oaz_trainer* t, const float* blob, size_t n);
 int oaz_trainer_get_weights(oaz_trainer* t, float* blob, size_t n);
+/* The trainer's parameters (and BN running statistics) as a .ot checkpoint (oaz_ot_write): the
+ * reference's save_vs on the training VarStore (train.rs:383-403, 414-430). */
+int oaz_trainer_save_ot(oaz_trainer* t, const char* path);
 /* The replay buffer: copy n host samples to the device (owned), or bind n samples already
  * resident on this GPU (e.g. oaz_samples_export_device; not owned, must outlive use). */
 int oaz_trainer_load_samples(oaz_trainer* t, const oaz_sample* samples, size_t n);

@@ -1087,6 +1087,13 @@ extern "C" int oaz_trainer_get_weights(oaz_trainer* t, float* blob, size_t n) {
     return 0;
 }
 
+extern "C" int oaz_trainer_save_ot(oaz_trainer* t, const char* path) {
+    if (!t || !path) return oaz_set_err(OAZ_ERR_ARG, "trainer_save_ot: null");
+    std::vector<float> blob(t->nparam);
+    if (int rc = oaz_trainer_get_weights(t, blob.data(), blob.size())) return rc;
+    return oaz_ot_write(path, blob.data(), blob.size(), t->cfg.blocks);
+}
+
 extern "C" int oaz_trainer_load_samples(oaz_trainer* t, const oaz_sample* s, size_t n) {
     if (!t || (!s && n)) return oaz_set_err(OAZ_ERR_ARG, "trainer: null samples");
     HIP_TRY(hipSetDevice(t->device));

@@ -240,6 +240,8 @@ _PROTOS = {
     "oaz_load_weights_named": (C.c_int, [_VOIDP, _VOIDP, _VOIDP, _VOIDP, C.c_size_t]),
     "oaz_ot_read": (C.c_int, [C.c_char_p, _VOIDP, C.c_size_t, _P(C.c_size_t), _P(C.c_int)]),
     "oaz_load_ot": (C.c_int, [_VOIDP, C.c_char_p]),
+    "oaz_ot_write": (C.c_int, [C.c_char_p, _VOIDP, C.c_size_t, C.c_int]),
+    "oaz_checkpoint_path": (C.c_int, [C.c_char_p, C.c_int64, C.c_int, C.c_char_p, C.c_char_p, C.c_size_t]),
     "oaz_sync": (C.c_int, [_VOIDP]),
     "oaz_set_timing": (C.c_int, [_VOIDP, C.c_int]),
     "oaz_kernel_times_get": (C.c_int, [_VOIDP, _P(oaz_kernel_times)]),
@@ -272,6 +274,7 @@ _PROTOS = {
     "oaz_trainer_set_stream": (C.c_int, [_VOIDP, _VOIDP]),
     "oaz_trainer_set_weights": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
     "oaz_trainer_get_weights": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
+    "oaz_trainer_save_ot": (C.c_int, [_VOIDP, C.c_char_p]),
     "oaz_trainer_load_samples": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
     "oaz_trainer_bind_device_samples": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
     "oaz_trainer_set_batches": (C.c_int, [_VOIDP, _VOIDP, C.c_int, C.c_int]),

@@ -77,6 +77,10 @@ class Trainer:
         self._check(self._lib.oaz_trainer_get_weights(self._h, _abi.ptr(out), out.size))
         return out
 
+    def save_ot(self, path: str) -> None:
+        """The training weights as a .ot checkpoint (oaz_trainer_save_ot; save_vs, train.rs:414-430)."""
+        self._check(self._lib.oaz_trainer_save_ot(self._h, str(path).encode()))
+
     def grads(self) -> np.ndarray:
         out = np.zeros(self.n_params, dtype=np.float32)
         self._check(self._lib.oaz_trainer_get_grads(self._h, _abi.ptr(out), out.size))

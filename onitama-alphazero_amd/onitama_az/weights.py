@@ -222,17 +222,24 @@ def _walk_pickle(data: bytes):
 
 
 def _find_tensors(obj, out):
-    if isinstance(obj, dict):
-        for k, v in obj.items():
-            if isinstance(v, _Sym) and v.name == "torch._utils _rebuild_tensor_v2":
-                out[k] = v.args
-            else:
-                _find_tensors(v, out)
-    elif isinstance(obj, _Sym):
-        _find_tensors(obj.args, out)
-    elif isinstance(obj, (list, tuple)):
-        for v in obj:
-            _find_tensors(v, out)
+    """name -> _rebuild_tensor_v2 args from every dict reachable from obj; iterative, and every
+    container is expanded once (memo aliasing can make shared or cyclic containers)."""
+    todo, seen = [obj], set()
+    while todo:
+        o = todo.pop()
+        if not isinstance(o, (dict, list, tuple, _Sym)) or id(o) in seen:
+            continue
+        seen.add(id(o))
+        if isinstance(o, dict):
+            for k, v in o.items():
+                if isinstance(v, _Sym) and v.name == "torch._utils _rebuild_tensor_v2":
+                    out[k] = v.args
+                else:
+                    todo.append(v)
+        elif isinstance(o, _Sym):
+            todo.append(o.args)
+        else:
+            todo.extend(o)
 
 
 def read_ot(path: str) -> Dict[str, np.ndarray]:
@@ -264,6 +271,10 @@ def read_ot(path: str) -> Dict[str, np.ndarray]:
 
 
 # ---- .ot writer (train.rs:414-430 save_vs) -------------------------------------------------------
+# The product writer is the library's (oaz_ot_write, through save_blob_ot / Trainer.save_ot); the
+# Python writer below is an independent restatement of the same archive (Python's zipfile, a
+# different zip implementation), kept to write archives from arbitrary named tensors in tests and
+# to cross-check the C writer byte for byte (tests/test_host.py).
 def _pk_str(s: str) -> bytes:
     b = s.encode("utf-8")
     return b"X" + len(b).to_bytes(4, "little") + b
@@ -319,13 +330,12 @@ class _AlignedZip:
     def __init__(self, path: str):
         self.z = zipfile.ZipFile(path, "w", compression=zipfile.ZIP_STORED)
 
-    def add(self, name: str, data: bytes, deflate: bool = False):
+    def add(self, name: str, data: bytes):
         info = zipfile.ZipInfo(name, date_time=(1980, 1, 1, 0, 0, 0))
-        info.compress_type = zipfile.ZIP_DEFLATED if deflate else zipfile.ZIP_STORED
-        if not deflate:
-            start = self.z.fp.tell() + 30 + len(name.encode())
-            pad = (-(start + 4)) % 64
-            info.extra = b"FB" + pad.to_bytes(2, "little") + b"Z" * pad
+        info.compress_type = zipfile.ZIP_STORED
+        start = self.z.fp.tell() + 30 + len(name.encode())
+        pad = (-(start + 4)) % 64
+        info.extra = b"FB" + pad.to_bytes(2, "little") + b"Z" * pad
         self.z.writestr(info, data)
 
     def close(self):
@@ -333,9 +343,9 @@ class _AlignedZip:
 
 
 def write_ot(path: str, named: Dict[str, np.ndarray], archive: str = None) -> None:
-    """Write named fp32 tensors as a tch VarStore .ot archive (TorchScript zip: data.pkl,
-    data/<i>, code/__torch__.py, constants.pkl, version), the format read_ot and the reference's
-    VarStore::load read."""
+    """Write named fp32 tensors as a tch VarStore .ot archive (TorchScript zip: data/<i>, data.pkl,
+    code/__torch__.py, constants.pkl, version; every member stored), the format read_ot and the
+    reference's VarStore::load read. Python restatement of oaz_ot_write (see above)."""
     import os
     archive = archive or os.path.splitext(os.path.basename(path))[0]
     names = list(named)
@@ -345,17 +355,23 @@ def write_ot(path: str, named: Dict[str, np.ndarray], archive: str = None) -> No
         for i, n in enumerate(names):
             z.add(f"{archive}/data/{i}", np.ascontiguousarray(named[n], dtype="<f4").tobytes())
         z.add(f"{archive}/data.pkl", _data_pkl(entries))
-        z.add(f"{archive}/code/__torch__.py", _torch_py(names), deflate=True)
+        z.add(f"{archive}/code/__torch__.py", _torch_py(names))
         z.add(f"{archive}/constants.pkl", b"\x80\x02).")
         z.add(f"{archive}/version", b"3\n")
     finally:
         z.close()
 
 
-def checkpoint_path(folder: str, iteration: int, is_best: bool, stamp: str) -> str:
-    """save_vs naming (train.rs:414-422): <folder>/[best_]model_<iter>_<YYYYmmdd_HHMMSS>.ot"""
-    return f"{folder}/{'best_' if is_best else ''}model_{iteration}_{stamp}.ot"
+def checkpoint_path(folder: str, iteration: int, is_best: bool, stamp: str = None) -> str:
+    """save_vs naming (train.rs:414-422): <folder>/[best_]model_<iter>_<YYYYmmdd_HHMMSS>.ot, by the
+    library (oaz_checkpoint_path); stamp None = the local time now."""
+    buf = C.create_string_buffer(4096)
+    _abi.check(_abi.load().oaz_checkpoint_path(str(folder).encode(), int(iteration), int(bool(is_best)),
+                                               None if stamp is None else str(stamp).encode(), buf, len(buf)))
+    return buf.value.decode()
 
 
 def save_blob_ot(path: str, blob: np.ndarray, blocks: int) -> None:
-    write_ot(path, named_from_blob(blob, blocks))
+    """A canonical blob as a .ot checkpoint, written by the library (oaz_ot_write)."""
+    b = np.ascontiguousarray(blob, dtype=np.float32)
+    _abi.check(_abi.load().oaz_ot_write(str(path).encode(), _abi.ptr(b), b.size, int(blocks)))

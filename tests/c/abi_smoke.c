@@ -6,7 +6,10 @@
  *   does (alphazero_mcts/mod.rs:89-105) — by path (oaz_load_ot) and by name (oaz_load_weights_named,
  *   the tensors in shuffled order with tch's '.' separator, as `vs.variables()` hands them over) —
  *   and compares oaz_nn_forward with the golden policy/value (golden.bin: n, then n states, n x 50
- *   policy and n values). */
+ *   policy and n values).
+ *   abi_smoke model.ot golden.bin out_dir: also writes the model back as a checkpoint the way save_vs
+ *   does (train.rs:414-430: oaz_checkpoint_path + oaz_ot_write, <out_dir>/best_model_7_<stamp>.ot),
+ *   reads it back bit-equal, and (with a GPU) saves the trainer's weights with oaz_trainer_save_ot. */
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -29,7 +32,7 @@ int hipMemcpy(void* dst, const void* src, size_t bytes, int kind); /* kind 2 = d
     } while (0)
 
 /* The model file by path and by name (host side: no GPU). Fills *blob (canonical order). */
-static int model_host(const char* ot, float** blob, size_t* nblob) {
+static int model_host(const char* ot, const char* out_dir, float** blob, size_t* nblob) {
     size_t n = 0;
     int blocks = -1;
     CHECK(oaz_ot_read(ot, NULL, 0, &n, &blocks) == 0 && blocks == 3 && n == oaz_weight_count(3, 64, 21));
@@ -63,6 +66,20 @@ static int model_host(const char* ot, float** blob, size_t* nblob) {
     CHECK(oaz_weights_from_named(3, np, dp, sz, nt - 1, w2, n) == OAZ_ERR_WEIGHTS && strstr(oaz_last_error(), "missing"));
     CHECK(oaz_weights_from_named(2, np, dp, sz, nt, w2, n) == OAZ_ERR_WEIGHTS); /* resnet_2 is not in 2 blocks */
     free(w2);
+    if (out_dir) { /* save_vs: the checkpoint path and the archive, read back bit-equal */
+        char path[1024];
+        CHECK(oaz_checkpoint_path(out_dir, 7, 1, "20260101_120000", path, 8) == OAZ_ERR_CAPACITY);
+        CHECK(oaz_checkpoint_path(out_dir, 7, 1, "20260101_120000", path, sizeof path) == 0);
+        CHECK(strstr(path, "/best_model_7_20260101_120000.ot") != NULL);
+        CHECK(oaz_ot_write(path, w, n - 1, 3) == OAZ_ERR_ARG); /* wrong size for 3 blocks */
+        CHECK(oaz_ot_write(path, w, n, 3) == 0);
+        float* w3 = (float*)malloc(n * sizeof(float));
+        size_t n3 = 0;
+        int b3 = -1;
+        CHECK(oaz_ot_read(path, w3, n, &n3, &b3) == 0 && n3 == n && b3 == 3 && memcmp(w, w3, n * sizeof(float)) == 0);
+        free(w3);
+        printf("OK ot-write %s\n", path);
+    }
     free(names);
     free(np);
     free(dp);
@@ -147,7 +164,7 @@ int main(int argc, char** argv) {
     float* model = NULL;
     size_t nmodel = 0;
     if (argc >= 3) {
-        if (model_host(argv[1], &model, &nmodel)) return 1;
+        if (model_host(argv[1], argc >= 4 ? argv[3] : NULL, &model, &nmodel)) return 1;
         printf("OK model-host\n");
     }
     int ndev = 0;
@@ -250,6 +267,19 @@ int main(int argc, char** argv) {
     CHECK(oaz_trainer_set_batches(t, idx, 1, 32) == 0 && oaz_trainer_train(t, 0, 1) == 0);
     CHECK(oaz_trainer_losses(t, losses) == 0 && losses[2] == 1.0 && losses[0] >= 0.0 && losses[1] > 0.0);
     printf("OK train loss %.4f %.4f\n", losses[0], losses[1]);
+    if (argc >= 4) { /* the trained weights as a checkpoint (save_vs on the training VarStore) */
+        char path[1024];
+        CHECK(oaz_checkpoint_path(argv[3], 1, 0, NULL, path, sizeof path) == 0);
+        CHECK(oaz_trainer_save_ot(t, path) == 0);
+        float *tw = (float*)malloc(nw * sizeof(float)), *rw = (float*)malloc(nw * sizeof(float));
+        size_t nr = 0;
+        int br = -1;
+        CHECK(oaz_trainer_get_weights(t, tw, nw) == 0 && oaz_ot_read(path, rw, nw, &nr, &br) == 0 && nr == nw && br == 3);
+        CHECK(memcmp(tw, rw, nw * sizeof(float)) == 0 && memcmp(tw, w, nw * sizeof(float)) != 0);
+        free(tw);
+        free(rw);
+        printf("OK trainer-save %s\n", path);
+    }
     oaz_trainer_destroy(t);
     oaz_destroy(e);
     free(buf);

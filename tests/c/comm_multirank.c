@@ -1,0 +1,250 @@
+/* comm_multirank.c — the product multi-GPU exchange (csrc/oaz_comm.cpp) at world > 1, from plain C.
+ * Each rank is a host thread with its own engine and communicator on GPU 0; librccl.so.1 is the
+ * test double tests/c/rccl_stub.c (put first on LD_LIBRARY_PATH by tests/test_c_abi.py), so the
+ * grouped-broadcast all-gatherv, the counts all-gather, the failure sentinel, the broadcast and the
+ * all-reduce run with several ranks on a one-GPU box. Reference: the join of the self-play workers'
+ * buffers, alphazero-training/src/train.rs:241-244 (`data_buffer.extend(handle.join())` in worker
+ * order = rank order here).
+ *
+ *   comm_multirank W      (2 <= W <= 4)
+ *
+ * Per rank r: engine A (the exchange) and engine B (the expectation) get the same config (G_r game
+ * slots, rank r of W, HASH evaluator, root noise on) and play the same number of plies P_r, ragged
+ * over the ranks and 0 for rank 1 (a rank with no samples). B's samples are fetched to the host;
+ * self-play is deterministic, so they are what A holds. Then, on every rank:
+ *   1. oaz_allgather_samples with cap = total - 1: OAZ_ERR_CAPACITY, *n_total = total, nothing consumed;
+ *   2. the last rank passes a NULL engine: it gets OAZ_ERR_ARG, every other rank OAZ_ERR_COMM naming
+ *      that rank (the kLocalFailure sentinel through the counts all-gather), nothing consumed;
+ *   3. cap = total: counts_out = every rank's count; every rank's device output byte-equal to every
+ *      other rank's; block r of it holds exactly rank r's samples (as a set: the engine appends the
+ *      samples of games that finish in the same move kernel in atomic order, so two engines playing
+ *      the same games may order a ply's samples differently); own buffer drained; stats (ranks,
+ *      records, own records);
+ *   4. again with every buffer empty: total 0, success;
+ *   5. oaz_comm_broadcast from each root in turn (in place, NULL and explicit streams);
+ *   6. oaz_comm_allreduce_sum_f32 (exact small sums) on the communicator's and on a caller stream.
+ * Prints "OK rank r ..." per rank and "OK multirank W" at the end; exit 0 only if every rank passed. */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "onitama_az.h"
+
+typedef void* hipStream_t;
+int hipMalloc(void** ptr, size_t size);
+int hipFree(void* ptr);
+int hipMemcpy(void* dst, const void* src, size_t bytes, int kind); /* 1 = H2D, 2 = D2H */
+int hipStreamCreate(hipStream_t* s);
+int hipStreamDestroy(hipStream_t s);
+int hipStreamSynchronize(hipStream_t s);
+uint64_t rccl_stub_ops(void); /* from the stub: proves it served the calls */
+
+#define MAXW 4
+static int W;
+static oaz_comm_id g_id;
+static oaz_sample* g_expect[MAXW]; /* rank r's samples, sorted (bytewise) */
+static oaz_sample* g_out[MAXW];    /* rank r's whole all-gather output, as received */
+static size_t g_count[MAXW];
+/* host barrier between the rank threads, with a timeout so a rank that fails early ends the run
+ * instead of leaving the others waiting */
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t g_cv = PTHREAD_COND_INITIALIZER;
+static int g_arrived;
+static unsigned g_gen;
+static int bar_wait(void) {
+    pthread_mutex_lock(&g_mu);
+    const unsigned gen = g_gen;
+    if (++g_arrived == W) {
+        g_arrived = 0;
+        g_gen++;
+        pthread_cond_broadcast(&g_cv);
+        pthread_mutex_unlock(&g_mu);
+        return 1;
+    }
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    ts.tv_sec += 150;
+    while (g_gen == gen)
+        if (pthread_cond_timedwait(&g_cv, &g_mu, &ts) != 0) break;
+    const int ok = g_gen != gen;
+    pthread_mutex_unlock(&g_mu);
+    return ok;
+}
+static int g_fail[MAXW];
+
+static const int kGames[MAXW] = {24, 16, 32, 8};
+static const int kPlies[MAXW] = {45, 0, 70, 30};
+
+static int cmp_sample(const void* a, const void* b) { return memcmp(a, b, sizeof(oaz_sample)); }
+
+#define CHECK(c)                                                                                          \
+    do {                                                                                                  \
+        if (!(c)) {                                                                                       \
+            fprintf(stderr, "FAIL rank %d %s:%d %s (%s)\n", rank, __FILE__, __LINE__, #c, oaz_last_error()); \
+            g_fail[rank] = 1;                                                                             \
+            goto done;                                                                                    \
+        }                                                                                                 \
+    } while (0)
+
+static oaz_engine* make_engine(int rank) {
+    oaz_config cfg;
+    oaz_config_default(&cfg);
+    cfg.blocks = 0;
+    cfg.evaluator = OAZ_EVAL_HASH;
+    cfg.sims = 12;
+    cfg.games = kGames[rank];
+    cfg.train_noise = 1;
+    cfg.max_plies = 150;
+    cfg.seed = 20260101ull;
+    cfg.rank = rank;
+    cfg.world = W;
+    return oaz_create(&cfg, 0);
+}
+
+static void* rank_main(void* arg) {
+    const int rank = (int)(intptr_t)arg;
+    oaz_engine *a = NULL, *b = NULL;
+    oaz_comm* comm = NULL;
+    void *dev = NULL, *buf = NULL;
+    oaz_sample* host = NULL;
+    float* fh = NULL;
+    hipStream_t s = NULL;
+    int synced = 0;
+    /* expectation: engine B plays the same plies and hands its samples to the host */
+    a = make_engine(rank);
+    b = make_engine(rank);
+    CHECK(a && b);
+    CHECK(oaz_selfplay_reset(a) == 0 && oaz_selfplay_reset(b) == 0);
+    CHECK(oaz_selfplay_step(a, kPlies[rank]) == 0 && oaz_selfplay_step(b, kPlies[rank]) == 0);
+    oaz_selfplay_stats sa, sb;
+    CHECK(oaz_selfplay_stats_get(a, &sa) == 0 && oaz_selfplay_stats_get(b, &sb) == 0);
+    CHECK(sa.samples_ready == sb.samples_ready && sa.samples_dropped == 0);
+    g_count[rank] = sb.samples_ready;
+    g_expect[rank] = (oaz_sample*)malloc((g_count[rank] + 1) * sizeof(oaz_sample));
+    size_t got = 0;
+    CHECK(oaz_samples_fetch(b, g_expect[rank], g_count[rank], &got) == 0 && got == g_count[rank]);
+    qsort(g_expect[rank], g_count[rank], sizeof(oaz_sample), cmp_sample);
+    CHECK((rank == 1) == (g_count[rank] == 0)); /* rank 1 played no ply: the zero-count rank */
+    comm = oaz_comm_init(&g_id, rank, W, 0);
+    CHECK(comm != NULL);
+    synced = 1;
+    CHECK(bar_wait()); /* every g_count / g_expect is written */
+    size_t total = 0;
+    for (int r = 0; r < W; ++r) total += g_count[r];
+    CHECK(total > 0);
+    CHECK(hipMalloc(&dev, (total + 1) * sizeof(oaz_sample)) == 0);
+    host = (oaz_sample*)malloc((total + 1) * sizeof(oaz_sample));
+    uint64_t counts[MAXW];
+    size_t n_total = 0;
+    /* 1. capacity error on every rank alike, nothing consumed */
+    CHECK(oaz_allgather_samples(a, comm, (oaz_sample*)dev, total - 1, &n_total, counts) == OAZ_ERR_CAPACITY);
+    CHECK(n_total == total && strstr(oaz_last_error(), "cap") != NULL);
+    CHECK(oaz_selfplay_stats_get(a, &sa) == 0 && sa.samples_ready == g_count[rank]);
+    /* 2. a local failure on the last rank reaches every rank through the counts all-gather */
+    const int bad = W - 1;
+    const int rc2 = oaz_allgather_samples(rank == bad ? NULL : a, comm, (oaz_sample*)dev, total, &n_total, counts);
+    if (rank == bad) {
+        CHECK(rc2 == OAZ_ERR_ARG);
+    } else {
+        char want[64];
+        snprintf(want, sizeof want, "rank %d failed", bad);
+        CHECK(rc2 == OAZ_ERR_COMM && strstr(oaz_last_error(), want) != NULL);
+    }
+    CHECK(oaz_selfplay_stats_get(a, &sa) == 0 && sa.samples_ready == g_count[rank]);
+    /* 3. the exchange: every rank's records, in rank order */
+    memset(counts, 0xff, sizeof counts);
+    CHECK(oaz_allgather_samples(a, comm, (oaz_sample*)dev, total, &n_total, counts) == 0 && n_total == total);
+    for (int r = 0; r < W; ++r) CHECK(counts[r] == g_count[r]);
+    CHECK(hipMemcpy(host, dev, total * sizeof(oaz_sample), 2) == 0);
+    size_t off = 0;
+    for (int r = 0; r < W; ++r) {
+        qsort(host + off, g_count[r], sizeof(oaz_sample), cmp_sample); /* sorts the host copy only */
+        CHECK(g_count[r] == 0 || memcmp(host + off, g_expect[r], g_count[r] * sizeof(oaz_sample)) == 0);
+        off += g_count[r];
+    }
+    CHECK(hipMemcpy(host, dev, total * sizeof(oaz_sample), 2) == 0); /* as received again */
+    g_out[rank] = host;
+    CHECK(bar_wait());
+    int same = 1;
+    for (int r = 0; r < W; ++r) same &= memcmp(g_out[r], host, total * sizeof(oaz_sample)) == 0;
+    CHECK(bar_wait()); /* every rank compared before any frees its copy */
+    CHECK(same);
+    CHECK(oaz_selfplay_stats_get(a, &sa) == 0 && sa.samples_ready == 0);
+    oaz_comm_stats cs;
+    CHECK(oaz_comm_stats_get(comm, &cs) == 0 && cs.ranks == W && cs.rank == rank && cs.allgather_calls == 1 &&
+          cs.allgather_records == total && cs.own_records == g_count[rank] &&
+          cs.allgather_bytes == total * sizeof(oaz_sample));
+    /* 4. every buffer empty: a zero-total exchange succeeds */
+    CHECK(oaz_allgather_samples(a, comm, (oaz_sample*)dev, total, &n_total, counts) == 0 && n_total == 0);
+    for (int r = 0; r < W; ++r) CHECK(counts[r] == 0);
+    /* 5. broadcast from every root, in place */
+    const size_t nb = 4096 + 36; /* not a multiple of anything convenient */
+    CHECK(hipMalloc(&buf, nb) == 0);
+    unsigned char* hb = (unsigned char*)malloc(nb);
+    for (int root = 0; root < W; ++root) {
+        for (size_t i = 0; i < nb; ++i) hb[i] = (unsigned char)(rank * 37 + i * 7 + 1);
+        CHECK(hipMemcpy(buf, hb, nb, 1) == 0);
+        CHECK(oaz_comm_broadcast(comm, buf, nb, root, NULL) == 0 && oaz_comm_sync(comm) == 0);
+        CHECK(hipMemcpy(hb, buf, nb, 2) == 0);
+        for (size_t i = 0; i < nb; ++i) CHECK(hb[i] == (unsigned char)(root * 37 + i * 7 + 1));
+    }
+    CHECK(oaz_comm_broadcast(comm, buf, nb, W, NULL) == OAZ_ERR_ARG); /* root out of range: local, no collective */
+    free(hb);
+    /* 6. all-reduce (sum), exact: x_i = (rank + 1) * i + 0.5 -> sum = i * W(W+1)/2 + W/2 */
+    const size_t nf = 1000;
+    fh = (float*)malloc(nf * sizeof(float));
+    CHECK(hipStreamCreate(&s) == 0);
+    for (int pass = 0; pass < 2; ++pass) {
+        for (size_t i = 0; i < nf; ++i) fh[i] = (float)((rank + 1) * (int)i) + 0.5f;
+        CHECK(hipMemcpy(dev, fh, nf * sizeof(float), 1) == 0);
+        if (pass == 0) {
+            CHECK(oaz_comm_allreduce_sum_f32(comm, (float*)dev, nf, NULL) == 0 && oaz_comm_sync(comm) == 0);
+        } else {
+            CHECK(oaz_comm_allreduce_sum_f32(comm, (float*)dev, nf, s) == 0 && hipStreamSynchronize(s) == 0);
+        }
+        CHECK(hipMemcpy(fh, dev, nf * sizeof(float), 2) == 0);
+        for (size_t i = 0; i < nf; ++i) CHECK(fh[i] == (float)((int)i * W * (W + 1) / 2) + 0.5f * (float)W);
+    }
+    printf("OK rank %d: %zu own of %zu records gathered byte-equal; capacity, failure sentinel, empty, "
+           "broadcast x%d, allreduce x2\n", rank, g_count[rank], total, W);
+done:
+    if (!synced) bar_wait(); /* never leave the others waiting at the first barrier */
+    if (s) hipStreamDestroy(s);
+    if (comm) oaz_comm_destroy(comm);
+    if (buf) hipFree(buf);
+    if (dev) hipFree(dev);
+    free(host);
+    free(fh);
+    if (a) oaz_destroy(a);
+    if (b) oaz_destroy(b);
+    return NULL;
+}
+
+int main(int argc, char** argv) {
+    W = argc > 1 ? atoi(argv[1]) : 2;
+    if (W < 2 || W > MAXW) {
+        fprintf(stderr, "usage: comm_multirank W (2..%d)\n", MAXW);
+        return 2;
+    }
+    int ndev = 0;
+    if (oaz_device_count(&ndev) != 0 || ndev == 0) {
+        fprintf(stderr, "no GPU\n");
+        return 2;
+    }
+    if (oaz_comm_unique_id(&g_id) != 0) {
+        fprintf(stderr, "FAIL unique id: %s\n", oaz_last_error());
+        return 1;
+    }
+    pthread_t th[MAXW];
+    for (int r = 0; r < W; ++r) pthread_create(&th[r], NULL, rank_main, (void*)(intptr_t)r);
+    for (int r = 0; r < W; ++r) pthread_join(th[r], NULL);
+    int fails = 0;
+    for (int r = 0; r < W; ++r) fails += g_fail[r];
+    for (int r = 0; r < W; ++r) free(g_expect[r]);
+    if (fails) return 1;
+    printf("OK multirank %d (%llu stub collectives)\n", W, (unsigned long long)rccl_stub_ops());
+    return 0;
+}

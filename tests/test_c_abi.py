@@ -2,6 +2,7 @@
 include/onitama_az.h and linked to the in-tree libonitama_az.so — the way a non-Python host
 (the reference's Rust through `extern "C"`) uses the engine."""
 import os
+import re
 import shutil
 import subprocess
 from pathlib import Path
@@ -47,21 +48,102 @@ def _model_files(tmp_path):
     return ot, gold
 
 
-def _run(exe, *args):
-    return subprocess.run([str(exe), *map(str, args)], capture_output=True, text=True, timeout=300)
+def _run(exe, *args, env=None):
+    return subprocess.run([str(exe), *map(str, args)], capture_output=True, text=True, timeout=300, env=env)
+
+
+def _rccl_symbols():
+    """The RCCL entry points the product resolves with dlsym (csrc/oaz_comm.cpp rccl_load)."""
+    src = (ROOT / "onitama-alphazero_amd/csrc/oaz_comm.cpp").read_text()
+    names = re.findall(r'sym\(h, "(\w+)"', src)
+    assert len(names) == 10, names
+    return names
+
+
+def _build_multirank(tmp_path):
+    """tests/c/rccl_stub.c as tmp/librccl.so.1 (soname librccl.so.1) and tests/c/comm_multirank.c
+    linked to it and to libonitama_az.so. The stub is a NEEDED library of the program, so the
+    engine's dlopen("librccl.so.1") returns the stub already mapped (same soname); the run also puts
+    its directory first on LD_LIBRARY_PATH."""
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    rocm = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / "lib"
+    stub = tmp_path / "librccl.so.1"
+    subprocess.run([cc, "-O1", "-Wall", "-shared", "-fPIC", "-o", str(stub), "-Wl,-soname,librccl.so.1",
+                    str(ROOT / "tests/c/rccl_stub.c"), f"-L{rocm}", "-lamdhip64", f"-Wl,-rpath,{rocm}", "-lpthread"],
+                   check=True)
+    exe = tmp_path / "comm_multirank"
+    lib_dir = _abi.LIB_PATH.parent
+    subprocess.run([cc, "-O1", "-Wall", "-o", str(exe), str(ROOT / "tests/c/comm_multirank.c"), f"-I{ROOT / 'include'}",
+                    f"-L{lib_dir}", "-lonitama_az", f"-Wl,-rpath,{lib_dir}", f"-L{tmp_path}", "-l:librccl.so.1",
+                    f"-Wl,-rpath,{tmp_path}", f"-L{rocm}", "-lamdhip64", f"-Wl,-rpath,{rocm}", "-lpthread"],
+                   check=True)
+    env = dict(os.environ, LD_LIBRARY_PATH=f"{tmp_path}:" + os.environ.get("LD_LIBRARY_PATH", ""))
+    return stub, exe, env
+
+
+def _check_written_checkpoint(out_dir):
+    """The checkpoint the C program wrote (oaz_ot_write, save_vs naming) is byte-equal to the Python
+    restatement of the writer (weights.write_ot, Python's zipfile) for the same tensors, and reads back
+    through the Python safe reader."""
+    from onitama_az.weights import named_from_blob, read_ot, write_ot, blob_from_named
+    blob = np.load(ROOT / "tests/golden/weights_3block_trained.npy")
+    p = out_dir / "best_model_7_20260101_120000.ot"
+    assert p.exists(), sorted(out_dir.iterdir())
+    ref_dir = out_dir / "py"
+    ref_dir.mkdir()
+    write_ot(str(ref_dir / p.name), named_from_blob(blob, 3))
+    assert p.read_bytes() == (ref_dir / p.name).read_bytes()
+    assert np.array_equal(blob_from_named(read_ot(str(p)), 3), blob)
 
 
 def test_c_host_without_device(tmp_path):
     if _abi.device_count() > 0:
         pytest.skip("a GPU is visible")
-    r = _run(_build(tmp_path), *_model_files(tmp_path))
+    out = tmp_path / "ckpt"
+    out.mkdir()
+    r = _run(_build(tmp_path), *_model_files(tmp_path), out)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK host" in r.stdout and "OK model-host" in r.stdout and "OK no-device" in r.stdout
+    assert "OK ot-write" in r.stdout
+    _check_written_checkpoint(out)
 
 
 @pytest.mark.gpu
 def test_c_host_on_gpu(tmp_path):
-    r = _run(_build(tmp_path), *_model_files(tmp_path))
+    out = tmp_path / "ckpt"
+    out.mkdir()
+    r = _run(_build(tmp_path), *_model_files(tmp_path), out)
     assert r.returncode == 0, r.stdout + r.stderr
-    for tag in ("OK model-host", "OK model ", "OK search", "OK selfplay", "OK comm", "OK pure_mcts", "OK train"):
+    for tag in ("OK model-host", "OK ot-write", "OK model ", "OK search", "OK selfplay", "OK comm", "OK pure_mcts",
+                "OK train", "OK trainer-save"):
         assert tag in r.stdout, r.stdout
+    _check_written_checkpoint(out)
+
+
+def test_rccl_stub_exports_what_the_product_resolves(tmp_path):
+    """The multi-rank test double exports every RCCL symbol oaz_comm.cpp dlsym()s (CPU: build + nm)."""
+    stub, exe, _ = _build_multirank(tmp_path)
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(stub)], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in nm.splitlines() if ln.strip()}
+    missing = [s for s in _rccl_symbols() if s not in exported]
+    assert not missing, missing
+    assert exe.exists()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_c_allgather_samples_multirank(tmp_path, world):
+    """The product exchange (oaz_allgather_samples, oaz_comm_broadcast, oaz_comm_allreduce_sum_f32) at
+    world 2 and 3: ranks are threads of one plain C process on GPU 0 over the RCCL test double
+    (tests/c/rccl_stub.c). Ragged counts with a zero-count rank, the capacity error, a local failure
+    on one rank seen by every rank (kLocalFailure), and every rank's output byte-equal to the
+    rank-order concatenation (train.rs:241-244). See tests/c/comm_multirank.c."""
+    _, exe, env = _build_multirank(tmp_path)
+    r = _run(exe, world, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for rank in range(world):
+        assert f"OK rank {rank}:" in r.stdout, r.stdout
+    assert f"OK multirank {world}" in r.stdout and "stub collectives" in r.stdout, r.stdout
+    print(r.stdout)

@@ -187,6 +187,67 @@ def test_ot_writer_round_trip(trained3, tmp_path):
         assert np.array_equal(params[k].detach().numpy(), v), k
 
 
+def test_c_ot_writer_bytes_equal_python_writer(tmp_path):
+    """oaz_ot_write (the product writer, C) emits byte for byte the archive the independent Python
+    restatement (weights.write_ot over Python's zipfile) writes for the same tensors, for 0, 3 and 5
+    blocks, and both readers read it back bit-equal (save_vs, train.rs:414-430)."""
+    for blocks, blob in ((0, W.random_weights(3, 0)),
+                         (3, np.load(ROOT / "tests/golden/weights_3block_trained.npy")),
+                         (5, np.load(ROOT / "tests/golden/weights_5block_trained.npy"))):
+        c_path, py_dir = tmp_path / f"model_{blocks}_20260101_120000.ot", tmp_path / f"py{blocks}"
+        py_dir.mkdir()
+        W.save_blob_ot(str(c_path), blob, blocks)
+        W.write_ot(str(py_dir / c_path.name), W.named_from_blob(blob, blocks))
+        assert c_path.read_bytes() == (py_dir / c_path.name).read_bytes(), blocks
+        got, b = W.ot_blob(str(c_path))
+        assert b == blocks and np.array_equal(got, blob)
+        assert np.array_equal(W.blob_from_named(W.read_ot(str(c_path)), blocks), blob)
+        assert not (tmp_path / (c_path.name + ".tmp")).exists()
+    with pytest.raises(_abi.OazError, match="floats given"):
+        W.save_blob_ot(str(tmp_path / "bad.ot"), np.zeros(5, np.float32), 3)
+    with pytest.raises(_abi.OazError, match="cannot create"):
+        W.save_blob_ot(str(tmp_path / "no" / "such" / "dir.ot"), W.random_weights(3, 0), 0)
+
+
+def _pickle_archive(path, pkl: bytes):
+    """A zip whose only member is data.pkl = pkl (stored), as VarStore archives hold it."""
+    z = W._AlignedZip(str(path))
+    z.add("m/data.pkl", pkl)
+    z.close()
+
+
+def test_ot_readers_bounded_on_crafted_pickles(tmp_path):
+    """Crafted data.pkl inputs that alias containers through the memo: a list appended
+    to itself, a 64-level doubling DAG (2^64 paths for a tree walk), a 200 000-deep chain of nested
+    lists, and a two-list cycle. The C reader refuses or reads them in bounded time and memory
+    (index arena, visited set, explicit stack: no exponential walk, no recursive destructor, no
+    leaked cycle), ending in OAZ_ERR_WEIGHTS; the Python reader terminates too."""
+    import time
+    cases = {
+        "self_append": b"\x80\x02]q\x00h\x00ah\x00a.",
+        "doubling_dag": b"\x80\x02]r\x00\x00\x00\x00" + b"".join(
+            b"]r" + k.to_bytes(4, "little") + (b"j" + (k - 1).to_bytes(4, "little") + b"a") * 2
+            for k in range(1, 65)) + b".",
+        "deep_chain": b"\x80\x02" + b"]" * 200_000 + b"a" * 199_999 + b".",
+        "two_cycle": b"\x80\x02]q\x00]q\x01h\x00ah\x01a.",
+        "self_setitem": b"\x80\x02}q\x00X\x01\x00\x00\x00kh\x00s.",
+    }
+    for name, pkl in cases.items():
+        p = tmp_path / f"{name}.ot"
+        _pickle_archive(p, pkl)
+        t0 = time.perf_counter()
+        with pytest.raises(_abi.OazError):
+            W.ot_blob(str(p))
+        assert time.perf_counter() - t0 < 5.0, name
+        if name != "deep_chain":  # pickletools' genops walk of 400k opcodes is merely slow
+            try:
+                W.read_ot(str(p))
+            except (ValueError, KeyError, IndexError, AttributeError, TypeError):
+                pass
+    with pytest.raises(_abi.OazError, match="APPEND"):  # the direct self-reference is refused by name
+        W.ot_blob(str(tmp_path / "self_append.ot"))
+
+
 def test_no_device_is_a_loud_error(lib):
     if _abi.device_count() > 0:
         pytest.skip("a GPU is visible")
@@ -224,6 +285,43 @@ def test_root_noise_host_matches_oracle_and_distribution():
         se = np.sqrt(var / len(xs))
         assert abs(xs.mean() - 1.0 / K) < 5 * se, (K, xs.mean())
         assert abs(xs.var() / var - 1.0) < 0.2, (K, xs.var(), var)
+
+
+def test_root_noise_distribution_ks():
+    """The root-noise draw against its target law, Beta(alpha, (K - 1) alpha) — the marginal of one
+    component of the reference's Dirichlet(alpha; K) sample (rand_distr 0.4.3, mcts_arena.rs:190-203)
+    — with 2 * 10^5 host draws per K (bit-identical to the device's, test above and the noise-on tree
+    tests): a Kolmogorov-Smirnov distance and the mass at quantiles 1 % ... 99 %.
+    An f32 draw cannot resolve the law's two ends at alpha = 0.03: below ~6e-39 (e^-88, where the
+    sampler's exp(ly - lx) overflows) the draw is 0, and within ~6e-8 of 1 (f32's spacing there) it
+    is 1.0 — at K = 2 that is 4 % and 30 % of the mass. Each end's mass is compared as a whole
+    (P(X <= x0), P(X >= x1) against their binomial spread), and the KS sup runs over x0 < x < x1
+    (a sup over a subset: the full-sample Kolmogorov null is conservative for it)."""
+    from scipy import stats
+    lib = _abi.load()
+    x0, x1, n = 1e-37, 1.0 - 1e-6, 200_000
+    for K in (2, 14, 40):
+        law = stats.beta(0.03, 0.03 * (K - 1))
+        xs = np.sort(np.array([lib.oaz_root_noise(11, g, 0, s, 5, 0.03, K) for g in range(2000) for s in range(100)]))
+        f0, m0 = law.cdf(x0), float(np.mean(xs <= x0))  # the two ends, as masses
+        f1, m1 = law.sf(x1), float(np.mean(xs >= x1))
+        assert abs(m0 - f0) < 5 * np.sqrt(f0 * (1 - f0) / n), (K, m0, f0)
+        assert abs(m1 - f1) < 5 * np.sqrt(max(f1 * (1 - f1), 1.0 / n) / n), (K, m1, f1)
+        mid = xs[(xs > x0) & (xs < x1)]  # KS distance over x0 < x < x1
+        lo = np.searchsorted(xs, mid, side="left") / n  # ECDF just below each value
+        hi = np.searchsorted(xs, mid, side="right") / n  # ECDF at each value
+        F = law.cdf(mid)
+        d = float(max(np.max(hi - F), np.max(F - lo)))
+        p = float(stats.kstwo(n).sf(d))
+        print(f"K={K}: mass <= 1e-37 {m0:.4f} (law {f0:.4f}), >= 1-1e-6 {m1:.4f} (law {f1:.4f}); "
+              f"KS D={d:.5f} p={p:.3f}")
+        assert p > 1e-3, (K, d, p)
+        for q in (0.01, 0.05, 0.25, 0.5, 0.75, 0.95, 0.99):
+            xq = law.ppf(q)
+            if not x0 < xq < x1:
+                continue  # inside an end's mass, checked above
+            frac = float(np.mean(xs <= xq))
+            assert abs(frac - q) < 5 * np.sqrt(q * (1 - q) / n), (K, q, frac)
 
 
 @pytest.mark.parametrize("kw", [dict(compact=3), dict(compact=-1), dict(parts=3), dict(parts=-1)])

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Coverage-guided fuzzing of the C .ot reader (oaz_ot_read) under AddressSanitizer + UBSan, on the
 # host (no GPU). Seeds: .ot files written by onitama_az.weights.write_ot (trained 3-block, random
-# 0- and 1-block networks).
+# 0- and 1-block networks), one written by the C writer (oaz_ot_write), and archives whose data.pkl
+# aliases containers through the memo (self-append, a 64-level doubling DAG, a 100 000-deep chain,
+# a two-list cycle: the inputs of tests/test_host.py test_ot_readers_bounded_on_crafted_pickles).
 #   tools/ot_fuzz.sh [seconds=120] [workers=4]
 set -euo pipefail
 cd "$(dirname "$0")/.."
@@ -22,6 +24,18 @@ d = sys.argv[1]
 W.write_ot(f"{d}/trained3.ot", W.named_from_blob(np.load("tests/golden/weights_3block_trained.npy"), 3))
 for b in (0, 1):
     W.write_ot(f"{d}/random{b}.ot", W.named_from_blob(W.random_weights(b, b), b))
+W.save_blob_ot(f"{d}/c_writer2.ot", W.random_weights(2, 2), 2)
+crafted = {
+    "self_append": b"\x80\x02]q\x00h\x00ah\x00a.",
+    "doubling_dag": b"\x80\x02]r\x00\x00\x00\x00" + b"".join(
+        b"]r" + k.to_bytes(4, "little") + (b"j" + (k - 1).to_bytes(4, "little") + b"a") * 2 for k in range(1, 65)) + b".",
+    "deep_chain": b"\x80\x02" + b"]" * 100_000 + b"a" * 99_999 + b".",
+    "two_cycle": b"\x80\x02]q\x00]q\x01h\x00ah\x01a.",
+}
+for name, pkl in crafted.items():
+    z = W._AlignedZip(f"{d}/{name}.ot")
+    z.add("m/data.pkl", pkl)
+    z.close()
 EOF
 # (libFuzzer writes its per-worker fuzz-<n>.log into the working directory)
 cd "$OUT"
