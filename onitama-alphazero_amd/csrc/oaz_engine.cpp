@@ -1071,6 +1071,12 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
                                                      : nullptr;
     w.fallback = e->nn_fallback;
     w.tm = tm ? *tm : TileMap{nullptr, 0, 0};
+    // k_nn_h3s (one position per workgroup) while the launch fits one round of workgroups on the CUs;
+    // k_nn_h3 (16 per workgroup) above. The two give bit-identical outputs.
+    w.small_max = e->cus;
+#if OAZ_AB  // A/B build only: OAZ_NN_SMALL_MAX=n overrides
+    if (const char* v = getenv("OAZ_NN_SMALL_MAX")) w.small_max = atoi(v);
+#endif
     return timed(e, 1, counted, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, st); }, st);
 }
 

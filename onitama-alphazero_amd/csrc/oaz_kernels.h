@@ -99,6 +99,7 @@ struct NNView {
     const float* blob_x6;             // OAZ_FP32_SPLIT16: the OAZ_FP32_SPLIT blob of the same weights
     unsigned long long* fallback;     // OAZ_FP32_SPLIT16: tiles recomputed by the k_nn_x6 body (fp16 range)
     TileMap tm;                       // compacted leaves (tm.bcnt null: rows [0, B))
+    int32_t small_max;                // OAZ_FP32_SPLIT16: launches of <= this many positions run k_nn_h3s
 };
 
 // rules

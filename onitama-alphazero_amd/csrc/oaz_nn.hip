@@ -1373,7 +1373,7 @@ __device__ __forceinline__ uint32_t l1_tap8(uint32_t bb) {  // square SQ+6 (tap 
     if constexpr (SQ / 5 == 4 || SQ % 5 == 4) return 0u;
     else return ((bb >> (25 - SQ)) & 1u) ? 0x3C00u : 0u;
 }
-__device__ __forceinline__ void l1_lut_build(char* lds, int tid) {  // entry P, element t: bit pos(t) of P
+__device__ __forceinline__ void l1_lut_build(char* lut, int tid) {  // entry P, element t: bit pos(t) of P
     constexpr int pos[8] = {2, 1, 0, 5, 4, 3, 7, 6};
     const int P = tid >> 1, h = tid & 1;
     uint32_t w[2];
@@ -1382,7 +1382,7 @@ __device__ __forceinline__ void l1_lut_build(char* lds, int tid) {  // entry P, 
         const int t0 = 4 * h + 2 * k;
         w[k] = (((P >> pos[t0]) & 1) ? 0x3C00u : 0u) | (((P >> pos[t0 + 1]) & 1) ? 0x3C000000u : 0u);
     }
-    *reinterpret_cast<uint2*>(lds + h3::kLutOff + P * 16 + h * 8) = uint2{w[0], w[1]};
+    *reinterpret_cast<uint2*>(lut + P * 16 + h * 8) = uint2{w[0], w[1]};
 }
 // K block 1 of square sq depends on sq only through its on-board tap set (the constant planes'
 // table T[sq] sums over those taps; tap 8's weights are square-independent): 9 classes (corner,
@@ -1602,7 +1602,7 @@ __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states,
             pinfo[tid] = c0 | (c1 << 4) | (blue << 8);
         }
         if constexpr (kF16)
-            for (int t = tid; t < 512; t += 64 * C::WAVES) l1_lut_build(img, t);
+            for (int t = tid; t < 512; t += 64 * C::WAVES) l1_lut_build(img + h3::kLutOff, t);
         const f32x4 bias1t = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
         if (b0 >= B) return false;  // an empty tile of a compacted bucket (uniform over the workgroup)
         __syncthreads();
@@ -1757,6 +1757,366 @@ __global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3(const oaz_state* __rest
     }
 }
 
+// ---- small batches: one position per workgroup (k_nn_h3s, OAZ_FP32_SPLIT16) ---------------------------
+// k_nn_h3 evaluates 16 positions per workgroup (square-major tiles), so below ~16 x 256 positions a
+// launch leaves CUs idle and a single position (the Agent API's generate_move, alphazero_mcts/mod.rs:
+// 122-144; an arena's last games, evaluator.rs:355-399) still costs a whole 16-position workgroup
+// lifetime (~60-70 us). Here a workgroup evaluates ONE position: the GEMM columns are the position's
+// squares (two 16-column tiles, 25 of 32 used).
+// The arithmetic is k_nn_h3's, element for element, so the two kernels give bit-identical outputs
+// (the tree-parity tests rely on the network being batch-independent): the same packed fp16 hi/lo
+// weights as the MFMA A operand, the image as B with the same channel-to-k mapping, per output element
+// the same MFMA sequence (steps = (tap, K-half) in order, each lo*hi, hi*hi, hi*lo) — a (square, tap)
+// that k_nn_h3 skips because the neighbour is off the board reads the zero row here and adds an exact
+// +-0 — the same epilogue (fma(acc, 1/s, bias), residual, ReLU, RNE hi / exact lo split), the same
+// first-layer K blocks (the square-class-dependent K block 1 is applied once per class present in
+// the tile, with the B columns of the other classes zeroed), the same head 1x1-conv MFMAs and heads_mm.
+// The fp16-range guard and its in-kernel recompute (the k_nn_x6 body for this position) are k_nn_h3's.
+// Bound: one position's weights (147 KB of fp16 hi/lo per 3x3 conv) through ONE CU's vector memory
+// path (~64 B/clk), not the MFMAs (1.7k cycles per conv per SIMD). So every conv weight is fetched
+// once per workgroup: waves 0-3 (one per SIMD) own an N-tile (16 output channels) and BOTH column
+// tiles (two independent accumulators share each weight fragment), keep a conv's 18 (tap, K-half)
+// steps x 2 pieces in registers (144 VGPRs) and request the next conv's step by step as this conv
+// retires them. Waves 4-7 take what would sit on that path's critical start and end: the first layer
+// (its fp32 results go to the compute waves through LDS as the first block's residual) and the heads'
+// 1x1 convs, their weights requested at kernel start. The image is two 26-row buffers (ping-pong: one
+// barrier per conv) with a zero row for off-board taps. 8 waves also make the k_nn_x6 fallback body
+// (8 waves) callable in the same launch.
+namespace h3s {
+constexpr int kRows = 26;  // 25 squares + the zero row
+constexpr int kZero = 25;
+constexpr int kRowB = 128;                  // one piece: 64 channels x f16
+constexpr int kPlaneB = kRows * kRowB;      // 3,328 B
+constexpr int kImageB = 2 * kPlaneB;        // hi + lo pieces
+constexpr int kSkipOff = 2 * kImageB;       // two image buffers, then the first layer's fp32 results:
+                                            // [4 N-tiles][64 lanes][2 tiles] f32x4
+constexpr int kHeadOff = kSkipOff + 4 * 64 * 2 * 16;  // the head parameters (value, policy, head 1x1 B pieces)
+constexpr int kHeadF = (int)(nn::kValueF + nn::kPolicyF + h3::kHeadB);  // 5,512 floats
+constexpr int kFeatOff = kHeadOff + ((kHeadF * 4 + 15) & ~15);  // features [16][80] + heads_mm's table [16][128]
+constexpr int kBytes = kFeatOff + (16 * 80 + 16 * 128) * 4;
+// 16-byte chunk c8 of a row at c8 ^ (row & 7): the 16 rows a 16-lane group reads spread over the banks
+__device__ __forceinline__ int chunk_off(int row, int c8) { return row * kRowB + ((c8 ^ (row & 7)) << 4); }
+}  // namespace h3s
+
+// l1_pattern / l1_tap8 for a run-time square (here a lane's column is a square, not a position)
+__device__ __forceinline__ uint32_t l1_pattern_rt(int sq, uint32_t bb) {
+    const int r = sq / 5, c = sq % 5;
+    const uint32_t a = r > 0 ? (bb >> (35 - sq)) & 7u : 0u;
+    const uint32_t m = (bb >> (30 - sq)) & 7u;
+    const uint32_t d = r < 4 ? (bb >> (26 - sq)) & 3u : 0u;
+    const uint32_t mask = (c == 0 ? ~0xA4u : ~0u) & (c == 4 ? ~0x09u : ~0u) & 0xFFu;
+    return (a | (m << 3) | (d << 6)) & mask;
+}
+// l1_lut_build's entry for pattern P, built in registers: element t = bit pos(t) of P as fp16 0 / 1.0
+__device__ __forceinline__ f16x8 l1_pattern_frag(uint32_t P) {
+    constexpr int pos[8] = {2, 1, 0, 5, 4, 3, 7, 6};
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        w[k] = (((P >> pos[2 * k]) & 1u) ? 0x3C00u : 0u) | (((P >> pos[2 * k + 1]) & 1u) ? 0x3C000000u : 0u);
+    return __builtin_bit_cast(f16x8, uint4{w[0], w[1], w[2], w[3]});
+}
+__device__ __forceinline__ uint32_t l1_tap8_rt(int sq, uint32_t bb) {
+    if (sq / 5 == 4 || sq % 5 == 4) return 0u;
+    return ((bb >> (25 - sq)) & 1u) ? 0x3C00u : 0u;
+}
+__device__ __forceinline__ int l1_cls_rt(int sq) {
+    const int r = sq / 5, c = sq % 5;
+    return (r == 0 ? 0 : r == 4 ? 2 : 1) * 3 + (c == 0 ? 0 : c == 4 ? 2 : 1);
+}
+// a representative square of each first-layer class (whose K block 1 is loaded)
+__constant__ int8_t c_cls_rep[9] = {0, 1, 4, 5, 6, 9, 20, 21, 24};
+
+struct H3sW {  // one conv's B pieces: 18 steps x (hi, lo)
+    f16x8 w[18][2];
+};
+// byte offset of the B fragment (K-half m) of square sq's neighbour for tap t: the zero row when it is
+// off the board or sq is a padding column
+__device__ __forceinline__ int h3s_boff(int sq, int t, int m, int kq) {
+    const int row = sq < 25 ? nbr_index(sq, t) : h3s::kZero;  // nbr_index: 25 = off the board
+    return h3s::chunk_off(row, 4 * m + kq);
+}
+
+template <class C>
+__device__ __forceinline__ bool nn_h3s_body(const oaz_state* __restrict__ states, int b, const float* __restrict__ blob,
+                                            int blocks, float* __restrict__ policy, float* __restrict__ value,
+                                            float* lds) {
+    static_assert(!C::BF && C::WAVES == 8, "k_nn_h3s: fp16x3 mode, 8 waves");
+    // DBG 2 (diagnostic build, timing only): per-wave s_memtime phase sums over the position's policy row:
+    // 0 kernel start to the first conv (helpers: the first layer), 2 conv MFMA loops, 3 conv epilogues +
+    // barriers, 4 heads 1x1 convs, 5 heads MLP / softmax
+    uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t tmk = C::DBG == 2 ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int k) {
+        if constexpr (C::DBG == 2) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            ph[k] += t - tmk;
+            tmk = t;
+        }
+    };
+    char* const base = reinterpret_cast<char*>(lds);
+    char* const img0 = base;
+    char* const img1 = base + h3s::kImageB;
+    f32x4* const skipx = reinterpret_cast<f32x4*>(base + h3s::kSkipOff);
+    float* const hl = reinterpret_cast<float*>(base + h3s::kHeadOff);  // the head parameters in LDS
+    float* const feat = reinterpret_cast<float*>(base + h3s::kFeatOff);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const bool compute = wave < 4;  // waves 0-3: the convs; 4-7: first layer, head parameters, head convs
+    const int nt = wave & 3;
+    const int i = lane & 15, kq = lane >> 4;
+    const int sq0 = i, sq1 = 16 + i;  // the lane's columns in tiles 0 and 1 (sq1 >= 25: padding)
+    const bool live1 = sq1 < 25;
+    const int cq = nt * 16 + 4 * kq;  // this lane's 4 output channels cq .. cq + 3
+    const int eo0 = h3s::chunk_off(sq0, cq >> 3) + (cq & 7) * 2;
+    const int eo1 = h3s::chunk_off(live1 ? sq1 : h3s::kZero, cq >> 3) + (cq & 7) * 2;
+    const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
+                       nn::kValueF + nn::kPolicyF + h3::kHeadB;
+    const float* p = blob + nn::kL1B + nn::kCh + nn::kL1Table;  // the first conv's packed weights
+    const float* ph0 = p + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh);  // the head parameters
+    uint32_t hmax = 0;
+    auto track = [&](const uint32_t (&pk)[2][2]) {  // the fp16 range guard (hi >= +0 after ReLU)
+        hmax = __builtin_bit_cast(
+            uint32_t, __builtin_elementwise_maximum(
+                          __builtin_elementwise_maximum(__builtin_bit_cast(f16x2, hmax), __builtin_bit_cast(f16x2, pk[0][0])),
+                          __builtin_bit_cast(f16x2, pk[0][1])));
+    };
+    auto store2 = [&](char* img, int eo, const uint32_t (&pk)[2][2]) {
+        *reinterpret_cast<uint2*>(img + eo) = uint2{pk[0][0], pk[0][1]};
+        *reinterpret_cast<uint2*>(img + h3s::kPlaneB + eo) = uint2{pk[1][0], pk[1][1]};
+    };
+    H3sW R;  // compute waves: the current conv's B pieces
+    if (compute) {
+        const X6W W0 = h3_w(p, lane, nt);
+#pragma unroll
+        for (int st = 0; st < 18; ++st) {  // the first conv's pieces, in flight during the first layer
+            R.w[st][0] = h3_ldb(W0, (st * 2 + 0) * 4);
+            R.w[st][1] = h3_ldb(W0, (st * 2 + 1) * 4);
+        }
+        if (tid < 32)  // the zero row of both buffers, both pieces (32 x 16 B)
+            *reinterpret_cast<uint4*>(base + (tid >> 4) * h3s::kImageB + ((tid >> 3) & 1) * h3s::kPlaneB +
+                                      h3s::kZero * h3s::kRowB + (tid & 7) * 16) = uint4{0u, 0u, 0u, 0u};
+    } else {  // ---- helpers: the first layer (k_nn_h3's K blocks) for N-tile nt, both tiles; no barrier inside
+        const oaz_state st = states[b];
+        X6W A;
+        A.r = __builtin_amdgcn_make_buffer_rsrc((void*)l1c, (short)0, (int)(26 * h3::kL1Frag * 4), 0x00020000);
+        A.voff = (nt * 64 + lane) * 16;
+        auto ld = [&](int blk, int pc) {  // [blk][pc][nt][lane]
+            return __builtin_bit_cast(f16x8,
+                                      __builtin_amdgcn_raw_buffer_load_b128(A.r, A.voff, (blk * 2 + pc) * 4 * 64 * 16, 0));
+        };
+        const f16x8 a0h = ld(0, 0), a0l = ld(0, 1);
+        f16x8 a1[9][2];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {  // every class occurs in one of the two tiles
+            a1[k][0] = ld(1 + c_cls_rep[k], 0);
+            a1[k][1] = ld(1 + c_cls_rep[k], 1);
+        }
+        const f32x4 bias1t = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
+        const f32x4 inv1 = *reinterpret_cast<const f32x4*>(l1c + 26 * h3::kL1Frag + cq);
+        const uint32_t bb = kq == 0 ? st.pawns[0] : kq == 1 ? st.kings[0] : kq == 2 ? st.pawns[1] : st.kings[1];
+        const int blue = st.to_move & 1;
+        const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
+        // block 1's constant planes: element e >= 1 of quarter q is constant plane c = 7q + e - 1
+        uint32_t kw[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = 2 * w + h, c = 7 * kq + e - 1;
+                const bool one = e > 0 && (c < 16 ? (c == c0 || c == c1) : (c == 16 && blue));
+                v |= one ? (0x3C00u << (16 * h)) : 0u;
+            }
+            kw[w] = v;
+        }
+        const int cls0 = l1_cls_rt(sq0), cls1 = live1 ? l1_cls_rt(sq1) : -1;
+        const f16x8 b00 = l1_pattern_frag(l1_pattern_rt(sq0, bb));
+        const f16x8 b01 = l1_pattern_frag(live1 ? l1_pattern_rt(sq1, bb) : 0u);
+        const f16x8 b10 = __builtin_bit_cast(f16x8, uint4{kw[0] | l1_tap8_rt(sq0, bb), kw[1], kw[2], kw[3]});
+        const f16x8 b11 = __builtin_bit_cast(f16x8, uint4{kw[0] | (live1 ? l1_tap8_rt(sq1, bb) : 0u), kw[1], kw[2], kw[3]});
+        const f16x8 bz = {};
+        f32x4 acc0 = {}, acc1 = {};
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0h, b00, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0h, b01, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0l, b00, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0l, b01, acc1, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const f16x8 bk0 = cls0 == k ? b10 : bz, bk1 = cls1 == k ? b11 : bz;
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[k][0], bk0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[k][0], bk1, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[k][1], bk0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[k][1], bk1, acc1, 0, 0, 0);
+        }
+        uint32_t pk[2][2];
+        f32x4 r0 = {}, r1 = {};
+        h3t_pack_one<true, false, 0>(acc0, pk, bias1t, inv1, r0);
+        track(pk);
+        store2(img0, eo0, pk);
+        h3t_pack_one<true, false, 0>(acc1, pk, bias1t, inv1, r1);
+        if (live1) {
+            track(pk);
+            store2(img0, eo1, pk);
+        }
+        skipx[(nt * 64 + lane) * 2 + 0] = r0;  // the first block's residual, for the compute waves
+        skipx[(nt * 64 + lane) * 2 + 1] = r1;
+    }
+    __syncthreads();  // the first layer's image and residual
+    stamp(0);
+    if (!compute) {  // the head parameters into LDS during the first conv (no global round trip at the end)
+        static_assert(h3s::kHeadF % 4 == 0, "float4 copy");
+        const float4* src = reinterpret_cast<const float4*>(ph0);
+        float4* dst = reinterpret_cast<float4*>(hl);
+        for (int k = tid - 256; k < h3s::kHeadF / 4; k += 256) dst[k] = src[k];
+    }
+    f32x4 skip0 = {}, skip1 = {};  // compute waves: the residual (fp32) of both tiles
+    if (compute) {
+        skip0 = skipx[(nt * 64 + lane) * 2 + 0];
+        skip1 = skipx[(nt * 64 + lane) * 2 + 1];
+    }
+    // the 2 * blocks convs in pairs (compile-time residual role, as k_nn_h3): conv c reads buffer c & 1
+    // and writes the other; the helpers only keep the barrier count
+    auto conv_one = [&](auto res, bool more, const char* rd, char* wr) {
+        constexpr int RES = decltype(res)::value;
+        if (compute) {
+            const f32x4 bbt = *reinterpret_cast<const f32x4*>(p + h3::kW + cq);
+            const f32x4 sct = *reinterpret_cast<const f32x4*>(p + h3::kW + nn::kCh + cq);
+            const X6W Wn = h3_w(p + h3::kW + 2 * nn::kCh, lane, nt);
+            f32x4 acc0 = {}, acc1 = {};
+            f16x8 xl0[2], xh0[2], xl1[2], xh1[2];
+            {
+                const int o0 = h3s_boff(sq0, 0, 0, kq), o1 = h3s_boff(sq1, 0, 0, kq);
+                xl0[0] = *reinterpret_cast<const f16x8*>(rd + h3s::kPlaneB + o0);
+                xh0[0] = *reinterpret_cast<const f16x8*>(rd + o0);
+                xl1[0] = *reinterpret_cast<const f16x8*>(rd + h3s::kPlaneB + o1);
+                xh1[0] = *reinterpret_cast<const f16x8*>(rd + o1);
+            }
+#pragma unroll
+            for (int s = 0; s < 18; ++s) {
+                if (s + 1 < 18) {  // the next step's fragments
+                    const int t = (s + 1) >> 1, m = (s + 1) & 1, n = (s + 1) & 1;
+                    const int o0 = h3s_boff(sq0, t, m, kq), o1 = h3s_boff(sq1, t, m, kq);
+                    xl0[n] = *reinterpret_cast<const f16x8*>(rd + h3s::kPlaneB + o0);
+                    xh0[n] = *reinterpret_cast<const f16x8*>(rd + o0);
+                    xl1[n] = *reinterpret_cast<const f16x8*>(rd + h3s::kPlaneB + o1);
+                    xh1[n] = *reinterpret_cast<const f16x8*>(rd + o1);
+                }
+                const int c = s & 1;
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(R.w[s][0], xl0[c], acc0, 0, 0, 0);  // lo * hi
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(R.w[s][0], xl1[c], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(R.w[s][0], xh0[c], acc0, 0, 0, 0);  // hi * hi
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(R.w[s][0], xh1[c], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(R.w[s][1], xh0[c], acc0, 0, 0, 0);  // hi * lo
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(R.w[s][1], xh1[c], acc1, 0, 0, 0);
+                if (more) {  // the next conv's step s (uniform branch)
+                    R.w[s][0] = h3_ldb(Wn, (s * 2 + 0) * 4);
+                    R.w[s][1] = h3_ldb(Wn, (s * 2 + 1) * 4);
+                }
+            }
+            if constexpr (C::DBG == 2) asm volatile("" ::"v"(acc0[0]), "v"(acc1[0]));  // the stamp follows the MFMAs
+            stamp(2);
+            uint32_t pk[2][2];
+            h3t_pack_one<false, false, RES>(acc0, pk, bbt, sct, skip0);
+            track(pk);
+            store2(wr, eo0, pk);
+            h3t_pack_one<false, false, RES>(acc1, pk, bbt, sct, skip1);
+            if (live1) {
+                track(pk);
+                store2(wr, eo1, pk);
+            }
+        }
+        p += h3::kW + 2 * nn::kCh;
+        __syncthreads();
+        stamp(3);
+    };
+    for (int c = 0; c < blocks; ++c) {
+        conv_one(std::integral_constant<int, 0>{}, true, img0, img1);
+        conv_one(std::integral_constant<int, 1>{}, c + 1 < blocks, img1, img0);
+    }
+    // heads (h3_heads' arithmetic, parameters from LDS): the 1x1 convs by waves 4, 5 with the image as A
+    // (rows = squares), then heads_mm over all 8 waves
+    {
+        HeadMM hm;
+        heads_mm_fetch(hm, hl, wave, lane);
+        const float hs = hl[nn::kValueF + nn::kPolicyF + 2 * 2 * 64 * 4 + (i < 3 ? i : 0)];
+        const float hbias = i == 0 ? hl[64] : i == 1 ? hl[nn::kValueF + 128] : hl[nn::kValueF + 129];
+        if (wave == 4 || wave == 5) {
+            const f16x8* HB = reinterpret_cast<const f16x8*>(hl + nn::kValueF + nn::kPolicyF);
+            f16x8 hb[2][2];
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int pc = 0; pc < 2; ++pc) hb[m][pc] = HB[(m * 2 + pc) * 64 + lane];
+            const int rt = wave - 4;
+            const int rsq = rt * 16 + i;  // A row = square
+            const int row = rsq < 25 ? rsq : h3s::kZero;
+            f32x4 hacc = {};
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const char* a = img0 + h3s::chunk_off(row, 4 * m + kq);
+                const f16x8 ah = *reinterpret_cast<const f16x8*>(a);
+                const f16x8 al = *reinterpret_cast<const f16x8*>(a + h3s::kPlaneB);
+                hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, hb[m][0], hacc, 0, 0, 0);
+                hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][0], hacc, 0, 0, 0);
+                hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hb[m][1], hacc, 0, 0, 0);
+            }
+            // C/D: reg r of lane l = (row 4 * kq + r = square rt * 16 + 4 * kq + r, column i = head output)
+            if (i < 3)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int s2 = rt * 16 + 4 * kq + r;
+                    const float v = __builtin_fmaf(hacc[r], hs, hbias);
+                    if (s2 < 25) feat[i * 25 + s2] = v > 0.0f ? v : 0.0f;
+                }
+        } else {
+            const int t0 = compute ? tid : tid - 256 + 128;  // waves 0-3, 6, 7: rows 1-15 (unused positions)
+            for (int k = t0; k < 15 * 80; k += 384) feat[80 + k] = 0.0f;
+        }
+        __syncthreads();
+        stamp(4);
+        heads_mm(hm, feat, feat + 16 * 80, wave, lane, b, b + 1, policy, value);
+    }
+    if constexpr (C::DBG == 2) {
+        stamp(5);
+        __syncthreads();
+        float v = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) v = lane == k ? (float)ph[k] : v;
+        if (lane < 6) policy[(size_t)b * 50 + wave * 6 + lane] = v;
+    }
+    return (hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u;  // an fp16 hi term overflowed
+}
+
+template <class C>
+__global__ void __launch_bounds__(64 * C::WAVES) k_nn_h3s(const oaz_state* __restrict__ states, int B,
+                                                         const float* __restrict__ blob, int blocks,
+                                                         float* __restrict__ policy, float* __restrict__ value,
+                                                         const float* __restrict__ xblob,
+                                                         unsigned long long* __restrict__ fallback, TileMap tm) {
+    __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
+    static_assert(h3s::kBytes <= H3Fallback<C>::kLds * 4, "k_nn_h3s LDS");
+    int b = (int)blockIdx.x, end = B, cap = B;
+    if (tm.bcnt) {  // compacted leaves: workgroup i takes row i / nb of bucket i % nb
+        const int bk = (int)blockIdx.x % tm.nb;
+        b = (bk << kBucketShift) + (int)blockIdx.x / tm.nb;
+        end = (bk << kBucketShift) + (int)tm.bcnt[bk];
+        cap = tm.cap;
+    }
+    if (b >= end) return;  // uniform over the workgroup
+    const bool ovf = nn_h3s_body<C>(states, b, blob, blocks, policy, value, lds);
+    if constexpr (H3Fallback<C>::kOn) {
+        using X = typename H3Fallback<C>::X;
+        if (__syncthreads_or(ovf)) {  // recompute this position as k_nn_h3 would (its fallback body)
+            const TileSpan sp{b, b + 1, cap};
+            if ((threadIdx.x >> 8) == 0)
+                nn_h3_fallback<X, X::GRP0>(states, sp, xblob, blocks, policy, value, lds);
+            else
+                nn_h3_fallback<X, X::GRP1>(states, sp, xblob, blocks, policy, value, lds);
+            if (threadIdx.x == 0) atomicAdd(fallback, 1ull);
+        }
+    }
+}
+
 // One kernel per precision. The A/B build (make AB=1, -DOAZ_AB=1) adds the diagnostic builds of
 // k_nn_h3, selected by OAZ_NN_X6_V (timing only, wrong results); the product build ignores it.
 hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* policy, float* value,
@@ -1769,6 +2129,16 @@ hipError_t launch_nn_forward(const NNView& w, const oaz_state* s, int B, float* 
     const dim3 block(64 * nn::kWaves);
     if (w.precision == OAZ_FP32_SPLIT16) {
         if (!w.fallback || !w.blob_x6) return hipErrorInvalidValue;
+        if (B <= w.small_max) {  // one position per workgroup (bit-identical results, ~10x less latency)
+            const unsigned g1 = w.tm.bcnt ? (unsigned)(w.tm.nb * (B < (int)kBucket ? B : (int)kBucket)) : (unsigned)B;
+            auto ks = k_nn_h3s<H3Cfg<0>>;
+#if OAZ_AB
+            if (w.x6_variant == 70) ks = k_nn_h3s<H3Cfg<0, 2>>;  // phase stamps (timing only)
+#endif
+            hipLaunchKernelGGL(ks, dim3(g1), block, 0, st, s, B, w.blob, w.blocks, policy, value,
+                               w.blob_x6, w.fallback, w.tm);
+            return hipGetLastError();
+        }
         // 8 waves, uneven 17 / 8 square split, batches of <= 4 squares, transposed C/D tiles, convs in
         // pairs (compile-time residual), in-kernel k_nn_x6 recompute of fp16-range tiles
         auto k = k_nn_h3<H3Cfg<0>>;

@@ -5,6 +5,7 @@ bit-exact (every node's N, W, P, move, children, flags) against the oracle whene
 the same evaluator outputs (HASH test evaluator, or the GPU network fed to the oracle).
 """
 import ctypes as C
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -16,6 +17,8 @@ from onitama_az.game import (Deck, DoneMove, GameState, Move, MoveResult, PieceK
                              ORIGINAL_CARDS, CARD_NAMES, current_state_batch, encode_batch, movegen_batch,
                              movegen_masks_batch, step_batch)
 from onitama_az.weights import random_weights
+
+ROOT = Path(__file__).resolve().parents[1]
 
 pytestmark = pytest.mark.gpu
 
@@ -124,63 +127,101 @@ def test_nn_split16_error_at_fp32_level(nn_golden, trained3, name, blocks):
     assert err[_abi.FP32_SPLIT16] <= 4 * err[_abi.FP32] + 1e-6, err
 
 
-def test_nn_split16_range_fallback_recomputes_all_tiles(nn_golden, trained3):
+# k_nn_h3s (one position per workgroup) runs launches of up to one round of workgroups (the CU count,
+# 256 on MI355X; >= 64 on any device), k_nn_h3 (16-position tiles) larger ones: B = 64 and B = 1024 pick
+# one each on every device.
+SMALL_B, BIG_B = 64, 1024
+
+
+@pytest.mark.parametrize("B,per_wg", [(SMALL_B, 1), (BIG_B, 16)])
+def test_nn_split16_range_fallback_recomputes_all_tiles(nn_golden, trained3, B, per_wg):
     """Activations beyond the fp16 range (here every position's: BN-folded first-layer bias 1e5) make
-    each workgroup recompute its 16 positions with the bf16x6 split inside the same launch: the
-    results equal the OAZ_FP32_SPLIT engine's bit for bit, and the fallback counts every tile."""
+    each workgroup recompute its positions (16, or 1 in k_nn_h3s) with the bf16x6 split inside the same
+    launch: the results equal the OAZ_FP32_SPLIT engine's bit for bit, and the fallback counts every
+    workgroup."""
     from onitama_az.weights import blob_from_named, named_from_blob
     named = {k: v.copy() for k, v in named_from_blob(trained3.copy(), 3).items()}
     named["bn1|bias"][:] = 1.0e5  # first-layer activations ~1e5 > 65504
     bad = blob_from_named(named, 3)
-    states = nn_golden["states"][:64]
-    with Engine(games=64, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT16) as e:
+    states = np.ascontiguousarray(np.tile(nn_golden["states"], (B + 255) // 256)[:B])
+    with Engine(games=B, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT16) as e:
         e.load_weights(bad)
         p16, v16 = e.nn_forward(states)
-        assert e.nn_fallbacks() == 4  # 64 positions = 4 tiles of 16
+        assert e.nn_fallbacks() == B // per_wg
         e.load_weights(trained3)
         p, _ = e.nn_forward(states)
-        assert e.nn_fallbacks() == 4  # sane weights: no further tile
-    assert np.abs(p - nn_golden["policy_trained3"][:64]).max() < 1e-5
-    with Engine(games=64, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT) as e:
+        assert e.nn_fallbacks() == B // per_wg  # sane weights: no further workgroup
+    gold = np.tile(nn_golden["policy_trained3"], ((B + 255) // 256, 1, 1))[:B]
+    assert np.abs(p - gold).max() < 1e-5
+    with Engine(games=B, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT) as e:
         e.load_weights(bad)
         px, vx = e.nn_forward(states)
     assert np.isfinite(px).all() and np.isfinite(vx).all()
     assert np.array_equal(p16, px) and np.array_equal(v16, vx)
 
 
-def test_nn_split16_range_fallback_only_overflowing_tiles(nn_golden, trained3):
+@pytest.mark.parametrize("reps,per_wg", [(1, 1), (4, 16)])
+def test_nn_split16_range_fallback_only_overflowing_tiles(nn_golden, trained3, reps, per_wg):
     """Only positions whose mover holds card 7 (Rooster) overflow (its first-layer plane weights are
-    scaled by 1e6): exactly the tiles containing such a position are recomputed (bit-equal to the
-    OAZ_FP32_SPLIT kernel), the other tiles keep the fp16x3 result (bit-equal to a batch of those
-    positions alone, and within 1e-5 of exact fp32)."""
+    scaled by 1e6): exactly the workgroups containing such a position are recomputed (bit-equal to the
+    OAZ_FP32_SPLIT kernel) — single positions at 256 (k_nn_h3s), 16-position tiles at 1024 (k_nn_h3) —
+    the others keep the fp16x3 result (bit-equal to a batch of those positions alone, and within 1e-5
+    of exact fp32)."""
     from onitama_az.game import encode_batch
     from onitama_az.weights import blob_from_named, named_from_blob
     named = {k: v.copy() for k, v in named_from_blob(trained3.copy(), 3).items()}
     named["conv_init_1|weight"][:, 4 + 7] *= 1.0e6
     bad = blob_from_named(named, 3)
-    states = nn_golden["states"]
+    states = np.ascontiguousarray(np.tile(nn_golden["states"], reps))
+    n = len(states)
     planes = encode_batch(states)
-    hot = planes[:, 4 + 7].reshape(256, -1).max(1) > 0  # the mover holds card 7
-    tiles_hot = hot.reshape(16, 16).any(1)
-    assert 0 < tiles_hot.sum() < 16
+    hot = planes[:, 4 + 7].reshape(n, -1).max(1) > 0  # the mover holds card 7
+    wg_hot = hot.reshape(n // per_wg, per_wg).any(1)
+    assert 0 < wg_hot.sum() < n // per_wg
     out = {}
     for prec in (_abi.FP32_SPLIT16, _abi.FP32_SPLIT, _abi.FP32):
-        with Engine(games=256, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=prec) as e:
+        with Engine(games=n, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=prec) as e:
             e.load_weights(bad)
             out[prec] = e.nn_forward(states)
             if prec == _abi.FP32_SPLIT16:
-                assert e.nn_fallbacks() == int(tiles_hot.sum())
+                assert e.nn_fallbacks() == int(wg_hot.sum())
     p16, px, pf = out[_abi.FP32_SPLIT16][0], out[_abi.FP32_SPLIT][0], out[_abi.FP32][0]
-    rows = np.repeat(tiles_hot, 16)
+    rows = np.repeat(wg_hot, per_wg)
     assert np.array_equal(p16[rows], px[rows])
     assert np.abs(p16[~rows] - pf[~rows]).max() < 1e-5
-    # the cold tiles alone in a clean batch: the same fp16x3 bits
+    # the cold workgroups alone in a clean batch: the same fp16x3 bits
     cold = np.ascontiguousarray(states[~rows])
-    with Engine(games=256, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT16) as e:
+    with Engine(games=n, sims=1, blocks=3, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT16) as e:
         e.load_weights(bad)
         pc, _ = e.nn_forward(cold)
         assert e.nn_fallbacks() == 0
     assert np.array_equal(pc, p16[~rows])
+
+
+@pytest.mark.parametrize("name,blocks", [("trained3", 3), ("trained5", 5), ("random6", 6), ("random0", 0)])
+def test_nn_small_batch_kernel_bitidentical_to_tiled(nn_golden, trained3, name, blocks):
+    """k_nn_h3s (one position per workgroup: small batches, the Agent API) and k_nn_h3 (16-position
+    tiles) compute the same fp16x3 arithmetic element for element, so a position's policy and value are
+    bit-identical whichever kernel the batch size picks (B = 1, 64 / 1024) — the network stays
+    batch-independent, which the real-network tree-parity tests rely on."""
+    if name == "trained5":
+        w = np.load(ROOT / "tests/golden/weights_5block_trained.npy")
+    else:
+        w = trained3 if name == "trained3" else random_weights(7, blocks)
+    st = nn_golden["states"]
+    with Engine(games=BIG_B, sims=1, blocks=blocks, evaluator=_abi.EVAL_NN, precision=_abi.FP32_SPLIT16) as e:
+        e.load_weights(w)
+        pb, vb = e.nn_forward(np.ascontiguousarray(np.tile(st, 4)))
+        ps, vs = e.nn_forward(np.ascontiguousarray(st[:SMALL_B]))
+        singles = [e.nn_forward(np.ascontiguousarray(st[k:k + 1])) for k in (0, 17, 200, 255)]
+        assert e.nn_fallbacks() == 0
+    assert np.array_equal(pb[256:512], pb[:256]) and np.array_equal(vb[768:], vb[:256])
+    assert np.array_equal(ps.view(np.uint32), pb[:SMALL_B].view(np.uint32))
+    assert np.array_equal(vs.view(np.uint32), vb[:SMALL_B].view(np.uint32))
+    for k, (p1, v1) in zip((0, 17, 200, 255), singles):
+        assert np.array_equal(p1[0].view(np.uint32), pb[k].view(np.uint32)) and v1[0] == vb[k], k
+    if name == "trained3":
+        assert np.abs(ps - nn_golden["policy_trained3"][:SMALL_B]).max() < 1e-5
 
 
 @pytest.mark.parametrize("name,blocks", [("trained3", 3), ("random3", 3), ("random6", 6)])
@@ -203,8 +244,11 @@ def test_nn_batch_position_invariance(orc, precision):
         p1, v1 = e.nn_forward(pos)
         big = np.concatenate([pos[::-1], pos, pos[:7]])
         p2, v2 = e.nn_forward(big)
+        huge = np.concatenate([pos[:5]] + [pos] * 14 + [pos[::-1]])  # > one round: the tiled kernel
+        p3, v3 = e.nn_forward(huge)
     assert np.array_equal(p2[64:128], p1) and np.array_equal(v2[64:128], v1)
     assert np.array_equal(p2[:64][::-1], p1)
+    assert np.array_equal(p3[5:69], p1) and np.array_equal(v3[-64:][::-1], v1)
 
 
 # ---- search ------------------------------------------------------------------------------

@@ -17,7 +17,8 @@ from onitama_az.weights import random_weights  # noqa: E402
 sims = int(sys.argv[1]) if len(sys.argv) > 1 else 400
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 out = {}
-for G in (1, 16, 256, 2048):
+Gs = [int(x) for x in os.environ.get("OAZ_LAT_G", "1,16,64,256,1024,2048").split(",")]
+for G in Gs:
     roots = np.concatenate([initial_state_np([0, 1, 2, 3, 4]) for _ in range(G)])
     with Engine(games=G, sims=sims, blocks=3, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_NN,
                 precision=_abi.FP32_SPLIT16) as e:
@@ -28,6 +29,12 @@ for G in (1, 16, 256, 2048):
             t0 = time.perf_counter()
             e.search(roots)
             ts.append(time.perf_counter() - t0)
+        e.set_timing(1)  # a separate timed search: per-launch kernel times (events add a little)
+        e.kernel_times_reset()
+        e.search(roots)
+        kt = e.kernel_times()
     out[G] = {"ms_median": 1e3 * float(np.median(ts)), "ms_min": 1e3 * min(ts),
-              "us_per_sim_step": 1e6 * float(np.median(ts)) / sims}
+              "us_per_sim_step": 1e6 * float(np.median(ts)) / sims,
+              "nn_us_per_launch": 1e3 * kt.nn_ms / max(kt.nn_n, 1),
+              "backup_select_us_per_launch": 1e3 * kt.backup_select_ms / max(kt.backup_select_n, 1)}
 print(json.dumps(out, indent=1))
