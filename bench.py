@@ -919,27 +919,38 @@ def main():
                              "xgmi_note": f"xGMI: {XGMI_LINK_GBPS:.0f} GB/s per link and direction, 7 links per GPU; "
                                           "collective_ms = HIP events on the communicator stream around the grouped "
                                           "broadcasts only (no host copies)"}
+        except Exception as ex:  # noqa: BLE001
+            print(f"bench: sample all-gather failed on rank {rank}: {ex!r}", file=sys.stderr, flush=True)
+            allgather = {"error": repr(ex)}
+        if comm is not None:
+            comm.close()
+        # The post-processing collectives run only when every rank's exchange succeeded: every rank joins
+        # this status reduction first (also a rank whose exchange raised), so no rank waits in a later
+        # collective that another skipped.
+        all_ok = "error" not in allgather
+        if world > 1:
+            okt = torch.tensor([1.0 if all_ok else 0.0], dtype=torch.float64, device=cdev)
+            dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+            all_ok = bool(okt.item() == 1.0)
+        if all_ok:
             # every rank: the gathered total is the sum of the ranks' own contributions
             chk = torch.tensor([float(own), float(total)], dtype=torch.float64, device=cdev)
+            ms = torch.tensor([allgather.get("collective_ms", 0.0)], dtype=torch.float64, device=cdev)
             if world > 1:
                 dist.all_reduce(chk[:1])
+                dist.all_reduce(ms, op=dist.ReduceOp.MAX)
             ok = int(chk[0].item()) == total and (counts is None or sum(counts) == total)
             if world > 1:
                 okt = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=cdev)
                 dist.all_reduce(okt, op=dist.ReduceOp.MIN)
                 ok = bool(okt.item() == 1.0)
             allgather.update(samples_total=int(total), bytes_per_sample=228, totals_consistent=ok)
+            if world > 1 and "collective_ms" in allgather:
+                allgather["collective_ms_max_over_ranks"] = float(ms.item())
             if not ok:
                 print(f"bench: all-gather totals inconsistent on rank {rank}", file=sys.stderr, flush=True)
-        except Exception as ex:  # noqa: BLE001
-            print(f"bench: sample all-gather failed on rank {rank}: {ex!r}", file=sys.stderr, flush=True)
-            allgather = {"error": repr(ex)}
-        if comm is not None:
-            comm.close()
-        if world > 1 and allgather is not None and "collective_ms" in allgather:
-            ms = torch.tensor([allgather["collective_ms"]], dtype=torch.float64, device=cdev)
-            dist.all_reduce(ms, op=dist.ReduceOp.MAX)
-            allgather["collective_ms_max_over_ranks"] = float(ms.item())
+        elif "error" not in allgather:
+            allgather["error"] = "another rank's exchange failed"
 
     if rank == 0:
         sims_steps = cfg["sims"]  # simulation steps (select -> NN -> expand launches) per bench step

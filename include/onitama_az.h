@@ -169,7 +169,12 @@ typedef struct oaz_config {
                                 after the first simulation step that ends at or past this wall-clock budget
                                 from its start; all games of the batch run the same number of playouts
                                 (>= 1, <= sims) and pi / the move come from those visits (oaz_last_sims) */
-    int32_t reserved[2];
+    int32_t step_kernels;    /* 0 = auto: a search of at most CU-count games with the fp16x3 network (or
+                                HASH), no root noise, no search_time budget and no leaf compaction runs as ONE
+                                launch, a workgroup per game doing all its simulations (the Agent API's
+                                one-position latency path); 1 = always the per-simulation-step launches.
+                                Trees, pi and samples are identical either way */
+    int32_t reserved;
 } oaz_config;
 
 typedef struct oaz_search_stats {
@@ -468,7 +473,8 @@ typedef struct oaz_pure_mcts_config {
     int32_t rollout_cap;      /* plies per rollout before it is scored as a draw (reference: none) */
     uint64_t seed;
     uint64_t game_id0;        /* RNG stream of root g = game_id0 + g */
-    int32_t reserved[4];
+    int32_t device;           /* HIP device the search runs on (its own stream; other work on it is not waited for) */
+    int32_t reserved[3];
 } oaz_pure_mcts_config;
 
 typedef struct oaz_pure_node { /* MctsNode (mcts_arena.rs:330-352) */

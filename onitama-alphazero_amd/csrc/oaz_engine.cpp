@@ -834,6 +834,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
     }
     if (cfg->blocks < 0 || cfg->blocks > 64 || cfg->sims < 1 || cfg->sims > 65535 || cfg->games < 1 ||
         cfg->max_plies < 0 || cfg->max_plies > 100000 || cfg->compact < 0 || cfg->compact > 2 || cfg->search_time_ns < 0 ||
+        cfg->step_kernels < 0 || cfg->step_kernels > 1 ||
         (cfg->parts != 0 && cfg->parts != 1 && cfg->parts != 2 && cfg->parts != 4)) {
         oaz_set_err(OAZ_ERR_ARG, "create: config out of range");
         return nullptr;
@@ -1051,14 +1052,7 @@ extern "C" int oaz_kernel_times_reset(oaz_engine* e) {
     return 0;
 }
 
-// B positions d_states[0, B) -> rows [0, B); with tm (compacted leaves, run_sims) the rows of the
-// bucket tiles (the HASH evaluator simply evaluates every row below B).
-static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float* d_pol, float* d_val,
-                    hipStream_t st = nullptr, const TileMap* tm = nullptr) {
-    if (!st) st = e->stream;
-    const uint32_t counted = tm ? 0u : B;  // compacted: the count is on the device (GS_EVALS)
-    if (e->cfg.evaluator == OAZ_EVAL_HASH)
-        return timed(e, 1, counted, [&] { return launch_hash_eval(d_states, (int)B, d_pol, d_val, st); }, st);
+static NNView nn_view(const oaz_engine* e, const TileMap* tm) {
     NNView w;
     w.blob = e->weights;
     w.blocks = e->cfg.blocks;
@@ -1077,6 +1071,18 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
 #if OAZ_AB  // A/B build only: OAZ_NN_SMALL_MAX=n overrides
     if (const char* v = getenv("OAZ_NN_SMALL_MAX")) w.small_max = atoi(v);
 #endif
+    return w;
+}
+
+// B positions d_states[0, B) -> rows [0, B); with tm (compacted leaves, run_sims) the rows of the
+// bucket tiles (the HASH evaluator simply evaluates every row below B).
+static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float* d_pol, float* d_val,
+                    hipStream_t st = nullptr, const TileMap* tm = nullptr) {
+    if (!st) st = e->stream;
+    const uint32_t counted = tm ? 0u : B;  // compacted: the count is on the device (GS_EVALS)
+    if (e->cfg.evaluator == OAZ_EVAL_HASH)
+        return timed(e, 1, counted, [&] { return launch_hash_eval(d_states, (int)B, d_pol, d_val, st); }, st);
+    const NNView w = nn_view(e, tm);
     return timed(e, 1, counted, [&] { return launch_nn_forward(w, d_states, (int)B, d_pol, d_val, st); }, st);
 }
 
@@ -1182,6 +1188,26 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
     const double t_start = budget_ns > 0 ? now_ns() : 0.0;
     e->last_sims = 0;
     const bool noise = e->cfg.train_noise && e->noise;
+    // the one-launch search (oaz_search_lat.hip): a workgroup per game runs all its simulations, when the
+    // per-step loop would launch one NN workgroup per game anyway and nothing needs the host or a second
+    // stream between simulation steps
+    const bool hash = e->cfg.evaluator == OAZ_EVAL_HASH;
+    if (e->cfg.step_kernels == 0 && !noise && budget_ns <= 0 && !compact_leaves(e, t.G) && t.G <= (uint32_t)e->cus &&
+        (hash || e->cfg.precision == OAZ_FP32_SPLIT16) && tree_seg_kernels()) {
+        const NNView w = nn_view(e, nullptr);
+        TreeView tl = t;  // rows = game ids (no compaction arrays)
+        tl.need = nullptr;
+        tl.slot = nullptr;
+        e->times.parts = 1;
+        e->timing_skip = false;
+        if (int rc = timed(e, 6, t.G, [&] {
+                return launch_search_lat(tl, roots, active, prm, (int)sims, hash ? nullptr : &w, e->policy, e->value,
+                                         e->stream);
+            }))
+            return rc;
+        e->last_sims = sims;
+        return 0;
+    }
     const size_t slot_elems = (size_t)kNoiseChunk * t.G * kNoiseStride;
     const uint32_t nchunks = (sims + kNoiseChunk - 1) / kNoiseChunk;
     // The games in nh parts, each on its own stream: one part's tree kernels, leaf compaction and NN
@@ -1249,7 +1275,12 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
         }
         const uint32_t s0 = c * kNoiseChunk, s1 = s0 + kNoiseChunk < sims ? s0 + kNoiseChunk : sims;
         for (uint32_t s = s0; s < s1; ++s) {
-            if (budget_ns > 0 && s > 0) {  // Q7: is the budget spent after simulation s - 1?
+            // Q7: is the budget spent after simulation s - 1? This waits for every part's stream before
+            // each simulation step, so a budgeted search gives up the parts' overlap (and the root-noise
+            // producer runs ahead at most to the step being waited on) and is not the one-launch search:
+            // its throughput is not comparable with an unbudgeted run's (the reference's own cutoff is a
+            // clock read per playout, mcts_arena.rs:78). Parity runs and the benches leave it off.
+            if (budget_ns > 0 && s > 0) {
                 for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamSynchronize(sh[h]));
                 if (now_ns() - t_start >= budget_ns) {
                     out_of_time = true;
@@ -1313,8 +1344,8 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
 }
 
 // The trees of games [g0, g0 + n) as a view of their own: every per-game array offset by g0, the
-// part's compaction buckets from bucket counter b0 (its compacted rows start at g0; a part's last
-// tile may read up to 15 rows of the next part's, which it never stores).
+// part's compaction buckets from bucket counter b0 (its compacted rows start at g0; the NN's row loads
+// are clamped to the part's own n rows by the TileMap cap, run_sims).
 static TreeView slice_view(const TreeView& t, uint32_t g0, uint32_t n, int b0) {
     TreeView v = t;
     v.nodes = t.nodes + (size_t)g0 * t.cap;

@@ -132,6 +132,12 @@ hipError_t launch_backup_select(const TreeView& t, const oaz_state* roots, const
                                 const float* value, const float* noise, SearchParams p, hipStream_t st);
 hipError_t launch_search_finalize(const TreeView& t, const oaz_state* roots, oaz_move* out_move,
                                   float* out_pi, hipStream_t st);
+// false when OAZ_TREE_SEG=0 selected the one-game-per-wave tree kernels
+bool tree_seg_kernels();
+// All `sims` simulations of every game in one launch, one workgroup per game (oaz_search_lat.hip):
+// w = the fp16x3 network, or null for the HASH test evaluator; no root noise; rows = game ids.
+hipError_t launch_search_lat(const TreeView& t, const oaz_state* roots, const uint8_t* active, SearchParams p,
+                             int sims, const NNView* w, float* policy, float* value, hipStream_t st);
 hipError_t launch_selfplay_move(const TreeView& t, const SlotView& s, hipStream_t st);
 hipError_t launch_selfplay_reset(const TreeView& t, const SlotView& s, hipStream_t st);
 hipError_t launch_stats_reduce(const uint64_t* per_game, uint32_t G, uint64_t* out /* GS_COUNT */,

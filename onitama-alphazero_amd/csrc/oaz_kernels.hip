@@ -637,10 +637,11 @@ __device__ __forceinline__ int root_fold(int K, int Kmax, const NodeRegs (&ch)[3
 }
 
 // k_select with 16 lanes per game: lane sl holds children j = 16c + sl (c < 3, K <= 40).
+// g: this segment's game (>= t.G: an idle segment); leaf_lds: also store the leaf position there (LDS of
+// the one-launch search, whose network reads it without a global round trip), or null.
 __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_state* __restrict__ roots,
                                                 const uint8_t* __restrict__ active, const float* __restrict__ noise,
-                                                const SearchParams& prm) {
-    const uint32_t g = seg_game();
+                                                const SearchParams& prm, uint32_t g, oaz_state* leaf_lds = nullptr) {
     const int sl = seg_lane(), sb = seg_base();
     const bool on = g < t.G && !(active && active[g] != 1);
     const bool fold_mode = prm.train_noise && noise;
@@ -736,6 +737,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
     if (on && sl == 0) {
         const bool need = leaf_needs_eval(nd.misc, s);
         store_state(&t.leaf_state[g], s);
+        if (leaf_lds) *leaf_lds = s;
         t.leaf[g] = node;
         t.depth[g] = depth;
         if (t.need) t.need[g] = need;
@@ -760,7 +762,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OAZ_TREE_WPE)))
 k_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
              const float* __restrict__ noise, SearchParams prm) {
-    select_seg_body(t, roots, active, noise, prm);
+    select_seg_body(t, roots, active, noise, prm, seg_game());
 }
 
 template <int N>
@@ -783,11 +785,11 @@ __device__ __forceinline__ void policy_sums(const float (&polm)[4], double& sum0
 
 // k_expand_backup with 16 lanes per game: lane sl generates the moves of (card, from) combos
 // 4 sl .. 4 sl + 3 (combo = card * 25 + from, the reference order), one segment scan places them.
+// g: this segment's game (>= t.G: an idle segment); sp: 52 floats of LDS for the segment's policy row.
 __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const oaz_state* __restrict__ roots,
                                                       const uint8_t* __restrict__ active,
                                                       const float* __restrict__ policy,
-                                                      const float* __restrict__ value) {
-    const uint32_t g = seg_game();
+                                                      const float* __restrict__ value, uint32_t g, float* sp) {
     const int sl = seg_lane();
     if (g >= t.G) return;                  // whole segments (G is not a multiple of 4 only at the end)
     if (active && active[g] != 1) return;  // uniform over the segment
@@ -822,10 +824,8 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
     asm volatile("" ::"v"(polr[0]), "v"(polr[1]), "v"(polr[2]), "v"(polr[3]), "v"(vrow));  // issued in trip 2
 
     if (!(node_flags(nd.misc) & 3)) {
-        // the policy row kept in registers for the renormalisation sums and in LDS for the
+        // the policy row kept in registers for the renormalisation sums and in LDS (sp) for the
         // children's priors
-        __shared__ float spol[kWavesPerBlock * 4][52];
-        float* sp = spol[threadIdx.x >> 4];  // this segment's row
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const int idx = 16 * c + sl;
@@ -923,7 +923,8 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const 
                                                               const uint8_t* __restrict__ active,
                                                               const float* __restrict__ policy,
                                                               const float* __restrict__ value) {
-    expand_backup_seg_body(t, roots, active, policy, value);
+    __shared__ float spol[kWavesPerBlock * 4][52];
+    expand_backup_seg_body(t, roots, active, policy, value, seg_game(), spol[threadIdx.x >> 4]);
 }
 
 // Simulation s's expand/backup and simulation s+1's select of the same four games in one launch:
@@ -934,10 +935,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OAZ
 k_backup_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
                     const float* __restrict__ policy, const float* __restrict__ value, const float* __restrict__ noise,
                     SearchParams prm) {
-    expand_backup_seg_body(t, roots, active, policy, value);
+    __shared__ float spol[kWavesPerBlock * 4][52];
+    const uint32_t g = seg_game();
+    expand_backup_seg_body(t, roots, active, policy, value, g, spol[threadIdx.x >> 4]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    select_seg_body(t, roots, active, noise, prm);
+    select_seg_body(t, roots, active, noise, prm, g);
 }
 
 // calculate_priors (mcts_arena.rs:104-124) + best child (87-94) for every root.
@@ -1167,6 +1170,7 @@ static bool tree_seg() {
     static const bool v = !(getenv("OAZ_TREE_SEG") && getenv("OAZ_TREE_SEG")[0] == '0');
     return v;
 }
+bool tree_seg_kernels() { return tree_seg(); }
 hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                          const float* noise, SearchParams p, hipStream_t st) {
     if (tree_seg())

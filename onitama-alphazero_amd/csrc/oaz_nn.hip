@@ -1837,10 +1837,29 @@ __device__ __forceinline__ int h3s_boff(int sq, int t, int m, int kq) {
     return h3s::chunk_off(row, 4 * m + kq);
 }
 
+// Operands the one-launch search (k_search_lat) keeps resident in LDS across its simulations (loaded
+// once per launch, again after an fp16-range recompute, which uses the whole LDS): the first layer's
+// K blocks (block 0 and one block-1 per square class: [10][2 pieces][4 N-tiles][64 lanes] f16x8), its
+// bias and inverse scales, and the head parameters; and the leaf position, written there by the walk.
+namespace h3s {
+constexpr int kL1Off = kBytes;                      // after the body's own LDS
+constexpr int kL1Bytes = 10 * 2 * 4 * 64 * 16;      // 80 KB
+constexpr int kL1BiasOff = kL1Off + kL1Bytes;       // bias1[64], inv1[64]
+constexpr int kStateOff = kL1BiasOff + 2 * 64 * 4;  // the leaf position (24 B)
+constexpr int kResidentBytes = kStateOff + 32;
+}  // namespace h3s
+struct H3sResident {
+    const oaz_state* state;  // LDS: the position to evaluate (null: states[b])
+    const char* l1;          // LDS: kL1Bytes of first-layer fragments + bias / inverse scales (null: global)
+    bool heads;              // the head parameters are already in the body's LDS (no copy)
+};
+// opaque: 0, produced by an asm statement when the body sits in a loop (k_search_lat), so that the
+// lane-dependent offsets are computed where they are used instead of being hoisted out of the loop and
+// kept live through the convs (which then spill)
 template <class C>
 __device__ __forceinline__ bool nn_h3s_body(const oaz_state* __restrict__ states, int b, const float* __restrict__ blob,
                                             int blocks, float* __restrict__ policy, float* __restrict__ value,
-                                            float* lds) {
+                                            float* lds, int opaque = 0, H3sResident res = H3sResident{nullptr, nullptr, false}) {
     static_assert(!C::BF && C::WAVES == 8, "k_nn_h3s: fp16x3 mode, 8 waves");
     // DBG 2 (diagnostic build, timing only): per-wave s_memtime phase sums over the position's policy row:
     // 0 kernel start to the first conv (helpers: the first layer), 2 conv MFMA loops, 3 conv epilogues +
@@ -1860,7 +1879,7 @@ __device__ __forceinline__ bool nn_h3s_body(const oaz_state* __restrict__ states
     f32x4* const skipx = reinterpret_cast<f32x4*>(base + h3s::kSkipOff);
     float* const hl = reinterpret_cast<float*>(base + h3s::kHeadOff);  // the head parameters in LDS
     float* const feat = reinterpret_cast<float*>(base + h3s::kFeatOff);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = (int)threadIdx.x + opaque, wave = tid >> 6, lane = tid & 63;
     const bool compute = wave < 4;  // waves 0-3: the convs; 4-7: first layer, head parameters, head convs
     const int nt = wave & 3;
     const int i = lane & 15, kq = lane >> 4;
@@ -1896,23 +1915,38 @@ __device__ __forceinline__ bool nn_h3s_body(const oaz_state* __restrict__ states
             *reinterpret_cast<uint4*>(base + (tid >> 4) * h3s::kImageB + ((tid >> 3) & 1) * h3s::kPlaneB +
                                       h3s::kZero * h3s::kRowB + (tid & 7) * 16) = uint4{0u, 0u, 0u, 0u};
     } else {  // ---- helpers: the first layer (k_nn_h3's K blocks) for N-tile nt, both tiles; no barrier inside
-        const oaz_state st = states[b];
-        X6W A;
-        A.r = __builtin_amdgcn_make_buffer_rsrc((void*)l1c, (short)0, (int)(26 * h3::kL1Frag * 4), 0x00020000);
-        A.voff = (nt * 64 + lane) * 16;
-        auto ld = [&](int blk, int pc) {  // [blk][pc][nt][lane]
-            return __builtin_bit_cast(f16x8,
-                                      __builtin_amdgcn_raw_buffer_load_b128(A.r, A.voff, (blk * 2 + pc) * 4 * 64 * 16, 0));
-        };
-        const f16x8 a0h = ld(0, 0), a0l = ld(0, 1);
-        f16x8 a1[9][2];
+        const oaz_state st = res.state ? *res.state : states[b];
+        f16x8 a0h, a0l, a1[9][2];
+        f32x4 bias1t, inv1;
+        if (res.l1) {  // resident in LDS: [slot][pc][nt][lane], slot 0 = block 0, 1 + k = class k's block 1
+            const f16x8* L = reinterpret_cast<const f16x8*>(res.l1) + nt * 64 + lane;
+            a0h = L[0];
+            a0l = L[256];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) {  // every class occurs in one of the two tiles
-            a1[k][0] = ld(1 + c_cls_rep[k], 0);
-            a1[k][1] = ld(1 + c_cls_rep[k], 1);
+            for (int k = 0; k < 9; ++k) {
+                a1[k][0] = L[((1 + k) * 2 + 0) * 256];
+                a1[k][1] = L[((1 + k) * 2 + 1) * 256];
+            }
+            bias1t = *reinterpret_cast<const f32x4*>(res.l1 + h3s::kL1Bytes + cq * 4);
+            inv1 = *reinterpret_cast<const f32x4*>(res.l1 + h3s::kL1Bytes + 256 + cq * 4);
+        } else {
+            X6W A;
+            A.r = __builtin_amdgcn_make_buffer_rsrc((void*)l1c, (short)0, (int)(26 * h3::kL1Frag * 4), 0x00020000);
+            A.voff = (nt * 64 + lane) * 16;
+            auto ld = [&](int blk, int pc) {  // [blk][pc][nt][lane]
+                return __builtin_bit_cast(
+                    f16x8, __builtin_amdgcn_raw_buffer_load_b128(A.r, A.voff, (blk * 2 + pc) * 4 * 64 * 16, 0));
+            };
+            a0h = ld(0, 0);
+            a0l = ld(0, 1);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {  // every class occurs in one of the two tiles
+                a1[k][0] = ld(1 + c_cls_rep[k], 0);
+                a1[k][1] = ld(1 + c_cls_rep[k], 1);
+            }
+            bias1t = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
+            inv1 = *reinterpret_cast<const f32x4*>(l1c + 26 * h3::kL1Frag + cq);
         }
-        const f32x4 bias1t = *reinterpret_cast<const f32x4*>(blob + nn::kL1B + cq);
-        const f32x4 inv1 = *reinterpret_cast<const f32x4*>(l1c + 26 * h3::kL1Frag + cq);
         const uint32_t bb = kq == 0 ? st.pawns[0] : kq == 1 ? st.kings[0] : kq == 2 ? st.pawns[1] : st.kings[1];
         const int blue = st.to_move & 1;
         const int c0 = (blue ? st.cards[2] : st.cards[0]) & 15, c1 = (blue ? st.cards[3] : st.cards[1]) & 15;
@@ -1963,7 +1997,7 @@ __device__ __forceinline__ bool nn_h3s_body(const oaz_state* __restrict__ states
     }
     __syncthreads();  // the first layer's image and residual
     stamp(0);
-    if (!compute) {  // the head parameters into LDS during the first conv (no global round trip at the end)
+    if (!compute && !res.heads) {  // the head parameters into LDS during the first conv (no global round trip at the end)
         static_assert(h3s::kHeadF % 4 == 0, "float4 copy");
         const float4* src = reinterpret_cast<const float4*>(ph0);
         float4* dst = reinterpret_cast<float4*>(hl);
@@ -2033,6 +2067,7 @@ __device__ __forceinline__ bool nn_h3s_body(const oaz_state* __restrict__ states
         conv_one(std::integral_constant<int, 0>{}, true, img0, img1);
         conv_one(std::integral_constant<int, 1>{}, c + 1 < blocks, img1, img0);
     }
+    if (blocks == 0) __syncthreads();  // the head parameters' copy (no conv barrier in between)
     // heads (h3_heads' arithmetic, parameters from LDS): the 1x1 convs by waves 4, 5 with the image as A
     // (rows = squares), then heads_mm over all 8 waves
     {
@@ -2085,6 +2120,26 @@ __device__ __forceinline__ bool nn_h3s_body(const oaz_state* __restrict__ states
         if (lane < 6) policy[(size_t)b * 50 + wave * 6 + lane] = v;
     }
     return (hmax & 0xffffu) >= 0x7C00u || (hmax >> 16) >= 0x7C00u;  // an fp16 hi term overflowed
+}
+
+// The one-launch search's resident operands (H3sResident): all threads of the workgroup, then a barrier.
+__device__ __forceinline__ void h3s_load_resident(char* lds, const float* blob, int blocks) {
+    const float* l1c = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh) +
+                       nn::kValueF + nn::kPolicyF + h3::kHeadB;
+    const float* ph0 = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh);
+    const int tid = (int)threadIdx.x;
+    uint4* d = reinterpret_cast<uint4*>(lds + h3s::kL1Off);
+    for (int k = tid; k < h3s::kL1Bytes / 16; k += (int)blockDim.x) {  // [slot][pc][nt][lane]
+        const int slot = k / 512, rest = k % 512;
+        const int blk = slot == 0 ? 0 : 1 + c_cls_rep[slot - 1];
+        d[k] = reinterpret_cast<const uint4*>(l1c)[blk * 512 + rest];
+    }
+    float* bi = reinterpret_cast<float*>(lds + h3s::kL1BiasOff);
+    if (tid < 64) bi[tid] = blob[nn::kL1B + tid];
+    else if (tid < 128) bi[tid] = l1c[26 * h3::kL1Frag + tid - 64];
+    float4* hd = reinterpret_cast<float4*>(lds + h3s::kHeadOff);
+    for (int k = tid; k < h3s::kHeadF / 4; k += (int)blockDim.x) hd[k] = reinterpret_cast<const float4*>(ph0)[k];
+    __syncthreads();
 }
 
 template <class C>

@@ -263,6 +263,8 @@ extern "C" int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pur
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return oaz_set_err(OAZ_ERR_NO_DEVICE, "pure_mcts: no HIP device");
+    if (cfg->device < 0 || cfg->device >= ndev)
+        return oaz_set_err(OAZ_ERR_ARG, "pure_mcts: device %d of %d", cfg->device, ndev);
     for (int g = 0; g < G; ++g)
         if ((roots[g].to_move & ~1) || (roots[g].cards[0] | roots[g].cards[1] | roots[g].cards[2] | roots[g].cards[3] |
                                         roots[g].cards[4]) > 15)
@@ -285,24 +287,30 @@ extern "C" int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pur
         rc = oaz_set_err(OAZ_ERR_HIP, "pure_mcts: %s: %s", what, hipGetErrorString(e));
     };
     hipError_t e;
-    if ((e = hipMalloc(&d_roots, sizeof(oaz_state) * G)) != hipSuccess) fail(e, "alloc");
+    // on cfg->device, on a stream of its own: a search on a worker thread neither lands on the thread's
+    // default device nor waits for (or stalls) the engines searching on the same GPU meanwhile
+    hipStream_t sm = nullptr;
+    if ((e = hipSetDevice(cfg->device)) != hipSuccess) fail(e, "set device");
+    else if ((e = hipStreamCreateWithFlags(&sm, hipStreamNonBlocking)) != hipSuccess) fail(e, "stream");
+    else if ((e = hipMalloc(&d_roots, sizeof(oaz_state) * G)) != hipSuccess) fail(e, "alloc");
     else if ((e = hipMalloc(&d_ln, sizeof(float) * ln.size())) != hipSuccess) fail(e, "alloc");
     else if ((e = hipMalloc(&d_val, sizeof(float) * G)) != hipSuccess) fail(e, "alloc");
     else if ((e = hipMalloc(&d_mv, sizeof(oaz_move) * G)) != hipSuccess) fail(e, "alloc");
     else if ((e = hipMalloc(&d_st, sizeof(uint64_t) * 8 * G)) != hipSuccess) fail(e, "alloc");
     else if ((e = hipMalloc(&d_nodes, sizeof(oaz_pure_node) * cap * G)) != hipSuccess) fail(e, "alloc tree");
     if (!rc) {
-        (void)hipMemcpy(d_roots, roots, sizeof(oaz_state) * G, hipMemcpyHostToDevice);
-        (void)hipMemcpy(d_ln, ln.data(), sizeof(float) * ln.size(), hipMemcpyHostToDevice);
-        hipLaunchKernelGGL(pm::k_pure_mcts, dim3((G + 63) / 64), dim3(64), 0, 0, d_roots, G, p, d_ln, d_nodes, d_mv,
+        (void)hipMemcpyAsync(d_roots, roots, sizeof(oaz_state) * G, hipMemcpyHostToDevice, sm);
+        (void)hipMemcpyAsync(d_ln, ln.data(), sizeof(float) * ln.size(), hipMemcpyHostToDevice, sm);
+        hipLaunchKernelGGL(pm::k_pure_mcts, dim3((G + 63) / 64), dim3(64), 0, sm, d_roots, G, p, d_ln, d_nodes, d_mv,
                            d_val, d_st);
-        if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess) fail(e, "kernel");
+        if ((e = hipGetLastError()) != hipSuccess || (e = hipStreamSynchronize(sm)) != hipSuccess) fail(e, "kernel");
     }
     if (!rc) {
-        (void)hipMemcpy(out_move, d_mv, sizeof(oaz_move) * G, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(out_value, d_val, sizeof(float) * G, hipMemcpyDeviceToHost);
         std::vector<uint64_t> st((size_t)G * 8);
-        (void)hipMemcpy(st.data(), d_st, sizeof(uint64_t) * st.size(), hipMemcpyDeviceToHost);
+        (void)hipMemcpyAsync(out_move, d_mv, sizeof(oaz_move) * G, hipMemcpyDeviceToHost, sm);
+        (void)hipMemcpyAsync(out_value, d_val, sizeof(float) * G, hipMemcpyDeviceToHost, sm);
+        (void)hipMemcpyAsync(st.data(), d_st, sizeof(uint64_t) * st.size(), hipMemcpyDeviceToHost, sm);
+        if ((e = hipStreamSynchronize(sm)) != hipSuccess) fail(e, "copy");
         if (stats)
             for (int g = 0; g < G; ++g) {
                 stats->playouts += st[g * 8 + 0];
@@ -313,16 +321,20 @@ extern "C" int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pur
                 if (st[g * 8 + 5] > stats->max_nodes) stats->max_nodes = st[g * 8 + 5];
                 stats->tree_full += st[g * 8 + 6];
             }
-        if (tree_out && tree_cap)
+        if (tree_out && tree_cap) {
             for (int g = 0; g < G; ++g)
-                (void)hipMemcpy(tree_out + (size_t)g * tree_cap, d_nodes + (size_t)g * cap,
-                                sizeof(oaz_pure_node) * (tree_cap < cap ? tree_cap : cap), hipMemcpyDeviceToHost);
+                (void)hipMemcpyAsync(tree_out + (size_t)g * tree_cap, d_nodes + (size_t)g * cap,
+                                     sizeof(oaz_pure_node) * (tree_cap < cap ? tree_cap : cap), hipMemcpyDeviceToHost, sm);
+            if ((e = hipStreamSynchronize(sm)) != hipSuccess) fail(e, "tree copy");
+        }
     }
+    if (sm) (void)hipStreamSynchronize(sm);
     if (d_roots) (void)hipFree(d_roots);
     if (d_ln) (void)hipFree(d_ln);
     if (d_val) (void)hipFree(d_val);
     if (d_mv) (void)hipFree(d_mv);
     if (d_st) (void)hipFree(d_st);
     if (d_nodes) (void)hipFree(d_nodes);
+    if (sm) (void)hipStreamDestroy(sm);
     return rc;
 }

@@ -86,7 +86,8 @@ class oaz_config(C.Structure):
         ("compact", C.c_int32),
         ("parts", C.c_int32),
         ("search_time_ns", C.c_int64),
-        ("reserved", C.c_int32 * 2),
+        ("step_kernels", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 
@@ -162,7 +163,8 @@ class oaz_pure_mcts_config(C.Structure):
         ("rollout_cap", C.c_int32),
         ("seed", C.c_uint64),
         ("game_id0", C.c_uint64),
-        ("reserved", C.c_int32 * 4),
+        ("device", C.c_int32),
+        ("reserved", C.c_int32 * 3),
     ]
 
 

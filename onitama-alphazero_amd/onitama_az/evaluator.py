@@ -267,18 +267,28 @@ class Evaluator:  # evaluator.rs:139-193
                           *self.ratings[1]),
             lambda: fight(self.config, AlphaZeroAgent(cfg, models[3]),
                           Mcts(search_time=0.4, min_node_visits=5, exploration_c=1.41, max_playouts=sims,
-                               seed=self.config.seed), *self.ratings[2]),
+                               seed=self.config.seed, device=self.new.options.device), *self.ratings[2]),
         ]
+        owned = [[models[0], models[1]], [models[2]], [models[3]]]  # each fight's network copies
+
+        def release(ms):  # a fight's engines (the reference drops each fight's VarStores)
+            for m in ms:
+                eng = m.__dict__.get("_search", {}).get("engine")
+                if eng is not None:
+                    eng.close()
+
         try:
             if concurrent:
                 with ThreadPoolExecutor(max_workers=len(fights)) as pool:  # handles joined in order
                     self_fight, random_fight, mcts_fight = [f.result() for f in [pool.submit(f) for f in fights]]
-            else:
-                self_fight, random_fight, mcts_fight = [f() for f in fights]
+            else:  # one fight after the other, each fight's engines released when it ends
+                out = []
+                for f, ms in zip(fights, owned):
+                    out.append(f())
+                    release(ms)
+                self_fight, random_fight, mcts_fight = out
         finally:
-            for m in models:  # the copies' engines (the reference drops each fight's VarStores)
-                eng = m.__dict__.get("_search", {}).get("engine")
-                if eng is not None:
-                    eng.close()
+            for ms in owned:
+                release(ms)
         return (PitStatistics(self_fight, random_fight, mcts_fight),
                 self_fight.winrate > self.config.winrate_percent)

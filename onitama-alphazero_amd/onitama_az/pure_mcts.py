@@ -33,11 +33,12 @@ class PureSearchResult:
 
 def pure_mcts_search(roots: np.ndarray, max_playouts: int = 5000, min_node_visits: int = 5,
                      exploration_c: float = math.sqrt(2.0), seed: int = 20260101, game_id0: int = 0,
-                     rollout_cap: int = 1000, with_trees: bool = False) -> PureSearchResult:
+                     rollout_cap: int = 1000, with_trees: bool = False, device: int = 0) -> PureSearchResult:
     roots = np.ascontiguousarray(roots, dtype=_abi.STATE_DTYPE).reshape(-1)
     cfg = default_config()
     cfg.max_playouts, cfg.min_node_visits = int(max_playouts), int(min_node_visits)
     cfg.exploration_c, cfg.seed, cfg.game_id0, cfg.rollout_cap = float(exploration_c), seed, game_id0, rollout_cap
+    cfg.device = int(device)
     lib = _abi.load()
     G = len(roots)
     moves = np.zeros(G, dtype=_abi.MOVE_DTYPE)
@@ -57,6 +58,7 @@ class Mcts:  # ai/mcts/mod.rs:13-30 (search_time is not used: searches run exact
     exploration_c: float = math.sqrt(2.0)
     max_playouts: int = 5000
     seed: int = 20260101
+    device: int = 0  # the GPU the searches run on (common.rs Options.device)
 
     def __post_init__(self):
         self._calls = 0
@@ -72,12 +74,13 @@ class Mcts:  # ai/mcts/mod.rs:13-30 (search_time is not used: searches run exact
         # a fresh rollout stream per call (the reference draws from thread_rng)
         g0 = self._calls << 20
         self._calls += 1
-        return pure_mcts_search(roots, self.max_playouts, self.min_node_visits, self.exploration_c, self.seed, g0)
+        return pure_mcts_search(roots, self.max_playouts, self.min_node_visits, self.exploration_c, self.seed, g0,
+                                device=self.device)
 
     def reserve(self, n: int) -> None:
         pass
 
-    def device_key(self):  # a stateless GPU search (its own buffers per call): may run beside an engine's
+    def device_key(self):  # a stateless GPU search (its own buffers and stream per call): may run beside an engine's
         return ("pure_mcts", id(self))
 
     def name(self) -> str:

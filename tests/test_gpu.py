@@ -330,6 +330,42 @@ def test_search_nn_trees_bitexact_with_gpu_evaluator(orc, precision, compact, pa
             assert _mv(r.moves[g]) == _mv(mv)
 
 
+@pytest.mark.parametrize("evaluator", [_abi.EVAL_HASH, _abi.EVAL_NN])
+@pytest.mark.parametrize("games", [1, 5, 256])
+def test_one_launch_search_equals_step_launches(orc, evaluator, games):
+    """oaz_config.step_kernels: 0 (auto) runs a search of <= CU-count games with no root noise as ONE
+    launch (a workgroup per game runs all its simulations: oaz_search_lat.hip), 1 the per-simulation
+    launches. Every tree node, pi, move and search statistic is identical; with HASH both equal the
+    oracle's trees (mcts_arena.rs:75-177)."""
+    roots = random_positions(orc, games, seed=707 + games)
+    w = random_weights(5, 3)
+    sims = 60
+    out = {}
+    for sk in (0, 1):
+        with Engine(games=games, sims=sims, c_puct=5.0, train_noise=0, evaluator=evaluator, blocks=3,
+                    precision=_abi.FP32_SPLIT16, step_kernels=sk) as e:
+            if evaluator == _abi.EVAL_NN:
+                e.load_weights(w)
+            e.set_timing(1)
+            r = e.search(roots, root_value=True)
+            kt = e.kernel_times()
+            trees = [e.tree(g) for g in sorted({0, games // 2, games - 1})]
+            out[sk] = (r, trees, kt)
+    (r0, t0, k0), (r1, t1, k1) = out[0], out[1]
+    assert k0.backup_select_n == 1 and k0.nn_n == 1 and k0.select_n == 0  # one search launch (+ the root value)
+    assert k1.select_n == 1 and k1.backup_select_n == sims - 1
+    assert np.array_equal(r0.pi, r1.pi) and r0.moves.tobytes() == r1.moves.tobytes()
+    assert np.array_equal(r0.root_value, r1.root_value)
+    for f in ("sims", "expansions", "children", "terminal_leaves", "depth_sum", "stuck_leaves", "max_nodes", "nn_evals"):
+        assert getattr(r0.stats, f) == getattr(r1.stats, f), f
+    for a, b in zip(t0, t1):
+        assert a.tobytes() == b.tobytes()
+    if evaluator == _abi.EVAL_HASH:
+        for g in sorted({0, games // 2, games - 1})[:2]:
+            mv, pi, nodes, _ = orc.search(orc.search_cfg(sims=sims, c_puct=5.0, evaluator=orc.EVAL_HASH), roots[g])
+            assert np.array_equal(r0.pi[g].reshape(-1), pi.reshape(-1)) and _mv(r0.moves[g]) == _mv(mv)
+
+
 def test_search_with_root_noise_is_deterministic_and_consistent(orc):
     roots = random_positions(orc, 16, seed=707)
     kw = dict(games=16, sims=64, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=99)
