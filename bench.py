@@ -701,7 +701,7 @@ def single_stream_leg(args, cfg, device, precision):
     with Engine(device=device, games=cfg["games"], sims=cfg["sims"], blocks=cfg["blocks"], c_puct=5.0,
                 train_noise=0 if args.no_noise else 1, max_plies=150, evaluator=_abi.EVAL_NN,
                 precision=getattr(_abi, PREC_ABI[precision]), fixed_deck=cfg["fixed_deck"], deck=[0, 1, 2, 3, 4],
-                seed=20260101, sample_capacity=cfg["games"] * 8, parts=1, compact=0) as e:
+                seed=20260101, sample_capacity=cfg["games"] * 8, parts=1, compact=0, step_kernels=1) as e:
         e.load_weights(random_weights(0, cfg["blocks"]))
         e.selfplay_reset()
         e.selfplay_step(2)
@@ -1017,6 +1017,25 @@ def main():
             "checks": checks,
         }
     eng.close()
+    # Up to 16 x CU-count games (C2) the engine runs each 16-simulation noise chunk as ONE launch of
+    # k_search_grp (16 games per workgroup: tree walks, k_nn_h3's body, backups); its launches are then
+    # the timed region's dominant kernel (kernel class backup_select, every launch timed).
+    grp_mode = kt.select_n == 0 and kt.nn_n == 0 and kt.backup_select_n > 0
+    if rank == 0 and grp_mode:
+        own_sims = st1.search.sims - st0.search.sims
+        per_launch = own_sims / kt.backup_select_n
+        avg_ms = kt.backup_select_ms / kt.backup_select_n
+        flops = FLOP_PER_SIM[cfg["blocks"]] * per_launch
+        out["search_kernel"] = {
+            "kernel": "k_search_grp (16 games per workgroup: select -> k_nn_h3 body -> expand/backup for a "
+                      "16-simulation noise chunk per launch; oaz_search_lat.hip)",
+            "launches": kt.backup_select_n, "avg_launch_ms": avg_ms, "sims_per_launch": per_launch,
+            "achieved_TFLOPs": flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0}
+        for k in ("backup_select_fused", "nn"):
+            out["kernel_ms_per_step"].pop(k, None)
+        out["kernel_ms_per_step"]["search_grp"] = kt.backup_select_ms / args.steps
+        out.pop("nn_in_loop", None)
+        out.pop("tree_kernels", None)
     if rank == 0:
         # the dominant kernel's roofline, on one stream (single_stream_leg): per-launch HIP events
         leg = single_stream_leg(args, cfg, local, cfg["precision"])
@@ -1051,6 +1070,18 @@ def main():
                 clock_note="sclk = GRBM_GUI_ACTIVE/8 cycles per k_nn_ launch (rocprofv3 pass on this box, one stream) "
                            "/ the HIP-event launch time above; rocprof_avg_launch_ms = the same pass's kernel-trace "
                            "duration of those launches (profiled launches run at profiled_clock_mhz)")
+        if grp_mode:  # the timed region's own dominant kernel (k_search_grp); the NN kernel's leg stays beside it
+            sk = out["search_kernel"]
+            nn_leg = dict(out["roofline"])
+            out["roofline"] = {
+                "bound": "mfma", "kernel": sk["kernel"], "achieved": sk["achieved_TFLOPs"],
+                "peak": PEAK_TFLOPS[cfg["precision"]], "unit": "TFLOP/s",
+                "frac": sk["achieved_TFLOPs"] / PEAK_TFLOPS[cfg["precision"]],
+                "traffic": None, "flop_per_launch": FLOP_PER_SIM[cfg["blocks"]] * sk["sims_per_launch"],
+                "avg_launch_ms": sk["avg_launch_ms"], "launches": sk["launches"],
+                "measured_on": "the timed region: HIP events around every k_search_grp launch (each covers "
+                               "16 simulations of every game, tree work and noise waits included)",
+                "flop_accounting": "SURVEY 8d dense MACs x2 per sim", "nn_kernel_single_stream": nn_leg}
         bs = (out.get("tree_kernels") or {}).get("backup_select") or {}
         sq = (bs.get("pmc") or {}).get("sq")
         if leg.get("tree_launch_us"):

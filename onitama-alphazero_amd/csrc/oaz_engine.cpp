@@ -1210,11 +1210,16 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
     }
     const size_t slot_elems = (size_t)kNoiseChunk * t.G * kNoiseStride;
     const uint32_t nchunks = (sims + kNoiseChunk - 1) / kNoiseChunk;
+    // up to one round of 16-game workgroups (k_search_grp): one launch per noise chunk of simulations,
+    // each workgroup walking, evaluating and backing up its 16 games without a grid-wide step
+    const bool grp = e->cfg.step_kernels == 0 && budget_ns <= 0 && !compact_leaves(e, t.G) &&
+                     (t.G + 15) / 16 <= (uint32_t)e->cus && (hash || e->cfg.precision == OAZ_FP32_SPLIT16) &&
+                     tree_seg_kernels();
     // The games in nh parts, each on its own stream: one part's tree kernels, leaf compaction and NN
     // tail run in the gaps of the others' launches (the NN holds a whole CU per workgroup, so the
     // tree kernels cannot share a CU with it, only fill the CUs it leaves idle). The parts meet only
     // through the root-noise ring: chunk c + 2 overwrites chunk c's slot once every part is done with it.
-    const int nh = game_parts(e, t.G);
+    const int nh = grp ? 1 : game_parts(e, t.G);
     auto produce = [&](uint32_t c) -> int {
         if (c >= 2)
             for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[c & 1][h], 0));
@@ -1274,7 +1279,18 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
             for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(sh[h], e->ev_ready[c & 1], 0));
         }
         const uint32_t s0 = c * kNoiseChunk, s1 = s0 + kNoiseChunk < sims ? s0 + kNoiseChunk : sims;
-        for (uint32_t s = s0; s < s1; ++s) {
+        if (grp) {  // the chunk's simulations in one launch
+            const NNView w = nn_view(e, nullptr);
+            e->timing_skip = false;
+            const float* nz = noise ? e->noise + (c & 1) * slot_elems : nullptr;
+            if (int rc = timed(e, 6, t.G * (s1 - s0), [&] {
+                    return launch_search_grp(tv[0], roots, active, prm, (int)s0, (int)s1, nz, hash ? nullptr : &w,
+                                             e->policy, e->value, sh[0]);
+                }, sh[0]))
+                return rc;
+            e->last_sims = s1;
+        }
+        for (uint32_t s = grp ? s1 : s0; s < s1; ++s) {
             // Q7: is the budget spent after simulation s - 1? This waits for every part's stream before
             // each simulation step, so a budgeted search gives up the parts' overlap (and the root-noise
             // producer runs ahead at most to the step being waited on) and is not the one-launch search:

@@ -138,6 +138,11 @@ bool tree_seg_kernels();
 // w = the fp16x3 network, or null for the HASH test evaluator; no root noise; rows = game ids.
 hipError_t launch_search_lat(const TreeView& t, const oaz_state* roots, const uint8_t* active, SearchParams p,
                              int sims, const NNView* w, float* policy, float* value, hipStream_t st);
+// Simulations [s0, s1) of every game, 16 games per workgroup, in one launch (oaz_search_lat.hip): noise =
+// the ring chunk holding simulation s0's draws ([s1 - s0][G][kNoiseStride]) or null; w as above. The
+// last simulation's expand / backup is the caller's (launch_expand_backup).
+hipError_t launch_search_grp(const TreeView& t, const oaz_state* roots, const uint8_t* active, SearchParams p, int s0,
+                             int s1, const float* noise, const NNView* w, float* policy, float* value, hipStream_t st);
 hipError_t launch_selfplay_move(const TreeView& t, const SlotView& s, hipStream_t st);
 hipError_t launch_selfplay_reset(const TreeView& t, const SlotView& s, hipStream_t st);
 hipError_t launch_stats_reduce(const uint64_t* per_game, uint32_t G, uint64_t* out /* GS_COUNT */,

@@ -476,9 +476,10 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup(TreeView t, const oaz_
         }
         if (l == 0) {
             t.n_nodes[g] = base + K;
-            T[leaf].first = base;
-            T[leaf].nch = (uint8_t)K;
-            T[leaf].flags = 1;
+            oaz_node* lp = &T[leaf];
+            lp->first = base;
+            lp->nch = (uint8_t)K;
+            lp->flags = 1;
             st[GS_EXPANSIONS] += 1;
             st[GS_CHILDREN] += K;
             if (base + K > st[GS_MAXNODES]) st[GS_MAXNODES] = base + K;
@@ -568,10 +569,8 @@ __device__ __forceinline__ T pick3(int c, const T& a, const T& b, const T& d) {
 
 // Per-game statistics from the segmented tree kernels: relaxed atomics whose result is unused
 // (no-return global atomics), so the update costs no load round trip at the end of a walk; each game's
-// counters have one writer at a time, the atomic form only drops the read.
-#ifndef OAZ_STAT_ATOMICS
-#define OAZ_STAT_ATOMICS 1
-#endif
+// counters have one writer at a time, the atomic form only drops the read. A walk's (and an expansion's)
+// counters go out as one vector atomic over a few lanes: one write request per game and kernel.
 __device__ __forceinline__ void stat_add(uint64_t* p, uint64_t v) {
     (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -637,11 +636,25 @@ __device__ __forceinline__ int root_fold(int K, int Kmax, const NodeRegs (&ch)[3
 }
 
 // k_select with 16 lanes per game: lane sl holds children j = 16c + sl (c < 3, K <= 40).
+// Where node i of a game's tree lives: its slot of t.nodes (the per-step kernels), or, in the one-launch
+// search (oaz_search_lat.hip), LDS for the first n nodes of the workgroup's one game (the top of the tree,
+// allocated first) and t.nodes beyond. Generic pointers: the same loads and stores reach either.
+struct NodesGlobal {
+    __device__ __forceinline__ oaz_node* at(oaz_node* T, uint32_t i) const { return T + i; }
+};
+struct NodesCached {
+    oaz_node* L;  // LDS: nodes [0, n)
+    uint32_t n;
+    __device__ __forceinline__ oaz_node* at(oaz_node* T, uint32_t i) const { return i < n ? L + i : T + i; }
+};
+
 // g: this segment's game (>= t.G: an idle segment); leaf_lds: also store the leaf position there (LDS of
 // the one-launch search, whose network reads it without a global round trip), or null.
+template <class NA = NodesGlobal>
 __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_state* __restrict__ roots,
                                                 const uint8_t* __restrict__ active, const float* __restrict__ noise,
-                                                const SearchParams& prm, uint32_t g, oaz_state* leaf_lds = nullptr) {
+                                                const SearchParams& prm, uint32_t g, oaz_state* leaf_lds = nullptr,
+                                                const NA& na = NA{}) {
     const int sl = seg_lane(), sb = seg_base();
     const bool on = g < t.G && !(active && active[g] != 1);
     const bool fold_mode = prm.train_noise && noise;
@@ -649,9 +662,11 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
     uint32_t* path = t.path + (size_t)(on ? g : 0) * t.pathcap;
     oaz_state s = load_state(&roots[on ? g : 0]);
     int color = s.to_move & 1;
-    NodeRegs nd = load_node(&T[0]);
+    NodeRegs nd = load_node(na.at(T, 0));
     uint32_t node = 0, depth = 0;
-    if (on && sl == 0) path[0] = 0;
+    // the path entries of depths 0..15 are held by segment lanes 0..15 (lane d: the node at depth d) and
+    // written with one store when the walk ends; deeper ones (rare) are written as the walk reaches them
+    uint32_t pathv = 0;
     bool stuck = false;
     bool go = on && (node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2);
     while (__builtin_amdgcn_read_exec() && __ballot(go)) {  // some segment is still walking
@@ -671,7 +686,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
             ch[c].N = 0;
             ch[c].first = 0;
             ch[c].misc = 0;
-            if (go && j < K) ch[c] = load_node(&T[nd.first + j]);
+            if (go && j < K) ch[c] = load_node(na.at(T, nd.first + j));
         }
         const double sqn = go ? t.sqrt_tab[nd.N] : 0.0;
         int best = 0;
@@ -724,35 +739,32 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
             color ^= 1;  // game_state.player_color.switch()
             if (is_win(res)) {
                 c.misc |= 2u << 24;
-                if (sl == 0) *flags_ptr(&T[cidx]) = (uint8_t)(node_flags(c.misc));
+                if (sl == 0) *flags_ptr(na.at(T, cidx)) = (uint8_t)(node_flags(c.misc));
             }
             ++depth;
-            if (sl == 0 && depth < t.pathcap) path[depth] = cidx;
+            if ((uint32_t)sl == depth) pathv = cidx;
+            else if (sl == 0 && depth >= (uint32_t)kSegLanes && depth < t.pathcap) path[depth] = cidx;
             node = cidx;
             nd = c;
             go = (node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2);
         }
     }
     s.to_move = (uint8_t)color;
-    if (on && sl == 0) {
+    if (on && (uint32_t)sl <= depth && (uint32_t)sl < t.pathcap) path[sl] = pathv;  // one store: depths 0..15
+    if (on && sl < 4) {
+        // the walk's statistics as ONE vector atomic (lane k: field k of SIMS, DEPTH, EVALS, STUCK) instead of
+        // four single-lane ones: one write request to the game's counters
         const bool need = leaf_needs_eval(nd.misc, s);
-        store_state(&t.leaf_state[g], s);
-        if (leaf_lds) *leaf_lds = s;
-        t.leaf[g] = node;
-        t.depth[g] = depth;
-        if (t.need) t.need[g] = need;
-        uint64_t* st = t.stats + (size_t)g * GS_COUNT;
-#if OAZ_STAT_ATOMICS
-        stat_add(&st[GS_SIMS], 1);
-        stat_add(&st[GS_DEPTH], depth);
-        stat_add(&st[GS_EVALS], need);
-        if (stuck) stat_add(&st[GS_STUCK], 1);
-#else
-        st[GS_SIMS] += 1;
-        st[GS_DEPTH] += depth;
-        st[GS_EVALS] += need;
-        if (stuck) st[GS_STUCK] += 1;
-#endif
+        const uint64_t v = sl == 0 ? 1u : sl == 1 ? (uint64_t)depth : sl == 2 ? (uint64_t)need : (uint64_t)stuck;
+        const int f = sl == 0 ? GS_SIMS : sl == 1 ? GS_DEPTH : sl == 2 ? GS_EVALS : GS_STUCK;  // one 128-B block
+        if (v) stat_add(t.stats + (size_t)g * GS_COUNT + f, v);
+        if (sl == 0) {
+            store_state(&t.leaf_state[g], s);
+            if (leaf_lds) *leaf_lds = s;
+            t.leaf[g] = node;
+            t.depth[g] = depth;
+            if (t.need) t.need[g] = need;
+        }
     } else if (!on && g < t.G && sl == 0 && t.need) {
         t.need[g] = 0;  // an idle slot: nothing to evaluate
     }
@@ -786,10 +798,12 @@ __device__ __forceinline__ void policy_sums(const float (&polm)[4], double& sum0
 // k_expand_backup with 16 lanes per game: lane sl generates the moves of (card, from) combos
 // 4 sl .. 4 sl + 3 (combo = card * 25 + from, the reference order), one segment scan places them.
 // g: this segment's game (>= t.G: an idle segment); sp: 52 floats of LDS for the segment's policy row.
+template <class NA = NodesGlobal>
 __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const oaz_state* __restrict__ roots,
                                                       const uint8_t* __restrict__ active,
                                                       const float* __restrict__ policy,
-                                                      const float* __restrict__ value, uint32_t g, float* sp) {
+                                                      const float* __restrict__ value, uint32_t g, float* sp,
+                                                      const NA& na = NA{}) {
     const int sl = seg_lane();
     if (g >= t.G) return;                  // whole segments (G is not a multiple of 4 only at the end)
     if (active && active[g] != 1) return;  // uniform over the segment
@@ -803,7 +817,7 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
     const uint32_t row = t.slot ? t.slot[g] : g;  // the leaf's evaluation row
     const uint32_t pn = (uint32_t)sl < t.pathcap ? path[sl] : 0u;
     const uint32_t nn0 = t.n_nodes[g];
-    const NodeRegs nd = load_node(&T[leaf]);
+    const NodeRegs nd = load_node(na.at(T, leaf));
     uint64_t* st = t.stats + (size_t)g * GS_COUNT;
     const float* pol = policy + (size_t)row * 50;
     float polr[4];  // lane sl: policy entries sl, 16+sl, 32+sl, 48+sl
@@ -818,11 +832,12 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
     uint32_t pN = 0;
     double pW = 0.0;
     if (mine) {
-        pN = T[pn].N;
-        pW = T[pn].W;
+        pN = na.at(T, pn)->N;
+        pW = na.at(T, pn)->W;
     }
     asm volatile("" ::"v"(polr[0]), "v"(polr[1]), "v"(polr[2]), "v"(polr[3]), "v"(vrow));  // issued in trip 2
 
+    uint32_t expanded = 0xFFFFFFFFu;  // children created by this expansion (none: all ones)
     if (!(node_flags(nd.misc) & 3)) {
         // the policy row kept in registers for the renormalisation sums and in LDS (sp) for the
         // children's priors
@@ -872,50 +887,49 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
                 mm &= ~sq_bit(to);
                 double p = (double)sp[k * 25 + to];
                 if (rs > 0.0) p = p / rs;
-                store_fresh_node(&T[base + o], p, pack_move(from, to, slot, piece));
+                store_fresh_node(na.at(T, base + o), p, pack_move(from, to, slot, piece));
                 ++o;
             }
         }
         if (sl == 0) {
             t.n_nodes[g] = base + K;
-            T[leaf].first = base;
-            T[leaf].nch = (uint8_t)K;
-            T[leaf].flags = 1;
-#if OAZ_STAT_ATOMICS
-            stat_add(&st[GS_EXPANSIONS], 1);
-            stat_add(&st[GS_CHILDREN], K);
+            // the leaf's header in two words: first, then mv | nch << 16 | flags << 24 (flags: expanded;
+            // the leaf was neither expanded nor terminal, mcts_arena.rs:159-161, 231-260)
+            oaz_node* lp = na.at(T, leaf);
+            lp->first = base;
+            *reinterpret_cast<uint32_t*>(&lp->mv) = (nd.misc & 0xFFFFu) | (K << 16) | (1u << 24);
             stat_max(&st[GS_MAXNODES], base + K);
-#else
-            st[GS_EXPANSIONS] += 1;
-            st[GS_CHILDREN] += K;
-            if (base + K > st[GS_MAXNODES]) st[GS_MAXNODES] = base + K;
-#endif
         }
+        expanded = K;
     }
     const int res = current_state(s);
+    const bool won = is_win(res);
     double r;
-    if (is_win(res)) {
+    if (won) {
         const int root_color = roots[g].to_move & 1;
         const int pc = depth == 0 ? root_color : (root_color ^ (int)((depth - 1) & 1));
         r = reward(res, pc);
-#if OAZ_STAT_ATOMICS
-        if (sl == 0) stat_add(&st[GS_TERMINAL], 1);
-#else
-        if (sl == 0) st[GS_TERMINAL] += 1;
-#endif
     } else {
         r = (double)vrow;
     }
+    if (sl < 3) {  // the expansion's statistics as one vector atomic (lanes 0-2: EXPANSIONS, CHILDREN, TERMINAL)
+        const uint64_t v = sl == 0 ? (expanded != 0xFFFFFFFFu ? 1u : 0u) : sl == 1 ? (expanded != 0xFFFFFFFFu ? expanded : 0u)
+                                                                                   : (uint64_t)won;
+        const int f = sl == 0 ? GS_EXPANSIONS : sl == 1 ? GS_CHILDREN : GS_TERMINAL;
+        if (v) stat_add(&st[f], v);
+    }
     if (mine) {
         const double rk = ((depth - (uint32_t)sl) & 1) ? -r : r;
-        T[pn].N = pN + 1;
-        T[pn].W = pW + rk;
+        oaz_node* pp = na.at(T, pn);
+        pp->N = pN + 1;
+        pp->W = pW + rk;
     }
     for (uint32_t k = (uint32_t)sl + kSegLanes; k <= plen; k += kSegLanes) {  // paths deeper than 16
         const uint32_t n = path[k];
         const double rk = ((depth - k) & 1) ? -r : r;
-        T[n].N += 1;
-        T[n].W += rk;
+        oaz_node* np = na.at(T, n);
+        np->N += 1;
+        np->W += rk;
     }
 }
 

@@ -1544,14 +1544,16 @@ __device__ __forceinline__ void h3_heads(const float* p, char* img, const int (&
 // The whole forward for the waves of square group GRP. Returns true in a lane that split an
 // activation beyond the fp16 range (an fp16 hi term that overflowed, or would have): the tile's
 // results are then invalid and k_nn_h3 recomputes them.
+// opaque: 0; from an asm statement when the body sits in a loop (k_search_grp), so that its lane offsets
+// are not hoisted out of the loop (see nn_h3s_body)
 template <class C, int GRP>
 __device__ __forceinline__ bool nn_h3_body(const oaz_state* __restrict__ states, const TileSpan sp,
                                            const float* __restrict__ blob, int blocks, float* __restrict__ policy,
-                                           float* __restrict__ value, float* lds) {
+                                           float* __restrict__ value, float* lds, int opaque = 0) {
     const int B = sp.end;
     constexpr int NS = C::NS;
     char* img = reinterpret_cast<char*>(lds);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = (int)threadIdx.x + opaque, wave = tid >> 6, lane = tid & 63;
     const int nt = wave & 3;
     const int b0 = sp.b0;
     // (bf16 mode with two image buffers: one piece plane each, so the image area is kImageB as well)

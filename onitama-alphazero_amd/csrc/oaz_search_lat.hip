@@ -22,18 +22,64 @@ namespace oaz {
 
 constexpr int kLatThreads = 512;  // 8 waves: k_nn_h3s's geometry; wave 4 also walks the tree
 
+// LDS of k_search_lat beside the network's (h3s::kBytes): the walker's per-game records (leaf position,
+// leaf, depth, node count), its path, and the top of the game's tree (nodes [0, kLatCache): the root and
+// the first expansions, which every walk passes through).
+constexpr int kLatStateOff = h3s::kBytes;          // oaz_state
+constexpr int kLatVarsOff = kLatStateOff + 32;     // leaf, depth, n_nodes
+constexpr int kLatPathOff = kLatVarsOff + 16;
+constexpr int kLatPath = 2048;                     // path entries held in LDS (pathcap = sims + 1)
+constexpr int kLatCacheOff = (kLatPathOff + kLatPath * 4 + 31) & ~31;
+constexpr int kLatLds = H3Fallback<H3Cfg<0>>::kLds * 4;
+constexpr uint32_t kLatCache = (uint32_t)((kLatLds - kLatCacheOff) / (int)sizeof(oaz_node));
+
 // The tree walk (wave 4 only) as calls of their own: the walk needs ~80 VGPRs, the network ~240 (the
 // compute waves hold a conv's weights), and inlined into one loop the two allocations spill; a call
 // per simulation costs a few register saves.
 __device__ __noinline__ void lat_backup(const TreeView& t, const oaz_state* roots, const uint8_t* active,
-                                        const float* policy, const float* value, uint32_t gs, float* sp) {
-    expand_backup_seg_body(t, roots, active, policy, value, gs, sp);
+                                        const float* policy, const float* value, uint32_t gs, float* sp,
+                                        const NodesCached& na) {
+    expand_backup_seg_body(t, roots, active, policy, value, gs, sp, na);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 __device__ __noinline__ void lat_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
-                                        const SearchParams& prm, uint32_t gs, oaz_state* leaf_lds) {
-    select_seg_body(t, roots, active, nullptr, prm, gs, leaf_lds);
+                                        const SearchParams& prm, uint32_t gs, const NodesCached& na) {
+    select_seg_body(t, roots, active, nullptr, prm, gs, nullptr, na);
+}
+
+// Copies the LDS-held tree state of the game to its global slots (out = true) or back (out = false):
+// before the fp16-range recompute (which uses the whole LDS) and, for the nodes and the node count, at
+// the end. All threads of the workgroup; the caller places the barriers.
+__device__ __forceinline__ void lat_sync_tree(const TreeView& tl, const TreeView& tg, uint32_t ncached, bool path_lds,
+                                              bool out) {
+    const int tid = (int)threadIdx.x;
+    const uint32_t nn = out ? *tl.n_nodes : *tg.n_nodes;
+    const uint32_t nc = nn < ncached ? nn : ncached;
+    uint4* lq = reinterpret_cast<uint4*>(tl.nodes);
+    uint4* gq = reinterpret_cast<uint4*>(tg.nodes);
+    for (uint32_t k = (uint32_t)tid; k < 2 * nc; k += blockDim.x) {
+        if (out) gq[k] = lq[k];
+        else lq[k] = gq[k];
+    }
+    if (path_lds)
+        for (uint32_t k = (uint32_t)tid; k < tg.pathcap; k += blockDim.x) {
+            if (out) tg.path[k] = tl.path[k];
+            else tl.path[k] = tg.path[k];
+        }
+    if (tid == 0) {
+        if (out) {
+            *tg.n_nodes = *tl.n_nodes;
+            *tg.leaf = *tl.leaf;
+            *tg.depth = *tl.depth;
+            *tg.leaf_state = *tl.leaf_state;
+        } else {
+            *tl.n_nodes = *tg.n_nodes;
+            *tl.leaf = *tg.leaf;
+            *tl.depth = *tg.depth;
+            *tl.leaf_state = *tg.leaf_state;
+        }
+    }
 }
 
 __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oaz_state* __restrict__ roots,
@@ -44,30 +90,60 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
                                                             float* value) {
     using C = H3Cfg<0>;
     __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
+    static_assert(kLatCacheOff + 64 * (int)sizeof(oaz_node) <= kLatLds, "k_search_lat LDS");
     const uint32_t g = blockIdx.x;
     if (g >= t.G || (active && active[g] != 1)) return;  // uniform over the workgroup
     const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
     const bool walker = wave == 4;
-    const uint32_t gs = walker && lane < 16 ? g : t.G;  // segments 1-3 of wave 4 idle (game >= G)
+    char* const lb = reinterpret_cast<char*>(lds);
+    // the game's slice of the tree arrays (one game: index 0), and the same with the per-game records,
+    // the path and the top of the tree in LDS
+    TreeView tg = t;
+    tg.nodes = t.nodes + (size_t)g * t.cap;
+    tg.n_nodes = t.n_nodes + g;
+    tg.path = t.path + (size_t)g * t.pathcap;
+    tg.depth = t.depth + g;
+    tg.leaf = t.leaf + g;
+    tg.leaf_state = t.leaf_state + g;
+    tg.stats = t.stats + (size_t)g * GS_COUNT;
+    tg.need = nullptr;
+    tg.slot = nullptr;
+    tg.G = 1;
+    const bool path_lds = t.pathcap <= (uint32_t)kLatPath;
+    TreeView tl = tg;
+    tl.leaf_state = reinterpret_cast<oaz_state*>(lb + kLatStateOff);
+    tl.leaf = reinterpret_cast<uint32_t*>(lb + kLatVarsOff);
+    tl.depth = tl.leaf + 1;
+    tl.n_nodes = tl.leaf + 2;
+    if (path_lds) tl.path = reinterpret_cast<uint32_t*>(lb + kLatPathOff);
+    tl.nodes = reinterpret_cast<oaz_node*>(lb + kLatCacheOff);
+    const uint32_t ncached = kLatCache < t.cap ? kLatCache : t.cap;
+    const NodesCached na{tl.nodes, ncached};
+    const oaz_state* rg = roots + g;
+    const uint8_t* ag = active ? active + g : nullptr;
+    const uint32_t gs = walker && lane < 16 ? 0u : 1u;  // the walker's segment 0 holds the game
     // the segment's policy row for expand: LDS the network rebuilds in every evaluation anyway
     float* const sp = lds + (threadIdx.x >> 4) * 52;
-    char* const lb = reinterpret_cast<char*>(lds);
-    static_assert(h3s::kResidentBytes <= H3Fallback<C>::kLds * 4, "k_search_lat LDS");
-    oaz_state* const leaf_lds = reinterpret_cast<oaz_state*>(lb + h3s::kStateOff);
-    bool resident = false;  // the network's resident operands are in LDS (H3sResident)
+    lat_sync_tree(tl, tg, ncached, path_lds, false);  // the root (k_tree_reset) and the node count
+    __syncthreads();
+    bool resident = false;  // the network's head parameters are in LDS (H3sResident)
     for (int s = 0; s < sims; ++s) {
         if (!hash_eval && !resident) {  // at the start, and after an fp16-range recompute used the whole LDS
-            h3s_load_resident(lb, blob, blocks);
+            const float* ph0 = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh);
+            float4* hd = reinterpret_cast<float4*>(lb + h3s::kHeadOff);
+            for (int k = (int)threadIdx.x; k < h3s::kHeadF / 4; k += kLatThreads)
+                hd[k] = reinterpret_cast<const float4*>(ph0)[k];
+            __syncthreads();
             resident = true;
         }
         if (walker) {
-            if (s > 0) lat_backup(t, roots, active, policy, value, gs, sp);  // simulation s - 1's expand / back up
-            lat_select(t, roots, active, prm, gs, leaf_lds);
+            if (s > 0) lat_backup(tl, rg, ag, policy + (size_t)g * 50, value + g, gs, sp, na);  // simulation s - 1's
+            lat_select(tl, rg, ag, prm, gs, na);
         }
-        __syncthreads();  // the leaf position of simulation s is in t.leaf_state[g] and in LDS
+        __syncthreads();  // the leaf position of simulation s is in LDS
         if (hash_eval) {
             if (threadIdx.x < 64) {
-                const oaz_state st = load_state(&t.leaf_state[g]);
+                const oaz_state st = *tl.leaf_state;
                 const uint64_t h = hash_state(st);
                 if (lane < 50) policy[(size_t)g * 50 + lane] = hash_policy(h, lane);
                 if (lane == 0) value[g] = hash_value(h);
@@ -76,9 +152,11 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
             int opaque;  // 0, opaque to the compiler: no lane offset of the body is hoisted out of this loop
             asm volatile("v_mov_b32 %0, 0" : "=v"(opaque));
             const bool ovf = nn_h3s_body<C>(t.leaf_state, (int)g, blob, blocks, policy, value, lds, opaque,
-                                            H3sResident{leaf_lds, lb + h3s::kL1Off, true});
-            if (__syncthreads_or(ovf)) {  // k_nn_h3s's recompute of this position (the k_nn_x6 body)
-                resident = false;
+                                            H3sResident{tl.leaf_state, nullptr, true});
+            if (__syncthreads_or(ovf)) {  // k_nn_h3s's recompute of this position (the k_nn_x6 body), which
+                                          // needs the whole LDS: the tree state goes out and comes back
+                lat_sync_tree(tl, tg, ncached, path_lds, true);
+                __syncthreads();
                 using X = typename H3Fallback<C>::X;
                 const TileSpan span{(int)g, (int)g + 1, (int)t.G};
                 if ((threadIdx.x >> 8) == 0)
@@ -86,11 +164,102 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
                 else
                     nn_h3_fallback<X, X::GRP1>(t.leaf_state, span, xblob, blocks, policy, value, lds);
                 if (threadIdx.x == 0) atomicAdd(fallback, 1ull);
+                __syncthreads();
+                lat_sync_tree(tl, tg, ncached, path_lds, false);
+                resident = false;
             }
         }
         __syncthreads();  // policy / value row g written; the network's LDS is free for the tree again
     }
-    if (walker) lat_backup(t, roots, active, policy, value, gs, sp);  // the last simulation's
+    if (walker) lat_backup(tl, rg, ag, policy + (size_t)g * 50, value + g, gs, sp, na);  // the last simulation's
+    __syncthreads();
+    lat_sync_tree(tl, tg, ncached, path_lds, true);  // the tree's top and the node count to global memory
+}
+
+// ---- one launch per noise chunk for up to 16 x CU-count games (k_search_grp) ---------------------------
+// The per-step loop's trouble at a few thousand games (BASELINE C2: 4 096) is that a simulation step is
+// one round of 16-position NN workgroups that does not fill the CUs (two game parts on two streams
+// half-fill them each), and every step waits for the slowest game's tree walk across the grid. Here a
+// workgroup owns 16 games for a chunk of simulations: waves 0-3 walk the 16 trees (one 16-lane segment
+// per game, the segmented kernels' bodies), then all 8 waves evaluate the 16 leaves with k_nn_h3's body
+// (16-position square-major tile, its fp16-range recompute), then the backups; no grid-wide step, no
+// launch per simulation. Root noise comes from the same ring k_root_noise fills per chunk of
+// simulations on the second stream. Results are bit-identical to the per-step launches.
+__device__ __noinline__ void grp_backup(const TreeView& t, const oaz_state* roots, const uint8_t* active,
+                                        const float* policy, const float* value, uint32_t gs, float* sp) {
+    expand_backup_seg_body(t, roots, active, policy, value, gs, sp);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __noinline__ void grp_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
+                                        const float* noise, const SearchParams& prm, uint32_t gs) {
+    select_seg_body(t, roots, active, noise, prm, gs);
+}
+
+template <class C>
+__global__ void __launch_bounds__(kLatThreads) k_search_grp(TreeView t, const oaz_state* __restrict__ roots,
+                                                            const uint8_t* __restrict__ active, SearchParams prm,
+                                                            int s0, int s1, const float* __restrict__ noise,
+                                                            int hash_eval, const float* __restrict__ blob, int blocks,
+                                                            const float* __restrict__ xblob,
+                                                            unsigned long long* __restrict__ fallback, float* policy,
+                                                            float* value) {
+    __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
+    const int b0 = (int)blockIdx.x * nn::kSB;
+    const int tid = (int)threadIdx.x, wave = tid >> 6;
+    const bool walker = wave < 4;  // waves 0-3: four games each (segments)
+    const uint32_t gs = walker ? (uint32_t)b0 + (uint32_t)(wave * 4 + ((tid >> 4) & 3)) : t.G;  // >= G: idle
+    float* const sp = lds + (tid >> 4) * 52;  // the segment's policy row (the network's LDS, free meanwhile)
+    const TileSpan span{b0, b0 + nn::kSB < (int)t.G ? b0 + nn::kSB : (int)t.G, (int)t.G};
+    for (int s = s0; s < s1; ++s) {
+        if (walker) {
+            if (s > 0) grp_backup(t, roots, active, policy, value, gs, sp);  // simulation s - 1's expand / back up
+            grp_select(t, roots, active, noise ? noise + (size_t)(s - s0) * t.G * kNoiseStride : nullptr, prm, gs);
+        }
+        __syncthreads();  // the 16 leaf positions of simulation s
+        if (hash_eval) {
+            for (int k = tid; k < nn::kSB * 50; k += kLatThreads) {
+                const int gi = b0 + k / 50, e = k % 50;
+                if (gi < (int)t.G) {
+                    const uint64_t h = hash_state(load_state(&t.leaf_state[gi]));
+                    policy[(size_t)gi * 50 + e] = hash_policy(h, e);
+                    if (e == 0) value[gi] = hash_value(h);
+                }
+            }
+        } else {
+            int opaque;  // 0, opaque to the compiler: no lane offset of the body is hoisted out of this loop
+            asm volatile("v_mov_b32 %0, 0" : "=v"(opaque));
+            bool ovf;
+            if ((tid >> 8) == 0) {
+                __builtin_amdgcn_s_setprio(1);
+                ovf = nn_h3_body<C, C::GRP0>(t.leaf_state, span, blob, blocks, policy, value, lds, opaque);
+            } else {
+                ovf = nn_h3_body<C, C::GRP1>(t.leaf_state, span, blob, blocks, policy, value, lds, opaque);
+            }
+            if constexpr (H3Fallback<C>::kOn) {
+                using X = typename H3Fallback<C>::X;
+                if (__syncthreads_or(ovf)) {
+                    if ((tid >> 8) == 0)
+                        nn_h3_fallback<X, X::GRP0>(t.leaf_state, span, xblob, blocks, policy, value, lds);
+                    else
+                        nn_h3_fallback<X, X::GRP1>(t.leaf_state, span, xblob, blocks, policy, value, lds);
+                    if (tid == 0) atomicAdd(fallback, 1ull);
+                }
+            }
+        }
+        __syncthreads();  // policy / value rows written; the LDS is the tree's again
+    }
+}
+
+hipError_t launch_search_grp(const TreeView& t, const oaz_state* roots, const uint8_t* active, SearchParams p, int s0,
+                             int s1, const float* noise, const NNView* w, float* policy, float* value, hipStream_t st) {
+    if (t.G == 0 || s1 <= s0) return hipSuccess;
+    if (w && (!w->fallback || !w->blob_x6 || w->precision != OAZ_FP32_SPLIT16)) return hipErrorInvalidValue;
+    const unsigned grid = (t.G + nn::kSB - 1) / nn::kSB;
+    hipLaunchKernelGGL(k_search_grp<H3Cfg<0>>, dim3(grid), dim3(kLatThreads), 0, st, t, roots, active, p, s0, s1, noise,
+                       w ? 0 : 1, w ? w->blob : nullptr, w ? w->blocks : 0, w ? w->blob_x6 : nullptr,
+                       w ? w->fallback : nullptr, policy, value);
+    return hipGetLastError();
 }
 
 hipError_t launch_search_lat(const TreeView& t, const oaz_state* roots, const uint8_t* active, SearchParams p,

@@ -330,37 +330,53 @@ def test_search_nn_trees_bitexact_with_gpu_evaluator(orc, precision, compact, pa
             assert _mv(r.moves[g]) == _mv(mv)
 
 
-@pytest.mark.parametrize("evaluator", [_abi.EVAL_HASH, _abi.EVAL_NN])
-@pytest.mark.parametrize("games", [1, 5, 256])
-def test_one_launch_search_equals_step_launches(orc, evaluator, games):
-    """oaz_config.step_kernels: 0 (auto) runs a search of <= CU-count games with no root noise as ONE
-    launch (a workgroup per game runs all its simulations: oaz_search_lat.hip), 1 the per-simulation
-    launches. Every tree node, pi, move and search statistic is identical; with HASH both equal the
-    oracle's trees (mcts_arena.rs:75-177)."""
+@pytest.mark.parametrize("evaluator", [_abi.EVAL_HASH, _abi.EVAL_NN, "nn_overflow"])
+@pytest.mark.parametrize("games,sims,noise", [(1, 400, 0), (5, 60, 0), (256, 60, 0), (5, 60, 1), (300, 40, 0),
+                                              (1000, 40, 1)])
+def test_one_launch_search_equals_step_launches(orc, trained3, evaluator, games, sims, noise):
+    """oaz_config.step_kernels 0 (auto) vs 1 (the per-simulation launches). Auto runs a search of <= CU-count
+    games without root noise as ONE launch (k_search_lat: a workgroup per game runs all its simulations
+    with the top of its tree in LDS), and otherwise up to 16 x CU-count games as one launch per noise
+    chunk (k_search_grp: 16 games per workgroup). Every tree node, pi, move and search statistic is
+    identical — also past the LDS-held nodes (400 simulations: ~5k nodes), with root noise, and when every
+    evaluation leaves the fp16 range (nn_overflow: the in-kernel recompute, which moves k_search_lat's tree
+    state out of LDS and back); with HASH both equal the oracle's trees (mcts_arena.rs:75-177)."""
     roots = random_positions(orc, games, seed=707 + games)
     w = random_weights(5, 3)
-    sims = 60
+    if evaluator == "nn_overflow":
+        from onitama_az.weights import blob_from_named, named_from_blob
+        named = {k: v.copy() for k, v in named_from_blob(trained3.copy(), 3).items()}
+        named["bn1|bias"][:] = 1.0e5
+        w = blob_from_named(named, 3)
+    ev = _abi.EVAL_HASH if evaluator == _abi.EVAL_HASH else _abi.EVAL_NN
     out = {}
     for sk in (0, 1):
-        with Engine(games=games, sims=sims, c_puct=5.0, train_noise=0, evaluator=evaluator, blocks=3,
-                    precision=_abi.FP32_SPLIT16, step_kernels=sk) as e:
-            if evaluator == _abi.EVAL_NN:
+        with Engine(games=games, sims=sims, c_puct=5.0, train_noise=noise, evaluator=ev, blocks=3,
+                    precision=_abi.FP32_SPLIT16, step_kernels=sk, seed=99) as e:
+            if ev == _abi.EVAL_NN:
                 e.load_weights(w)
             e.set_timing(1)
             r = e.search(roots, root_value=True)
             kt = e.kernel_times()
             trees = [e.tree(g) for g in sorted({0, games // 2, games - 1})]
             out[sk] = (r, trees, kt)
+            if evaluator == "nn_overflow":
+                assert e.nn_fallbacks() >= games * sims  # every evaluation recomputed
     (r0, t0, k0), (r1, t1, k1) = out[0], out[1]
-    assert k0.backup_select_n == 1 and k0.nn_n == 1 and k0.select_n == 0  # one search launch (+ the root value)
-    assert k1.select_n == 1 and k1.backup_select_n == sims - 1
+    if games <= 256 and not noise:  # k_search_lat: one launch (+ the root value's evaluation)
+        assert (k0.backup_select_n, k0.nn_n, k0.select_n, k0.expand_n) == (1, 1, 0, 0)
+    else:  # k_search_grp: one launch per 16-simulation noise chunk, then the last expand / backup
+        assert (k0.backup_select_n, k0.nn_n, k0.select_n, k0.expand_n) == ((sims + 15) // 16, 1, 0, 1)
+    assert k1.select_n == k1.parts and k1.backup_select_n == (sims - 1) * k1.parts
     assert np.array_equal(r0.pi, r1.pi) and r0.moves.tobytes() == r1.moves.tobytes()
     assert np.array_equal(r0.root_value, r1.root_value)
     for f in ("sims", "expansions", "children", "terminal_leaves", "depth_sum", "stuck_leaves", "max_nodes", "nn_evals"):
         assert getattr(r0.stats, f) == getattr(r1.stats, f), f
     for a, b in zip(t0, t1):
         assert a.tobytes() == b.tobytes()
-    if evaluator == _abi.EVAL_HASH:
+    if games == 1 and sims == 400:
+        assert r0.stats.max_nodes > 3000  # past the LDS-held top of the tree
+    if evaluator == _abi.EVAL_HASH and not noise:
         for g in sorted({0, games // 2, games - 1})[:2]:
             mv, pi, nodes, _ = orc.search(orc.search_cfg(sims=sims, c_puct=5.0, evaluator=orc.EVAL_HASH), roots[g])
             assert np.array_equal(r0.pi[g].reshape(-1), pi.reshape(-1)) and _mv(r0.moves[g]) == _mv(mv)

@@ -20,8 +20,9 @@ out = {}
 Gs = [int(x) for x in os.environ.get("OAZ_LAT_G", "1,16,64,256,1024,2048").split(",")]
 for G in Gs:
     roots = np.concatenate([initial_state_np([0, 1, 2, 3, 4]) for _ in range(G)])
-    with Engine(games=G, sims=sims, blocks=3, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_NN,
-                precision=_abi.FP32_SPLIT16) as e:
+    ev = _abi.EVAL_HASH if os.environ.get("OAZ_LAT_EVAL") == "hash" else _abi.EVAL_NN
+    with Engine(games=G, sims=sims, blocks=3, c_puct=5.0, train_noise=0, evaluator=ev,
+                precision=_abi.FP32_SPLIT16, step_kernels=int(os.environ.get("OAZ_LAT_STEP", "0"))) as e:
         e.load_weights(random_weights(0, 3))
         e.search(roots)
         ts = []
