@@ -51,12 +51,12 @@ __device__ __noinline__ void lat_select(const TreeView& t, const oaz_state* root
 // Copies the LDS-held tree state of the game to its global slots (out = true) or back (out = false):
 // before the fp16-range recompute (which uses the whole LDS) and, for the nodes and the node count, at
 // the end. All threads of the workgroup; the caller places the barriers.
-__device__ __forceinline__ void lat_sync_tree(const TreeView& tl, const TreeView& tg, uint32_t ncached, bool path_lds,
-                                              bool out) {
+__device__ __forceinline__ void lat_sync_tree(const TreeView& tl, const TreeView& tg, const NodesCached& na,
+                                              bool path_lds, bool out) {
     const int tid = (int)threadIdx.x;
     const uint32_t nn = out ? *tl.n_nodes : *tg.n_nodes;
-    const uint32_t nc = nn < ncached ? nn : ncached;
-    uint4* lq = reinterpret_cast<uint4*>(tl.nodes);
+    const uint32_t nc = nn < na.n ? nn : na.n;
+    uint4* lq = reinterpret_cast<uint4*>(na.L);
     uint4* gq = reinterpret_cast<uint4*>(tg.nodes);
     for (uint32_t k = (uint32_t)tid; k < 2 * nc; k += blockDim.x) {
         if (out) gq[k] = lq[k];
@@ -82,6 +82,10 @@ __device__ __forceinline__ void lat_sync_tree(const TreeView& tl, const TreeView
     }
 }
 
+// DBG 1 (diagnostic, A/B build only: OAZ_LAT_DBG=1): the walker's s_memtime cycles in the expand / back up, the
+// select, and the wait for the evaluation (barriers + network or HASH) are added to the game's statistics slots
+// GS_CUT / GS_RED / GS_BLUE (and the whole loop to GS_PASSES); the search's results are unchanged.
+template <int DBG = 0>
 __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oaz_state* __restrict__ roots,
                                                             const uint8_t* __restrict__ active, SearchParams prm,
                                                             int sims, int hash_eval, const float* __restrict__ blob,
@@ -116,17 +120,26 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
     tl.depth = tl.leaf + 1;
     tl.n_nodes = tl.leaf + 2;
     if (path_lds) tl.path = reinterpret_cast<uint32_t*>(lb + kLatPathOff);
-    tl.nodes = reinterpret_cast<oaz_node*>(lb + kLatCacheOff);
+    // tl.nodes stays the game's global slot: the node accessor maps nodes [0, ncached) to the LDS copy
     const uint32_t ncached = kLatCache < t.cap ? kLatCache : t.cap;
-    const NodesCached na{tl.nodes, ncached};
+    const NodesCached na{reinterpret_cast<oaz_node*>(lb + kLatCacheOff), ncached};
     const oaz_state* rg = roots + g;
     const uint8_t* ag = active ? active + g : nullptr;
     const uint32_t gs = walker && lane < 16 ? 0u : 1u;  // the walker's segment 0 holds the game
     // the segment's policy row for expand: LDS the network rebuilds in every evaluation anyway
     float* const sp = lds + (threadIdx.x >> 4) * 52;
-    lat_sync_tree(tl, tg, ncached, path_lds, false);  // the root (k_tree_reset) and the node count
+    lat_sync_tree(tl, tg, na, path_lds, false);  // the root (k_tree_reset) and the node count
     __syncthreads();
     bool resident = false;  // the network's head parameters are in LDS (H3sResident)
+    uint64_t cyc[4] = {0, 0, 0, 0}, tm0 = 0, tm = 0;  // DBG 1: backup, select, evaluation, loop
+    auto lap = [&](int k) {
+        if constexpr (DBG == 1) {
+            const uint64_t n = __builtin_amdgcn_s_memtime();
+            cyc[k] += n - tm;
+            tm = n;
+        }
+    };
+    if constexpr (DBG == 1) tm0 = tm = __builtin_amdgcn_s_memtime();
     for (int s = 0; s < sims; ++s) {
         if (!hash_eval && !resident) {  // at the start, and after an fp16-range recompute used the whole LDS
             const float* ph0 = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh);
@@ -137,8 +150,11 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
             resident = true;
         }
         if (walker) {
+            lap(2);
             if (s > 0) lat_backup(tl, rg, ag, policy + (size_t)g * 50, value + g, gs, sp, na);  // simulation s - 1's
+            lap(0);
             lat_select(tl, rg, ag, prm, gs, na);
+            lap(1);
         }
         __syncthreads();  // the leaf position of simulation s is in LDS
         if (hash_eval) {
@@ -155,7 +171,7 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
                                             H3sResident{tl.leaf_state, nullptr, true});
             if (__syncthreads_or(ovf)) {  // k_nn_h3s's recompute of this position (the k_nn_x6 body), which
                                           // needs the whole LDS: the tree state goes out and comes back
-                lat_sync_tree(tl, tg, ncached, path_lds, true);
+                lat_sync_tree(tl, tg, na, path_lds, true);
                 __syncthreads();
                 using X = typename H3Fallback<C>::X;
                 const TileSpan span{(int)g, (int)g + 1, (int)t.G};
@@ -165,15 +181,29 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
                     nn_h3_fallback<X, X::GRP1>(t.leaf_state, span, xblob, blocks, policy, value, lds);
                 if (threadIdx.x == 0) atomicAdd(fallback, 1ull);
                 __syncthreads();
-                lat_sync_tree(tl, tg, ncached, path_lds, false);
+                lat_sync_tree(tl, tg, na, path_lds, false);
                 resident = false;
             }
         }
         __syncthreads();  // policy / value row g written; the network's LDS is free for the tree again
     }
-    if (walker) lat_backup(tl, rg, ag, policy + (size_t)g * 50, value + g, gs, sp, na);  // the last simulation's
+    if (walker) {
+        lap(2);
+        lat_backup(tl, rg, ag, policy + (size_t)g * 50, value + g, gs, sp, na);  // the last simulation's
+        lap(0);
+        if constexpr (DBG == 1) {
+            cyc[3] = tm - tm0;
+            if (lane == 0) {
+                uint64_t* st = tg.stats;
+                atomicAdd((unsigned long long*)&st[GS_CUT], (unsigned long long)cyc[0]);
+                atomicAdd((unsigned long long*)&st[GS_RED], (unsigned long long)cyc[1]);
+                atomicAdd((unsigned long long*)&st[GS_BLUE], (unsigned long long)cyc[2]);
+                atomicAdd((unsigned long long*)&st[GS_PASSES], (unsigned long long)cyc[3]);
+            }
+        }
+    }
     __syncthreads();
-    lat_sync_tree(tl, tg, ncached, path_lds, true);  // the tree's top and the node count to global memory
+    lat_sync_tree(tl, tg, na, path_lds, true);  // the tree's top and the node count to global memory
 }
 
 // ---- one launch per noise chunk for up to 16 x CU-count games (k_search_grp) ---------------------------
@@ -266,7 +296,16 @@ hipError_t launch_search_lat(const TreeView& t, const oaz_state* roots, const ui
                              int sims, const NNView* w, float* policy, float* value, hipStream_t st) {
     if (t.G == 0 || sims <= 0) return hipSuccess;
     if (w && (!w->fallback || !w->blob_x6 || w->precision != OAZ_FP32_SPLIT16)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_search_lat, dim3(t.G), dim3(kLatThreads), 0, st, t, roots, active, p, sims, w ? 0 : 1,
+#if OAZ_AB
+    static const int dbg = getenv("OAZ_LAT_DBG") ? atoi(getenv("OAZ_LAT_DBG")) : 0;
+    if (dbg == 1) {
+        hipLaunchKernelGGL(k_search_lat<1>, dim3(t.G), dim3(kLatThreads), 0, st, t, roots, active, p, sims, w ? 0 : 1,
+                           w ? w->blob : nullptr, w ? w->blocks : 0, w ? w->blob_x6 : nullptr,
+                           w ? w->fallback : nullptr, policy, value);
+        return hipGetLastError();
+    }
+#endif
+    hipLaunchKernelGGL(k_search_lat<0>, dim3(t.G), dim3(kLatThreads), 0, st, t, roots, active, p, sims, w ? 0 : 1,
                        w ? w->blob : nullptr, w ? w->blocks : 0, w ? w->blob_x6 : nullptr,
                        w ? w->fallback : nullptr, policy, value);
     return hipGetLastError();

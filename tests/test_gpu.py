@@ -361,7 +361,9 @@ def test_one_launch_search_equals_step_launches(orc, trained3, evaluator, games,
             trees = [e.tree(g) for g in sorted({0, games // 2, games - 1})]
             out[sk] = (r, trees, kt)
             if evaluator == "nn_overflow":
-                assert e.nn_fallbacks() >= games * sims  # every evaluation recomputed
+                # every evaluation recomputed (the counter counts recomputed tiles: one position per workgroup in
+                # k_nn_h3s / k_search_lat, up to 16 in k_search_grp and k_nn_h3)
+                assert e.nn_fallbacks() >= (games + 15) // 16 * sims
     (r0, t0, k0), (r1, t1, k1) = out[0], out[1]
     if games <= 256 and not noise:  # k_search_lat: one launch (+ the root value's evaluation)
         assert (k0.backup_select_n, k0.nn_n, k0.select_n, k0.expand_n) == (1, 1, 0, 0)
