@@ -95,8 +95,6 @@ def parse():
                          "long as its longest game, so small fights are tail-bound)")
     ap.add_argument("--pm-playouts", type=int, default=400, help="pure_mcts mode: playouts per search")
     ap.add_argument("--train-batch", type=int, default=512, help="train mode: global batch (train.rs:142)")
-    ap.add_argument("--train-conv-exact", action="store_true",
-                    help="train mode: exact fp32 MFMA conv products (default: three-piece bf16 split products)")
     return ap.parse_args()
 
 
@@ -457,79 +455,62 @@ def train_main(args, world, rank, local):
     pi = rng.random((n_samples, 50)).astype(np.float32)
     samples["pi"] = pi / pi.sum(1, keepdims=True)
     samples["z"] = rng.integers(-1, 2, n_samples).astype(np.float32)
+    tr = Trainer(blocks=blocks, max_batch=shard, device=local)
+    tr.set_weights(random_weights(0, blocks))
     ts = torch.cuda.Stream()  # explicit: handle 0 would leave the trainer on its own, unordered stream
     torch.cuda.set_stream(ts)
+    tr.set_stream(ts.cuda_stream)
+    tr.load_samples(samples)
     nb = args.warmup + args.steps
     idx = choose_batches(np.random.default_rng(1), n_samples, B, nb)[:, rank * shard:(rank + 1) * shard]
+    tr.set_batches(idx)
+    grads = None
+    if world > 1:
+        ptr, n = tr.grads_device()
+        grads = torch.as_tensor(_DeviceArray(ptr, n), device=f"cuda:{local}")
 
-    def leg(conv_exact):
-        """warm-up + timed SGD steps on a fresh trainer; returns (max-rank seconds, losses)"""
-        tr = Trainer(blocks=blocks, max_batch=shard, device=local, conv_exact=conv_exact)
-        tr.set_weights(random_weights(0, blocks))
-        tr.set_stream(ts.cuda_stream)
-        tr.load_samples(samples)
-        tr.set_batches(idx)
-        grads = None
+    def step(b):
         if world > 1:
-            ptr, n = tr.grads_device()
-            grads = torch.as_tensor(_DeviceArray(ptr, n), device=f"cuda:{local}")
+            tr.backward(b)
+            dist.all_reduce(grads)
+            tr.apply(1.0 / world)
+        else:
+            tr.train(b, 1)
 
-        def step(b):
-            if world > 1:
-                tr.backward(b)
-                dist.all_reduce(grads)
-                tr.apply(1.0 / world)
-            else:
-                tr.train(b, 1)
-
-        def barrier_sync():
-            torch.cuda.synchronize()
-            tr.sync()
-            if world > 1:
-                dist.barrier()
-
-        for b in range(args.warmup):
-            step(b)
-        barrier_sync()
-        t0 = time.perf_counter()
-        for b in range(args.warmup, nb):
-            step(b)
-        barrier_sync()
-        elapsed = time.perf_counter() - t0
-        tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    def barrier_sync():
+        torch.cuda.synchronize()
+        tr.sync()
         if world > 1:
-            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        losses = tr.losses()
-        tr.close()
-        return float(tmax.item()), losses
+            dist.barrier()
 
-    T, (v, p, k) = leg(bool(args.train_conv_exact))
-    Tx = None
-    if not args.no_exact and not args.train_conv_exact:  # the exact-product kernels on the same steps
-        Tx, _ = leg(True)
+    for b in range(args.warmup):
+        step(b)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for b in range(args.warmup, nb):
+        step(b)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    T = float(tmax.item())
+    v, p, k = tr.losses()
     if rank == 0:
         fl = train_flop_per_sample(blocks) * shard
         ms = 1e3 * T / args.steps
         achieved = fl / (ms * 1e-3) / 1e12
         out = {"metric": TRAIN_METRIC, "value": B * args.steps / T, "unit": "samples/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
-               "scaling": "strong", "vs_baseline": None,
-               "dtype": "fp32" if args.train_conv_exact else "fp32 (conv products: three-piece bf16 split)",
+               "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
                "data": "synthetic (seeded deals, random pi/z, random-init weights seed 0)",
                "config": {"workload": f"train: {blocks}-block ResNet, global batch {B}, lr 5e-3, momentum 0.9, "
                                       f"wd 1e-4", "parallelism": f"dp{world} (RCCL all-reduce of gradients)"},
                "mean_losses": {"value": v / max(1, k), "policy": p / max(1, k)},
-               "roofline": {"bound": "mfma", "kernel": "whole SGD step (conv fwd/dgrad on " +
-                            ("v_mfma_f32_16x16x4_f32" if args.train_conv_exact else
-                             "v_mfma_f32_16x16x32_bf16, 6 split products") + ", wgrad on v_mfma_f32_32x32x2_f32)",
+               "roofline": {"bound": "mfma", "kernel": "whole SGD step (conv fwd/dgrad/wgrad on v_mfma_f32_16x16x4_f32)",
                             "achieved": achieved, "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
                             "frac": achieved / PEAK_TFLOPS["fp32"], "traffic": None,
-                            "flop_per_step_per_gpu": fl,
-                            "peak_note": "fp32 MFMA peak (the fp32-equivalent FLOPs of the step over it)"}}
-        if Tx is not None:
-            out["conv_exact"] = {"ms_per_step": 1e3 * Tx / args.steps, "value": B * args.steps / Tx,
-                                 "unit": "samples/s", "note": "oaz_train_config.conv_exact = 1: the same steps "
-                                 "with exact fp32 MFMA conv products"}
+                            "flop_per_step_per_gpu": fl}}
         if not args.no_cpu_baseline and world == 1:
             try:  # after the timed region: a baseline failure must not lose the measured line
                 out["cpu_baseline"] = train_cpu_baseline(blocks, B, args.cpu_seconds,
@@ -538,6 +519,7 @@ def train_main(args, world, rank, local):
                 print(f"bench: cpu_baseline failed: {ex!r}", file=sys.stderr, flush=True)
                 out["cpu_baseline"] = {"error": repr(ex)}
         print(json.dumps(out), flush=True)
+    tr.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -414,11 +414,7 @@ typedef struct oaz_train_config {
     double bn_momentum;           /* 0.1 (tch BatchNormConfig default) */
     double bn_eps;                /* 1e-5 */
     int32_t value_loss_broadcast; /* 1 = reference (Q16: z[B] - v[B,1] broadcasts to [B,B]), 0 = elementwise */
-    int32_t conv_exact;           /* 0 (default): 3x3 conv products (forward and input gradient) as fp32 by a
-                                     three-piece bf16 split of both operands, 6 products on bf16 MFMA (~2^-24
-                                     relative per product); 1: exact fp32 MFMA products. Weight gradients, BN
-                                     and heads are fp32 either way */
-    int32_t reserved[6];
+    int32_t reserved[7];
 } oaz_train_config;
 
 typedef struct oaz_trainer oaz_trainer;

@@ -569,8 +569,7 @@ __device__ __forceinline__ T pick3(int c, const T& a, const T& b, const T& d) {
 
 // Per-game statistics from the segmented tree kernels: relaxed atomics whose result is unused
 // (no-return global atomics), so the update costs no load round trip at the end of a walk; each game's
-// counters have one writer at a time, the atomic form only drops the read. A walk's (and an expansion's)
-// counters go out as one vector atomic over a few lanes: one write request per game and kernel.
+// counters have one writer at a time, the atomic form only drops the read.
 __device__ __forceinline__ void stat_add(uint64_t* p, uint64_t v) {
     (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -664,9 +663,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
     int color = s.to_move & 1;
     NodeRegs nd = load_node(na.at(T, 0));
     uint32_t node = 0, depth = 0;
-    // the path entries of depths 0..15 are held by segment lanes 0..15 (lane d: the node at depth d) and
-    // written with one store when the walk ends; deeper ones (rare) are written as the walk reaches them
-    uint32_t pathv = 0;
+    if (on && sl == 0) path[0] = 0;
     bool stuck = false;
     bool go = on && (node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2);
     while (__builtin_amdgcn_read_exec() && __ballot(go)) {  // some segment is still walking
@@ -742,29 +739,25 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
                 if (sl == 0) *flags_ptr(na.at(T, cidx)) = (uint8_t)(node_flags(c.misc));
             }
             ++depth;
-            if ((uint32_t)sl == depth) pathv = cidx;
-            else if (sl == 0 && depth >= (uint32_t)kSegLanes && depth < t.pathcap) path[depth] = cidx;
+            if (sl == 0 && depth < t.pathcap) path[depth] = cidx;
             node = cidx;
             nd = c;
             go = (node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2);
         }
     }
     s.to_move = (uint8_t)color;
-    if (on && (uint32_t)sl <= depth && (uint32_t)sl < t.pathcap) path[sl] = pathv;  // one store: depths 0..15
-    if (on && sl < 4) {
-        // the walk's statistics as ONE vector atomic (lane k: field k of SIMS, DEPTH, EVALS, STUCK) instead of
-        // four single-lane ones: one write request to the game's counters
+    if (on && sl == 0) {
         const bool need = leaf_needs_eval(nd.misc, s);
-        const uint64_t v = sl == 0 ? 1u : sl == 1 ? (uint64_t)depth : sl == 2 ? (uint64_t)need : (uint64_t)stuck;
-        const int f = sl == 0 ? GS_SIMS : sl == 1 ? GS_DEPTH : sl == 2 ? GS_EVALS : GS_STUCK;  // one 128-B block
-        if (v) stat_add(t.stats + (size_t)g * GS_COUNT + f, v);
-        if (sl == 0) {
-            store_state(&t.leaf_state[g], s);
-            if (leaf_lds) *leaf_lds = s;
-            t.leaf[g] = node;
-            t.depth[g] = depth;
-            if (t.need) t.need[g] = need;
-        }
+        store_state(&t.leaf_state[g], s);
+        if (leaf_lds) *leaf_lds = s;
+        t.leaf[g] = node;
+        t.depth[g] = depth;
+        if (t.need) t.need[g] = need;
+        uint64_t* st = t.stats + (size_t)g * GS_COUNT;
+        stat_add(&st[GS_SIMS], 1);
+        stat_add(&st[GS_DEPTH], depth);
+        stat_add(&st[GS_EVALS], need);
+        if (stuck) stat_add(&st[GS_STUCK], 1);
     } else if (!on && g < t.G && sl == 0 && t.need) {
         t.need[g] = 0;  // an idle slot: nothing to evaluate
     }
@@ -837,7 +830,6 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
     }
     asm volatile("" ::"v"(polr[0]), "v"(polr[1]), "v"(polr[2]), "v"(polr[3]), "v"(vrow));  // issued in trip 2
 
-    uint32_t expanded = 0xFFFFFFFFu;  // children created by this expansion (none: all ones)
     if (!(node_flags(nd.misc) & 3)) {
         // the policy row kept in registers for the renormalisation sums and in LDS (sp) for the
         // children's priors
@@ -893,30 +885,24 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
         }
         if (sl == 0) {
             t.n_nodes[g] = base + K;
-            // the leaf's header in two words: first, then mv | nch << 16 | flags << 24 (flags: expanded;
-            // the leaf was neither expanded nor terminal, mcts_arena.rs:159-161, 231-260)
             oaz_node* lp = na.at(T, leaf);
             lp->first = base;
-            *reinterpret_cast<uint32_t*>(&lp->mv) = (nd.misc & 0xFFFFu) | (K << 16) | (1u << 24);
+            lp->nch = (uint8_t)K;
+            lp->flags = 1;
+            stat_add(&st[GS_EXPANSIONS], 1);
+            stat_add(&st[GS_CHILDREN], K);
             stat_max(&st[GS_MAXNODES], base + K);
         }
-        expanded = K;
     }
     const int res = current_state(s);
-    const bool won = is_win(res);
     double r;
-    if (won) {
+    if (is_win(res)) {
         const int root_color = roots[g].to_move & 1;
         const int pc = depth == 0 ? root_color : (root_color ^ (int)((depth - 1) & 1));
         r = reward(res, pc);
+        if (sl == 0) stat_add(&st[GS_TERMINAL], 1);
     } else {
         r = (double)vrow;
-    }
-    if (sl < 3) {  // the expansion's statistics as one vector atomic (lanes 0-2: EXPANSIONS, CHILDREN, TERMINAL)
-        const uint64_t v = sl == 0 ? (expanded != 0xFFFFFFFFu ? 1u : 0u) : sl == 1 ? (expanded != 0xFFFFFFFFu ? expanded : 0u)
-                                                                                   : (uint64_t)won;
-        const int f = sl == 0 ? GS_EXPANSIONS : sl == 1 ? GS_CHILDREN : GS_TERMINAL;
-        if (v) stat_add(&st[f], v);
     }
     if (mine) {
         const double rk = ((depth - (uint32_t)sl) & 1) ? -r : r;

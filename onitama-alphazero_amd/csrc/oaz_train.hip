@@ -42,31 +42,6 @@ constexpr int kHeadVW = 64 * 25 + 64 + 64 + 1;              // vh_linear1 w,b + 
 constexpr int kHConvW = 64 + 1 + 128 + 2;                   // vh_conv w,b + policy_conv w,b
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// fp32 -> three bf16 pieces (hi = RNE(x), mid = RNE(x - hi), lo = RNE(x - hi - mid)): x to ~2^-26 relative, with
-// fp32's range, so activations and gradients of any magnitude split without scaling. Eight values = one MFMA
-// K-run. (Two pieces, ~2^-17, are not enough here: the BN backward's mean subtractions amplify the product
-// errors of the layers above ~100x, measured 1-3e-3 of the largest gradient against 2e-4.)
-__device__ __forceinline__ void split3_bf16x8(const float4& p, const float4& q, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
-    const float v[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
-    u32x4 h, m, l;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const bf16x2 hh = {(__bf16)v[2 * k], (__bf16)v[2 * k + 1]};
-        const float r0 = v[2 * k] - (float)hh[0], r1 = v[2 * k + 1] - (float)hh[1];
-        const bf16x2 mm = {(__bf16)r0, (__bf16)r1};
-        const bf16x2 ll = {(__bf16)(r0 - (float)mm[0]), (__bf16)(r1 - (float)mm[1])};
-        h[k] = __builtin_bit_cast(uint32_t, hh);
-        m[k] = __builtin_bit_cast(uint32_t, mm);
-        l[k] = __builtin_bit_cast(uint32_t, ll);
-    }
-    hi = __builtin_bit_cast(bf16x8, h);
-    mid = __builtin_bit_cast(bf16x8, m);
-    lo = __builtin_bit_cast(bf16x8, l);
-}
 
 __device__ __forceinline__ int nbr(int sq, int t) {
     const int y = sq / 5 + t / 3 - 1, x = sq % 5 + t % 3 - 1;
@@ -125,7 +100,7 @@ __global__ void k_set_batch(int32_t* cur, int v, int add) {
 enum { CONV_FWD = 0, CONV_DGRAD = 1 };
 
 struct ConvArgs {
-    const float* in;      // [R][16*chunks] (FUSE: the BN input below instead)
+    const float* in;      // [R][16*chunks]
     const float4* w;      // packed [9][chunks][4 nt][64 lanes]
     const float* bias;    // FWD
     float* out;           // FWD: Z ; DGRAD: m = (dgrad + skip) * (act > 0)
@@ -137,43 +112,22 @@ struct ConvArgs {
     const float* skip;    // DGRAD: residual gradient to add (or null)
     int chunks;           // input channels / 16
     int B;
-    // FUSE: the conv's input is computed from the layer below's BN at load time, on every tap, and the
-    // centre tap (the workgroup's own rows) also stores it for the kernels that read it later.
-    //   FWD:   in = relu((iz - mean) * invstd * gamma + beta [+ iskip])   (k_bn_act), stored to in_out
-    //   DGRAD: in = c1 * (iz - mm - xhat * mx), xhat = (iz2 - mean) * invstd (k_bn_bwd_apply), stored to
-    //          in_out, with its per-channel sums over the workgroup's rows (the conv bias gradient) in ipart [nwg][64]
-    const float* iz;      // FWD: Z of the layer below ; DGRAD: M of this layer
-    const float* iz2;     // DGRAD: Z of this layer
-    const float* iskip;   // FWD: the residual added before the ReLU (or null)
-    const float* ic[5];   // FWD: mean, invstd, gamma, beta ; DGRAD: mean, invstd, c1, mm, mx
-    float* in_out;        // the centre tap's input rows
-    float* ipart;         // DGRAD: per-wave sums of the input
 };
 
-// Workgroup = 16 * RG rows (sample tiles of 16) of one square x all 64 output channels; 4 waves = RG row
-// groups x (4 / RG) channel splits. Per on-board tap the tap's packed weights (16 KB for 64 input channels)
-// are staged once in LDS (double-buffered) and shared by the 4 waves; each wave keeps NPW accumulators (one
-// per 16-channel n-tile), so an A fragment feeds NPW MFMAs.
-// PREC 0: exact fp32 products (v_mfma_f32_16x16x4_f32; lane (i, kq) holds channels 16g + 4kq + 0..3).
-// PREC 1: fp32 by a three-piece bf16 split of both operands, six products (l*h + h*l + m*m + m*h + h*m + h*h;
-//         the dropped terms are ~2^-24 relative) on v_mfma_f32_16x16x32_bf16 with fp32 accumulate: 2.7x fewer
-//         MFMA cycles than the fp32 MFMA; lane (i, kq) holds channels 32ks + 8kq + 0..7 (ks = K-step of 32).
-template <int MODE, int CH, int RG, int FUSE, int PREC>  // CH = input channels / 16; RG = 16-row groups per workgroup
+// Workgroup = 64 rows (4 sample tiles of 16, one per wave) of one square x all 64 output
+// channels. Per on-board tap the tap's packed weights (CH x 4 n-tiles x 64 lanes float4 = 16 KB
+// for 64 input channels) are staged once in LDS (double-buffered) and shared by the 4 waves;
+// each wave keeps 4 accumulators (one per 16-channel n-tile), so an A fragment feeds 4 MFMAs.
+template <int MODE, int CH, int RG>  // CH = input channels / 16; RG = 16-row groups per workgroup
 __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
     constexpr int NPW = RG;  // n-tiles per wave: 4 waves = RG row groups x (4 / RG) channel splits
-    constexpr int WQ = PREC ? CH * 3 / 2 : CH;  // a tap's packed weights: WQ x 256 float4
-    __shared__ float4 sw[2][WQ * 256];
+    __shared__ float4 sw[2][CH * 256];
     __shared__ float red[RG][2][64];
-    __shared__ float4 coef[FUSE ? 5 : 1][16];  // FUSE: the input's per-channel BN coefficients (float4 = 4 channels)
-    __shared__ __attribute__((aligned(16))) float redi[FUSE && MODE == CONV_DGRAD ? RG : 1][64];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, kq = lane >> 4;
     const int rg = wave % RG, n0 = (wave / RG) * NPW;
     const int sq = blockIdx.y, B = a.B, b0 = blockIdx.x * 16 * RG + rg * 16;
     const bool active = b0 < B;  // B is a multiple of 16
     constexpr int rs = 16 * CH;
-    constexpr int NC = MODE == CONV_FWD ? 4 : 5;
-    if constexpr (FUSE)
-        for (int k = tid; k < NC * 64; k += 256) reinterpret_cast<float*>(coef)[k] = a.ic[k >> 6][k & 63];
     f32x4 acc[NPW];
 #pragma unroll
     for (int n = 0; n < NPW; ++n) acc[n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -182,137 +136,44 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
     // Inactive waves (sample tile past B) load the first tile and discard their results, so the
     // loads and MFMAs stay unconditional and the prefetch registers stay in VGPRs.
     const int bl = active ? b0 : 0;
-    // the lane's channels of fragment g (float4 g of its A row)
-    auto choff = [&](int g) { return PREC ? 32 * (g >> 1) + 8 * kq + 4 * (g & 1) : 16 * g + 4 * kq; };
-    float4 wr[WQ], av[CH], an[CH], xa[FUSE ? CH : 1], xn[FUSE ? CH : 1];
-    // FUSE: the tap's raw rows (v: iz, x: iskip or iz2) become the MFMA input here
-    auto fuse = [&](float4 (&v)[CH], const float4 (&x)[FUSE ? CH : 1], bool has_x) {
-        if constexpr (FUSE) {
-#pragma unroll
-            for (int g = 0; g < CH; ++g) {
-                const int q = choff(g) >> 2;  // channels 4q .. 4q + 3
-                float e[4] = {v[g].x, v[g].y, v[g].z, v[g].w};
-                const float xx[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
-                const float4 m = coef[0][q], is = coef[1][q], c2 = coef[2][q], c3 = coef[3][q];
-                const float mm[4] = {m.x, m.y, m.z, m.w}, ii[4] = {is.x, is.y, is.z, is.w};
-                const float k2[4] = {c2.x, c2.y, c2.z, c2.w}, k3[4] = {c3.x, c3.y, c3.z, c3.w};
-                if constexpr (MODE == CONV_FWD) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        float y = (e[j] - mm[j]) * ii[j] * k2[j] + k3[j];
-                        if (has_x) y += xx[j];
-                        e[j] = y > 0.0f ? y : 0.0f;
-                    }
-                } else {
-                    const float4 c4 = coef[4][q];
-                    const float k4[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float xh = (xx[j] - mm[j]) * ii[j];
-                        e[j] = k2[j] * (e[j] - k3[j] - xh * k4[j]);
-                    }
-                }
-                v[g] = make_float4(e[0], e[1], e[2], e[3]);
-            }
-        }
-    };
-    const float* const src = FUSE ? a.iz : a.in;
-    const float* const src2 = MODE == CONV_FWD ? a.iskip : a.iz2;
-    const bool has_x = FUSE && src2 != nullptr;
+    float4 wr[CH], av[CH], an[CH];
     int t = 0;
     while (nbr(sq, t) < 0) ++t;
     {
-        const float4* wt = a.w + (size_t)t * WQ * 256;
+        const float4* wt = a.w + (size_t)t * CH * 256;
 #pragma unroll
-        for (int k = 0; k < WQ; ++k) sw[0][k * 256 + tid] = wt[k * 256 + tid];
-        const size_t ro = (size_t)(nbr(sq, t) * B + bl + i) * rs;
+        for (int k = 0; k < CH; ++k) sw[0][k * 256 + tid] = wt[k * 256 + tid];
+        const float* base = a.in + (size_t)(nbr(sq, t) * B + bl + i) * rs + 4 * kq;
 #pragma unroll
-        for (int g = 0; g < CH; ++g) av[g] = *reinterpret_cast<const float4*>(src + ro + choff(g));
-        if constexpr (FUSE) {
-#pragma unroll
-            for (int g = 0; g < CH; ++g)
-                xa[g] = has_x ? *reinterpret_cast<const float4*>(src2 + ro + choff(g)) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int g = 0; g < CH; ++g) av[g] = *reinterpret_cast<const float4*>(base + 16 * g);
     }
     __syncthreads();
-    float bs[FUSE && MODE == CONV_DGRAD ? 4 * CH : 1];  // DGRAD FUSE: the lane's sums of the centre tap's input
-#pragma unroll
-    for (int k = 0; k < (FUSE && MODE == CONV_DGRAD ? 4 * CH : 1); ++k) bs[k] = 0.0f;
-    auto centre = [&](int tt) {  // the centre tap's input is this workgroup's own rows: store it once
-        if constexpr (FUSE) {
-            if (tt == 4 && active && n0 == 0) {
-                float* o = a.in_out + (size_t)(sq * B + b0 + i) * rs;
-#pragma unroll
-                for (int g = 0; g < CH; ++g) {
-                    *reinterpret_cast<float4*>(o + choff(g)) = av[g];
-                    if constexpr (MODE == CONV_DGRAD) {
-                        bs[4 * g + 0] = av[g].x;
-                        bs[4 * g + 1] = av[g].y;
-                        bs[4 * g + 2] = av[g].z;
-                        bs[4 * g + 3] = av[g].w;
-                    }
-                }
-            }
-        }
-    };
     for (int cur = 0; t < 9; cur ^= 1) {
         int tn = t + 1;
         while (tn < 9 && nbr(sq, tn) < 0) ++tn;
         const int tl = tn < 9 ? tn : t;  // after the last tap: a harmless reload
         {
-            const float4* wt = a.w + (size_t)tl * WQ * 256;
+            const float4* wt = a.w + (size_t)tl * CH * 256;
 #pragma unroll
-            for (int k = 0; k < WQ; ++k) wr[k] = wt[k * 256 + tid];
-            const size_t ro = (size_t)(nbr(sq, tl) * B + bl + i) * rs;
+            for (int k = 0; k < CH; ++k) wr[k] = wt[k * 256 + tid];
+            const float* base = a.in + (size_t)(nbr(sq, tl) * B + bl + i) * rs + 4 * kq;
 #pragma unroll
-            for (int g = 0; g < CH; ++g) an[g] = *reinterpret_cast<const float4*>(src + ro + choff(g));
-            if constexpr (FUSE) {
-#pragma unroll
-                for (int g = 0; g < CH; ++g)
-                    xn[g] = has_x ? *reinterpret_cast<const float4*>(src2 + ro + choff(g)) : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-        }
-        // this tap's rows (loaded one iteration ago) become the MFMA input while the next tap's loads fly
-        fuse(av, xa, has_x);
-        centre(t);
-        if constexpr (PREC == 0) {
-#pragma unroll
-            for (int g = 0; g < CH; ++g)
-#pragma unroll
-                for (int n = 0; n < NPW; ++n) {
-                    const float4 bv = sw[cur][(g * 4 + n0 + n) * 64 + lane];
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].x, bv.x, acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].y, bv.y, acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].z, bv.z, acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].w, bv.w, acc[n], 0, 0, 0);
-                }
-        } else {  // packed weights per tap: [ks][n-tile][piece hi / mid / lo][64 lanes] bf16x8
-            const bf16x8* wb = reinterpret_cast<const bf16x8*>(&sw[cur][0]);
-#pragma unroll
-            for (int ks = 0; ks < CH / 2; ++ks) {
-                bf16x8 ah, am, al;
-                split3_bf16x8(av[2 * ks], av[2 * ks + 1], ah, am, al);
-#pragma unroll
-                for (int n = 0; n < NPW; ++n) {
-                    const bf16x8* wp = wb + (ks * 4 + n0 + n) * 3 * 64 + lane;
-                    const bf16x8 bh = wp[0], bm = wp[64], bl2 = wp[128];
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl2, acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[n], 0, 0, 0);
-                }
-            }
+            for (int g = 0; g < CH; ++g) an[g] = *reinterpret_cast<const float4*>(base + 16 * g);
         }
 #pragma unroll
-        for (int k = 0; k < WQ; ++k) sw[cur ^ 1][k * 256 + tid] = wr[k];
+        for (int g = 0; g < CH; ++g)
+#pragma unroll
+            for (int n = 0; n < NPW; ++n) {
+                const float4 bv = sw[cur][(g * 4 + n0 + n) * 64 + lane];
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].x, bv.x, acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].y, bv.y, acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].z, bv.z, acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].w, bv.w, acc[n], 0, 0, 0);
+            }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) sw[cur ^ 1][k * 256 + tid] = wr[k];
 #pragma unroll
         for (int g = 0; g < CH; ++g) av[g] = an[g];
-        if constexpr (FUSE) {
-#pragma unroll
-            for (int g = 0; g < CH; ++g) xa[g] = xn[g];
-        }
         __syncthreads();
         t = tn;
     }
@@ -353,38 +214,14 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
             red[rg][1][co] = s2;
         }
     }
-    if constexpr (FUSE && MODE == CONV_DGRAD) {  // the centre rows' input sums over the 16 rows (lane bits 0-3)
-        if (n0 == 0) {
-#pragma unroll
-            for (int k = 0; k < 4 * CH; ++k) {
-                float v = bs[k];
-                v += __shfl_xor(v, 1);
-                v += __shfl_xor(v, 2);
-                v += __shfl_xor(v, 4);
-                v += __shfl_xor(v, 8);
-                bs[k] = v;
-            }
-            if (i == 0)
-#pragma unroll
-                for (int g = 0; g < CH; ++g)
-                    *reinterpret_cast<float4*>(&redi[rg][choff(g)]) =
-                        make_float4(bs[4 * g], bs[4 * g + 1], bs[4 * g + 2], bs[4 * g + 3]);
-        }
-    }
     __syncthreads();
-    const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
     if (tid < 128) {
         const int k = tid >> 6, c = tid & 63;
+        const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
         float v = 0.0f;
 #pragma unroll
         for (int r = 0; r < RG; ++r) v += red[r][k][c];
         a.part[wg * 128 + tid] = v;
-    } else if (FUSE && MODE == CONV_DGRAD && tid < 192) {  // the conv bias gradient's partial of these rows
-        const int c = tid - 128;
-        float v = 0.0f;
-#pragma unroll
-        for (int r = 0; r < RG; ++r) v += redi[r][c];
-        a.ipart[wg * kC + c] = v;
     }
 }
 
@@ -962,27 +799,10 @@ __global__ __launch_bounds__(256) void k_head_bwd_rows(const float* A, const flo
 // ---- optimiser + weight packing -------------------------------------------------------------------
 struct ConvTab {  // conv weight ranges of the blob and their packed copies (written by k_sgd)
     int n;
-    int prec;  // k_conv's PREC: the packed layout
     int off[kMaxConv], cin[kMaxConv];
     float* wf[kMaxConv];
     float* wd[kMaxConv];
 };
-
-// PREC 1 packed conv weights (bf16 elements): per tap [ks][n-tile][piece][64 lanes][8], lane = (out & 15) +
-// 16 * kq for input channels 32ks + 8kq + j. Element index of the hi piece of (tap, out, in); mid = hi + 512,
-// lo = hi + 1024.
-__device__ __forceinline__ size_t pack_bf16_pos(int t, int chunks, int out, int in) {
-    const int ks = in >> 5, kq = (in & 31) >> 3, j = in & 7, nt = out >> 4, lane = (out & 15) + 16 * kq;
-    return (((((size_t)t * (chunks >> 1) + ks) * 4 + nt) * 3) * 64 + lane) * 8 + j;
-}
-__device__ __forceinline__ void store_bf16_pieces(uint16_t* w, size_t pos, float v) {
-    const __bf16 h = (__bf16)v;
-    const float r = v - (float)h;
-    const __bf16 m = (__bf16)r, l = (__bf16)(r - (float)m);
-    w[pos] = __builtin_bit_cast(uint16_t, h);
-    w[pos + 512] = __builtin_bit_cast(uint16_t, m);
-    w[pos + 1024] = __builtin_bit_cast(uint16_t, l);
-}
 
 // SGD (torch semantics, dampening 0): d = g*scale + wd*p; buf = mom*buf + d; p -= lr*buf.
 // Conv weights are also scattered straight into the packed fwd / dgrad layouts of k_pack.
@@ -1001,11 +821,6 @@ __global__ void k_sgd(float* p, const float* g, float* buf, const uint8_t* mask,
         if (rel < 0 || rel >= (long long)kC * cin * 9) continue;
         const int t = (int)(rel % 9), ci = (int)((rel / 9) % cin), co = (int)(rel / (9 * cin));
         const int chunks = cin == kC ? 4 : 2;
-        if (tab.prec) {
-            store_bf16_pieces(reinterpret_cast<uint16_t*>(tab.wf[l]), pack_bf16_pos(t, chunks, co, ci), np);
-            if (tab.wd[l]) store_bf16_pieces(reinterpret_cast<uint16_t*>(tab.wd[l]), pack_bf16_pos(8 - t, 4, ci, co), np);
-            break;
-        }
         {
             const int gg = ci >> 4, kq = (ci & 15) >> 2, j = ci & 3, nt = co >> 4, lane = (co & 15) + 16 * kq;
             tab.wf[l][((((size_t)t * chunks + gg) * 4 + nt) * 64 + lane) * 4 + j] = np;
@@ -1036,15 +851,6 @@ __global__ void k_pack(const float* W, int cin, int chunks, float4* wf, float4* 
     }
     wf[id] = make_float4(v[0], v[1], v[2], v[3]);
     if (wd) wd[id] = make_float4(d[0], d[1], d[2], d[3]);
-}
-// the PREC 1 layout (pack_bf16_pos) of the same weights: one thread per (tap, out, in)
-__global__ void k_pack_bf16(const float* W, int cin, int chunks, uint16_t* wf, uint16_t* wd) {
-    const int id = blockIdx.x * blockDim.x + threadIdx.x;
-    const int cpad = 16 * chunks;
-    if (id >= 9 * kC * cpad) return;
-    const int ic = id % cpad, oc = (id / cpad) % kC, t = id / (cpad * kC);
-    store_bf16_pieces(wf, pack_bf16_pos(t, chunks, oc, ic), ic < cin ? W[((size_t)oc * cin + ic) * 9 + t] : 0.0f);
-    if (wd && ic < cin) store_bf16_pieces(wd, pack_bf16_pos(8 - t, 4, ic, oc), W[((size_t)oc * cin + ic) * 9 + t]);
 }
 
 }  // namespace tr
@@ -1103,8 +909,6 @@ struct oaz_trainer {
     Layout L{};
     int nconv = 0, maxB = 0;
     int conv_rg = 2;  // 16-row groups per conv workgroup (OAZ_CONV_RG=1|2|4 overrides; tuning knob)
-    int fuse = 1;     // BN apply folded into the next conv's loads (OAZ_TRAIN_FUSE=0 in the A/B build: separate kernels)
-    int prec = 1;     // k_conv PREC: 1 = three-piece bf16 split products, 0 = exact fp32 (oaz_train_config.conv_exact)
     size_t nparam = 0;
     std::vector<void*> allocs;
     float *P = nullptr, *G = nullptr, *MOM = nullptr;
@@ -1189,14 +993,10 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
     t->nconv = 1 + 2 * cfg->blocks;
     t->maxB = cfg->max_batch;
     t->L = make_layout(cfg->blocks);
-    t->prec = cfg->conv_exact ? 0 : 1;
 #if OAZ_AB  // A/B build only: conv row-group override
     if (const char* e = getenv("OAZ_CONV_RG")) {
         const int v = atoi(e);
         if (v == 1 || v == 2 || v == 4) t->conv_rg = v;
-    }
-    if (const char* e = getenv("OAZ_TRAIN_FUSE")) {
-        t->fuse = atoi(e) != 0;
     }
 #endif
     t->nparam = t->L.total;
@@ -1217,15 +1017,15 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
         return fail();
     for (int l = 0; l < t->nconv; ++l) {
         const int chunks = l == 0 ? 2 : 4;
-        if (t->alloc(t->wf[l], (size_t)9 * chunks * 384)) return fail();  // PREC 1: 3 bf16 pieces per weight
-        if (l > 0 && t->alloc(t->wd[l], (size_t)9 * chunks * 384)) return fail();
+        if (t->alloc(t->wf[l], (size_t)9 * chunks * 256)) return fail();
+        if (l > 0 && t->alloc(t->wd[l], (size_t)9 * chunks * 256)) return fail();
         if (t->alloc(t->Z[l], R * kC) || t->alloc(t->A[l], R * kC) || t->alloc(t->M[l], R * kC) ||
             t->alloc(t->mean[l], 64) || t->alloc(t->invstd[l], 64))
             return fail();
     }
     const size_t nwg_conv = R / 16;
     if (t->alloc(t->X0, R * kInPad) || t->alloc(t->DZ[0], R * kC) || t->alloc(t->DZ[1], R * kC) || t->alloc(t->bcoef, 3 * 64) ||
-        t->alloc(t->part, nwg_conv * 128) || t->alloc(t->bpart[0], (nwg_conv + 64) * 64) || t->alloc(t->bpart[1], (nwg_conv + 64) * 64) ||
+        t->alloc(t->part, nwg_conv * 128) || t->alloc(t->bpart[0], (R + 63) / 64 * 64) || t->alloc(t->bpart[1], (R + 63) / 64 * 64) ||
         t->alloc(t->wpart, (size_t)9 * 25 * kWSplit * 64 * 64) || t->alloc(t->hz, R * 4) || t->alloc(t->g3, R * 4) ||
         t->alloc(t->hstat, 16) || t->alloc(t->hpart, ((R + 255) / 256 + (size_t)t->maxB / kHS + 1) * 8) ||
         t->alloc(t->hwpart, ((size_t)t->maxB / kHS + 1) * kHeadW) ||
@@ -1261,12 +1061,6 @@ extern "C" int oaz_trainer_set_stream(oaz_trainer* t, void* stream) {
 static int repack(oaz_trainer* t) {
     for (int l = 0; l < t->nconv; ++l) {
         const int chunks = l == 0 ? 2 : 4, cin = l == 0 ? kIn : kC;
-        if (t->prec) {
-            const int n = 9 * kC * 16 * chunks;
-            hipLaunchKernelGGL(k_pack_bf16, dim3((n + 255) / 256), dim3(256), 0, t->st, t->P + t->L.cw[l], cin, chunks,
-                               reinterpret_cast<uint16_t*>(t->wf[l]), reinterpret_cast<uint16_t*>(t->wd[l]));
-            continue;
-        }
         const int n = 9 * chunks * 256;
         hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, t->st, t->P + t->L.cw[l], cin, chunks,
                            t->wf[l], t->wd[l]);
@@ -1348,20 +1142,15 @@ extern "C" int oaz_trainer_set_batches(oaz_trainer* t, const int32_t* idx, int n
     return 0;
 }
 
-template <int MODE, int FUSE, int PREC>
-static void launch_conv_p(int ch, int rg, dim3 grid, hipStream_t st, const ConvArgs& a) {
-#define OAZ_CONV(CHV, RGV) hipLaunchKernelGGL((k_conv<MODE, CHV, RGV, FUSE, PREC>), grid, dim3(256), 0, st, a)
+template <int MODE>
+static void launch_conv(int ch, int rg, dim3 grid, hipStream_t st, const ConvArgs& a) {
+#define OAZ_CONV(CHV, RGV) hipLaunchKernelGGL((k_conv<MODE, CHV, RGV>), grid, dim3(256), 0, st, a)
     if (ch == 2) {
         if (rg == 1) OAZ_CONV(2, 1); else if (rg == 2) OAZ_CONV(2, 2); else OAZ_CONV(2, 4);
     } else {
         if (rg == 1) OAZ_CONV(4, 1); else if (rg == 2) OAZ_CONV(4, 2); else OAZ_CONV(4, 4);
     }
 #undef OAZ_CONV
-}
-template <int MODE, int FUSE>
-static void launch_conv(int prec, int ch, int rg, dim3 grid, hipStream_t st, const ConvArgs& a) {
-    if (prec) launch_conv_p<MODE, FUSE, 1>(ch, rg, grid, st, a);
-    else launch_conv_p<MODE, FUSE, 0>(ch, rg, grid, st, a);
 }
 
 static int backward(oaz_trainer* t, int bi) {
@@ -1378,10 +1167,7 @@ static int backward(oaz_trainer* t, int bi) {
     if (bi >= 0) hipLaunchKernelGGL(k_set_batch, dim3(1), dim3(64), 0, st, t->cur, bi, 0);
     hipLaunchKernelGGL(k_gather, dim3((R + 51 * B + 255) / 256), dim3(256), 0, st, t->samples, t->idx, t->cur, B,
                        t->X0, t->pi, t->z);
-    // ---- forward. fuse: conv l computes its input relu(BN(Z[l-1]) [+ skip]) while loading it (and stores
-    // A[l-1] from its centre tap), so only the last layer's activation needs k_bn_act.
-    auto skip_of = [&](int l) -> const float* { return (l >= 2 && l % 2 == 0) ? t->A[l - 2] : nullptr; };
-    const long long nact = (long long)R * kC;
+    // ---- forward
     for (int l = 0; l < nl; ++l) {
         ConvArgs a{};
         a.in = l == 0 ? t->X0 : t->A[l - 1];
@@ -1391,23 +1177,13 @@ static int backward(oaz_trainer* t, int bi) {
         a.part = t->part;
         a.chunks = l == 0 ? 2 : 4;
         a.B = B;
-        if (t->fuse && l > 0) {
-            a.iz = t->Z[l - 1];
-            a.iskip = skip_of(l - 1);
-            a.ic[0] = t->mean[l - 1];
-            a.ic[1] = t->invstd[l - 1];
-            a.ic[2] = P + L.bg[l - 1];
-            a.ic[3] = P + L.bb[l - 1];
-            a.in_out = t->A[l - 1];
-            launch_conv<CONV_FWD, 1>(t->prec, 4, rg, conv_grid, st, a);
-        } else {
-            launch_conv<CONV_FWD, 0>(t->prec, l == 0 ? 2 : 4, rg, conv_grid, st, a);
-        }
+        launch_conv<CONV_FWD>(l == 0 ? 2 : 4, rg, conv_grid, st, a);
         hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_conv, 64, 0, 64, (double)R,
                            P + L.brm[l], P + L.brv[l], bn_mom, eps, t->mean[l], t->invstd[l]);
-        if (!t->fuse || l == nl - 1)
-            hipLaunchKernelGGL(k_bn_act, dim3((unsigned)((nact / 4 + 255) / 256)), dim3(256), 0, st, t->Z[l],
-                               t->mean[l], t->invstd[l], P + L.bg[l], P + L.bb[l], skip_of(l), t->A[l], nact);
+        const float* skip = (l >= 2 && l % 2 == 0) ? t->A[l - 2] : nullptr;  // block output adds the block input
+        const long long n = (long long)R * kC;
+        hipLaunchKernelGGL(k_bn_act, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, t->Z[l], t->mean[l],
+                           t->invstd[l], P + L.bg[l], P + L.bb[l], skip, t->A[l], n);
     }
     (void)NB;
     // ---- heads
@@ -1445,9 +1221,6 @@ static int backward(oaz_trainer* t, int bi) {
     // ---- trunk backward; t->part holds the BN-backward partials of layer l (nwg, [2][64]).
     // dZ of layer l feeds both dgrad(l) (on st, the critical path) and wgrad(l) (on st2); dZ and
     // the bias partials are double-buffered so st never overwrites what st2 still reads.
-    // fuse: dgrad(l) computes dZ of layer l from M[l] and Z[l] while loading it (k_bn_bwd_apply's
-    // arithmetic), stores it from its centre tap for wgrad(l) and sums it for the conv bias gradient; only
-    // layer 0, which has no dgrad, still runs k_bn_bwd_apply.
     int nwg_part = nwg_rows;
     bool used[2] = {false, false};
     for (int l = nl - 1; l >= 0; --l) {
@@ -1456,39 +1229,11 @@ static int backward(oaz_trainer* t, int bi) {
         float* mm = t->bcoef + 64;
         float* mx = t->bcoef + 128;
         float* dz = t->DZ[k];
-        const bool fused = t->fuse && l > 0;
         hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_part, 64, 0, 64, (double)R,
                            P + L.bg[l], t->invstd[l], G + L.bg[l], G + L.bb[l], c1, mm, mx);
         if (used[k]) HIP_TRY(hipStreamWaitEvent(st, t->ev_w[k], 0));
-        ConvArgs a{};
-        if (l > 0) {
-            a.in = dz;
-            a.w = t->wd[l];
-            a.out = t->M[l - 1];
-            a.part = t->part;
-            a.act = t->A[l - 1];
-            a.zprev = t->Z[l - 1];
-            a.mean = t->mean[l - 1];
-            a.invstd = t->invstd[l - 1];
-            a.skip = (l % 2 == 1) ? t->M[l + 1] : nullptr;  // first conv of a block: add the block-output gradient
-            a.chunks = 4;
-            a.B = B;
-        }
-        if (fused) {
-            a.iz = t->M[l];
-            a.iz2 = t->Z[l];
-            a.ic[0] = t->mean[l];
-            a.ic[1] = t->invstd[l];
-            a.ic[2] = c1;
-            a.ic[3] = mm;
-            a.ic[4] = mx;
-            a.in_out = dz;
-            a.ipart = t->bpart[k];
-            launch_conv<CONV_DGRAD, 1>(t->prec, 4, rg, conv_grid, st, a);
-        } else {
-            hipLaunchKernelGGL(k_bn_bwd_apply, dim3(nwg_rows), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
-                               t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
-        }
+        hipLaunchKernelGGL(k_bn_bwd_apply, dim3(nwg_rows), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
+                           t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
         HIP_TRY(hipEventRecord(t->ev_dz[k], st));
         HIP_TRY(hipStreamWaitEvent(t->st2, t->ev_dz[k], 0));
         const float* X = l == 0 ? t->X0 : t->A[l - 1];
@@ -1500,12 +1245,23 @@ static int backward(oaz_trainer* t, int bi) {
         const int nred = 9 * kC * cin;
         hipLaunchKernelGGL(k_wgrad_reduce, dim3((nred + 255) / 256), dim3(256), 0, t->st2, t->wpart,
                            l == 0 ? kInPad : kC, cin, G + L.cw[l]);
-        hipLaunchKernelGGL(k_colsum, dim3(1), dim3(1024), 0, t->st2, t->bpart[k], fused ? nwg_conv : nwg_rows, 64, 0,
-                           64, G + L.cb[l]);
+        hipLaunchKernelGGL(k_colsum, dim3(1), dim3(1024), 0, t->st2, t->bpart[k], nwg_rows, 64, 0, 64, G + L.cb[l]);
         HIP_TRY(hipEventRecord(t->ev_w[k], t->st2));
         used[k] = true;
         if (l == 0) break;
-        if (!fused) launch_conv<CONV_DGRAD, 0>(t->prec, 4, rg, conv_grid, st, a);
+        ConvArgs a{};
+        a.in = dz;
+        a.w = t->wd[l];
+        a.out = t->M[l - 1];
+        a.part = t->part;
+        a.act = t->A[l - 1];
+        a.zprev = t->Z[l - 1];
+        a.mean = t->mean[l - 1];
+        a.invstd = t->invstd[l - 1];
+        a.skip = (l % 2 == 1) ? t->M[l + 1] : nullptr;  // first conv of a block: add the block-output gradient
+        a.chunks = 4;
+        a.B = B;
+        launch_conv<CONV_DGRAD>(4, rg, conv_grid, st, a);
         nwg_part = nwg_conv;
     }
     HIP_TRY(hipEventRecord(t->ev_done, t->st2));
@@ -1540,7 +1296,6 @@ static int apply(oaz_trainer* t, float scale) {
     const long long n = (long long)t->nparam;
     ConvTab tab{};
     tab.n = t->nconv;
-    tab.prec = t->prec;
     for (int l = 0; l < t->nconv; ++l) {
         tab.off[l] = (int)t->L.cw[l];
         tab.cin[l] = l == 0 ? kIn : kC;

@@ -151,8 +151,7 @@ class oaz_train_config(C.Structure):
         ("bn_momentum", C.c_double),
         ("bn_eps", C.c_double),
         ("value_loss_broadcast", C.c_int32),
-        ("conv_exact", C.c_int32),
-        ("reserved", C.c_int32 * 6),
+        ("reserved", C.c_int32 * 7),
     ]
 
 

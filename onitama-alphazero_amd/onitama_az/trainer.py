@@ -33,15 +33,13 @@ class EpochLoss:  # the per-epoch line of train.rs:316-324
 
 class Trainer:
     def __init__(self, blocks: int, max_batch: int = 512, learning_rate: float = 5e-3, momentum: float = 0.9,
-                 weight_decay: float = 1e-4, value_loss_broadcast: bool = True, device: int = 0,
-                 conv_exact: bool = False):
+                 weight_decay: float = 1e-4, value_loss_broadcast: bool = True, device: int = 0):
         lib = _abi.load()
         cfg = _abi.oaz_train_config()
         lib.oaz_train_config_default(C.byref(cfg))
         cfg.blocks, cfg.max_batch = int(blocks), int(max_batch)
         cfg.learning_rate, cfg.momentum, cfg.weight_decay = learning_rate, momentum, weight_decay
         cfg.value_loss_broadcast = int(bool(value_loss_broadcast))
-        cfg.conv_exact = int(bool(conv_exact))  # 0: conv products by the three-piece bf16 split
         h = lib.oaz_trainer_create(C.byref(cfg), int(device))
         if not h:
             raise _abi.OazError(f"oaz_trainer_create failed: {lib.oaz_last_error().decode()}")

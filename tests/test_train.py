@@ -2,9 +2,7 @@
 torch-CPU restatement of net.rs forward(train=true) + alphaloss + tch SGD (train.rs:264-313).
 
 Tolerances (fp32 GPU vs fp64 CPU): gradients within 2e-4 x the tensor's max |g| (+1e-7), losses
-within 1e-5 relative, parameters / running stats within 1e-6 + 1e-5 relative after the step; the same
-bars for both conv product modes (oaz_train_config.conv_exact = 0, the default: a three-piece bf16 split of
-both operands, six products, ~2^-24 relative per product; 1: exact fp32 MFMA products).
+within 1e-5 relative, parameters / running stats within 1e-6 + 1e-5 relative after the step.
 """
 import sys
 from pathlib import Path
@@ -54,8 +52,8 @@ def _close_grads(got, ref):
     for k, g in ref.items():
         scale = float(np.abs(g).max())
         errs[k] = (float(np.abs(got[k].reshape(g.shape) - g).max()), scale)
-    worst = sorted(errs.items(), key=lambda kv: -kv[1][0] / (2e-4 * kv[1][1] + 1e-7))[:6]
-    print("worst gradient errors (err / max|g|):", [(k, f"{e / (sc + 1e-30):.2e}") for k, (e, sc) in worst])
+    worst = sorted(errs.items(), key=lambda kv: -kv[1][0] / (2e-4 * kv[1][1] + 1e-7))[:4]  # closest to the bar
+    print("gradient errors closest to the bar (err, max|g|):", [(k, f"{e:.2e}", f"{sc:.2e}") for k, (e, sc) in worst])
     for k, (err, scale) in errs.items():
         assert err <= 2e-4 * scale + 1e-7, (k, err, scale)
 
@@ -102,14 +100,13 @@ def test_trainer_without_device_is_a_loud_error(lib):
 
 
 # ---- GPU parity ---------------------------------------------------------------------------------
-def _run_steps(orc, blocks, B, steps, broadcast=True, seed=1, conv_exact=False):
+def _run_steps(orc, blocks, B, steps, broadcast=True, seed=1):
     from onitama_az.trainer import Trainer
     from train_ref import train_step
     samples, planes = _batch(orc, B * steps, seed)
     w = _weights(seed, blocks)
     named = named_from_blob(w, blocks)
-    ltol = 1e-5
-    with Trainer(blocks=blocks, max_batch=B, value_loss_broadcast=broadcast, conv_exact=conv_exact) as tr:
+    with Trainer(blocks=blocks, max_batch=B, value_loss_broadcast=broadcast) as tr:
         tr.set_weights(w)
         tr.load_samples(samples)
         idx = np.arange(B * steps, dtype=np.int32).reshape(steps, B)[:, ::-1].copy()  # non-trivial gather
@@ -125,20 +122,18 @@ def _run_steps(orc, blocks, B, steps, broadcast=True, seed=1, conv_exact=False):
             tr.apply(1.0)
             v, p, k = tr.losses()
             assert k == 1
-            assert abs(v - lv) <= ltol * abs(lv) + 1e-7 and abs(p - lp) <= ltol * abs(lp) + 1e-7, (v, lv, p, lp)
+            assert abs(v - lv) <= 1e-5 * abs(lv) + 1e-7 and abs(p - lp) <= 1e-5 * abs(lp) + 1e-7, (v, lv, p, lp)
             _close_params(named_from_blob(tr.get_weights(), blocks), named)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("conv_exact", [False, True])
-def test_train_step_matches_reference_restatement(orc, conv_exact):
-    _run_steps(orc, blocks=3, B=64, steps=1, conv_exact=conv_exact)
+def test_train_step_matches_reference_restatement(orc):
+    _run_steps(orc, blocks=3, B=64, steps=1)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("conv_exact", [False, True])
-def test_train_two_steps_momentum(orc, conv_exact):
-    _run_steps(orc, blocks=2, B=32, steps=2, seed=5, conv_exact=conv_exact)
+def test_train_two_steps_momentum(orc):
+    _run_steps(orc, blocks=2, B=32, steps=2, seed=5)
 
 
 @pytest.mark.gpu
@@ -147,9 +142,8 @@ def test_train_step_elementwise_value_loss(orc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("conv_exact", [False, True])
-def test_train_step_reference_batch_512(orc, conv_exact):
-    _run_steps(orc, blocks=3, B=512, steps=1, seed=9, conv_exact=conv_exact)
+def test_train_step_reference_batch_512(orc):
+    _run_steps(orc, blocks=3, B=512, steps=1, seed=9)
 
 
 @pytest.mark.gpu
