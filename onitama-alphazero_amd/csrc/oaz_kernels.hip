@@ -638,13 +638,33 @@ __device__ __forceinline__ int root_fold(int K, int Kmax, const NodeRegs (&ch)[3
 // Where node i of a game's tree lives: its slot of t.nodes (the per-step kernels), or, in the one-launch
 // search (oaz_search_lat.hip), LDS for the first n nodes of the workgroup's one game (the top of the tree,
 // allocated first) and t.nodes beyond. Generic pointers: the same loads and stores reach either.
+// The same accessor serves the walk's other per-level / per-simulation reads: sqrt(N) from the host-built
+// table (one dependent load per tree level) and the game's root position.
 struct NodesGlobal {
     __device__ __forceinline__ oaz_node* at(oaz_node* T, uint32_t i) const { return T + i; }
+    __device__ __forceinline__ double sqrt_n(const TreeView& t, uint32_t n) const { return t.sqrt_tab[n]; }
+    __device__ __forceinline__ const oaz_state* root(const oaz_state* roots, uint32_t g) const { return &roots[g]; }
+    __device__ __forceinline__ void add(uint64_t* st, int f, uint64_t v) const { stat_add(&st[f], v); }
+    __device__ __forceinline__ void max(uint64_t* st, int f, uint64_t v) const { stat_max(&st[f], v); }
 };
 struct NodesCached {
-    oaz_node* L;  // LDS: nodes [0, n)
+    oaz_node* L;        // LDS: nodes [0, n)
     uint32_t n;
+    const double* sq;   // LDS: sqrt_tab [0, nsq)
+    uint32_t nsq;
+    const oaz_state* rt;  // LDS: the workgroup's game's root position
+    uint64_t* stl;        // LDS: the game's statistics, added to its global slots once at the end of the launch
     __device__ __forceinline__ oaz_node* at(oaz_node* T, uint32_t i) const { return i < n ? L + i : T + i; }
+    __device__ __forceinline__ double sqrt_n(const TreeView& t, uint32_t k) const {
+        return k < nsq ? sq[k] : t.sqrt_tab[k];
+    }
+    __device__ __forceinline__ const oaz_state* root(const oaz_state*, uint32_t) const { return rt; }
+    __device__ __forceinline__ void add(uint64_t*, int f, uint64_t v) const {
+        (void)__hip_atomic_fetch_add(&stl[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __device__ __forceinline__ void max(uint64_t*, int f, uint64_t v) const {
+        (void)__hip_atomic_fetch_max(&stl[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
 };
 
 // g: this segment's game (>= t.G: an idle segment); leaf_lds: also store the leaf position there (LDS of
@@ -659,7 +679,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
     const bool fold_mode = prm.train_noise && noise;
     oaz_node* T = t.nodes + (size_t)(on ? g : 0) * t.cap;
     uint32_t* path = t.path + (size_t)(on ? g : 0) * t.pathcap;
-    oaz_state s = load_state(&roots[on ? g : 0]);
+    oaz_state s = load_state(na.root(roots, on ? g : 0));
     int color = s.to_move & 1;
     NodeRegs nd = load_node(na.at(T, 0));
     uint32_t node = 0, depth = 0;
@@ -685,7 +705,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
             ch[c].misc = 0;
             if (go && j < K) ch[c] = load_node(na.at(T, nd.first + j));
         }
-        const double sqn = go ? t.sqrt_tab[nd.N] : 0.0;
+        const double sqn = go ? na.sqrt_n(t, nd.N) : 0.0;
         int best = 0;
         if (depth == 0 && fold_mode) {
             // root with noise: the sequential Iterator::max_by fold of k_select, every segment's
@@ -754,10 +774,10 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
         t.depth[g] = depth;
         if (t.need) t.need[g] = need;
         uint64_t* st = t.stats + (size_t)g * GS_COUNT;
-        stat_add(&st[GS_SIMS], 1);
-        stat_add(&st[GS_DEPTH], depth);
-        stat_add(&st[GS_EVALS], need);
-        if (stuck) stat_add(&st[GS_STUCK], 1);
+        na.add(st, GS_SIMS, 1);
+        na.add(st, GS_DEPTH, depth);
+        na.add(st, GS_EVALS, need);
+        if (stuck) na.add(st, GS_STUCK, 1);
     } else if (!on && g < t.G && sl == 0 && t.need) {
         t.need[g] = 0;  // an idle slot: nothing to evaluate
     }
@@ -889,18 +909,18 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
             lp->first = base;
             lp->nch = (uint8_t)K;
             lp->flags = 1;
-            stat_add(&st[GS_EXPANSIONS], 1);
-            stat_add(&st[GS_CHILDREN], K);
-            stat_max(&st[GS_MAXNODES], base + K);
+            na.add(st, GS_EXPANSIONS, 1);
+            na.add(st, GS_CHILDREN, K);
+            na.max(st, GS_MAXNODES, base + K);
         }
     }
     const int res = current_state(s);
     double r;
     if (is_win(res)) {
-        const int root_color = roots[g].to_move & 1;
+        const int root_color = na.root(roots, g)->to_move & 1;
         const int pc = depth == 0 ? root_color : (root_color ^ (int)((depth - 1) & 1));
         r = reward(res, pc);
-        if (sl == 0) stat_add(&st[GS_TERMINAL], 1);
+        if (sl == 0) na.add(st, GS_TERMINAL, 1);
     } else {
         r = (double)vrow;
     }

@@ -23,13 +23,20 @@ namespace oaz {
 constexpr int kLatThreads = 512;  // 8 waves: k_nn_h3s's geometry; wave 4 also walks the tree
 
 // LDS of k_search_lat beside the network's (h3s::kBytes): the walker's per-game records (leaf position,
-// leaf, depth, node count), its path, and the top of the game's tree (nodes [0, kLatCache): the root and
-// the first expansions, which every walk passes through).
+// leaf, depth, node count), the leaf's evaluation (the network's heads write it here), the game's statistics,
+// its path, the root position and the sqrt(N) table (each walk level and each simulation would otherwise wait
+// on a global round trip for them), and the top of the game's tree (nodes [0, kLatCache): the root and the
+// first expansions, which every walk passes through).
 constexpr int kLatStateOff = h3s::kBytes;          // oaz_state
 constexpr int kLatVarsOff = kLatStateOff + 32;     // leaf, depth, n_nodes
-constexpr int kLatPathOff = kLatVarsOff + 16;
+constexpr int kLatPolOff = kLatVarsOff + 16;       // the leaf's evaluation: policy[50], value
+constexpr int kLatStatOff = kLatPolOff + 52 * 4;   // the game's statistics (added to its global slots at the end)
+constexpr int kLatPathOff = kLatStatOff + GS_COUNT * 8;
 constexpr int kLatPath = 2048;                     // path entries held in LDS (pathcap = sims + 1)
-constexpr int kLatCacheOff = (kLatPathOff + kLatPath * 4 + 31) & ~31;
+constexpr int kLatRootOff = kLatPathOff + kLatPath * 4;  // the game's root position
+constexpr int kLatSqOff = kLatRootOff + 32;        // sqrt_tab [0, kLatSq): the walk's per-level sqrt(N)
+constexpr int kLatSq = 1024;
+constexpr int kLatCacheOff = (kLatSqOff + kLatSq * 8 + 31) & ~31;
 constexpr int kLatLds = H3Fallback<H3Cfg<0>>::kLds * 4;
 constexpr uint32_t kLatCache = (uint32_t)((kLatLds - kLatCacheOff) / (int)sizeof(oaz_node));
 
@@ -122,7 +129,34 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
     if (path_lds) tl.path = reinterpret_cast<uint32_t*>(lb + kLatPathOff);
     // tl.nodes stays the game's global slot: the node accessor maps nodes [0, ncached) to the LDS copy
     const uint32_t ncached = kLatCache < t.cap ? kLatCache : t.cap;
-    const NodesCached na{reinterpret_cast<oaz_node*>(lb + kLatCacheOff), ncached};
+    const uint32_t nsq = (uint32_t)sims + 1 < (uint32_t)kLatSq ? (uint32_t)sims + 1 : (uint32_t)kLatSq;
+    uint64_t* const stl = reinterpret_cast<uint64_t*>(lb + kLatStatOff);
+    const NodesCached na{reinterpret_cast<oaz_node*>(lb + kLatCacheOff), ncached,
+                         reinterpret_cast<const double*>(lb + kLatSqOff), nsq,
+                         reinterpret_cast<const oaz_state*>(lb + kLatRootOff), stl};
+    float* const pol = reinterpret_cast<float*>(lb + kLatPolOff);  // the leaf's policy row, value at [50]
+    // the root position and sqrt(0 .. sims) (read-only for the launch) and zeroed statistics: at the start and
+    // after an fp16-range recompute (which uses the whole LDS)
+    auto fill_resident = [&] {
+        double* sq = reinterpret_cast<double*>(lb + kLatSqOff);
+        for (uint32_t k = threadIdx.x; k < nsq; k += kLatThreads) sq[k] = t.sqrt_tab[k];
+        static_assert(sizeof(oaz_state) % 4 == 0 && sizeof(oaz_state) <= 32, "root copy");
+        if (threadIdx.x < sizeof(oaz_state) / 4)
+            reinterpret_cast<uint32_t*>(lb + kLatRootOff)[threadIdx.x] =
+                reinterpret_cast<const uint32_t*>(roots + g)[threadIdx.x];
+        if (threadIdx.x < GS_COUNT) stl[threadIdx.x] = 0;
+    };
+    auto flush_stats = [&] {  // the statistics gathered in LDS to the game's slots (one writer: this workgroup)
+        if (threadIdx.x < GS_COUNT) {
+            const uint64_t v = stl[threadIdx.x];
+            if (threadIdx.x == GS_MAXNODES) {
+                if (v > tg.stats[threadIdx.x]) tg.stats[threadIdx.x] = v;
+            } else if (v) {
+                tg.stats[threadIdx.x] += v;
+            }
+        }
+    };
+    fill_resident();
     const oaz_state* rg = roots + g;
     const uint8_t* ag = active ? active + g : nullptr;
     const uint32_t gs = walker && lane < 16 ? 0u : 1u;  // the walker's segment 0 holds the game
@@ -151,7 +185,7 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
         }
         if (walker) {
             lap(2);
-            if (s > 0) lat_backup(tl, rg, ag, policy + (size_t)g * 50, value + g, gs, sp, na);  // simulation s - 1's
+            if (s > 0) lat_backup(tl, rg, ag, pol, pol + 50, gs, sp, na);  // simulation s - 1's
             lap(0);
             lat_select(tl, rg, ag, prm, gs, na);
             lap(1);
@@ -161,16 +195,18 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
             if (threadIdx.x < 64) {
                 const oaz_state st = *tl.leaf_state;
                 const uint64_t h = hash_state(st);
-                if (lane < 50) policy[(size_t)g * 50 + lane] = hash_policy(h, lane);
-                if (lane == 0) value[g] = hash_value(h);
+                if (lane < 50) pol[lane] = hash_policy(h, lane);
+                if (lane == 0) pol[50] = hash_value(h);
             }
         } else {
             int opaque;  // 0, opaque to the compiler: no lane offset of the body is hoisted out of this loop
             asm volatile("v_mov_b32 %0, 0" : "=v"(opaque));
-            const bool ovf = nn_h3s_body<C>(t.leaf_state, (int)g, blob, blocks, policy, value, lds, opaque,
+            // row 0 of (pol, pol + 50): the heads write the evaluation to LDS, where the backup reads it
+            const bool ovf = nn_h3s_body<C>(t.leaf_state, 0, blob, blocks, pol, pol + 50, lds, opaque,
                                             H3sResident{tl.leaf_state, nullptr, true});
             if (__syncthreads_or(ovf)) {  // k_nn_h3s's recompute of this position (the k_nn_x6 body), which
                                           // needs the whole LDS: the tree state goes out and comes back
+                flush_stats();
                 lat_sync_tree(tl, tg, na, path_lds, true);
                 __syncthreads();
                 using X = typename H3Fallback<C>::X;
@@ -182,6 +218,8 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
                 if (threadIdx.x == 0) atomicAdd(fallback, 1ull);
                 __syncthreads();
                 lat_sync_tree(tl, tg, na, path_lds, false);
+                fill_resident();
+                if (threadIdx.x < 51) pol[threadIdx.x] = threadIdx.x < 50 ? policy[(size_t)g * 50 + threadIdx.x] : value[g];
                 resident = false;
             }
         }
@@ -189,7 +227,7 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
     }
     if (walker) {
         lap(2);
-        lat_backup(tl, rg, ag, policy + (size_t)g * 50, value + g, gs, sp, na);  // the last simulation's
+        lat_backup(tl, rg, ag, pol, pol + 50, gs, sp, na);  // the last simulation's
         lap(0);
         if constexpr (DBG == 1) {
             cyc[3] = tm - tm0;
@@ -204,6 +242,7 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
     }
     __syncthreads();
     lat_sync_tree(tl, tg, na, path_lds, true);  // the tree's top and the node count to global memory
+    flush_stats();
 }
 
 // ---- one launch per noise chunk for up to 16 x CU-count games (k_search_grp) ---------------------------
