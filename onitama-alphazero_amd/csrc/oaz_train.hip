@@ -137,6 +137,22 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
     // loads and MFMAs stay unconditional and the prefetch registers stay in VGPRs.
     const int bl = active ? b0 : 0;
     float4 wr[CH], av[CH], an[CH];
+    // DGRAD: the epilogue's operands (skip, the activation and pre-BN output of the layer below) do not
+    // depend on the MFMAs: requested now, they arrive while the taps run instead of after the last one
+    float ep[MODE == CONV_DGRAD ? NPW : 1][3][4];
+    if constexpr (MODE == CONV_DGRAD) {
+#pragma unroll
+        for (int n = 0; n < NPW; ++n) {
+            const int co = (n0 + n) * 16 + i;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const size_t o = (size_t)(sq * B + bl + kq * 4 + r) * kC + co;
+                ep[n][0][r] = a.skip ? a.skip[o] : 0.0f;
+                ep[n][1][r] = a.act[o];
+                ep[n][2][r] = a.zprev[o];
+            }
+        }
+    }
     int t = 0;
     while (nbr(sq, t) < 0) ++t;
     {
@@ -199,11 +215,11 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
                 for (int r = 0; r < 4; ++r) {
                     const size_t o = (size_t)(sq * B + b0 + kq * 4 + r) * kC + co;
                     float d = acc[n][r];
-                    if (a.skip) d += a.skip[o];
-                    const float m = a.act[o] > 0.0f ? d : 0.0f;
+                    if (a.skip) d += ep[n][0][r];
+                    const float m = ep[n][1][r] > 0.0f ? d : 0.0f;
                     a.out[o] = m;
                     s1 += m;
-                    s2 += m * ((a.zprev[o] - mu) * is);
+                    s2 += m * ((ep[n][2][r] - mu) * is);
                 }
             }
         }
@@ -229,8 +245,11 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
 // part [nwg][2][pstride] (sum, sumsq) columns coff..coff+C-1; torch batch_norm(training=True):
 // y = (x - mean) * invstd * gamma + beta, invstd = 1/sqrt(var_biased + eps);
 // running = (1 - m) * running + m * {mean, var_unbiased}.
+// Channels c >= split take their running statistics from rmean2 / rvar2 [c - split] (the two heads' BN
+// layers in one launch: the value head's channel, then the policy head's two); split = C: one layer.
 __global__ __launch_bounds__(1024) void k_bn_fwd_fin(const float* part, int nwg, int pstride, int coff, int C, double N,
-                             float* rmean, float* rvar, float bn_mom, float eps, float* mean, float* invstd) {
+                             float* rmean, float* rvar, float bn_mom, float eps, float* mean, float* invstd,
+                             int split, float* rmean2, float* rvar2) {
     __shared__ double sh[2][16][64];
     const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
     double s1 = 0.0, s2 = 0.0;
@@ -266,8 +285,10 @@ __global__ __launch_bounds__(1024) void k_bn_fwd_fin(const float* part, int nwg,
         if (var < 0.0) var = 0.0;
         mean[c] = (float)mu;
         invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-        rmean[c] = (float)((1.0 - bn_mom) * rmean[c] + bn_mom * mu);
-        rvar[c] = (float)((1.0 - bn_mom) * rvar[c] + bn_mom * var * N / (N - 1.0));
+        float* rm = c < split ? rmean + c : rmean2 + (c - split);
+        float* rv = c < split ? rvar + c : rvar2 + (c - split);
+        *rm = (float)((1.0 - bn_mom) * *rm + bn_mom * mu);
+        *rv = (float)((1.0 - bn_mom) * *rv + bn_mom * var * N / (N - 1.0));
     }
 }
 
@@ -292,9 +313,11 @@ __global__ void k_bn_act(const float* Z, const float* mean, const float* invstd,
 }
 
 // ---- BN backward finalisation: dgamma = sum m*xhat, dbeta = sum m; dx coefficients -----------------
+// Channels c >= split: gamma2 / ggamma2 / gbeta2 [c - split] (both heads in one launch, as k_bn_fwd_fin).
 __global__ __launch_bounds__(1024) void k_bn_bwd_fin(const float* part, int nwg, int pstride, int coff, int C, double N,
                              const float* gamma, const float* invstd, float* ggamma, float* gbeta,
-                             float* c1, float* mm, float* mx) {
+                             float* c1, float* mm, float* mx, int split, const float* gamma2, float* ggamma2,
+                             float* gbeta2) {
     __shared__ double sh[2][16][64];
     const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
     double s1 = 0.0, s2 = 0.0;
@@ -325,9 +348,10 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_fin(const float* part, int nwg,
             s1 += sh[0][k][c];
             s2 += sh[1][k][c];
         }
-        gbeta[c] = (float)s1;
-        ggamma[c] = (float)s2;
-        c1[c] = gamma[c] * invstd[c];
+        const bool lo = c < split;
+        (lo ? gbeta + c : gbeta2 + (c - split))[0] = (float)s1;
+        (lo ? ggamma + c : ggamma2 + (c - split))[0] = (float)s2;
+        c1[c] = (lo ? gamma[c] : gamma2[c - split]) * invstd[c];
         mm[c] = (float)(s1 / N);
         mx[c] = (float)(s2 / N);
     }
@@ -513,22 +537,21 @@ struct HeadStats {  // head BN batch statistics (channel 0 = value, 1..2 = polic
 };
 
 // Value MLP (25 -> 64 -> 1, tanh), policy linear (50 -> 50) + softmax, alphaloss terms
-// (net.rs:234-243) and their backward down to the head BN outputs. 16 lanes per sample (an
-// aligned 16-lane group: reductions are 4 xor-shuffles), 16 samples per workgroup.
+// (net.rs:234-243) and their backward down to the head BN outputs. One wave (64 lanes) per sample,
+// kHS = 4 samples per workgroup: at batch 512 that is 128 workgroups, and each lane's dependent
+// chains of LDS reads are a quarter of a 16-lane-per-sample layout's (one wave per SIMD cannot hide
+// them; the kernel is on the step's critical path).
 // Q16: with value_loss_broadcast the value loss is mean_{i,j} (z_j - v_i)^2 over [B,B].
-constexpr int kHS = 16;  // samples per workgroup
-__device__ __forceinline__ float sum16(float v) {
-    v += __shfl_xor(v, 1);
-    v += __shfl_xor(v, 2);
-    v += __shfl_xor(v, 4);
-    v += __shfl_xor(v, 8);
+constexpr int kHS = 4;           // samples per workgroup
+constexpr int kTPS = 256 / kHS;  // lanes per sample (a whole wave)
+__device__ __forceinline__ float sumT(float v) {
+#pragma unroll
+    for (int o = 1; o < kTPS; o <<= 1) v += __shfl_xor(v, o);
     return v;
 }
-__device__ __forceinline__ float max16(float v) {
-    v = fmaxf(v, __shfl_xor(v, 1));
-    v = fmaxf(v, __shfl_xor(v, 2));
-    v = fmaxf(v, __shfl_xor(v, 4));
-    v = fmaxf(v, __shfl_xor(v, 8));
+__device__ __forceinline__ float maxT(float v) {
+#pragma unroll
+    for (int o = 1; o < kTPS; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
     return v;
 }
 
@@ -539,7 +562,7 @@ __global__ __launch_bounds__(256) void k_head_sample(const float* hz, const floa
     __shared__ float W[kHeadW];  // l1w[64][25] l1b[64] l2w[64] l2b | plw[50][50] plb[50]
     __shared__ float hv[kHS][25], h1[kHS][64], dh1[kHS][64], hp[kHS][50], dl[kHS][50], du[kHS];
     __shared__ float red[4][8];
-    const int tid = threadIdx.x, j = tid & 15, sl = tid >> 4, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, j = tid % kTPS, sl = tid / kTPS, lane = tid & 63, wave = tid >> 6;
     for (int k = tid; k < kHeadVW; k += 256) W[k] = P[o.l1w + k];
     for (int k = tid; k < 2550; k += 256) W[kHeadVW + k] = P[o.plw + k];
     float sz = 0.0f, sz2 = 0.0f;
@@ -569,12 +592,12 @@ __global__ __launch_bounds__(256) void k_head_sample(const float* hz, const floa
     const int b = blockIdx.x * kHS + sl;
     const bool ok = b < B;
     const float vm = hst_mean[0], vi = hst_inv[0], vg = P[o.vg], vb = P[o.vb];
-    for (int sq = j; sq < 25; sq += 16) {
+    for (int sq = j; sq < 25; sq += kTPS) {
         float y = 0.0f;
         if (ok) y = (hz[(size_t)(sq * B + b) * 4] - vm) * vi * vg + vb;
         hv[sl][sq] = y > 0.0f ? y : 0.0f;
     }
-    for (int k = j; k < 50; k += 16) {
+    for (int k = j; k < 50; k += kTPS) {
         const int c = k / 25, sq = k % 25;
         float y = 0.0f;
         if (ok) y = (hz[(size_t)(sq * B + b) * 4 + 1 + c] - hst_mean[1 + c]) * hst_inv[1 + c] * P[o.pg + c] + P[o.pb + c];
@@ -583,20 +606,21 @@ __global__ __launch_bounds__(256) void k_head_sample(const float* hz, const floa
     __syncthreads();
     // value MLP forward
     float up = 0.0f;
-    for (int oo = j; oo < 64; oo += 16) {
+    for (int oo = j; oo < 64; oo += kTPS) {
         float a = l1b[oo];
         for (int sq = 0; sq < 25; ++sq) a += l1w[oo * 25 + sq] * hv[sl][sq];
         a = a > 0.0f ? a : 0.0f;
         h1[sl][oo] = a;
         up += l2w[oo] * a;
     }
-    const float v = tanhf(sum16(up) + l2b);
+    const float v = tanhf(sumT(up) + l2b);
     // policy linear + softmax
-    float lg[4];
+    constexpr int NQ = (50 + kTPS - 1) / kTPS;  // policy entries per lane
+    float lg[NQ];
     float mxl = -INFINITY;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int jj = j + 16 * q;
+    for (int q = 0; q < NQ; ++q) {
+        const int jj = j + kTPS * q;
         lg[q] = -INFINITY;
         if (jj < 50) {
             float a = plb[jj];
@@ -605,24 +629,24 @@ __global__ __launch_bounds__(256) void k_head_sample(const float* hz, const floa
             mxl = fmaxf(mxl, a);
         }
     }
-    mxl = max16(mxl);
+    mxl = maxT(mxl);
     float se = 0.0f, spi = 0.0f;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int jj = j + 16 * q;
+    for (int q = 0; q < NQ; ++q) {
+        const int jj = j + kTPS * q;
         if (jj < 50) {
             lg[q] = expf(lg[q] - mxl);
             se += lg[q];
             spi += ok ? pi[(size_t)b * 50 + jj] : 0.0f;
         }
     }
-    se = sum16(se);
-    spi = sum16(spi);
+    se = sumT(se);
+    spi = sumT(spi);
     const float inv25B = 1.0f / (25.0f * (float)B);
     float lp = 0.0f;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int jj = j + 16 * q;
+    for (int q = 0; q < NQ; ++q) {
+        const int jj = j + kTPS * q;
         if (jj < 50) {
             const float p = lg[q] / se;
             const float t = ok ? pi[(size_t)b * 50 + jj] : 0.0f;
@@ -630,7 +654,7 @@ __global__ __launch_bounds__(256) void k_head_sample(const float* hz, const floa
             dl[sl][jj] = ok ? (p * spi - t) * inv25B : 0.0f;
         }
     }
-    lp = sum16(lp) * inv25B;
+    lp = sumT(lp) * inv25B;
     // value loss and d/dv
     const float fB = (float)B;
     float lv = 0.0f, dv = 0.0f;
@@ -646,12 +670,12 @@ __global__ __launch_bounds__(256) void k_head_sample(const float* hz, const floa
     }
     const float duv = dv * (1.0f - v * v);
     if (j == 0) du[sl] = duv;
-    for (int oo = j; oo < 64; oo += 16) dh1[sl][oo] = h1[sl][oo] > 0.0f ? duv * l2w[oo] : 0.0f;
+    for (int oo = j; oo < 64; oo += kTPS) dh1[sl][oo] = h1[sl][oo] > 0.0f ? duv * l2w[oo] : 0.0f;
     __syncthreads();
     // backward into the head BN outputs
     float bnp[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // (sum g, sum g*xhat) x channel
     if (ok) {
-        for (int sq = j; sq < 25; sq += 16) {
+        for (int sq = j; sq < 25; sq += kTPS) {
             float d = 0.0f;
             for (int oo = 0; oo < 64; ++oo) d += l1w[oo * 25 + sq] * dh1[sl][oo];
             const float g = hv[sl][sq] > 0.0f ? d : 0.0f;
@@ -660,7 +684,7 @@ __global__ __launch_bounds__(256) void k_head_sample(const float* hz, const floa
             bnp[0] += g;
             bnp[1] += g * ((hz[r * 4] - vm) * vi);
         }
-        for (int k = j; k < 50; k += 16) {
+        for (int k = j; k < 50; k += kTPS) {
             float d = 0.0f;
             for (int jj = 0; jj < 50; ++jj) d += plw[jj * 50 + k] * dl[sl][jj];
             const float g = hp[sl][k] > 0.0f ? d : 0.0f;
@@ -727,17 +751,25 @@ __global__ __launch_bounds__(1024) void k_colsum(const float* part, int nwg, int
     }
 }
 
-// Loss accumulators (double) += this step's sums
+// Loss accumulators (double) += this step's sums (one wave: lane-strided partials, then a fixed-order
+// tree over the lanes)
 __global__ void k_loss_acc(const float* part_loss, int nwg, double* acc) {
-    if (threadIdx.x != 0) return;
+    const int lane = threadIdx.x;
     double v = 0.0, p = 0.0;
-    for (int w = 0; w < nwg; ++w) {
+    for (int w = lane; w < nwg; w += 64) {
         v += part_loss[2 * w];
         p += part_loss[2 * w + 1];
     }
-    acc[0] += v;
-    acc[1] += p;
-    acc[2] += 1.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        v += __shfl_xor(v, o);
+        p += __shfl_xor(p, o);
+    }
+    if (lane == 0) {
+        acc[0] += v;
+        acc[1] += p;
+        acc[2] += 1.0;
+    }
 }
 
 // Per trunk row: head BN backward -> dA = wv * dzv + wp0 * dzp0 + wp1 * dzp1; m = dA * (A > 0);
@@ -905,7 +937,7 @@ struct oaz_trainer {
     int device = 0;
     hipStream_t own = nullptr, st = nullptr;
     hipStream_t st2 = nullptr;  // weight-gradient stream: wgrad(l) overlaps dgrad(l) on st
-    hipEvent_t ev_dz[2] = {}, ev_w[2] = {}, ev_done = nullptr;
+    hipEvent_t ev_dz[2] = {}, ev_w[2] = {}, ev_h[2] = {}, ev_done = nullptr;
     Layout L{};
     int nconv = 0, maxB = 0;
     int conv_rg = 2;  // 16-row groups per conv workgroup (OAZ_CONV_RG=1|2|4 overrides; tuning knob)
@@ -952,6 +984,8 @@ struct oaz_trainer {
             if (ev_w[k]) (void)hipEventDestroy(ev_w[k]);
         }
         if (ev_done) (void)hipEventDestroy(ev_done);
+        for (hipEvent_t ev : ev_h)
+            if (ev) (void)hipEventDestroy(ev);
         if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
         if (graph) (void)hipGraphDestroy(graph);
         if (st2) (void)hipStreamDestroy(st2);
@@ -1006,7 +1040,8 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
                  hipEventCreateWithFlags(&t->ev_done, hipEventDisableTiming) == hipSuccess;
     for (int k = 0; k < 2 && ev_ok; ++k)
         ev_ok = hipEventCreateWithFlags(&t->ev_dz[k], hipEventDisableTiming) == hipSuccess &&
-                hipEventCreateWithFlags(&t->ev_w[k], hipEventDisableTiming) == hipSuccess;
+                hipEventCreateWithFlags(&t->ev_w[k], hipEventDisableTiming) == hipSuccess &&
+                hipEventCreateWithFlags(&t->ev_h[k], hipEventDisableTiming) == hipSuccess;
     if (!ev_ok || hipStreamCreateWithFlags(&t->own, hipStreamNonBlocking) != hipSuccess) {
         oaz_set_err(OAZ_ERR_HIP, "trainer: stream");
         return fail();
@@ -1179,7 +1214,7 @@ static int backward(oaz_trainer* t, int bi) {
         a.B = B;
         launch_conv<CONV_FWD>(l == 0 ? 2 : 4, rg, conv_grid, st, a);
         hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_conv, 64, 0, 64, (double)R,
-                           P + L.brm[l], P + L.brv[l], bn_mom, eps, t->mean[l], t->invstd[l]);
+                           P + L.brm[l], P + L.brv[l], bn_mom, eps, t->mean[l], t->invstd[l], 64, nullptr, nullptr);
         const float* skip = (l >= 2 && l % 2 == 0) ? t->A[l - 2] : nullptr;  // block output adds the block input
         const long long n = (long long)R * kC;
         hipLaunchKernelGGL(k_bn_act, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, t->Z[l], t->mean[l],
@@ -1195,29 +1230,31 @@ static int backward(oaz_trainer* t, int bi) {
     float* hc1 = t->hstat + 6;
     float* hmm = t->hstat + 9;
     float* hmx = t->hstat + 12;
-    hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->hpart, nwg_hc, 4, 0, 1, (double)R,
-                       P + h.vrm, P + h.vrv, bn_mom, eps, hmean, hinv);
-    hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->hpart, nwg_hc, 4, 1, 2, (double)R,
-                       P + h.prm, P + h.prv, bn_mom, eps, hmean + 1, hinv + 1);
+    hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->hpart, nwg_hc, 4, 0, 3, (double)R,
+                       P + h.vrm, P + h.vrv, bn_mom, eps, hmean, hinv, 1, P + h.prm, P + h.prv);
     const int nwg_hs = (B + kHS - 1) / kHS;
     float* hbpart = t->hpart + (size_t)nwg_hc * 8;
     hipLaunchKernelGGL(k_head_sample, dim3(nwg_hs), dim3(256), 0, st, t->hz, hmean, hinv, P, h, t->pi, t->z, B,
                        t->cfg.value_loss_broadcast, t->g3, hbpart, t->hwpart, t->hlpart);
-    hipLaunchKernelGGL(k_loss_acc, dim3(1), dim3(64), 0, st, t->hlpart, nwg_hs, t->loss_acc);
-    hipLaunchKernelGGL(k_colsum, dim3((kHeadVW + 63) / 64), dim3(1024), 0, st, t->hwpart, nwg_hs, kHeadW, 0,
+    // the losses and the heads' weight gradients are off the critical path: the weight-gradient stream
+    // sums them (st waits for st2 before SGD, and the next step's head_sample, ev_done)
+    HIP_TRY(hipEventRecord(t->ev_h[0], st));
+    HIP_TRY(hipStreamWaitEvent(t->st2, t->ev_h[0], 0));
+    hipLaunchKernelGGL(k_loss_acc, dim3(1), dim3(64), 0, t->st2, t->hlpart, nwg_hs, t->loss_acc);
+    hipLaunchKernelGGL(k_colsum, dim3((kHeadVW + 63) / 64), dim3(1024), 0, t->st2, t->hwpart, nwg_hs, kHeadW, 0,
                        kHeadVW, G + h.l1w);
-    hipLaunchKernelGGL(k_colsum, dim3((2550 + 63) / 64), dim3(1024), 0, st, t->hwpart, nwg_hs, kHeadW, kHeadVW,
+    hipLaunchKernelGGL(k_colsum, dim3((2550 + 63) / 64), dim3(1024), 0, t->st2, t->hwpart, nwg_hs, kHeadW, kHeadVW,
                        2550, G + h.plw);
-    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, hbpart, nwg_hs, 4, 0, 1, (double)R, P + h.vg,
-                       hinv, G + h.vg, G + h.vb, hc1, hmm, hmx);
-    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, hbpart, nwg_hs, 4, 1, 2, (double)R, P + h.pg,
-                       hinv + 1, G + h.pg, G + h.pb, hc1 + 1, hmm + 1, hmx + 1);
+    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, hbpart, nwg_hs, 4, 0, 3, (double)R, P + h.vg,
+                       hinv, G + h.vg, G + h.vb, hc1, hmm, hmx, 1, P + h.pg, G + h.pg, G + h.pb);
     const int nwg_rows = (R + 63) / 64;
     hipLaunchKernelGGL(k_head_bwd_rows, dim3(nwg_rows), dim3(256), 0, st, AL, t->Z[nl - 1], t->mean[nl - 1],
                        t->invstd[nl - 1], t->hz, t->g3, hmean, hinv, hc1, hmm, hmx, P, h, t->M[nl - 1], t->part,
                        t->hcpart, R);
-    hipLaunchKernelGGL(k_colsum, dim3(2), dim3(1024), 0, st, t->hcpart, nwg_rows, kHConvW, 0, 65, G + h.vcw);
-    hipLaunchKernelGGL(k_colsum, dim3(3), dim3(1024), 0, st, t->hcpart, nwg_rows, kHConvW, 65, 130, G + h.pcw);
+    HIP_TRY(hipEventRecord(t->ev_h[1], st));
+    HIP_TRY(hipStreamWaitEvent(t->st2, t->ev_h[1], 0));
+    hipLaunchKernelGGL(k_colsum, dim3(2), dim3(1024), 0, t->st2, t->hcpart, nwg_rows, kHConvW, 0, 65, G + h.vcw);
+    hipLaunchKernelGGL(k_colsum, dim3(3), dim3(1024), 0, t->st2, t->hcpart, nwg_rows, kHConvW, 65, 130, G + h.pcw);
     // ---- trunk backward; t->part holds the BN-backward partials of layer l (nwg, [2][64]).
     // dZ of layer l feeds both dgrad(l) (on st, the critical path) and wgrad(l) (on st2); dZ and
     // the bias partials are double-buffered so st never overwrites what st2 still reads.
@@ -1230,7 +1267,8 @@ static int backward(oaz_trainer* t, int bi) {
         float* mx = t->bcoef + 128;
         float* dz = t->DZ[k];
         hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_part, 64, 0, 64, (double)R,
-                           P + L.bg[l], t->invstd[l], G + L.bg[l], G + L.bb[l], c1, mm, mx);
+                           P + L.bg[l], t->invstd[l], G + L.bg[l], G + L.bb[l], c1, mm, mx, 64, nullptr, nullptr,
+                           nullptr);
         if (used[k]) HIP_TRY(hipStreamWaitEvent(st, t->ev_w[k], 0));
         hipLaunchKernelGGL(k_bn_bwd_apply, dim3(nwg_rows), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
                            t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
