@@ -25,20 +25,32 @@ constexpr int kLatThreads = 512;  // 8 waves: k_nn_h3s's geometry; wave 4 also w
 // LDS of k_search_lat beside the network's (h3s::kBytes): the walker's per-game records (leaf position,
 // leaf, depth, node count), the leaf's evaluation (the network's heads write it here), the game's statistics,
 // its path, the root position and the sqrt(N) table (each walk level and each simulation would otherwise wait
-// on a global round trip for them), and the top of the game's tree (nodes [0, kLatCache): the root and the
-// first expansions, which every walk passes through).
+// on a global round trip for them), and the top of the game's tree (its first nodes, as many as fit: the root
+// and the first expansions, which every walk passes through; lat_layout).
 constexpr int kLatStateOff = h3s::kBytes;          // oaz_state
 constexpr int kLatVarsOff = kLatStateOff + 32;     // leaf, depth, n_nodes
 constexpr int kLatPolOff = kLatVarsOff + 16;       // the leaf's evaluation: policy[50], value
 constexpr int kLatStatOff = kLatPolOff + 52 * 4;   // the game's statistics (added to its global slots at the end)
 constexpr int kLatPathOff = kLatStatOff + GS_COUNT * 8;
-constexpr int kLatPath = 2048;                     // path entries held in LDS (pathcap = sims + 1)
-constexpr int kLatRootOff = kLatPathOff + kLatPath * 4;  // the game's root position
-constexpr int kLatSqOff = kLatRootOff + 32;        // sqrt_tab [0, kLatSq): the walk's per-level sqrt(N)
-constexpr int kLatSq = 1024;
-constexpr int kLatCacheOff = (kLatSqOff + kLatSq * 8 + 31) & ~31;
+constexpr int kLatPath = 2048;                     // most path entries held in LDS (pathcap = sims + 1)
+constexpr int kLatSq = 2048;                       // most sqrt(N) entries held in LDS
 constexpr int kLatLds = H3Fallback<H3Cfg<0>>::kLds * 4;
-constexpr uint32_t kLatCache = (uint32_t)((kLatLds - kLatCacheOff) / (int)sizeof(oaz_node));
+// From kLatPathOff on the layout follows the launch's simulation count: the path (pathcap entries), the
+// root position, sqrt(0 .. sims), then as many tree nodes as the rest of the LDS holds.
+struct LatLayout {
+    int root, sq, cache;
+    uint32_t nsq, ncached;
+};
+__device__ __forceinline__ LatLayout lat_layout(uint32_t pathcap, bool path_lds, int sims, uint32_t cap) {
+    LatLayout l;
+    l.root = kLatPathOff + (path_lds ? (int)((pathcap * 4 + 15) & ~15u) : 0);
+    l.sq = l.root + 32;
+    l.nsq = (uint32_t)sims + 1 < (uint32_t)kLatSq ? (uint32_t)sims + 1 : (uint32_t)kLatSq;
+    l.cache = (l.sq + (int)l.nsq * 8 + 31) & ~31;
+    const uint32_t fit = (uint32_t)((kLatLds - l.cache) / (int)sizeof(oaz_node));
+    l.ncached = fit < cap ? fit : cap;
+    return l;
+}
 
 // The tree walk (wave 4 only) as calls of their own: the walk needs ~80 VGPRs, the network ~240 (the
 // compute waves hold a conv's weights), and inlined into one loop the two allocations spill; a call
@@ -53,6 +65,11 @@ __device__ __noinline__ void lat_backup(const TreeView& t, const oaz_state* root
 __device__ __noinline__ void lat_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                                         const SearchParams& prm, uint32_t gs, const NodesCached& na) {
     select_seg_body(t, roots, active, nullptr, prm, gs, nullptr, na);
+}
+// DBG 2 probe: a call with lat_select's arguments that only reads two of them
+__device__ __noinline__ void lat_probe(const TreeView& t, const oaz_state*, const uint8_t*, const SearchParams& prm,
+                                       uint32_t gs, const NodesCached& na) {
+    if (gs == 0 && threadIdx.x == 1000) *t.leaf = na.n + (uint32_t)prm.seed;  // never true: keeps the reads
 }
 
 // Copies the LDS-held tree state of the game to its global slots (out = true) or back (out = false):
@@ -89,7 +106,7 @@ __device__ __forceinline__ void lat_sync_tree(const TreeView& tl, const TreeView
     }
 }
 
-// DBG 1 (diagnostic, A/B build only: OAZ_LAT_DBG=1): the walker's s_memtime cycles in the expand / back up, the
+// DBG 1 (diagnostic, A/B build only: OAZ_LAT_DBG=1; 2 adds a probe call, GS_DROPPED): the walker's s_memtime cycles in the expand / back up, the
 // select, and the wait for the evaluation (barriers + network or HASH) are added to the game's statistics slots
 // GS_CUT / GS_RED / GS_BLUE (and the whole loop to GS_PASSES); the search's results are unchanged.
 template <int DBG = 0>
@@ -101,7 +118,8 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
                                                             float* value) {
     using C = H3Cfg<0>;
     __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
-    static_assert(kLatCacheOff + 64 * (int)sizeof(oaz_node) <= kLatLds, "k_search_lat LDS");
+    static_assert(kLatPathOff + kLatPath * 4 + 32 + kLatSq * 8 + 64 * (int)sizeof(oaz_node) <= kLatLds,
+                  "k_search_lat LDS");
     const uint32_t g = blockIdx.x;
     if (g >= t.G || (active && active[g] != 1)) return;  // uniform over the workgroup
     const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
@@ -128,21 +146,21 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
     tl.n_nodes = tl.leaf + 2;
     if (path_lds) tl.path = reinterpret_cast<uint32_t*>(lb + kLatPathOff);
     // tl.nodes stays the game's global slot: the node accessor maps nodes [0, ncached) to the LDS copy
-    const uint32_t ncached = kLatCache < t.cap ? kLatCache : t.cap;
-    const uint32_t nsq = (uint32_t)sims + 1 < (uint32_t)kLatSq ? (uint32_t)sims + 1 : (uint32_t)kLatSq;
+    const LatLayout ly = lat_layout(t.pathcap, path_lds, sims, t.cap);
+    const uint32_t ncached = ly.ncached, nsq = ly.nsq;
     uint64_t* const stl = reinterpret_cast<uint64_t*>(lb + kLatStatOff);
-    const NodesCached na{reinterpret_cast<oaz_node*>(lb + kLatCacheOff), ncached,
-                         reinterpret_cast<const double*>(lb + kLatSqOff), nsq,
-                         reinterpret_cast<const oaz_state*>(lb + kLatRootOff), stl};
+    const NodesCached na{reinterpret_cast<oaz_node*>(lb + ly.cache), ncached,
+                         reinterpret_cast<const double*>(lb + ly.sq), nsq,
+                         reinterpret_cast<const oaz_state*>(lb + ly.root), stl};
     float* const pol = reinterpret_cast<float*>(lb + kLatPolOff);  // the leaf's policy row, value at [50]
     // the root position and sqrt(0 .. sims) (read-only for the launch) and zeroed statistics: at the start and
     // after an fp16-range recompute (which uses the whole LDS)
     auto fill_resident = [&] {
-        double* sq = reinterpret_cast<double*>(lb + kLatSqOff);
+        double* sq = reinterpret_cast<double*>(lb + ly.sq);
         for (uint32_t k = threadIdx.x; k < nsq; k += kLatThreads) sq[k] = t.sqrt_tab[k];
         static_assert(sizeof(oaz_state) % 4 == 0 && sizeof(oaz_state) <= 32, "root copy");
         if (threadIdx.x < sizeof(oaz_state) / 4)
-            reinterpret_cast<uint32_t*>(lb + kLatRootOff)[threadIdx.x] =
+            reinterpret_cast<uint32_t*>(lb + ly.root)[threadIdx.x] =
                 reinterpret_cast<const uint32_t*>(roots + g)[threadIdx.x];
         if (threadIdx.x < GS_COUNT) stl[threadIdx.x] = 0;
     };
@@ -165,15 +183,15 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
     lat_sync_tree(tl, tg, na, path_lds, false);  // the root (k_tree_reset) and the node count
     __syncthreads();
     bool resident = false;  // the network's head parameters are in LDS (H3sResident)
-    uint64_t cyc[4] = {0, 0, 0, 0}, tm0 = 0, tm = 0;  // DBG 1: backup, select, evaluation, loop
+    uint64_t cyc[5] = {0, 0, 0, 0, 0}, tm0 = 0, tm = 0;  // DBG: backup, select, evaluation, loop, probe call
     auto lap = [&](int k) {
-        if constexpr (DBG == 1) {
+        if constexpr (DBG >= 1) {
             const uint64_t n = __builtin_amdgcn_s_memtime();
             cyc[k] += n - tm;
             tm = n;
         }
     };
-    if constexpr (DBG == 1) tm0 = tm = __builtin_amdgcn_s_memtime();
+    if constexpr (DBG >= 1) tm0 = tm = __builtin_amdgcn_s_memtime();
     for (int s = 0; s < sims; ++s) {
         if (!hash_eval && !resident) {  // at the start, and after an fp16-range recompute used the whole LDS
             const float* ph0 = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh);
@@ -189,6 +207,10 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
             lap(0);
             lat_select(tl, rg, ag, prm, gs, na);
             lap(1);
+            if constexpr (DBG == 2) {  // the cost of a call alone: same arguments, no work (timed into slot 4)
+                lat_probe(tl, rg, ag, prm, gs, na);
+                lap(4);
+            }
         }
         __syncthreads();  // the leaf position of simulation s is in LDS
         if (hash_eval) {
@@ -229,7 +251,7 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
         lap(2);
         lat_backup(tl, rg, ag, pol, pol + 50, gs, sp, na);  // the last simulation's
         lap(0);
-        if constexpr (DBG == 1) {
+        if constexpr (DBG >= 1) {
             cyc[3] = tm - tm0;
             if (lane == 0) {
                 uint64_t* st = tg.stats;
@@ -237,6 +259,7 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
                 atomicAdd((unsigned long long*)&st[GS_RED], (unsigned long long)cyc[1]);
                 atomicAdd((unsigned long long*)&st[GS_BLUE], (unsigned long long)cyc[2]);
                 atomicAdd((unsigned long long*)&st[GS_PASSES], (unsigned long long)cyc[3]);
+                atomicAdd((unsigned long long*)&st[GS_DROPPED], (unsigned long long)cyc[4]);
             }
         }
     }
@@ -337,6 +360,12 @@ hipError_t launch_search_lat(const TreeView& t, const oaz_state* roots, const ui
     if (w && (!w->fallback || !w->blob_x6 || w->precision != OAZ_FP32_SPLIT16)) return hipErrorInvalidValue;
 #if OAZ_AB
     static const int dbg = getenv("OAZ_LAT_DBG") ? atoi(getenv("OAZ_LAT_DBG")) : 0;
+    if (dbg == 2) {
+        hipLaunchKernelGGL(k_search_lat<2>, dim3(t.G), dim3(kLatThreads), 0, st, t, roots, active, p, sims, w ? 0 : 1,
+                           w ? w->blob : nullptr, w ? w->blocks : 0, w ? w->blob_x6 : nullptr,
+                           w ? w->fallback : nullptr, policy, value);
+        return hipGetLastError();
+    }
     if (dbg == 1) {
         hipLaunchKernelGGL(k_search_lat<1>, dim3(t.G), dim3(kLatThreads), 0, st, t, roots, active, p, sims, w ? 0 : 1,
                            w ? w->blob : nullptr, w ? w->blocks : 0, w ? w->blob_x6 : nullptr,

@@ -27,14 +27,17 @@ with Engine(games=G, sims=sims, blocks=3, c_puct=5.0, train_noise=0, evaluator=e
     e.set_timing(1)
     for _ in range(5):
         e.kernel_times_reset()
-        e.search(roots)
+        r = e.search(roots)
         kt = e.kernel_times()
         st = e.selfplay_stats()
+        walk = {"mean_depth": r.stats.depth_sum / max(1, r.stats.sims), "nodes": int(r.stats.max_nodes),
+                "expansions_per_sim": r.stats.expansions / max(1, r.stats.sims)}
         loop = st.passes / G
         us = 1e3 * kt.backup_select_ms / max(kt.backup_select_n, 1)
-        res.append({"launch_us": us, "cycles_per_us": loop / us,
+        res.append({"launch_us": us, "cycles_per_us": loop / us, "walk": walk,
                     "per_sim_cycles": {"backup": st.games_cut / G / sims, "select": st.red_wins / G / sims,
-                                       "evaluation": st.blue_wins / G / sims, "loop": loop / sims}})
+                                       "evaluation": st.blue_wins / G / sims, "loop": loop / sims,
+                                       "probe_call": st.samples_dropped / G / sims}})
 r = res[len(res) // 2]
 r["per_sim_us"] = {k: v / r["cycles_per_us"] for k, v in r["per_sim_cycles"].items()}
 print(json.dumps({"sims": sims, "G": G, "evaluator": "hash" if ev == _abi.EVAL_HASH else "nn", **r}, indent=1))
