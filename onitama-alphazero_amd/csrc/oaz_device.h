@@ -98,6 +98,52 @@ OAZ_HD int make_move(oaz_state& s, int from, int to, int piece, int slot, int co
     return res;
 }
 
+// Register-only forms of the colour- and slot-indexed accesses, for code that holds the state in registers
+// across a loop (the one-launch search's walk): a runtime index into the struct (s.pawns[color],
+// s.cards[slot]) can make the compiler keep the whole state in scratch memory, a memory round trip per
+// access. cards[0..3] are one little-endian word.
+OAZ_HD int state_card(const oaz_state& s, int i) {
+    uint32_t w;
+    __builtin_memcpy(&w, s.cards, 4);
+    return i < 4 ? (int)((w >> (8 * i)) & 0xFFu) : (int)s.cards[4];
+}
+OAZ_HD void state_rotate(oaz_state& s, int slot) {  // Deck::rotate (deck.rs:87-90): cards[slot] <-> cards[4]
+    uint32_t w;
+    __builtin_memcpy(&w, s.cards, 4);
+    const uint32_t sh = 8u * (uint32_t)slot;
+    const uint8_t t = (uint8_t)(w >> sh);
+    w = (w & ~(0xFFu << sh)) | ((uint32_t)s.cards[4] << sh);
+    __builtin_memcpy(s.cards, &w, 4);
+    s.cards[4] = t;
+}
+// make_move with the same result and state, through selects
+OAZ_HD int make_move_regs(oaz_state& s, int from, int to, int piece, int slot, int color) {
+    const uint32_t fb = sq_bit(from), tb = sq_bit(to);
+    const bool blue = color != OAZ_RED;
+    uint32_t mp = blue ? s.pawns[1] : s.pawns[0], mk = blue ? s.kings[1] : s.kings[0];
+    uint32_t ep = blue ? s.pawns[0] : s.pawns[1], ek = blue ? s.kings[0] : s.kings[1];
+    if (piece == OAZ_PAWN) mp &= ~fb;
+    else mk &= ~fb;
+    int res = OAZ_IN_PROGRESS;
+    if (ep & tb) {
+        ep &= ~tb;
+        res = OAZ_CAPTURE;
+    } else if (ek & tb) {
+        ek &= ~tb;
+        res = color == OAZ_RED ? OAZ_RED_WIN : OAZ_BLUE_WIN;
+    }
+    if (piece == OAZ_PAWN) mp |= tb;
+    else mk |= tb;
+    if (piece == OAZ_KING && to == (color == OAZ_RED ? kBlueTemple : kRedTemple))
+        res = color == OAZ_RED ? OAZ_RED_WIN : OAZ_BLUE_WIN;
+    s.pawns[0] = blue ? ep : mp;
+    s.pawns[1] = blue ? mp : ep;
+    s.kings[0] = blue ? ek : mk;
+    s.kings[1] = blue ? mk : ek;
+    if (slot < 4) state_rotate(s, slot);
+    return res;
+}
+
 // State::current_state (state.rs:120-134)
 OAZ_HD int current_state(const oaz_state& s) {
     if (s.kings[0] == 0 || s.kings[1] == kRedKingStart) return OAZ_BLUE_WIN;

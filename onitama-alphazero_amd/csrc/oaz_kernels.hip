@@ -646,6 +646,9 @@ struct NodesGlobal {
     __device__ __forceinline__ const oaz_state* root(const oaz_state* roots, uint32_t g) const { return &roots[g]; }
     __device__ __forceinline__ void add(uint64_t* st, int f, uint64_t v) const { stat_add(&st[f], v); }
     __device__ __forceinline__ void max(uint64_t* st, int f, uint64_t v) const { stat_max(&st[f], v); }
+    __device__ __forceinline__ uint32_t pawns(const oaz_state& s, int c) const { return s.pawns[c]; }
+    __device__ __forceinline__ uint32_t kings(const oaz_state& s, int c) const { return s.kings[c]; }
+    __device__ __forceinline__ int card(const oaz_state& s, int i) const { return s.cards[i]; }
 };
 struct NodesCached {
     oaz_node* L;        // LDS: nodes [0, n)
@@ -665,6 +668,11 @@ struct NodesCached {
     __device__ __forceinline__ void max(uint64_t*, int f, uint64_t v) const {
         (void)__hip_atomic_fetch_max(&stl[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    // the one-launch search holds the leaf position in registers across its calls: register-only reads
+    // (state_card; a runtime index would put the state in scratch memory)
+    __device__ __forceinline__ uint32_t pawns(const oaz_state& s, int c) const { return c ? s.pawns[1] : s.pawns[0]; }
+    __device__ __forceinline__ uint32_t kings(const oaz_state& s, int c) const { return c ? s.kings[1] : s.kings[0]; }
+    __device__ __forceinline__ int card(const oaz_state& s, int i) const { return state_card(s, i); }
 };
 
 // g: this segment's game (>= t.G: an idle segment); leaf_lds: also store the leaf position there (LDS of
@@ -859,14 +867,14 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
             if (idx < 50) sp[idx] = polr[c];
         }
         const int color = s.to_move & 1;
-        const uint32_t pawns = s.pawns[color], king = s.kings[color], own = pawns | king;
+        const uint32_t pawns = na.pawns(s, color), king = na.kings(s, color), own = pawns | king;
         uint32_t mask[4];
         uint32_t cnt = 0, r0 = 0, r1 = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int cb = 4 * sl + i, k = cb >= 25 ? 1 : 0, from = cb - 25 * k;
             uint32_t m = 0;
-            if (cb < 50 && (own & sq_bit(from))) m = c_attack.m[color][s.cards[(color ? 2 : 0) + k] & 15][from] & ~own;
+            if (cb < 50 && (own & sq_bit(from))) m = c_attack.m[color][na.card(s, (color ? 2 : 0) + k) & 15][from] & ~own;
             mask[i] = m;
             cnt += (uint32_t)__popc(m);
             if (k) r1 |= m; else r0 |= m;

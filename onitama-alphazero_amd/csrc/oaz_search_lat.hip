@@ -62,11 +62,108 @@ __device__ __noinline__ void lat_backup(const TreeView& t, const oaz_state* root
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
-__device__ __noinline__ void lat_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
-                                        const SearchParams& prm, uint32_t gs, const NodesCached& na) {
-    select_seg_body(t, roots, active, nullptr, prm, gs, nullptr, na);
+// The walk of the workgroup's one game on the whole walker wave: lane l holds child l (K <= 40 < 64), so a
+// level evaluates each child's PUCT once instead of three children per lane of a 16-lane segment. Same
+// expressions and the same last-maximum rule as select_seg_body / k_select (mcts_arena.rs:183-223): the
+// arg-max runs within each 16-lane row by DPP and across the four rows on scalars, the chosen child's
+// fields are read from its lane with v_readlane. No root noise here (k_search_lat's condition).
+// DBG (diagnostic build): s_memtime cycles of the prologue (root position and node) into GS_MOVES and of each
+// level's child loads + PUCT keys into GS_FINISHED
+template <int DBG = 0>
+__device__ __noinline__ void lat_select_wide(const TreeView& t, const SearchParams& prm, const NodesCached& na) {
+    uint64_t d0 = DBG ? __builtin_amdgcn_s_memtime() : 0, dl = 0;
+    const int l = (int)(threadIdx.x & 63);
+    oaz_node* T = t.nodes;
+    uint32_t* path = t.path;
+    oaz_state s = load_state(na.rt);
+    int color = s.to_move & 1;
+    NodeRegs nd = load_node(na.at(T, 0));
+    uint32_t node = 0, depth = 0;
+    if (l == 0) path[0] = 0;
+    bool stuck = false;
+    if constexpr (DBG) {
+        asm volatile("" ::"v"(nd.misc), "v"(s.pawns[0]));
+        const uint64_t d1 = __builtin_amdgcn_s_memtime();
+        if (l == 0) na.add(nullptr, GS_MOVES, d1 - d0);
+    }
+    while ((node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2)) {
+        const int K = node_nch(nd.misc);
+        if (K == 0) {  // reference would panic in select (Q6): stop here, treat as a leaf
+            stuck = true;
+            break;
+        }
+        const uint64_t da = DBG ? __builtin_amdgcn_s_memtime() : 0;
+        NodeRegs ch;
+        ch.W = 0.0;
+        ch.P = 0.0;
+        ch.N = 0;
+        ch.first = 0;
+        ch.misc = 0;
+        if (l < K) ch = load_node(na.at(T, nd.first + l));
+        const double sqn = na.sqrt_n(t, nd.N);
+        int64_t key = INT64_MIN;
+        if (l < K) {
+            const double q = ch.N ? ch.W / (double)ch.N : 0.0;
+            const double sq = sqn / (double)(ch.N + 1);
+            const double u = q + prm.c_puct * ch.P * sq;  // mcts_arena.rs:204-207
+            key = total_key(u);
+        }
+        if constexpr (DBG) {
+            asm volatile("" ::"v"(key));
+            dl += __builtin_amdgcn_s_memtime() - da;
+        }
+        int idx = l;
+        seg_amax_step<0xB1>(key, idx);   // within each row of 16 lanes (every lane ends with its row's best)
+        seg_amax_step<0x4E>(key, idx);
+        seg_amax_step<0x141>(key, idx);
+        seg_amax_step<0x140>(key, idx);
+        int best = __builtin_amdgcn_readlane(idx, 0);
+        int64_t bkey = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)key >> 32), 0) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)key, 0));
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {  // rows hold ascending children: a tie goes to the later row
+            const int64_t rk =
+                (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)key >> 32), 16 * r) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)key, 16 * r));
+            const int ri = __builtin_amdgcn_readlane(idx, 16 * r);
+            if (rk > bkey || (rk == bkey && ri > best)) {
+                bkey = rk;
+                best = ri;
+            }
+        }
+        NodeRegs c;  // (the walk reads only N, first and misc of the node it descends to)
+        c.W = 0.0;
+        c.P = 0.0;
+        c.N = (uint32_t)__builtin_amdgcn_readlane((int)ch.N, best);
+        c.first = (uint32_t)__builtin_amdgcn_readlane((int)ch.first, best);
+        c.misc = (uint32_t)__builtin_amdgcn_readlane((int)ch.misc, best);
+        const uint32_t cidx = nd.first + (uint32_t)best;
+        const int res = make_move_regs(s, mv_from(c.misc), mv_to(c.misc), mv_piece(c.misc), mv_slot(c.misc), color);
+        color ^= 1;  // game_state.player_color.switch()
+        if (is_win(res)) {
+            c.misc |= 2u << 24;
+            if (l == 0) *flags_ptr(na.at(T, cidx)) = (uint8_t)(node_flags(c.misc));
+        }
+        ++depth;
+        if (l == 0 && depth < t.pathcap) path[depth] = cidx;
+        node = cidx;
+        nd = c;
+    }
+    s.to_move = (uint8_t)color;
+    if (l == 0) {
+        const bool need = leaf_needs_eval(nd.misc, s);
+        store_state(t.leaf_state, s);
+        *t.leaf = node;
+        *t.depth = depth;
+        na.add(nullptr, GS_SIMS, 1);
+        na.add(nullptr, GS_DEPTH, depth);
+        na.add(nullptr, GS_EVALS, need);
+        if (stuck) na.add(nullptr, GS_STUCK, 1);
+        if constexpr (DBG) na.add(nullptr, GS_FINISHED, dl);
+    }
 }
-// DBG 2 probe: a call with lat_select's arguments that only reads two of them
+
+// DBG 2 probe: a call with the walker's arguments that only reads two of them
 __device__ __noinline__ void lat_probe(const TreeView& t, const oaz_state*, const uint8_t*, const SearchParams& prm,
                                        uint32_t gs, const NodesCached& na) {
     if (gs == 0 && threadIdx.x == 1000) *t.leaf = na.n + (uint32_t)prm.seed;  // never true: keeps the reads
@@ -205,7 +302,7 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
             lap(2);
             if (s > 0) lat_backup(tl, rg, ag, pol, pol + 50, gs, sp, na);  // simulation s - 1's
             lap(0);
-            lat_select(tl, rg, ag, prm, gs, na);
+            lat_select_wide<DBG>(tl, prm, na);
             lap(1);
             if constexpr (DBG == 2) {  // the cost of a call alone: same arguments, no work (timed into slot 4)
                 lat_probe(tl, rg, ag, prm, gs, na);

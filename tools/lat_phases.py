@@ -37,7 +37,9 @@ with Engine(games=G, sims=sims, blocks=3, c_puct=5.0, train_noise=0, evaluator=e
         res.append({"launch_us": us, "cycles_per_us": loop / us, "walk": walk,
                     "per_sim_cycles": {"backup": st.games_cut / G / sims, "select": st.red_wins / G / sims,
                                        "evaluation": st.blue_wins / G / sims, "loop": loop / sims,
-                                       "probe_call": st.samples_dropped / G / sims}})
+                                       "probe_call": st.samples_dropped / G / sims,
+                                       "walk_prologue": st.moves / G / sims,
+                                       "walk_loads_keys": st.games_finished / G / sims}})
 r = res[len(res) // 2]
 r["per_sim_us"] = {k: v / r["cycles_per_us"] for k, v in r["per_sim_cycles"].items()}
 print(json.dumps({"sims": sims, "G": G, "evaluator": "hash" if ev == _abi.EVAL_HASH else "nn", **r}, indent=1))
