@@ -649,6 +649,20 @@ struct NodesGlobal {
     __device__ __forceinline__ uint32_t pawns(const oaz_state& s, int c) const { return s.pawns[c]; }
     __device__ __forceinline__ uint32_t kings(const oaz_state& s, int c) const { return s.kings[c]; }
     __device__ __forceinline__ int card(const oaz_state& s, int i) const { return s.cards[i]; }
+    __device__ __forceinline__ int move(oaz_state& s, int from, int to, int piece, int slot, int color) const {
+        return make_move(s, from, to, piece, slot, color);
+    }
+};
+// The bodies called as functions (k_search_grp's walker waves): the same global nodes, the position's
+// colour- and slot-indexed fields read and written register-only (make_move_regs, state_card): in a called
+// function a runtime index into the state otherwise sends it through scratch memory.
+struct NodesGlobalRegs : NodesGlobal {
+    __device__ __forceinline__ uint32_t pawns(const oaz_state& s, int c) const { return c ? s.pawns[1] : s.pawns[0]; }
+    __device__ __forceinline__ uint32_t kings(const oaz_state& s, int c) const { return c ? s.kings[1] : s.kings[0]; }
+    __device__ __forceinline__ int card(const oaz_state& s, int i) const { return state_card(s, i); }
+    __device__ __forceinline__ int move(oaz_state& s, int from, int to, int piece, int slot, int color) const {
+        return make_move_regs(s, from, to, piece, slot, color);
+    }
 };
 struct NodesCached {
     oaz_node* L;        // LDS: nodes [0, n)
@@ -673,6 +687,9 @@ struct NodesCached {
     __device__ __forceinline__ uint32_t pawns(const oaz_state& s, int c) const { return c ? s.pawns[1] : s.pawns[0]; }
     __device__ __forceinline__ uint32_t kings(const oaz_state& s, int c) const { return c ? s.kings[1] : s.kings[0]; }
     __device__ __forceinline__ int card(const oaz_state& s, int i) const { return state_card(s, i); }
+    __device__ __forceinline__ int move(oaz_state& s, int from, int to, int piece, int slot, int color) const {
+        return make_move_regs(s, from, to, piece, slot, color);
+    }
 };
 
 // g: this segment's game (>= t.G: an idle segment); leaf_lds: also store the leaf position there (LDS of
@@ -760,7 +777,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
         c.misc = (uint32_t)__shfl((int)pick3(bc, ch[0].misc, ch[1].misc, ch[2].misc), src);
         if (go) {
             const uint32_t cidx = nd.first + (uint32_t)best;
-            const int res = make_move(s, mv_from(c.misc), mv_to(c.misc), mv_piece(c.misc), mv_slot(c.misc), color);
+            const int res = na.move(s, mv_from(c.misc), mv_to(c.misc), mv_piece(c.misc), mv_slot(c.misc), color);
             color ^= 1;  // game_state.player_color.switch()
             if (is_win(res)) {
                 c.misc |= 2u << 24;

@@ -376,13 +376,13 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
 // simulations on the second stream. Results are bit-identical to the per-step launches.
 __device__ __noinline__ void grp_backup(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                                         const float* policy, const float* value, uint32_t gs, float* sp) {
-    expand_backup_seg_body(t, roots, active, policy, value, gs, sp);
+    expand_backup_seg_body(t, roots, active, policy, value, gs, sp, NodesGlobalRegs{});
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 __device__ __noinline__ void grp_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                                         const float* noise, const SearchParams& prm, uint32_t gs) {
-    select_seg_body(t, roots, active, noise, prm, gs);
+    select_seg_body(t, roots, active, noise, prm, gs, nullptr, NodesGlobalRegs{});
 }
 
 template <class C>
