@@ -835,6 +835,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
     if (cfg->blocks < 0 || cfg->blocks > 64 || cfg->sims < 1 || cfg->sims > 65535 || cfg->games < 1 ||
         cfg->max_plies < 0 || cfg->max_plies > 100000 || cfg->compact < 0 || cfg->compact > 2 || cfg->search_time_ns < 0 ||
         cfg->step_kernels < 0 || cfg->step_kernels > 1 ||
+        (uint64_t)cfg->games * ((uint64_t)cfg->sims + 1) >= (1ull << 32) ||  // 32-bit path offsets (k_select_seg)
         (cfg->parts != 0 && cfg->parts != 1 && cfg->parts != 2 && cfg->parts != 4)) {
         oaz_set_err(OAZ_ERR_ARG, "create: config out of range");
         return nullptr;

@@ -703,12 +703,16 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
     const bool on = g < t.G && !(active && active[g] != 1);
     const bool fold_mode = prm.train_noise && noise;
     oaz_node* T = t.nodes + (size_t)(on ? g : 0) * t.cap;
-    uint32_t* path = t.path + (size_t)(on ? g : 0) * t.pathcap;
+    // the path by a 32-bit element offset from the (scalar) base, not a 64-bit per-lane pointer: the walk
+    // keeps it live across every level, and as a VGPR pair it was the fused kernel's spill (a scratch
+    // round trip per level); G * pathcap < 2^32 (oaz_create bounds both)
+    const uint32_t pbase = (on ? g : 0u) * t.pathcap;
+    uint32_t* const path = t.path;
     oaz_state s = load_state(na.root(roots, on ? g : 0));
     int color = s.to_move & 1;
     NodeRegs nd = load_node(na.at(T, 0));
     uint32_t node = 0, depth = 0;
-    if (on && sl == 0) path[0] = 0;
+    if (on && sl == 0) path[pbase] = 0;
     bool stuck = false;
     bool go = on && (node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2);
     while (__builtin_amdgcn_read_exec() && __ballot(go)) {  // some segment is still walking
@@ -784,7 +788,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
                 if (sl == 0) *flags_ptr(na.at(T, cidx)) = (uint8_t)(node_flags(c.misc));
             }
             ++depth;
-            if (sl == 0 && depth < t.pathcap) path[depth] = cidx;
+            if (sl == 0 && depth < t.pathcap) path[pbase + depth] = cidx;
             node = cidx;
             nd = c;
             go = (node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2);
