@@ -9,7 +9,8 @@
 //
 // Kernels per step (N residual blocks, L = 1 + 2N convs):
 //   gather                      samples[idx] -> X0 [R][32], pi [B][50], z [B]
-//   per conv: conv_fwd (MFMA 16x16x4 f32, + per-16-row BN partial sums) -> bn_fwd_fin -> bn_act
+//   per conv: conv_fwd (MFMA 16x16x4 f32, + per-16-row BN partial sums) -> bn_act_cfin (every
+//          workgroup finalises the batch statistics from the partials, then applies BN + skip + ReLU)
 //   heads: head_conv (1x1, 3 channels) -> bn_fwd_fin x2 -> head_sample (value MLP, policy
 //          linear + softmax, loss, their backward, per-sample) -> head_bwd_fin -> head_bwd_rows
 //   per conv, last to first: bn_bwd_fin -> bn_bwd_apply -> wgrad (MFMA, per (tap, square)
@@ -312,6 +313,74 @@ __global__ void k_bn_act(const float* Z, const float* mean, const float* invstd,
     reinterpret_cast<float4*>(A)[t] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// Consumer-side forward finalisation: k_bn_fwd_fin and k_bn_act in one launch (0.805 -> 0.762 ms per
+// batch-512 step). Every workgroup re-reduces the conv's [nwg][2][64] partials in its prologue (the same fixed
+// order in every workgroup, so all of them apply the same statistics); workgroup 0 also writes the batch
+// mean / invstd for the backward pass and updates the running statistics.
+__global__ __launch_bounds__(1024) void k_bn_act_cfin(const float* part, int nwg, double N, float* rmean, float* rvar,
+                                                      float bn_mom, float eps, float* mean_out, float* invstd_out,
+                                                      const float* Z, const float* gamma, const float* beta,
+                                                      const float* skip, float* A, long long n) {
+    __shared__ double sh[2][16][64];
+    __shared__ float cf[4][64];  // mean, invstd, gamma, beta
+    const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+    {
+        double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
+        int w = q;
+        for (; w + 48 < nwg; w += 64) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                a1[u] += part[(size_t)(w + 16 * u) * 128 + c];
+                a2[u] += part[(size_t)(w + 16 * u) * 128 + 64 + c];
+            }
+        }
+        for (; w < nwg; w += 16) {
+            a1[0] += part[(size_t)w * 128 + c];
+            a2[0] += part[(size_t)w * 128 + 64 + c];
+        }
+        sh[0][q][c] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+        sh[1][q][c] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+    }
+    __syncthreads();
+    if (q == 0) {
+        double s1 = 0.0, s2 = 0.0;
+        for (int k = 0; k < 16; ++k) {
+            s1 += sh[0][k][c];
+            s2 += sh[1][k][c];
+        }
+        const double mu = s1 / N;
+        double var = s2 / N - mu * mu;
+        if (var < 0.0) var = 0.0;
+        const float muf = (float)mu, isf = (float)(1.0 / sqrt(var + (double)eps));
+        cf[0][c] = muf;
+        cf[1][c] = isf;
+        cf[2][c] = gamma[c];
+        cf[3][c] = beta[c];
+        if (blockIdx.x == 0) {
+            mean_out[c] = muf;
+            invstd_out[c] = isf;
+            rmean[c] = (float)((1.0 - bn_mom) * rmean[c] + bn_mom * mu);
+            rvar[c] = (float)((1.0 - bn_mom) * rvar[c] + bn_mom * var * N / (N - 1.0));
+        }
+    }
+    __syncthreads();
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t * 4 < n; t += (long long)gridDim.x * blockDim.x) {
+        const int c0 = (int)((t * 4) & 63);
+        const float4 z = reinterpret_cast<const float4*>(Z)[t];
+        float v[4] = {z.x, z.y, z.z, z.w};
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (skip) s = reinterpret_cast<const float4*>(skip)[t];
+        const float sk[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float y = (v[k] - cf[0][c0 + k]) * cf[1][c0 + k] * cf[2][c0 + k] + cf[3][c0 + k];
+            if (skip) y += sk[k];
+            v[k] = y > 0.0f ? y : 0.0f;
+        }
+        reinterpret_cast<float4*>(A)[t] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+}
+
 // ---- BN backward finalisation: dgamma = sum m*xhat, dbeta = sum m; dx coefficients -----------------
 // Channels c >= split: gamma2 / ggamma2 / gbeta2 [c - split] (both heads in one launch, as k_bn_fwd_fin).
 __global__ __launch_bounds__(1024) void k_bn_bwd_fin(const float* part, int nwg, int pstride, int coff, int C, double N,
@@ -380,6 +449,77 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* M, const floa
     sh[q][c] = s;
     __syncthreads();
     if (q == 0) part[(size_t)blockIdx.x * 64 + c] = sh[0][c] + sh[1][c] + sh[2][c] + sh[3][c];
+}
+
+// Consumer-side backward finalisation (A/B build, OAZ_TRAIN_CFIN_BWD=1): k_bn_bwd_fin and k_bn_bwd_apply
+// in one launch. Every workgroup
+// (64 rows, 1024 threads) re-reduces the [nwg][2][64] partials (sum m, sum m*xhat) in the same fixed
+// order; workgroup 0 writes dgamma / dbeta.
+__global__ __launch_bounds__(1024) void k_bn_bwd_apply_cfin(const float* bpart, int nwg, double N, const float* gamma,
+                                                            float* ggamma, float* gbeta, const float* M,
+                                                            const float* Z, const float* mean, const float* invstd,
+                                                            float* dZ, float* part, int R) {
+    __shared__ double sh[2][16][64];
+    __shared__ float cf[5][64];  // mean, invstd, gamma*invstd, mean(m), mean(m*xhat)
+    __shared__ float shs[16][64];
+    const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+    {
+        double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
+        int w = q;
+        for (; w + 48 < nwg; w += 64) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                a1[u] += bpart[(size_t)(w + 16 * u) * 128 + c];
+                a2[u] += bpart[(size_t)(w + 16 * u) * 128 + 64 + c];
+            }
+        }
+        for (; w < nwg; w += 16) {
+            a1[0] += bpart[(size_t)w * 128 + c];
+            a2[0] += bpart[(size_t)w * 128 + 64 + c];
+        }
+        sh[0][q][c] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+        sh[1][q][c] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+    }
+    __syncthreads();
+    if (q == 0) {
+        double s1 = 0.0, s2 = 0.0;
+        for (int k = 0; k < 16; ++k) {
+            s1 += sh[0][k][c];
+            s2 += sh[1][k][c];
+        }
+        const float is = invstd[c];
+        cf[0][c] = mean[c];
+        cf[1][c] = is;
+        cf[2][c] = gamma[c] * is;
+        cf[3][c] = (float)(s1 / N);
+        cf[4][c] = (float)(s2 / N);
+        if (blockIdx.x == 0) {
+            gbeta[c] = (float)s1;
+            ggamma[c] = (float)s2;
+        }
+    }
+    __syncthreads();
+    const int r0 = blockIdx.x * 64;
+    const float mu = cf[0][c], is = cf[1][c], k1 = cf[2][c], k2 = cf[3][c], k3 = cf[4][c];
+    float s = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int r = r0 + q + 16 * u;
+        if (r < R) {
+            const size_t o = (size_t)r * kC + c;
+            const float xh = (Z[o] - mu) * is;
+            const float d = k1 * (M[o] - k2 - xh * k3);
+            dZ[o] = d;
+            s += d;
+        }
+    }
+    shs[q][c] = s;
+    __syncthreads();
+    if (q == 0) {
+        float t = 0.0f;
+        for (int k = 0; k < 16; ++k) t += shs[k][c];
+        part[(size_t)blockIdx.x * 64 + c] = t;
+    }
 }
 
 // ---- weight gradient: per (tap, square, row split z) partial D[co][ci] = sum_b dZ[sq,b][co] * X[nbr,b][ci]
@@ -940,6 +1080,9 @@ struct oaz_trainer {
     hipEvent_t ev_dz[2] = {}, ev_w[2] = {}, ev_h[2] = {}, ev_done = nullptr;
     Layout L{};
     int nconv = 0, maxB = 0;
+    int cfin = -1;     // forward BN finalisation in k_bn_act_cfin (-1: one float4 per thread; A/B build: 0 = the
+                       // separate k_bn_fwd_fin + k_bn_act launches, n > 0 = n workgroups)
+    bool cfin_bwd = false;  // A/B build: consumer-side backward BN finalisation
     int conv_rg = 2;  // 16-row groups per conv workgroup (OAZ_CONV_RG=1|2|4 overrides; tuning knob)
     size_t nparam = 0;
     std::vector<void*> allocs;
@@ -1032,6 +1175,8 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
         const int v = atoi(e);
         if (v == 1 || v == 2 || v == 4) t->conv_rg = v;
     }
+    if (const char* e = getenv("OAZ_TRAIN_CFIN")) t->cfin = atoi(e) > 0 ? atoi(e) : 0;
+    t->cfin_bwd = getenv("OAZ_TRAIN_CFIN_BWD") != nullptr;
 #endif
     t->nparam = t->L.total;
     const size_t R = (size_t)t->maxB * 25;
@@ -1213,10 +1358,17 @@ static int backward(oaz_trainer* t, int bi) {
         a.chunks = l == 0 ? 2 : 4;
         a.B = B;
         launch_conv<CONV_FWD>(l == 0 ? 2 : 4, rg, conv_grid, st, a);
-        hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_conv, 64, 0, 64, (double)R,
-                           P + L.brm[l], P + L.brv[l], bn_mom, eps, t->mean[l], t->invstd[l], 64, nullptr, nullptr);
         const float* skip = (l >= 2 && l % 2 == 0) ? t->A[l - 2] : nullptr;  // block output adds the block input
         const long long n = (long long)R * kC;
+        if (t->cfin) {
+            const unsigned nwg_act = t->cfin > 0 ? (unsigned)t->cfin : (unsigned)((n / 4 + 1023) / 1024);
+            hipLaunchKernelGGL(k_bn_act_cfin, dim3(nwg_act), dim3(1024), 0, st, t->part, nwg_conv, (double)R,
+                               P + L.brm[l], P + L.brv[l], bn_mom, eps, t->mean[l], t->invstd[l], t->Z[l],
+                               P + L.bg[l], P + L.bb[l], skip, t->A[l], n);
+            continue;
+        }
+        hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_conv, 64, 0, 64, (double)R,
+                           P + L.brm[l], P + L.brv[l], bn_mom, eps, t->mean[l], t->invstd[l], 64, nullptr, nullptr);
         hipLaunchKernelGGL(k_bn_act, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, t->Z[l], t->mean[l],
                            t->invstd[l], P + L.bg[l], P + L.bb[l], skip, t->A[l], n);
     }
@@ -1266,12 +1418,18 @@ static int backward(oaz_trainer* t, int bi) {
         float* mm = t->bcoef + 64;
         float* mx = t->bcoef + 128;
         float* dz = t->DZ[k];
-        hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_part, 64, 0, 64, (double)R,
-                           P + L.bg[l], t->invstd[l], G + L.bg[l], G + L.bb[l], c1, mm, mx, 64, nullptr, nullptr,
-                           nullptr);
         if (used[k]) HIP_TRY(hipStreamWaitEvent(st, t->ev_w[k], 0));
-        hipLaunchKernelGGL(k_bn_bwd_apply, dim3(nwg_rows), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
-                           t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
+        if (t->cfin_bwd) {
+            hipLaunchKernelGGL(k_bn_bwd_apply_cfin, dim3(nwg_rows), dim3(1024), 0, st, t->part, nwg_part, (double)R,
+                               P + L.bg[l], G + L.bg[l], G + L.bb[l], t->M[l], t->Z[l], t->mean[l], t->invstd[l], dz,
+                               t->bpart[k], R);
+        } else {
+            hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_part, 64, 0, 64, (double)R,
+                               P + L.bg[l], t->invstd[l], G + L.bg[l], G + L.bb[l], c1, mm, mx, 64, nullptr,
+                               nullptr, nullptr);
+            hipLaunchKernelGGL(k_bn_bwd_apply, dim3(nwg_rows), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
+                               t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
+        }
         HIP_TRY(hipEventRecord(t->ev_dz[k], st));
         HIP_TRY(hipStreamWaitEvent(t->st2, t->ev_dz[k], 0));
         const float* X = l == 0 ? t->X0 : t->A[l - 1];
