@@ -526,7 +526,10 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_apply_cfin(const float* bpart, 
 // v_mfma_f32_32x32x2_f32: lane l supplies A[m = l&31][k = l>>5] and B[k = l>>5][n = l&31], so one
 // k-pair = two rows, read as 128-B row segments. A wave owns the whole 64 x (32*NNT) tile (2 x NNT
 // accumulators); the 4 waves of a workgroup take interleaved row pairs and are summed in LDS.
-constexpr int kWSplit = 2;  // row splits per (tap, square)
+#ifndef OAZ_WSPLIT
+#define OAZ_WSPLIT 2
+#endif
+constexpr int kWSplit = OAZ_WSPLIT;  // row splits per (tap, square) (-DOAZ_WSPLIT: A/B variants)
 template <int NNT>  // input-channel tiles of 32 (2 for 64 channels, 1 for the padded 32)
 __global__ __launch_bounds__(256) void k_wgrad(const float* dZ, const float* X, int B, float* part) {
     __shared__ float red[3][64 * 64];
