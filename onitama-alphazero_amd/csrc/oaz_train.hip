@@ -426,17 +426,18 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_fin(const float* part, int nwg,
     }
 }
 
-// dZ = gamma*invstd * (m - mean(m) - xhat * mean(m*xhat)); per-64-row partial sums of dZ (conv bias grad)
+// dZ = gamma*invstd * (m - mean(m) - xhat * mean(m*xhat)); per-(4U)-row partial sums of dZ (conv bias grad)
+template <int U>
 __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* M, const float* Z, const float* mean,
                                                       const float* invstd, const float* c1, const float* mm,
                                                       const float* mx, float* dZ, float* part, int R) {
     __shared__ float sh[4][64];
     const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
-    const int r0 = blockIdx.x * 64;
+    const int r0 = blockIdx.x * 4 * U;
     const float mu = mean[c], is = invstd[c], k1 = c1[c], k2 = mm[c], k3 = mx[c];
     float s = 0.0f;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < U; ++u) {
         const int r = r0 + q + 4 * u;
         if (r < R) {
             const size_t o = (size_t)r * kC + c;
@@ -1086,6 +1087,7 @@ struct oaz_trainer {
     int cfin = -1;     // forward BN finalisation in k_bn_act_cfin (-1: one float4 per thread; A/B build: 0 = the
                        // separate k_bn_fwd_fin + k_bn_act launches, n > 0 = n workgroups)
     bool cfin_bwd = false;  // A/B build: consumer-side backward BN finalisation
+    int bwd_u = 16;         // k_bn_bwd_apply rows per workgroup / 4 (A/B build: OAZ_TRAIN_BWD_U=4|8|32)
     int conv_rg = 2;  // 16-row groups per conv workgroup (OAZ_CONV_RG=1|2|4 overrides; tuning knob)
     size_t nparam = 0;
     std::vector<void*> allocs;
@@ -1180,6 +1182,7 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
     }
     if (const char* e = getenv("OAZ_TRAIN_CFIN")) t->cfin = atoi(e) > 0 ? atoi(e) : 0;
     t->cfin_bwd = getenv("OAZ_TRAIN_CFIN_BWD") != nullptr;
+    if (const char* e = getenv("OAZ_TRAIN_BWD_U")) t->bwd_u = atoi(e) == 4 ? 4 : atoi(e) == 8 ? 8 : atoi(e) == 32 ? 32 : 16;
 #endif
     t->nparam = t->L.total;
     const size_t R = (size_t)t->maxB * 25;
@@ -1208,7 +1211,7 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
     }
     const size_t nwg_conv = R / 16;
     if (t->alloc(t->X0, R * kInPad) || t->alloc(t->DZ[0], R * kC) || t->alloc(t->DZ[1], R * kC) || t->alloc(t->bcoef, 3 * 64) ||
-        t->alloc(t->part, nwg_conv * 128) || t->alloc(t->bpart[0], (R + 63) / 64 * 64) || t->alloc(t->bpart[1], (R + 63) / 64 * 64) ||
+        t->alloc(t->part, nwg_conv * 128) || t->alloc(t->bpart[0], (R + 15) / 16 * 64) || t->alloc(t->bpart[1], (R + 15) / 16 * 64) ||
         t->alloc(t->wpart, (size_t)9 * 25 * kWSplit * 64 * 64) || t->alloc(t->hz, R * 4) || t->alloc(t->g3, R * 4) ||
         t->alloc(t->hstat, 16) || t->alloc(t->hpart, ((R + 255) / 256 + (size_t)t->maxB / kHS + 1) * 8) ||
         t->alloc(t->hwpart, ((size_t)t->maxB / kHS + 1) * kHeadW) ||
@@ -1414,6 +1417,7 @@ static int backward(oaz_trainer* t, int bi) {
     // dZ of layer l feeds both dgrad(l) (on st, the critical path) and wgrad(l) (on st2); dZ and
     // the bias partials are double-buffered so st never overwrites what st2 still reads.
     int nwg_part = nwg_rows;
+    const int nwg_bwd = (R + 4 * t->bwd_u - 1) / (4 * t->bwd_u);  // k_bn_bwd_apply<bwd_u> workgroups
     bool used[2] = {false, false};
     for (int l = nl - 1; l >= 0; --l) {
         const int k = l & 1;
@@ -1430,8 +1434,18 @@ static int backward(oaz_trainer* t, int bi) {
             hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_part, 64, 0, 64, (double)R,
                                P + L.bg[l], t->invstd[l], G + L.bg[l], G + L.bb[l], c1, mm, mx, 64, nullptr,
                                nullptr, nullptr);
-            hipLaunchKernelGGL(k_bn_bwd_apply, dim3(nwg_rows), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
-                               t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
+            if (t->bwd_u == 4)
+                hipLaunchKernelGGL(k_bn_bwd_apply<4>, dim3(nwg_bwd), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
+                                   t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
+            else if (t->bwd_u == 32)
+                hipLaunchKernelGGL(k_bn_bwd_apply<32>, dim3(nwg_bwd), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
+                                   t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
+            else if (t->bwd_u == 8)
+                hipLaunchKernelGGL(k_bn_bwd_apply<8>, dim3(nwg_bwd), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
+                                   t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
+            else
+                hipLaunchKernelGGL(k_bn_bwd_apply<16>, dim3(nwg_bwd), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
+                                   t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
         }
         HIP_TRY(hipEventRecord(t->ev_dz[k], st));
         HIP_TRY(hipStreamWaitEvent(t->st2, t->ev_dz[k], 0));
@@ -1444,7 +1458,8 @@ static int backward(oaz_trainer* t, int bi) {
         const int nred = 9 * kC * cin;
         hipLaunchKernelGGL(k_wgrad_reduce, dim3((nred + 255) / 256), dim3(256), 0, t->st2, t->wpart,
                            l == 0 ? kInPad : kC, cin, G + L.cw[l]);
-        hipLaunchKernelGGL(k_colsum, dim3(1), dim3(1024), 0, t->st2, t->bpart[k], nwg_rows, 64, 0, 64, G + L.cb[l]);
+        hipLaunchKernelGGL(k_colsum, dim3(1), dim3(1024), 0, t->st2, t->bpart[k], t->cfin_bwd ? nwg_rows : nwg_bwd,
+                           64, 0, 64, G + L.cb[l]);
         HIP_TRY(hipEventRecord(t->ev_w[k], t->st2));
         used[k] = true;
         if (l == 0) break;
