@@ -634,6 +634,53 @@ __device__ __forceinline__ int root_fold(int K, int Kmax, const NodeRegs (&ch)[3
     return acc;
 }
 
+#ifndef OAZ_FOLD_CP
+#define OAZ_FOLD_CP 0
+#endif
+// The same fold by change points (A/B build -DOAZ_FOLD_CP=1): with the running best fixed, every later
+// comparison j is evaluated at once (lane j & 15 of chunk j >> 4, the same operands and operation order
+// as fold_step, so the same results) and the first takeover found by ballot becomes the new running
+// best; one round per takeover instead of one step per child. Rows (games) advance independently.
+__device__ __forceinline__ int root_fold_cp(int K, const NodeRegs (&ch)[3], const float (&na)[3], const float (&nb)[3],
+                                            double sqn, const SearchParams& prm) {
+    const int sl = seg_lane(), sb = seg_base(), row = sb >> 4;
+    FoldCh f[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) f[c] = fold_chunk(ch[c], na[c], nb[c], sqn, prm);
+    int acc = 0;
+    double qa = bcast_f64<0>(f[0].q), ba = bcast_f64<0>(f[0].base), sa = bcast_f64<0>(f[0].sq);
+    bool live = K > 1;
+    while (__ballot(live)) {
+        int first = 64;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int j = 16 * c + sl;
+            const double ua = qa + prm.c_puct * (ba + f[c].nae) * sa;
+            const bool take = live && j > acc && j < K &&
+                              !(total_key(ua) > __builtin_bit_cast(int64_t, f[c].kub));
+            const uint64_t m = __ballot(take);
+            const uint32_t rm = (uint32_t)(m >> (16 * row)) & 0xFFFFu;
+            if (first == 64 && rm) first = 16 * c + __builtin_ctz(rm);
+        }
+        const int fs = first < 64 ? first : 0;
+        const int src = sb + (fs & 15), fc = fs >> 4;
+        const double qn = shfl_f64(pick3(fc, f[0].q, f[1].q, f[2].q), src);
+        const double bn = shfl_f64(pick3(fc, f[0].base, f[1].base, f[2].base), src);
+        const double sn = shfl_f64(pick3(fc, f[0].sq, f[1].sq, f[2].sq), src);
+        if (live) {
+            if (first < 64) {
+                acc = first;
+                qa = qn;
+                ba = bn;
+                sa = sn;
+            } else {
+                live = false;
+            }
+        }
+    }
+    return acc;
+}
+
 // k_select with 16 lanes per game: lane sl holds children j = 16c + sl (c < 3, K <= 40).
 // Where node i of a game's tree lives: its slot of t.nodes (the per-step kernels), or, in the one-launch
 // search (oaz_search_lat.hip), LDS for the first n nodes of the workgroup's one game (the top of the tree,
@@ -753,7 +800,12 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
             }
             const int Kmax = max(max(__builtin_amdgcn_readlane(K, 0), __builtin_amdgcn_readlane(K, 16)),
                                  max(__builtin_amdgcn_readlane(K, 32), __builtin_amdgcn_readlane(K, 48)));
+#if OAZ_FOLD_CP
+            (void)Kmax;
+            best = root_fold_cp(K, ch, na, nb, sqn, prm);
+#else
             best = root_fold(K, Kmax, ch, na, nb, sqn, prm, std::make_integer_sequence<int, 39>{});
+#endif
         } else {
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
