@@ -145,7 +145,7 @@ typedef struct oaz_config {
     double dirichlet_eps;    /* 0.25 (mcts_arena.rs:186) */
     int32_t games;           /* parallel game slots G (also the max batch of oaz_search) */
     int32_t evaluator;       /* OAZ_EVAL_NN or OAZ_EVAL_HASH */
-    int32_t precision;       /* OAZ_FP32, OAZ_BF16, OAZ_FP32_SPLIT or OAZ_FP32_SPLIT16 */
+    int32_t precision;       /* OAZ_FP32, OAZ_BF16, OAZ_FP32_SPLIT or OAZ_FP32_SPLIT16 (default) */
     int32_t fixed_deck;      /* 1: every game uses deck[]; 0: random 5 of 16 per game (deck.rs:139-151) */
     uint8_t deck[5];
     uint8_t pad0[3];
@@ -167,8 +167,12 @@ typedef struct oaz_config {
                                 `playouts < max_playouts && elapsed < search_time`). 0 = off (default, the
                                 parity mode: exactly `sims` playouts). > 0: a search (or self-play ply) stops
                                 after the first simulation step that ends at or past this wall-clock budget
-                                from its start; all games of the batch run the same number of playouts
-                                (>= 1, <= sims) and pi / the move come from those visits (oaz_last_sims) */
+                                from its start, and pi / the move come from the visits that ran. A search
+                                of the one-launch sizes (step_kernels 0: <= CU-count games without root
+                                noise, or <= 16 x CU-count games) reads the device clock before every
+                                simulation, each game (k_search_grp: each 16-game group) on its own, so the
+                                games of a batch may run different counts (>= 1, <= sims;
+                                oaz_search_playouts); larger batches stop together after a simulation step */
     int32_t step_kernels;    /* 0 = auto: a search of at most CU-count games with the fp16x3 network (or
                                 HASH), no root noise, no search_time budget and no leaf compaction runs as ONE
                                 launch, a workgroup per game doing all its simulations (the Agent API's
@@ -280,8 +284,11 @@ int oaz_set_search_params(oaz_engine* eng, int sims, double c_puct, int train_no
  * bin/tournament.rs:121-129) for the following searches / plies: oaz_config.search_time_ns. 0 = off. */
 int oaz_set_search_time(oaz_engine* eng, int64_t search_time_ns);
 /* Simulations per game run by the last search / self-play ply (= sims unless a search_time_ns budget
- * stopped it earlier). */
+ * stopped it earlier; with per-game counts, their maximum). */
 int oaz_last_sims(oaz_engine* eng, int* sims);
+/* Playouts each of the first G games of the last search / ply ran (the reference's
+ * MctsArena.playouts after search(), mcts_arena.rs:75-81); G <= the last call's games. */
+int oaz_search_playouts(oaz_engine* eng, int* out, int G);
 /* Weights in canonical order (n == oaz_weight_count). BN is folded on the host. */
 int oaz_load_weights(oaz_engine* eng, const float* blob, size_t n);
 
@@ -497,7 +504,8 @@ void oaz_pure_mcts_config_default(oaz_pure_mcts_config* cfg);
 size_t oaz_pure_mcts_tree_capacity(const oaz_pure_mcts_config* cfg);
 /* One search per root (colour = root.to_move). out_value = winrate of the chosen child. A root with
  * no legal move returns the pass move (from = to = 25). tree_out (optional, G x tree_cap nodes)
- * receives each game's tree. */
+ * receives each game's tree. Runs on cfg->device on a stream of its own; the calling thread's current
+ * HIP device is restored before the call returns. */
 int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pure_mcts_config* cfg, oaz_move* out_move,
                          float* out_value, oaz_pure_mcts_stats* stats, oaz_pure_node* tree_out, size_t tree_cap);
 

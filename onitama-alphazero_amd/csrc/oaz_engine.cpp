@@ -58,7 +58,9 @@ extern "C" void oaz_config_default(oaz_config* c) {
     c->dirichlet_eps = 0.25;
     c->games = 4096;
     c->evaluator = OAZ_EVAL_NN;
-    c->precision = OAZ_FP32;
+    // the fp32 network by the fp16x3 split (within 1e-5 of fp32, tests/test_gpu.py): the precision the
+    // one-launch Agent search (k_search_lat) and the C3 headline run; OAZ_FP32 is the exact-fp32 MFMA kernel
+    c->precision = OAZ_FP32_SPLIT16;
     c->fixed_deck = 0;
     for (int i = 0; i < 5; ++i) c->deck[i] = (uint8_t)i;  // ORIGINAL_CARDS[0..5]
     c->seed = 20260101ull;
@@ -654,6 +656,14 @@ struct oaz_engine {
     float* s_rootp = nullptr;
     uint32_t search_calls = 0;
     uint32_t last_sims = 0;  // simulations per game of the last run_sims (Q7 budget: may be < cfg.sims)
+    // Q7 on the device (the one-launch searches): the deadline on the device clock, each game's simulation
+    // count (last_sims_dev: the last run_sims wrote them for its last_G games; last_sims is then their maximum)
+    uint64_t* deadline = nullptr;
+    uint32_t* sims_run = nullptr;
+    int wall_khz = 0;  // hipDeviceAttributeWallClockRate (kHz)
+    bool last_sims_dev = false;
+    uint32_t last_G = 0;
+    std::vector<uint32_t> sims_host;  // per-game counts of the last device-budgeted run (empty: all last_sims)
     uint32_t* s_ply = nullptr;
     // self-play
     oaz_state* root = nullptr;
@@ -896,6 +906,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         }
     if (hipDeviceGetAttribute(&e->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || e->cus < 1)
         e->cus = 256;
+    if (hipDeviceGetAttribute(&e->wall_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess) e->wall_khz = 0;
     const size_t G = e->G;
     if (dalloc(&e->nodes, G * e->cap) || dalloc(&e->n_nodes, G) || dalloc(&e->path, G * e->pathcap) ||
         dalloc(&e->depth, G) || dalloc(&e->leaf, G) || dalloc(&e->leaf_state, G) ||
@@ -908,6 +919,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         dalloc(&e->root, G) || dalloc(&e->ply, G) || dalloc(&e->seq, G) ||
         dalloc(&e->game_id, G) || dalloc(&e->active, G) || dalloc(&e->hist, G * e->hcap) ||
         dalloc(&e->out, (size_t)e->out_cap) || dalloc(&e->out_count, (size_t)1) || dalloc(&e->nn_fallback, (size_t)1) ||
+        dalloc(&e->deadline, (size_t)1) || dalloc(&e->sims_run, G) ||
         (cfg->train_noise && dalloc(&e->noise, 2 * kNoiseChunk * G * kNoiseStride)))
         return fail();
     // sqrt((double)n) from the host libm (IEEE correctly rounded), so device PUCT = oracle PUCT
@@ -955,7 +967,7 @@ extern "C" void oaz_destroy(oaz_engine* e) {
                     e->stats_sum, e->sqrt_tab, e->policy, e->value, e->weights, e->s_roots,
                     e->s_move, e->s_pi, e->s_rootv, e->s_rootp, e->s_ply, e->root, e->ply,
                     e->seq, e->game_id, e->active, e->hist, e->out, e->out_count, e->noise, e->nn_fallback,
-                    e->need, e->slot, e->cstate, e->bcnt};
+                    e->need, e->slot, e->cstate, e->bcnt, e->deadline, e->sims_run};
     for (void* p : ptrs) dfree(p);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
@@ -988,9 +1000,36 @@ extern "C" int oaz_set_search_time(oaz_engine* e, int64_t search_time_ns) {
     return 0;
 }
 
+// The device-budgeted searches leave each game's count on the device; read them once.
+static int fetch_sims_run(oaz_engine* e) {
+    if (!e->last_sims_dev) return 0;
+    HIP_TRY(hipSetDevice(e->device));
+    std::vector<uint32_t> n(e->last_G);
+    if (e->last_G) {
+        HIP_TRY(hipMemcpyAsync(n.data(), e->sims_run, (size_t)e->last_G * 4, hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+    }
+    uint32_t m = 0;
+    for (uint32_t v : n) m = v > m ? v : m;
+    e->last_sims = m;
+    e->last_sims_dev = false;
+    e->sims_host = std::move(n);
+    return 0;
+}
+
 extern "C" int oaz_last_sims(oaz_engine* e, int* sims) {
     if (!e || !sims) return oaz_set_err(OAZ_ERR_ARG, "last_sims: null");
+    if (int rc = fetch_sims_run(e)) return rc;
     *sims = (int)e->last_sims;
+    return 0;
+}
+
+extern "C" int oaz_search_playouts(oaz_engine* e, int* out, int G) {
+    if (!e || (!out && G > 0) || G < 0) return oaz_set_err(OAZ_ERR_ARG, "search_playouts: bad arguments");
+    if ((uint32_t)G > e->last_G)
+        return oaz_set_err(OAZ_ERR_ARG, "search_playouts: G=%d > %u games in the last search", G, e->last_G);
+    if (int rc = fetch_sims_run(e)) return rc;
+    for (int g = 0; g < G; ++g) out[g] = e->sims_host.empty() ? (int)e->last_sims : (int)e->sims_host[(size_t)g];
     return 0;
 }
 
@@ -1181,19 +1220,38 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
     const SearchParams prm = search_params(e);
     const uint32_t sims = (uint32_t)e->cfg.sims;
     // Q7 (opt-in, oaz_config.search_time_ns): the reference's loop runs playouts while
-    // `playouts < max_playouts && elapsed < search_time` (mcts_arena.rs:78). Here all games advance
-    // together, so the clock is read between simulation steps (after the streams drained) and the
-    // search stops after the first step that ends at or past the budget: every game of the batch then
-    // has run the same number of playouts (>= 1), and pi / the move come from those visits.
+    // `playouts < max_playouts && elapsed < search_time` (mcts_arena.rs:78). The one-launch searches
+    // (k_search_lat, k_search_grp: the Agent / arena sizes) read the device clock before every simulation
+    // and each workgroup stops on its own (oaz_search_playouts: each game's count, >= 1). The per-step loop
+    // (larger batches) advances all games together, so there the clock is read between simulation steps
+    // (after the streams drained) and the search stops after the first step that ends at or past the
+    // budget: every game then has run the same number of playouts (>= 1). pi / the move come from the
+    // visits that ran.
     const double budget_ns = (double)e->cfg.search_time_ns;
     const double t_start = budget_ns > 0 ? now_ns() : 0.0;
     e->last_sims = 0;
+    e->last_sims_dev = false;
+    e->sims_host.clear();
+    e->last_G = t.G;
+    // the one-launch searches check the budget on the device (oaz_search_lat.hip): the deadline is the
+    // device clock when k_deadline_start runs + the budget in clock ticks
+    auto device_budget = [&]() -> int {
+        if (budget_ns <= 0) return 0;
+        if (e->wall_khz <= 0) return oaz_set_err(OAZ_ERR_HIP, "search_time: the device reports no wall clock rate");
+        const double ticks = budget_ns * (double)e->wall_khz * 1e-6;
+        HIP_TRY(launch_deadline_start(e->deadline, ticks < 1.8e19 ? (uint64_t)ticks : (uint64_t)1.8e19, e->stream));
+        HIP_TRY(hipMemsetAsync(e->sims_run, 0, (size_t)t.G * 4, e->stream));
+        e->last_sims_dev = true;
+        return 0;
+    };
+    uint64_t* const dl = budget_ns > 0 ? e->deadline : nullptr;
+    uint32_t* const sr = budget_ns > 0 ? e->sims_run : nullptr;
     const bool noise = e->cfg.train_noise && e->noise;
     // the one-launch search (oaz_search_lat.hip): a workgroup per game runs all its simulations, when the
     // per-step loop would launch one NN workgroup per game anyway and nothing needs the host or a second
     // stream between simulation steps
     const bool hash = e->cfg.evaluator == OAZ_EVAL_HASH;
-    if (e->cfg.step_kernels == 0 && !noise && budget_ns <= 0 && !compact_leaves(e, t.G) && t.G <= (uint32_t)e->cus &&
+    if (e->cfg.step_kernels == 0 && !noise && !compact_leaves(e, t.G) && t.G <= (uint32_t)e->cus &&
         (hash || e->cfg.precision == OAZ_FP32_SPLIT16) && tree_seg_kernels()) {
         const NNView w = nn_view(e, nullptr);
         TreeView tl = t;  // rows = game ids (no compaction arrays)
@@ -1201,19 +1259,20 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
         tl.slot = nullptr;
         e->times.parts = 1;
         e->timing_skip = false;
+        if (int rc = device_budget()) return rc;
         if (int rc = timed(e, 6, t.G, [&] {
                 return launch_search_lat(tl, roots, active, prm, (int)sims, hash ? nullptr : &w, e->policy, e->value,
-                                         e->stream);
+                                         dl, sr, e->stream);
             }))
             return rc;
-        e->last_sims = sims;
+        e->last_sims = sims;  // (with a budget: replaced by the games' largest count when it is asked for)
         return 0;
     }
     const size_t slot_elems = (size_t)kNoiseChunk * t.G * kNoiseStride;
     const uint32_t nchunks = (sims + kNoiseChunk - 1) / kNoiseChunk;
     // up to one round of 16-game workgroups (k_search_grp): one launch per noise chunk of simulations,
     // each workgroup walking, evaluating and backing up its 16 games without a grid-wide step
-    const bool grp = e->cfg.step_kernels == 0 && budget_ns <= 0 && !compact_leaves(e, t.G) &&
+    const bool grp = e->cfg.step_kernels == 0 && !compact_leaves(e, t.G) &&
                      (t.G + 15) / 16 <= (uint32_t)e->cus && (hash || e->cfg.precision == OAZ_FP32_SPLIT16) &&
                      tree_seg_kernels();
     // The games in nh parts, each on its own stream: one part's tree kernels, leaf compaction and NN
@@ -1221,6 +1280,8 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
     // tree kernels cannot share a CU with it, only fill the CUs it leaves idle). The parts meet only
     // through the root-noise ring: chunk c + 2 overwrites chunk c's slot once every part is done with it.
     const int nh = grp ? 1 : game_parts(e, t.G);
+    if (grp)
+        if (int rc = device_budget()) return rc;
     auto produce = [&](uint32_t c) -> int {
         if (c >= 2)
             for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[c & 1][h], 0));
@@ -1286,7 +1347,7 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
             const float* nz = noise ? e->noise + (c & 1) * slot_elems : nullptr;
             if (int rc = timed(e, 6, t.G * (s1 - s0), [&] {
                     return launch_search_grp(tv[0], roots, active, prm, (int)s0, (int)s1, nz, hash ? nullptr : &w,
-                                             e->policy, e->value, sh[0]);
+                                             e->policy, e->value, dl, sr, sh[0]);
                 }, sh[0]))
                 return rc;
             e->last_sims = s1;

@@ -136,13 +136,20 @@ hipError_t launch_search_finalize(const TreeView& t, const oaz_state* roots, oaz
 bool tree_seg_kernels();
 // All `sims` simulations of every game in one launch, one workgroup per game (oaz_search_lat.hip):
 // w = the fp16x3 network, or null for the HASH test evaluator; no root noise; rows = game ids.
+// deadline / sims_run (Q7 search_time, both null without a budget): each workgroup stops before a simulation
+// s >= 1 at which the device clock is at or past *deadline; sims_run[g] = the simulations game g ran.
 hipError_t launch_search_lat(const TreeView& t, const oaz_state* roots, const uint8_t* active, SearchParams p,
-                             int sims, const NNView* w, float* policy, float* value, hipStream_t st);
+                             int sims, const NNView* w, float* policy, float* value, const uint64_t* deadline,
+                             uint32_t* sims_run, hipStream_t st);
 // Simulations [s0, s1) of every game, 16 games per workgroup, in one launch (oaz_search_lat.hip): noise =
 // the ring chunk holding simulation s0's draws ([s1 - s0][G][kNoiseStride]) or null; w as above. The
-// last simulation's expand / backup is the caller's (launch_expand_backup).
+// last simulation's expand / backup is the caller's (launch_expand_backup). deadline / sims_run as above, per
+// 16-game group; a group that stopped in an earlier chunk exits at once (sims_run must start at 0).
 hipError_t launch_search_grp(const TreeView& t, const oaz_state* roots, const uint8_t* active, SearchParams p, int s0,
-                             int s1, const float* noise, const NNView* w, float* policy, float* value, hipStream_t st);
+                             int s1, const float* noise, const NNView* w, float* policy, float* value,
+                             const uint64_t* deadline, uint32_t* sims_run, hipStream_t st);
+// *deadline = the device clock (wall_clock64, hipDeviceAttributeWallClockRate) when the kernel runs + ticks
+hipError_t launch_deadline_start(uint64_t* deadline, uint64_t ticks, hipStream_t st);
 hipError_t launch_selfplay_move(const TreeView& t, const SlotView& s, hipStream_t st);
 hipError_t launch_selfplay_reset(const TreeView& t, const SlotView& s, hipStream_t st);
 hipError_t launch_stats_reduce(const uint64_t* per_game, uint32_t G, uint64_t* out /* GS_COUNT */,

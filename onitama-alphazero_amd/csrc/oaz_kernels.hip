@@ -557,11 +557,6 @@ __device__ __forceinline__ uint32_t seg_incl_scan(uint32_t v) {  // row_shr 1, 2
     v += dpp_u32<0x118>(v);
     return v;
 }
-__device__ __forceinline__ double shfl_f64(double v, int src) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)b, src), hi = (uint32_t)__shfl((int)(uint32_t)(b >> 32), src);
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
 template <class T>
 __device__ __forceinline__ T pick3(int c, const T& a, const T& b, const T& d) {
     return c == 0 ? a : c == 1 ? b : d;
@@ -631,53 +626,6 @@ __device__ __forceinline__ int root_fold(int K, int Kmax, const NodeRegs (&ch)[3
     double qa = bcast_f64<0>(f.q), ba = bcast_f64<0>(f.base), sa = bcast_f64<0>(f.sq);
     // j = I + 1 = 1 .. 39; stop once every segment's K is passed (wave-uniform)
     (void)((I + 1 < Kmax ? (fold_step<I + 1>(acc, qa, ba, sa, K, f, ch, na, nb, sqn, prm), true) : false) && ...);
-    return acc;
-}
-
-#ifndef OAZ_FOLD_CP
-#define OAZ_FOLD_CP 0
-#endif
-// The same fold by change points (A/B build -DOAZ_FOLD_CP=1): with the running best fixed, every later
-// comparison j is evaluated at once (lane j & 15 of chunk j >> 4, the same operands and operation order
-// as fold_step, so the same results) and the first takeover found by ballot becomes the new running
-// best; one round per takeover instead of one step per child. Rows (games) advance independently.
-__device__ __forceinline__ int root_fold_cp(int K, const NodeRegs (&ch)[3], const float (&na)[3], const float (&nb)[3],
-                                            double sqn, const SearchParams& prm) {
-    const int sl = seg_lane(), sb = seg_base(), row = sb >> 4;
-    FoldCh f[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) f[c] = fold_chunk(ch[c], na[c], nb[c], sqn, prm);
-    int acc = 0;
-    double qa = bcast_f64<0>(f[0].q), ba = bcast_f64<0>(f[0].base), sa = bcast_f64<0>(f[0].sq);
-    bool live = K > 1;
-    while (__ballot(live)) {
-        int first = 64;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const int j = 16 * c + sl;
-            const double ua = qa + prm.c_puct * (ba + f[c].nae) * sa;
-            const bool take = live && j > acc && j < K &&
-                              !(total_key(ua) > __builtin_bit_cast(int64_t, f[c].kub));
-            const uint64_t m = __ballot(take);
-            const uint32_t rm = (uint32_t)(m >> (16 * row)) & 0xFFFFu;
-            if (first == 64 && rm) first = 16 * c + __builtin_ctz(rm);
-        }
-        const int fs = first < 64 ? first : 0;
-        const int src = sb + (fs & 15), fc = fs >> 4;
-        const double qn = shfl_f64(pick3(fc, f[0].q, f[1].q, f[2].q), src);
-        const double bn = shfl_f64(pick3(fc, f[0].base, f[1].base, f[2].base), src);
-        const double sn = shfl_f64(pick3(fc, f[0].sq, f[1].sq, f[2].sq), src);
-        if (live) {
-            if (first < 64) {
-                acc = first;
-                qa = qn;
-                ba = bn;
-                sa = sn;
-            } else {
-                live = false;
-            }
-        }
-    }
     return acc;
 }
 
@@ -800,12 +748,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
             }
             const int Kmax = max(max(__builtin_amdgcn_readlane(K, 0), __builtin_amdgcn_readlane(K, 16)),
                                  max(__builtin_amdgcn_readlane(K, 32), __builtin_amdgcn_readlane(K, 48)));
-#if OAZ_FOLD_CP
-            (void)Kmax;
-            best = root_fold_cp(K, ch, na, nb, sqn, prm);
-#else
             best = root_fold(K, Kmax, ch, na, nb, sqn, prm, std::make_integer_sequence<int, 39>{});
-#endif
         } else {
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -1324,6 +1267,17 @@ hipError_t launch_selfplay_reset(const TreeView& t, const SlotView& s, hipStream
 }
 hipError_t launch_stats_reduce(const uint64_t* per_game, uint32_t G, uint64_t* out, hipStream_t st) {
     hipLaunchKernelGGL(k_stats_reduce, dim3(GS_COUNT), dim3(256), 0, st, per_game, G, out);
+    return hipGetLastError();
+}
+
+// Q7 search_time on the device: the search's deadline on the device's constant-rate clock, taken when this
+// kernel runs (just before the search's first kernel on the same stream; mcts_arena.rs:75-78 starts its
+// Instant at the top of search()).
+__global__ void k_deadline_start(uint64_t* deadline, uint64_t ticks) {
+    if (threadIdx.x == 0) *deadline = (uint64_t)wall_clock64() + ticks;
+}
+hipError_t launch_deadline_start(uint64_t* deadline, uint64_t ticks, hipStream_t st) {
+    hipLaunchKernelGGL(k_deadline_start, dim3(1), dim3(64), 0, st, deadline, ticks);
     return hipGetLastError();
 }
 

@@ -290,6 +290,8 @@ extern "C" int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pur
     // on cfg->device, on a stream of its own: a search on a worker thread neither lands on the thread's
     // default device nor waits for (or stalls) the engines searching on the same GPU meanwhile
     hipStream_t sm = nullptr;
+    int prev_dev = -1;  // the calling thread's current device, restored on return
+    if ((e = hipGetDevice(&prev_dev)) != hipSuccess) prev_dev = -1;
     if ((e = hipSetDevice(cfg->device)) != hipSuccess) fail(e, "set device");
     else if ((e = hipStreamCreateWithFlags(&sm, hipStreamNonBlocking)) != hipSuccess) fail(e, "stream");
     else if ((e = hipMalloc(&d_roots, sizeof(oaz_state) * G)) != hipSuccess) fail(e, "alloc");
@@ -311,7 +313,7 @@ extern "C" int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pur
         (void)hipMemcpyAsync(out_value, d_val, sizeof(float) * G, hipMemcpyDeviceToHost, sm);
         (void)hipMemcpyAsync(st.data(), d_st, sizeof(uint64_t) * st.size(), hipMemcpyDeviceToHost, sm);
         if ((e = hipStreamSynchronize(sm)) != hipSuccess) fail(e, "copy");
-        if (stats)
+        if (stats && !rc)
             for (int g = 0; g < G; ++g) {
                 stats->playouts += st[g * 8 + 0];
                 stats->expansions += st[g * 8 + 1];
@@ -321,7 +323,7 @@ extern "C" int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pur
                 if (st[g * 8 + 5] > stats->max_nodes) stats->max_nodes = st[g * 8 + 5];
                 stats->tree_full += st[g * 8 + 6];
             }
-        if (tree_out && tree_cap) {
+        if (tree_out && tree_cap && !rc) {
             for (int g = 0; g < G; ++g)
                 (void)hipMemcpyAsync(tree_out + (size_t)g * tree_cap, d_nodes + (size_t)g * cap,
                                      sizeof(oaz_pure_node) * (tree_cap < cap ? tree_cap : cap), hipMemcpyDeviceToHost, sm);
@@ -336,5 +338,6 @@ extern "C" int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pur
     if (d_st) (void)hipFree(d_st);
     if (d_nodes) (void)hipFree(d_nodes);
     if (sm) (void)hipStreamDestroy(sm);
+    if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
     return rc;
 }

@@ -16,8 +16,18 @@
 // other segments idle), the network is k_nn_h3s's body (bit-identical to k_nn_h3) with its in-kernel
 // fp16-range recompute, or the HASH test evaluator. Used when the per-step loop would launch one NN
 // workgroup per game anyway (games <= CUs), with the fp16x3 network or HASH, no root noise (the
-// Agent / arena config, train = false), no search-time budget and no leaf compaction
-// (oaz_engine.cpp run_sims; oaz_config.step_kernels = 1 turns it off).
+// Agent / arena config, train = false) and no leaf compaction (oaz_engine.cpp run_sims;
+// oaz_config.step_kernels = 1 turns it off).
+//
+// Q7 search_time on the device (both kernels): the reference's loop runs a playout while
+// `playouts < max_playouts && elapsed < search_time` (mcts_arena.rs:75-81), one clock read per playout.
+// Here thread 0 of a workgroup reads the device's constant-rate clock (wall_clock64) before every
+// simulation after the first and the workgroup stops there when it is at or past `*deadline` (written by
+// k_deadline_start on the same stream just before the search: its start + the budget), so a budgeted
+// search is still one launch (k_search_lat) or one launch per noise chunk (k_search_grp), never a host
+// round trip per simulation. Each workgroup stops on its own clock read: k_search_lat's games (one per
+// workgroup, as each reference agent has its own clock) and k_search_grp's 16-game groups may run different
+// playout counts (>= 1); sims_run[g] records game g's.
 namespace oaz {
 
 constexpr int kLatThreads = 512;  // 8 waves: k_nn_h3s's geometry; wave 4 also walks the tree
@@ -212,7 +222,8 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
                                                             int sims, int hash_eval, const float* __restrict__ blob,
                                                             int blocks, const float* __restrict__ xblob,
                                                             unsigned long long* __restrict__ fallback, float* policy,
-                                                            float* value) {
+                                                            float* value, const uint64_t* __restrict__ deadline,
+                                                            uint32_t* __restrict__ sims_run) {
     using C = H3Cfg<0>;
     __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
     static_assert(kLatPathOff + kLatPath * 4 + 32 + kLatSq * 8 + 64 * (int)sizeof(oaz_node) <= kLatLds,
@@ -289,6 +300,8 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
         }
     };
     if constexpr (DBG >= 1) tm0 = tm = __builtin_amdgcn_s_memtime();
+    const uint64_t dl = deadline ? *deadline : 0;  // Q7 (null: no budget, exactly `sims` simulations)
+    int ran = sims;
     for (int s = 0; s < sims; ++s) {
         if (!hash_eval && !resident) {  // at the start, and after an fp16-range recompute used the whole LDS
             const float* ph0 = blob + nn::kL1B + nn::kCh + nn::kL1Table + (size_t)blocks * 2 * (h3::kW + 2 * nn::kCh);
@@ -342,7 +355,16 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
                 resident = false;
             }
         }
-        __syncthreads();  // policy / value row g written; the network's LDS is free for the tree again
+        // policy / value row g written; the network's LDS is free for the tree again. With a budget, thread 0's
+        // clock read decides for the workgroup whether simulation s + 1 runs (its backup of s follows the loop)
+        if (deadline) {
+            if (__syncthreads_or(threadIdx.x == 0 && (uint64_t)wall_clock64() >= dl) && s + 1 < sims) {
+                ran = s + 1;
+                break;
+            }
+        } else {
+            __syncthreads();
+        }
     }
     if (walker) {
         lap(2);
@@ -363,6 +385,7 @@ __global__ void __launch_bounds__(kLatThreads) k_search_lat(TreeView t, const oa
     __syncthreads();
     lat_sync_tree(tl, tg, na, path_lds, true);  // the tree's top and the node count to global memory
     flush_stats();
+    if (deadline && threadIdx.x == 0) sims_run[g] = (uint32_t)ran;
 }
 
 // ---- one launch per noise chunk for up to 16 x CU-count games (k_search_grp) ---------------------------
@@ -392,15 +415,23 @@ __global__ void __launch_bounds__(kLatThreads) k_search_grp(TreeView t, const oa
                                                             int hash_eval, const float* __restrict__ blob, int blocks,
                                                             const float* __restrict__ xblob,
                                                             unsigned long long* __restrict__ fallback, float* policy,
-                                                            float* value) {
+                                                            float* value, const uint64_t* __restrict__ deadline,
+                                                            uint32_t* __restrict__ sims_run) {
     __shared__ __attribute__((aligned(16))) float lds[H3Fallback<C>::kLds];
     const int b0 = (int)blockIdx.x * nn::kSB;
+    // Q7: a group that stopped in an earlier chunk stays stopped (its count is below this chunk's start; the
+    // count is the same for the group's 16 games). Stopping before simulation s leaves s - 1's expand / back up
+    // pending, which the caller's final launch_expand_backup runs as after an unbudgeted search.
+    const uint64_t dl = deadline ? *deadline : 0;
+    if (deadline && s0 > 0 && sims_run[b0] < (uint32_t)s0) return;  // uniform over the workgroup
+    int s = s0;
     const int tid = (int)threadIdx.x, wave = tid >> 6;
     const bool walker = wave < 4;  // waves 0-3: four games each (segments)
     const uint32_t gs = walker ? (uint32_t)b0 + (uint32_t)(wave * 4 + ((tid >> 4) & 3)) : t.G;  // >= G: idle
     float* const sp = lds + (tid >> 4) * 52;  // the segment's policy row (the network's LDS, free meanwhile)
     const TileSpan span{b0, b0 + nn::kSB < (int)t.G ? b0 + nn::kSB : (int)t.G, (int)t.G};
-    for (int s = s0; s < s1; ++s) {
+    for (; s < s1; ++s) {
+        if (deadline && s > 0 && __syncthreads_or(tid == 0 && (uint64_t)wall_clock64() >= dl)) break;
         if (walker) {
             if (s > 0) grp_backup(t, roots, active, policy, value, gs, sp);  // simulation s - 1's expand / back up
             grp_select(t, roots, active, noise ? noise + (size_t)(s - s0) * t.G * kNoiseStride : nullptr, prm, gs);
@@ -438,21 +469,26 @@ __global__ void __launch_bounds__(kLatThreads) k_search_grp(TreeView t, const oa
         }
         __syncthreads();  // policy / value rows written; the LDS is the tree's again
     }
+    if (deadline && tid < nn::kSB && b0 + tid < (int)t.G) sims_run[b0 + tid] = (uint32_t)s;  // simulations run
 }
 
 hipError_t launch_search_grp(const TreeView& t, const oaz_state* roots, const uint8_t* active, SearchParams p, int s0,
-                             int s1, const float* noise, const NNView* w, float* policy, float* value, hipStream_t st) {
+                             int s1, const float* noise, const NNView* w, float* policy, float* value,
+                             const uint64_t* deadline, uint32_t* sims_run, hipStream_t st) {
+    if (deadline && !sims_run) return hipErrorInvalidValue;
     if (t.G == 0 || s1 <= s0) return hipSuccess;
     if (w && (!w->fallback || !w->blob_x6 || w->precision != OAZ_FP32_SPLIT16)) return hipErrorInvalidValue;
     const unsigned grid = (t.G + nn::kSB - 1) / nn::kSB;
     hipLaunchKernelGGL(k_search_grp<H3Cfg<0>>, dim3(grid), dim3(kLatThreads), 0, st, t, roots, active, p, s0, s1, noise,
                        w ? 0 : 1, w ? w->blob : nullptr, w ? w->blocks : 0, w ? w->blob_x6 : nullptr,
-                       w ? w->fallback : nullptr, policy, value);
+                       w ? w->fallback : nullptr, policy, value, deadline, sims_run);
     return hipGetLastError();
 }
 
 hipError_t launch_search_lat(const TreeView& t, const oaz_state* roots, const uint8_t* active, SearchParams p,
-                             int sims, const NNView* w, float* policy, float* value, hipStream_t st) {
+                             int sims, const NNView* w, float* policy, float* value, const uint64_t* deadline,
+                             uint32_t* sims_run, hipStream_t st) {
+    if (deadline && !sims_run) return hipErrorInvalidValue;
     if (t.G == 0 || sims <= 0) return hipSuccess;
     if (w && (!w->fallback || !w->blob_x6 || w->precision != OAZ_FP32_SPLIT16)) return hipErrorInvalidValue;
 #if OAZ_AB
@@ -460,19 +496,19 @@ hipError_t launch_search_lat(const TreeView& t, const oaz_state* roots, const ui
     if (dbg == 2) {
         hipLaunchKernelGGL(k_search_lat<2>, dim3(t.G), dim3(kLatThreads), 0, st, t, roots, active, p, sims, w ? 0 : 1,
                            w ? w->blob : nullptr, w ? w->blocks : 0, w ? w->blob_x6 : nullptr,
-                           w ? w->fallback : nullptr, policy, value);
+                           w ? w->fallback : nullptr, policy, value, deadline, sims_run);
         return hipGetLastError();
     }
     if (dbg == 1) {
         hipLaunchKernelGGL(k_search_lat<1>, dim3(t.G), dim3(kLatThreads), 0, st, t, roots, active, p, sims, w ? 0 : 1,
                            w ? w->blob : nullptr, w ? w->blocks : 0, w ? w->blob_x6 : nullptr,
-                           w ? w->fallback : nullptr, policy, value);
+                           w ? w->fallback : nullptr, policy, value, deadline, sims_run);
         return hipGetLastError();
     }
 #endif
     hipLaunchKernelGGL(k_search_lat<0>, dim3(t.G), dim3(kLatThreads), 0, st, t, roots, active, p, sims, w ? 0 : 1,
                        w ? w->blob : nullptr, w ? w->blocks : 0, w ? w->blob_x6 : nullptr,
-                       w ? w->fallback : nullptr, policy, value);
+                       w ? w->fallback : nullptr, policy, value, deadline, sims_run);
     return hipGetLastError();
 }
 

@@ -452,77 +452,6 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* M, const floa
     if (q == 0) part[(size_t)blockIdx.x * 64 + c] = sh[0][c] + sh[1][c] + sh[2][c] + sh[3][c];
 }
 
-// Consumer-side backward finalisation (A/B build, OAZ_TRAIN_CFIN_BWD=1): k_bn_bwd_fin and k_bn_bwd_apply
-// in one launch. Every workgroup
-// (64 rows, 1024 threads) re-reduces the [nwg][2][64] partials (sum m, sum m*xhat) in the same fixed
-// order; workgroup 0 writes dgamma / dbeta.
-__global__ __launch_bounds__(1024) void k_bn_bwd_apply_cfin(const float* bpart, int nwg, double N, const float* gamma,
-                                                            float* ggamma, float* gbeta, const float* M,
-                                                            const float* Z, const float* mean, const float* invstd,
-                                                            float* dZ, float* part, int R) {
-    __shared__ double sh[2][16][64];
-    __shared__ float cf[5][64];  // mean, invstd, gamma*invstd, mean(m), mean(m*xhat)
-    __shared__ float shs[16][64];
-    const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
-    {
-        double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
-        int w = q;
-        for (; w + 48 < nwg; w += 64) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                a1[u] += bpart[(size_t)(w + 16 * u) * 128 + c];
-                a2[u] += bpart[(size_t)(w + 16 * u) * 128 + 64 + c];
-            }
-        }
-        for (; w < nwg; w += 16) {
-            a1[0] += bpart[(size_t)w * 128 + c];
-            a2[0] += bpart[(size_t)w * 128 + 64 + c];
-        }
-        sh[0][q][c] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
-        sh[1][q][c] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
-    }
-    __syncthreads();
-    if (q == 0) {
-        double s1 = 0.0, s2 = 0.0;
-        for (int k = 0; k < 16; ++k) {
-            s1 += sh[0][k][c];
-            s2 += sh[1][k][c];
-        }
-        const float is = invstd[c];
-        cf[0][c] = mean[c];
-        cf[1][c] = is;
-        cf[2][c] = gamma[c] * is;
-        cf[3][c] = (float)(s1 / N);
-        cf[4][c] = (float)(s2 / N);
-        if (blockIdx.x == 0) {
-            gbeta[c] = (float)s1;
-            ggamma[c] = (float)s2;
-        }
-    }
-    __syncthreads();
-    const int r0 = blockIdx.x * 64;
-    const float mu = cf[0][c], is = cf[1][c], k1 = cf[2][c], k2 = cf[3][c], k3 = cf[4][c];
-    float s = 0.0f;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int r = r0 + q + 16 * u;
-        if (r < R) {
-            const size_t o = (size_t)r * kC + c;
-            const float xh = (Z[o] - mu) * is;
-            const float d = k1 * (M[o] - k2 - xh * k3);
-            dZ[o] = d;
-            s += d;
-        }
-    }
-    shs[q][c] = s;
-    __syncthreads();
-    if (q == 0) {
-        float t = 0.0f;
-        for (int k = 0; k < 16; ++k) t += shs[k][c];
-        part[(size_t)blockIdx.x * 64 + c] = t;
-    }
-}
-
 // ---- weight gradient: per (tap, square, row split z) partial D[co][ci] = sum_b dZ[sq,b][co] * X[nbr,b][ci]
 // v_mfma_f32_32x32x2_f32: lane l supplies A[m = l&31][k = l>>5] and B[k = l>>5][n = l&31], so one
 // k-pair = two rows, read as 128-B row segments. A wave owns the whole 64 x (32*NNT) tile (2 x NNT
@@ -1086,8 +1015,6 @@ struct oaz_trainer {
     int nconv = 0, maxB = 0;
     int cfin = -1;     // forward BN finalisation in k_bn_act_cfin (-1: one float4 per thread; A/B build: 0 = the
                        // separate k_bn_fwd_fin + k_bn_act launches, n > 0 = n workgroups)
-    bool cfin_bwd = false;  // A/B build: consumer-side backward BN finalisation
-    int bwd_u = 16;         // k_bn_bwd_apply rows per workgroup / 4 (A/B build: OAZ_TRAIN_BWD_U=4|8|32)
     int conv_rg = 2;  // 16-row groups per conv workgroup (OAZ_CONV_RG=1|2|4 overrides; tuning knob)
     size_t nparam = 0;
     std::vector<void*> allocs;
@@ -1181,8 +1108,6 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
         if (v == 1 || v == 2 || v == 4) t->conv_rg = v;
     }
     if (const char* e = getenv("OAZ_TRAIN_CFIN")) t->cfin = atoi(e) > 0 ? atoi(e) : 0;
-    t->cfin_bwd = getenv("OAZ_TRAIN_CFIN_BWD") != nullptr;
-    if (const char* e = getenv("OAZ_TRAIN_BWD_U")) t->bwd_u = atoi(e) == 4 ? 4 : atoi(e) == 8 ? 8 : atoi(e) == 32 ? 32 : 16;
 #endif
     t->nparam = t->L.total;
     const size_t R = (size_t)t->maxB * 25;
@@ -1417,7 +1342,8 @@ static int backward(oaz_trainer* t, int bi) {
     // dZ of layer l feeds both dgrad(l) (on st, the critical path) and wgrad(l) (on st2); dZ and
     // the bias partials are double-buffered so st never overwrites what st2 still reads.
     int nwg_part = nwg_rows;
-    const int nwg_bwd = (R + 4 * t->bwd_u - 1) / (4 * t->bwd_u);  // k_bn_bwd_apply<bwd_u> workgroups
+    constexpr int kBwdU = 16;  // k_bn_bwd_apply rows per workgroup / 4 (4, 8, 32 measured slower)
+    const int nwg_bwd = (R + 4 * kBwdU - 1) / (4 * kBwdU);
     bool used[2] = {false, false};
     for (int l = nl - 1; l >= 0; --l) {
         const int k = l & 1;
@@ -1426,27 +1352,11 @@ static int backward(oaz_trainer* t, int bi) {
         float* mx = t->bcoef + 128;
         float* dz = t->DZ[k];
         if (used[k]) HIP_TRY(hipStreamWaitEvent(st, t->ev_w[k], 0));
-        if (t->cfin_bwd) {
-            hipLaunchKernelGGL(k_bn_bwd_apply_cfin, dim3(nwg_rows), dim3(1024), 0, st, t->part, nwg_part, (double)R,
-                               P + L.bg[l], G + L.bg[l], G + L.bb[l], t->M[l], t->Z[l], t->mean[l], t->invstd[l], dz,
-                               t->bpart[k], R);
-        } else {
-            hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_part, 64, 0, 64, (double)R,
-                               P + L.bg[l], t->invstd[l], G + L.bg[l], G + L.bb[l], c1, mm, mx, 64, nullptr,
-                               nullptr, nullptr);
-            if (t->bwd_u == 4)
-                hipLaunchKernelGGL(k_bn_bwd_apply<4>, dim3(nwg_bwd), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
-                                   t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
-            else if (t->bwd_u == 32)
-                hipLaunchKernelGGL(k_bn_bwd_apply<32>, dim3(nwg_bwd), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
-                                   t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
-            else if (t->bwd_u == 8)
-                hipLaunchKernelGGL(k_bn_bwd_apply<8>, dim3(nwg_bwd), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
-                                   t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
-            else
-                hipLaunchKernelGGL(k_bn_bwd_apply<16>, dim3(nwg_bwd), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
-                                   t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
-        }
+        hipLaunchKernelGGL(k_bn_bwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_part, 64, 0, 64, (double)R,
+                           P + L.bg[l], t->invstd[l], G + L.bg[l], G + L.bb[l], c1, mm, mx, 64, nullptr,
+                           nullptr, nullptr);
+        hipLaunchKernelGGL(k_bn_bwd_apply<kBwdU>, dim3(nwg_bwd), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
+                           t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
         HIP_TRY(hipEventRecord(t->ev_dz[k], st));
         HIP_TRY(hipStreamWaitEvent(t->st2, t->ev_dz[k], 0));
         const float* X = l == 0 ? t->X0 : t->A[l - 1];
@@ -1458,7 +1368,7 @@ static int backward(oaz_trainer* t, int bi) {
         const int nred = 9 * kC * cin;
         hipLaunchKernelGGL(k_wgrad_reduce, dim3((nred + 255) / 256), dim3(256), 0, t->st2, t->wpart,
                            l == 0 ? kInPad : kC, cin, G + L.cw[l]);
-        hipLaunchKernelGGL(k_colsum, dim3(1), dim3(1024), 0, t->st2, t->bpart[k], t->cfin_bwd ? nwg_rows : nwg_bwd,
+        hipLaunchKernelGGL(k_colsum, dim3(1), dim3(1024), 0, t->st2, t->bpart[k], nwg_bwd,
                            64, 0, 64, G + L.cb[l]);
         HIP_TRY(hipEventRecord(t->ev_w[k], t->st2));
         used[k] = true;

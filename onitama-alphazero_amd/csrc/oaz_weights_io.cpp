@@ -354,7 +354,7 @@ int unpickle(const uint8_t* p, size_t n, Arena& A, uint32_t* result) {
                 if (st.size() < k) return bad("TUPLEn");
                 xs.assign(st.end() - (long)k, st.end());
                 st.resize(st.size() - k);
-                if (!mk(Val::TUPLE, &a)) return bad("TUPLEn");
+                if (k > kMaxRefs - refs || !mk(Val::TUPLE, &a)) return bad("TUPLEn");
                 A[a].items = xs;
                 refs += k;
                 st.push_back(a);
@@ -578,17 +578,20 @@ struct Bytes {
     void str(const std::string& s) { b += s; }
 };
 
-uint32_t crc32(const uint8_t* p, size_t n) {
-    static uint32_t table[256];
-    static bool init = false;
-    if (!init) {  // benign race: every thread writes the same values
+struct Crc32Table {
+    uint32_t t[256];
+    constexpr Crc32Table() : t{} {
         for (uint32_t i = 0; i < 256; ++i) {
             uint32_t c = i;
             for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-            table[i] = c;
+            t[i] = c;
         }
-        init = true;
     }
+};
+constexpr Crc32Table kCrc32;  // built at compile time: no lazy initialisation shared between threads
+
+uint32_t crc32(const uint8_t* p, size_t n) {
+    const uint32_t* table = kCrc32.t;
     uint32_t c = 0xFFFFFFFFu;
     for (size_t i = 0; i < n; ++i) c = table[(c ^ p[i]) & 0xFF] ^ (c >> 8);
     return c ^ 0xFFFFFFFFu;

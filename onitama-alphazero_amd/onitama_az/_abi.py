@@ -235,6 +235,7 @@ _PROTOS = {
     "oaz_set_search_params": (C.c_int, [_VOIDP, C.c_int, C.c_double, C.c_int]),
     "oaz_set_search_time": (C.c_int, [_VOIDP, C.c_int64]),
     "oaz_last_sims": (C.c_int, [_VOIDP, _P(C.c_int)]),
+    "oaz_search_playouts": (C.c_int, [_VOIDP, _VOIDP, C.c_int]),
     "oaz_load_weights": (C.c_int, [_VOIDP, _VOIDP, C.c_size_t]),
     "oaz_weight_tensor_count": (C.c_size_t, [C.c_int]),
     "oaz_weight_tensor_info": (C.c_int, [C.c_int, C.c_size_t, C.c_char_p, C.c_size_t, _P(C.c_size_t)]),

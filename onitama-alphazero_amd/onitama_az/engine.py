@@ -80,6 +80,13 @@ class Engine:
         _abi.check(self._lib.oaz_last_sims(self._h, C.byref(n)))
         return int(n.value)
 
+    def search_playouts(self, games: int) -> np.ndarray:
+        """Playouts each of the first `games` games of the last search ran (a device-side search_time
+        budget stops every game, or 16-game group, on its own clock read)."""
+        out = np.zeros(int(games), dtype=np.int32)
+        _abi.check(self._lib.oaz_search_playouts(self._h, _abi.ptr(out), int(games)))
+        return out
+
     def sync(self) -> None:
         _abi.check(self._lib.oaz_sync(self._h))
 

@@ -24,9 +24,10 @@ class AlphaZeroMctsConfig:  # alphazero_mcts/mod.rs:26-43
     exploration_c: float = math.sqrt(2.0)
     max_playouts: int = 5000
     train: bool = False
-    # Q7: False (default, the parity mode) runs exactly max_playouts playouts per search; True stops a
-    # search at the first simulation step that ends past search_time, as the reference's loop
-    # `while playouts < max_playouts && elapsed < search_time` (mcts_arena.rs:78) does
+    # Q7: False (default, the parity mode) runs exactly max_playouts playouts per search; True stops each
+    # game's search at the first playout that ends past search_time, as the reference's loop
+    # `while playouts < max_playouts && elapsed < search_time` (mcts_arena.rs:78) does (on the device
+    # clock inside the one-launch search; a batch of more than 16 x CU-count games stops together)
     enforce_search_time: bool = False
 
 
@@ -47,7 +48,8 @@ class ConvResNetConfig:  # net.rs:74-89
 
 @dataclass
 class Options:  # common.rs:8-23 (kind/device): precision and GPU ordinal
-    precision: int = _abi.FP32
+    # fp32 by the fp16x3 split (fp32-level error, the one-launch search's network); _abi.FP32 = exact fp32 MFMA
+    precision: int = _abi.FP32_SPLIT16
     device: int = 0
 
 

@@ -623,42 +623,56 @@ def test_set_search_params_per_agent_config(orc):
 
 
 # ---- Q7: the wall-clock search budget (opt-in) -------------------------------------------------
-def test_search_time_budget_stops_early_and_matches_oracle_at_that_budget(orc):
+@pytest.mark.parametrize("step_kernels", [0, 1])
+def test_search_time_budget_stops_early_and_matches_oracle_at_that_budget(orc, step_kernels):
     """oaz_config.search_time_ns (mcts_arena.rs:78: `while playouts < max_playouts && elapsed <
-    search_time`): a 25 ms budget on a 20 000-playout search stops early; every game ran the same
-    number of playouts, and trees, pi and moves equal the oracle's search with that many playouts."""
+    search_time`): a 25 ms budget on a 20 000-playout search stops early, and trees, pi and moves equal the
+    oracle's search with the playouts each game ran. step_kernels 0: the one-launch search (k_search_lat)
+    reads the device clock before every simulation, each game on its own, and stays ONE launch;
+    1: the per-step loop stops every game after the same simulation step."""
     roots = random_positions(orc, 8, seed=1313)
     with Engine(games=8, sims=20000, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_HASH, blocks=0,
-                parts=2) as e:
+                parts=2, step_kernels=step_kernels) as e:
+        e.set_timing(1)
         e.set_search_time(0.025)
         r = e.search(roots)
-        n = e.last_sims()
-        assert 1 <= n < 20000, n
-        assert r.stats.sims == 8 * n
+        k = e.kernel_times()
+        n = e.search_playouts(8)
+        assert np.all((n >= 1) & (n < 20000)), n
+        assert e.last_sims() == int(n.max()) and r.stats.sims == int(n.sum())
+        if step_kernels == 0:
+            assert (k.backup_select_n, k.select_n, k.expand_n) == (1, 0, 0)  # one launch, no host round trip
+        else:
+            assert np.all(n == n[0])
         for g in range(8):
-            mv, pi, nodes, _ = orc.search(orc.search_cfg(sims=n, c_puct=5.0, evaluator=orc.EVAL_HASH), roots[g])
+            mv, pi, nodes, _ = orc.search(orc.search_cfg(sims=int(n[g]), c_puct=5.0, evaluator=orc.EVAL_HASH), roots[g])
             _compare_trees(e, g, nodes)
             assert np.array_equal(r.pi[g].reshape(-1), pi.reshape(-1)) and _mv(r.moves[g]) == _mv(mv)
         e.set_search_time(0.0)  # off again: exactly `sims` playouts (the parity mode)
         e.set_search_params(64, 5.0, False)
         r = e.search(roots)
         assert e.last_sims() == 64 and r.stats.sims == 8 * 64
+        assert np.array_equal(e.search_playouts(8), np.full(8, 64))
 
 
-def test_search_time_budget_with_root_noise_then_full_search(orc):
+@pytest.mark.parametrize("step_kernels", [0, 1])
+def test_search_time_budget_with_root_noise_then_full_search(orc, step_kernels):
     """Q7 with root noise: the budget stops the search wherever the clock says, usually inside a
-    noise chunk whose successor's draws are already requested on the noise stream. The trees equal
-    the oracle's noisy search with the playouts that ran, and the engine's next search (ply 1, no
-    budget, its noise ring restarted) equals the oracle's as well (mcts_arena.rs:75-81, 183-223)."""
+    noise chunk whose successor's draws are already requested on the noise stream (step_kernels 0:
+    k_search_grp checks the device clock before every simulation, its 16-game group stops together and
+    the chunk launches after it exit at once; 1: the per-step loop). The trees equal the oracle's noisy
+    search with the playouts that ran, and the engine's next search (ply 1, no budget, its noise ring
+    restarted) equals the oracle's as well (mcts_arena.rs:75-81, 183-223)."""
     roots = random_positions(orc, 8, seed=1414)
     with Engine(games=8, sims=20000, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=77,
-                parts=2) as e:
+                parts=2, step_kernels=step_kernels) as e:
         e.set_search_time(0.02)
         e.search(roots)
-        n = e.last_sims()
-        assert 1 <= n < 20000, n
+        n = e.search_playouts(8)
+        assert np.all((n >= 1) & (n < 20000)) and np.all(n == n[0]), n  # one 16-game group / one step loop
         for g in range(8):
-            cfg = orc.search_cfg(sims=n, c_puct=5.0, evaluator=orc.EVAL_HASH, train_noise=1, seed=77, game_id=g, ply=0)
+            cfg = orc.search_cfg(sims=int(n[g]), c_puct=5.0, evaluator=orc.EVAL_HASH, train_noise=1, seed=77,
+                                 game_id=g, ply=0)
             _, _, nodes, _ = orc.search(cfg, roots[g])
             _compare_trees(e, g, nodes)
         e.set_search_time(0.0)
@@ -667,6 +681,27 @@ def test_search_time_budget_with_root_noise_then_full_search(orc):
         assert e.last_sims() == 48 and r.stats.sims == 8 * 48
         for g in range(8):
             cfg = orc.search_cfg(sims=48, c_puct=5.0, evaluator=orc.EVAL_HASH, train_noise=1, seed=77, game_id=g, ply=1)
+            mv, pi, nodes, _ = orc.search(cfg, roots[g])
+            _compare_trees(e, g, nodes)
+            assert np.array_equal(r.pi[g].reshape(-1), pi.reshape(-1)) and _mv(r.moves[g]) == _mv(mv)
+
+
+def test_search_time_budget_groups_stop_independently(orc):
+    """k_search_grp with a budget over several 16-game groups (40 games: three workgroups, the last one
+    partial): each group stops on its own clock read, the games of one group share a count, and every tree
+    equals the oracle's noisy search at its game's count."""
+    roots = random_positions(orc, 40, seed=1616)
+    with Engine(games=40, sims=20000, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=78) as e:
+        e.set_search_time(0.015)
+        r = e.search(roots)
+        n = e.search_playouts(40)
+        assert np.all((n >= 1) & (n < 20000)), n
+        for b in range(0, 40, 16):
+            assert np.all(n[b: b + 16] == n[b]), n
+        assert r.stats.sims == int(n.sum())
+        for g in (0, 17, 39):
+            cfg = orc.search_cfg(sims=int(n[g]), c_puct=5.0, evaluator=orc.EVAL_HASH, train_noise=1, seed=78,
+                                 game_id=g, ply=0)
             mv, pi, nodes, _ = orc.search(cfg, roots[g])
             _compare_trees(e, g, nodes)
             assert np.array_equal(r.pi[g].reshape(-1), pi.reshape(-1)) and _mv(r.moves[g]) == _mv(mv)

@@ -246,6 +246,21 @@ def test_ot_readers_bounded_on_crafted_pickles(tmp_path):
                 pass
     with pytest.raises(_abi.OazError, match="APPEND"):  # the direct self-reference is refused by name
         W.ot_blob(str(tmp_path / "self_append.ot"))
+    # container items up to one below the reader's cap (2^20) through APPENDS, then a TUPLE3 that would
+    # cross it: refused there (before ADVICE r4 TUPLE1..3 skipped the cap check, so the count passed the
+    # cap and every later check's unsigned subtraction wrapped, turning the cap off)
+    cap, chunk = 1 << 20, 65000
+    body = [b"\x80\x02Nq\x00]q\x01"]
+    left = cap - 1
+    while left:
+        k = min(chunk, left)
+        body.append(b"(" + b"h\x00" * k + b"e")
+        left -= k
+    body.append(b"h\x00h\x00h\x00\x87(" + b"h\x00" * 10 + b"e.")
+    p = tmp_path / "tuple3_over_cap.ot"
+    _pickle_archive(p, b"".join(body))
+    with pytest.raises(_abi.OazError, match="TUPLEn"):
+        W.ot_blob(str(p))
 
 
 def test_no_device_is_a_loud_error(lib):
