@@ -408,7 +408,11 @@ __device__ __noinline__ void grp_select(const TreeView& t, const oaz_state* root
     select_seg_body(t, roots, active, noise, prm, gs, nullptr, NodesGlobalRegs{});
 }
 
-template <class C>
+// DBG 1 (diagnostic, A/B build only: OAZ_GRP_DBG=1): thread 0's s_memtime cycles in the backups (wave 0's
+// four games), the selects, the barrier after them (the other walker waves' walks), and the evaluation with
+// its barriers, added to game b0's statistics slots GS_CUT / GS_RED / GS_MOVES / GS_BLUE (the whole loop to
+// GS_PASSES); the search's results are unchanged.
+template <class C, int DBG = 0>
 __global__ void __launch_bounds__(kLatThreads) k_search_grp(TreeView t, const oaz_state* __restrict__ roots,
                                                             const uint8_t* __restrict__ active, SearchParams prm,
                                                             int s0, int s1, const float* __restrict__ noise,
@@ -430,13 +434,26 @@ __global__ void __launch_bounds__(kLatThreads) k_search_grp(TreeView t, const oa
     const uint32_t gs = walker ? (uint32_t)b0 + (uint32_t)(wave * 4 + ((tid >> 4) & 3)) : t.G;  // >= G: idle
     float* const sp = lds + (tid >> 4) * 52;  // the segment's policy row (the network's LDS, free meanwhile)
     const TileSpan span{b0, b0 + nn::kSB < (int)t.G ? b0 + nn::kSB : (int)t.G, (int)t.G};
+    uint64_t cyc[5] = {0, 0, 0, 0, 0}, tm = 0, tm0 = 0;  // DBG: backup, select, walk barrier, evaluation, loop
+    auto lap = [&](int k) {
+        if constexpr (DBG >= 1) {
+            const uint64_t n = __builtin_amdgcn_s_memtime();
+            cyc[k] += n - tm;
+            tm = n;
+        }
+    };
+    if constexpr (DBG >= 1) tm0 = tm = __builtin_amdgcn_s_memtime();
     for (; s < s1; ++s) {
         if (deadline && s > 0 && __syncthreads_or(tid == 0 && (uint64_t)wall_clock64() >= dl)) break;
         if (walker) {
+            lap(3);
             if (s > 0) grp_backup(t, roots, active, policy, value, gs, sp);  // simulation s - 1's expand / back up
+            lap(0);
             grp_select(t, roots, active, noise ? noise + (size_t)(s - s0) * t.G * kNoiseStride : nullptr, prm, gs);
+            lap(1);
         }
         __syncthreads();  // the 16 leaf positions of simulation s
+        lap(2);
         if (hash_eval) {
             for (int k = tid; k < nn::kSB * 50; k += kLatThreads) {
                 const int gi = b0 + k / 50, e = k % 50;
@@ -469,6 +486,17 @@ __global__ void __launch_bounds__(kLatThreads) k_search_grp(TreeView t, const oa
         }
         __syncthreads();  // policy / value rows written; the LDS is the tree's again
     }
+    if constexpr (DBG >= 1) {
+        lap(3);
+        if (tid == 0 && b0 < (int)t.G) {
+            uint64_t* st = t.stats + (size_t)b0 * GS_COUNT;
+            atomicAdd((unsigned long long*)&st[GS_CUT], (unsigned long long)cyc[0]);
+            atomicAdd((unsigned long long*)&st[GS_RED], (unsigned long long)cyc[1]);
+            atomicAdd((unsigned long long*)&st[GS_MOVES], (unsigned long long)cyc[2]);
+            atomicAdd((unsigned long long*)&st[GS_BLUE], (unsigned long long)cyc[3]);
+            atomicAdd((unsigned long long*)&st[GS_PASSES], (unsigned long long)(tm - tm0));
+        }
+    }
     if (deadline && tid < nn::kSB && b0 + tid < (int)t.G) sims_run[b0 + tid] = (uint32_t)s;  // simulations run
 }
 
@@ -479,6 +507,15 @@ hipError_t launch_search_grp(const TreeView& t, const oaz_state* roots, const ui
     if (t.G == 0 || s1 <= s0) return hipSuccess;
     if (w && (!w->fallback || !w->blob_x6 || w->precision != OAZ_FP32_SPLIT16)) return hipErrorInvalidValue;
     const unsigned grid = (t.G + nn::kSB - 1) / nn::kSB;
+#if OAZ_AB
+    static const int dbg = getenv("OAZ_GRP_DBG") ? atoi(getenv("OAZ_GRP_DBG")) : 0;
+    if (dbg == 1) {
+        hipLaunchKernelGGL((k_search_grp<H3Cfg<0>, 1>), dim3(grid), dim3(kLatThreads), 0, st, t, roots, active, p, s0, s1,
+                           noise, w ? 0 : 1, w ? w->blob : nullptr, w ? w->blocks : 0, w ? w->blob_x6 : nullptr,
+                           w ? w->fallback : nullptr, policy, value, deadline, sims_run);
+        return hipGetLastError();
+    }
+#endif
     hipLaunchKernelGGL(k_search_grp<H3Cfg<0>>, dim3(grid), dim3(kLatThreads), 0, st, t, roots, active, p, s0, s1, noise,
                        w ? 0 : 1, w ? w->blob : nullptr, w ? w->blocks : 0, w ? w->blob_x6 : nullptr,
                        w ? w->fallback : nullptr, policy, value, deadline, sims_run);

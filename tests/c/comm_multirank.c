@@ -23,6 +23,10 @@
  *   4. again with every buffer empty: total 0, success;
  *   5. oaz_comm_broadcast from each root in turn (in place, NULL and explicit streams);
  *   6. oaz_comm_allreduce_sum_f32 (exact small sums) on the communicator's and on a caller stream.
+ * The stub is asynchronous as RCCL is (a collective is enqueued on the caller's stream and the call
+ * returns before it ran), so these results also check the product's stream ordering: the counts copy
+ * and the records behind the collectives on the communicator's stream, the read cursor advanced only
+ * after the exchange completed, the all-reduce ordered on a caller's stream.
  * Prints "OK rank r ..." per rank and "OK multirank W" at the end; exit 0 only if every rank passed. */
 #include <pthread.h>
 #include <stdint.h>
@@ -37,10 +41,11 @@ typedef void* hipStream_t;
 int hipMalloc(void** ptr, size_t size);
 int hipFree(void* ptr);
 int hipMemcpy(void* dst, const void* src, size_t bytes, int kind); /* 1 = H2D, 2 = D2H */
-int hipStreamCreate(hipStream_t* s);
+int hipStreamCreateWithFlags(hipStream_t* s, unsigned flags); /* 1 = hipStreamNonBlocking */
 int hipStreamDestroy(hipStream_t s);
 int hipStreamSynchronize(hipStream_t s);
 uint64_t rccl_stub_ops(void); /* from the stub: proves it served the calls */
+uint64_t rccl_stub_pending_at_return(void); /* ... and that they returned before their operations ran */
 
 #define MAXW 4
 static int W;
@@ -196,7 +201,10 @@ static void* rank_main(void* arg) {
     /* 6. all-reduce (sum), exact: x_i = (rank + 1) * i + 0.5 -> sum = i * W(W+1)/2 + W/2 */
     const size_t nf = 1000;
     fh = (float*)malloc(nf * sizeof(float));
-    CHECK(hipStreamCreate(&s) == 0);
+    /* non-blocking, as a multi-GPU host's streams are: the ranks here share one process, whose legacy
+     * default stream (the hipMemcpy calls) would otherwise wait on this stream's pending collective while
+     * its peers have not yet issued theirs */
+    CHECK(hipStreamCreateWithFlags(&s, 1) == 0);
     for (int pass = 0; pass < 2; ++pass) {
         for (size_t i = 0; i < nf; ++i) fh[i] = (float)((rank + 1) * (int)i) + 0.5f;
         CHECK(hipMemcpy(dev, fh, nf * sizeof(float), 1) == 0);
@@ -245,6 +253,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < W; ++r) fails += g_fail[r];
     for (int r = 0; r < W; ++r) free(g_expect[r]);
     if (fails) return 1;
-    printf("OK multirank %d (%llu stub collectives)\n", W, (unsigned long long)rccl_stub_ops());
+    printf("OK multirank %d (%llu stub collectives, %llu calls returned before their collective ran)\n", W,
+           (unsigned long long)rccl_stub_ops(), (unsigned long long)rccl_stub_pending_at_return());
     return 0;
 }

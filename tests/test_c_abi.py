@@ -48,8 +48,8 @@ def _model_files(tmp_path):
     return ot, gold
 
 
-def _run(exe, *args, env=None):
-    return subprocess.run([str(exe), *map(str, args)], capture_output=True, text=True, timeout=300, env=env)
+def _run(exe, *args, env=None, timeout=300):
+    return subprocess.run([str(exe), *map(str, args)], capture_output=True, text=True, timeout=timeout, env=env)
 
 
 def _rccl_symbols():
@@ -133,17 +133,29 @@ def test_rccl_stub_exports_what_the_product_resolves(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_c_allgather_samples_multirank(tmp_path, world):
+@pytest.mark.parametrize("world,delay_us", [(2, 0), (3, 0), (4, 0), (3, 3000)])
+def test_c_allgather_samples_multirank(tmp_path, world, delay_us):
     """The product exchange (oaz_allgather_samples, oaz_comm_broadcast, oaz_comm_allreduce_sum_f32) at
-    world 2 and 3: ranks are threads of one plain C process on GPU 0 over the RCCL test double
-    (tests/c/rccl_stub.c). Ragged counts with a zero-count rank, the capacity error, a local failure
-    on one rank seen by every rank (kLocalFailure), and every rank's output byte-equal to the
-    rank-order concatenation (train.rs:241-244). See tests/c/comm_multirank.c."""
+    world 2, 3 and 4: ranks are threads of one plain C process on GPU 0 over the RCCL test double
+    (tests/c/rccl_stub.c), which is asynchronous as RCCL is: each collective is enqueued on the caller's
+    stream and runs later on a proxy thread, so the results also test the product's stream ordering.
+    Ragged counts with a zero-count rank, the capacity error, a local failure on one rank seen by every
+    rank (kLocalFailure), and every rank's output byte-equal to the rank-order concatenation
+    (train.rs:241-244). With delay_us the stub sleeps that long on each stream before an operation's copies,
+    so every call returns well before its data moves (all of them counted as pending). See
+    tests/c/comm_multirank.c."""
     _, exe, env = _build_multirank(tmp_path)
-    r = _run(exe, world, env=env)
+    env["RCCL_STUB_DELAY_US"] = str(delay_us)
+    r = _run(exe, world, env=env, timeout=100)  # (the stub's own rendezvous timeout is 60 s)
     assert r.returncode == 0, r.stdout + r.stderr
     for rank in range(world):
         assert f"OK rank {rank}:" in r.stdout, r.stdout
-    assert f"OK multirank {world}" in r.stdout and "stub collectives" in r.stdout, r.stdout
+    m = re.search(rf"OK multirank {world} \((\d+) stub collectives, (\d+) calls returned before", r.stdout)
+    assert m, r.stdout
+    ops, pending = int(m.group(1)), int(m.group(2))
+    # per rank: 4 counts all-gathers, W - 1 grouped broadcasts, W broadcasts, 2 all-reduces; most of them
+    # (the ones that move bytes on the GPU) usually still pending when the call returned
+    assert ops >= world * (5 + 2 * world) and pending > 0, r.stdout
+    if delay_us:  # every operation that moves bytes on a rank: the counts all-gathers, the root's peers' copies
+        assert pending >= world * 4, r.stdout
     print(r.stdout)
