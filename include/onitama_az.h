@@ -174,7 +174,7 @@ typedef struct oaz_config {
                                 games of a batch may run different counts (>= 1, <= sims;
                                 oaz_search_playouts); larger batches stop together after a simulation step */
     int32_t step_kernels;    /* 0 = auto: a search of at most CU-count games with the fp16x3 network (or
-                                HASH), no root noise, no search_time budget and no leaf compaction runs as ONE
+                                HASH), no root noise and no leaf compaction runs as ONE
                                 launch, a workgroup per game doing all its simulations (the Agent API's
                                 one-position latency path); 1 = always the per-simulation-step launches.
                                 Trees, pi and samples are identical either way */

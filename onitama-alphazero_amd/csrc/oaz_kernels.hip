@@ -735,16 +735,22 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
             // root with noise: the sequential Iterator::max_by fold of k_select, every segment's
             // fold state (acc, operand a) held uniformly across its 16 lanes; child j's operands
             // are broadcast within each 16-lane row by DPP row_newbcast (j compile-time)
-            // the three chunks' draw pairs load unconditionally (index clamped inside the game's
-            // slot) so they are one round trip, not three; unused lanes then select 0
+            // the draw pairs of children 1 .. K-1 only: buffer loads whose lanes past K (or idle) get an
+            // offset past the resource's range, which returns 0 without a memory access (the noise ring
+            // holds 80 floats per game and simulation, most of them past a root's K). Unconditional
+            // instructions, so all three chunks' loads are in flight together: one round trip (exec-masked
+            // loads in branches get a wait each)
             float na[3], nb[3];
+            const __amdgpu_buffer_rsrc_t nr = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)noise, (short)0, (int)(t.G * (uint32_t)kNoiseStride * 4u), 0x00020000);
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                const int j = 16 * c + sl, jj = j < OAZ_MAX_MOVES ? j : OAZ_MAX_MOVES - 1;
-                const float2 d = *reinterpret_cast<const float2*>(noise + (size_t)(on ? g : 0) * kNoiseStride + 2 * jj);
-                const bool use = go && j >= 1 && j < K;
-                na[c] = use ? d.x : 0.0f;
-                nb[c] = use ? d.y : 0.0f;
+                const int j = 16 * c + sl;
+                const uint32_t off = go && j >= 1 && j < K ? (g * (uint32_t)kNoiseStride + 2u * (uint32_t)j) * 4u
+                                                          : 0x80000000u;
+                const auto d = __builtin_amdgcn_raw_buffer_load_b64(nr, (int)off, 0, 0);
+                na[c] = __uint_as_float(d[0]);
+                nb[c] = __uint_as_float(d[1]);
             }
             const int Kmax = max(max(__builtin_amdgcn_readlane(K, 0), __builtin_amdgcn_readlane(K, 16)),
                                  max(__builtin_amdgcn_readlane(K, 32), __builtin_amdgcn_readlane(K, 48)));
