@@ -687,6 +687,29 @@ struct NodesCached {
     }
 };
 
+// Per-wave statistics: the segment leads (lane 0 of each 16-lane segment) set in m contribute; the first
+// of them adds the wave's sums to its own game's row, one atomic per counter, so four segments' counters
+// dirty one line instead of four (the rows are only summed, and GS_MAXNODES maximised, over the games:
+// oaz_search_stats). m comes from a ballot, so a lead outside the exec mask never contributes.
+constexpr uint64_t kLeadLanes = 0x0001000100010001ull;
+__device__ __forceinline__ uint32_t lead_sum(uint32_t v, uint64_t m) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if ((m >> (16 * k)) & 1) r += (uint32_t)__builtin_amdgcn_readlane((int)v, 16 * k);
+    return r;
+}
+__device__ __forceinline__ uint32_t lead_max(uint32_t v, uint64_t m) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if ((m >> (16 * k)) & 1) {
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, 16 * k);
+            r = x > r ? x : r;
+        }
+    return r;
+}
+
 // g: this segment's game (>= t.G: an idle segment); leaf_lds: also store the leaf position there (LDS of
 // the one-launch search, whose network reads it without a global round trip), or null.
 template <class NA = NodesGlobal>
@@ -796,20 +819,26 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
         }
     }
     s.to_move = (uint8_t)color;
+    const bool need = leaf_needs_eval(nd.misc, s);
     if (on && sl == 0) {
-        const bool need = leaf_needs_eval(nd.misc, s);
         store_state(&t.leaf_state[g], s);
         if (leaf_lds) *leaf_lds = s;
         t.leaf[g] = node;
         t.depth[g] = depth;
         if (t.need) t.need[g] = need;
-        uint64_t* st = t.stats + (size_t)g * GS_COUNT;
-        na.add(st, GS_SIMS, 1);
-        na.add(st, GS_DEPTH, depth);
-        na.add(st, GS_EVALS, need);
-        if (stuck) na.add(st, GS_STUCK, 1);
     } else if (!on && g < t.G && sl == 0 && t.need) {
         t.need[g] = 0;  // an idle slot: nothing to evaluate
+    }
+    const uint64_t m = __ballot(on && sl == 0) & kLeadLanes;
+    if (m) {
+        const uint32_t dsum = lead_sum(depth, m), esum = lead_sum(need ? 1u : 0u, m), ssum = lead_sum(stuck ? 1u : 0u, m);
+        if (lane_id() == __builtin_ctzll(m)) {
+            uint64_t* st = t.stats + (size_t)g * GS_COUNT;
+            na.add(st, GS_SIMS, (uint64_t)__popcll(m));
+            na.add(st, GS_DEPTH, dsum);
+            na.add(st, GS_EVALS, esum);
+            if (ssum) na.add(st, GS_STUCK, ssum);
+        }
     }
 }
 
@@ -879,6 +908,8 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
         pW = na.at(T, pn)->W;
     }
     asm volatile("" ::"v"(polr[0]), "v"(polr[1]), "v"(polr[2]), "v"(polr[3]), "v"(vrow));  // issued in trip 2
+    bool expanded = false;  // this segment's statistics (summed per wave below)
+    uint32_t kids = 0, nodes_end = 0;
 
     if (!(node_flags(nd.misc) & 3)) {
         // the policy row kept in registers for the renormalisation sums and in LDS (sp) for the
@@ -939,10 +970,10 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
             lp->first = base;
             lp->nch = (uint8_t)K;
             lp->flags = 1;
-            na.add(st, GS_EXPANSIONS, 1);
-            na.add(st, GS_CHILDREN, K);
-            na.max(st, GS_MAXNODES, base + K);
         }
+        expanded = true;
+        kids = K;
+        nodes_end = base + K;
     }
     const int res = current_state(s);
     double r;
@@ -950,9 +981,21 @@ __device__ __forceinline__ void expand_backup_seg_body(const TreeView& t, const 
         const int root_color = na.root(roots, g)->to_move & 1;
         const int pc = depth == 0 ? root_color : (root_color ^ (int)((depth - 1) & 1));
         r = reward(res, pc);
-        if (sl == 0) na.add(st, GS_TERMINAL, 1);
     } else {
         r = (double)vrow;
+    }
+    {  // the statistics of the wave's segments that got here (the others returned above), per wave
+        const uint64_t m = __ballot(sl == 0) & kLeadLanes;
+        const uint32_t xs = lead_sum(expanded ? 1u : 0u, m), ks = lead_sum(kids, m), mx = lead_max(nodes_end, m);
+        const uint32_t ts = lead_sum(is_win(res) ? 1u : 0u, m);
+        if (m && lane_id() == __builtin_ctzll(m)) {
+            if (xs) {
+                na.add(st, GS_EXPANSIONS, xs);
+                na.add(st, GS_CHILDREN, ks);
+                na.max(st, GS_MAXNODES, mx);
+            }
+            if (ts) na.add(st, GS_TERMINAL, ts);
+        }
     }
     if (mine) {
         const double rk = ((depth - (uint32_t)sl) & 1) ? -r : r;
