@@ -710,13 +710,76 @@ __device__ __forceinline__ uint32_t lead_max(uint32_t v, uint64_t m) {
     return r;
 }
 
+// The root's noise draw pairs (operand a, operand b) of this lane's children j = 16c + sl, 1 <= j < K:
+// buffer loads whose lanes past K (or idle) get an offset past the resource's range, which returns 0
+// without a memory access (the noise ring holds 80 floats per game and simulation, most of them past a
+// root's K). Unconditional instructions, so all three chunks' loads are in flight together: one round
+// trip (exec-masked loads in branches get a wait each).
+__device__ __forceinline__ void root_noise_pairs(const TreeView& t, const float* noise, uint32_t g, bool go, int K,
+                                                 float (&na)[3], float (&nb)[3]) {
+    const int sl = seg_lane();
+    const __amdgpu_buffer_rsrc_t nr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)noise, (short)0, (int)(t.G * (uint32_t)kNoiseStride * 4u), 0x00020000);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const int j = 16 * c + sl;
+        const uint32_t off =
+            go && j >= 1 && j < K ? (g * (uint32_t)kNoiseStride + 2u * (uint32_t)j) * 4u : 0x80000000u;
+        const auto d = __builtin_amdgcn_raw_buffer_load_b64(nr, (int)off, 0, 0);
+        na[c] = __uint_as_float(d[0]);
+        nb[c] = __uint_as_float(d[1]);
+    }
+}
+
+// The root noise folds of a workgroup's 32 games, one lane per game (k_select_seg / k_backup_select_seg).
+// The fold is sequential by definition (a fresh draw per comparison against the running best,
+// mcts_arena.rs:183-223), so in the per-segment form every wave issued ~27 instructions per comparison for
+// its 4 games, Kmax - 1 times; here every segment stages its children's fold operands (everything that
+// does not depend on the running best, computed in parallel per child as before) in LDS, and ONE wave folds
+// all 32 games at once: ~1/6 of the fold's instructions per workgroup. Structure of arrays [child][game],
+// so the folding lanes' reads are bank-conflict free. 46.3 KB: three 8-wave workgroups per CU still fit
+// (the kernels' register budget allows three).
+constexpr int kWgGames = kWavesPerBlock * 4;
+struct WgFold {
+    int64_t kub[OAZ_MAX_MOVES][kWgGames];  // total_key of operand b (child j with its own draw)
+    double q[OAZ_MAX_MOVES][kWgGames];     // operand a's parts when child j is the running best
+    double base[OAZ_MAX_MOVES][kWgGames];
+    double sq[OAZ_MAX_MOVES][kWgGames];
+    float na[OAZ_MAX_MOVES][kWgGames];     // operand a's draw of comparison j (x eps in the fold)
+    int32_t K[kWgGames], best[kWgGames];
+};
+// lane = game gi of the workgroup (threadIdx.x < kWgGames): fold_step's comparisons in the same order and
+// with the same operands and expressions, so the same best child
+__device__ __forceinline__ void wg_fold_lane(WgFold* wf, const SearchParams& prm) {
+    const int gi = (int)threadIdx.x;
+    const int K = wf->K[gi];
+    int acc = 0;
+    double qa = wf->q[0][gi], ba = wf->base[0][gi], sa = wf->sq[0][gi];
+    for (int j = 1; __ballot(j < K) != 0; ++j) {  // uniform: until every game's K is passed
+        const double nae = (double)wf->na[j][gi] * prm.eps;
+        const int64_t kb = wf->kub[j][gi];
+        const double qj = wf->q[j][gi], bj = wf->base[j][gi], sj = wf->sq[j][gi];
+        const double ua = qa + prm.c_puct * (ba + nae) * sa;
+        if (j < K && !(total_key(ua) > kb)) {
+            acc = j;
+            qa = qj;
+            ba = bj;
+            sa = sj;
+        }
+    }
+    wf->best[gi] = acc;
+}
+
 // g: this segment's game (>= t.G: an idle segment); leaf_lds: also store the leaf position there (LDS of
 // the one-launch search, whose network reads it without a global round trip), or null.
-template <class NA = NodesGlobal>
+// WGF (k_select_seg / k_backup_select_seg: every thread of the workgroup calls this body): the root's noise
+// fold for the workgroup's games at once in wf (WgFold), the root level peeled off the walk so that every
+// wave reaches its two barriers; otherwise each segment folds its own game (16 lanes, DPP broadcasts).
+template <class NA = NodesGlobal, bool WGF = false>
 __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_state* __restrict__ roots,
                                                 const uint8_t* __restrict__ active, const float* __restrict__ noise,
                                                 const SearchParams& prm, uint32_t g, oaz_state* leaf_lds = nullptr,
-                                                const NA& na = NA{}) {
+                                                const NA& na = NA{}, WgFold* wf = nullptr) {
     const int sl = seg_lane(), sb = seg_base();
     const bool on = g < t.G && !(active && active[g] != 1);
     const bool fold_mode = prm.train_noise && noise;
@@ -733,69 +796,8 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
     if (on && sl == 0) path[pbase] = 0;
     bool stuck = false;
     bool go = on && (node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2);
-    while (__builtin_amdgcn_read_exec() && __ballot(go)) {  // some segment is still walking
-        const int K = go ? node_nch(nd.misc) : 0;
-        if (go && K == 0) {  // reference would panic in select (Q6): stop here, treat as a leaf
-            stuck = true;
-            go = false;
-        }
-        NodeRegs ch[3];
-        int64_t bkey = INT64_MIN;
-        int bidx = sl;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const int j = 16 * c + sl;
-            ch[c].W = 0.0;
-            ch[c].P = 0.0;
-            ch[c].N = 0;
-            ch[c].first = 0;
-            ch[c].misc = 0;
-            if (go && j < K) ch[c] = load_node(na.at(T, nd.first + j));
-        }
-        const double sqn = go ? na.sqrt_n(t, nd.N) : 0.0;
-        int best = 0;
-        if (depth == 0 && fold_mode) {
-            // root with noise: the sequential Iterator::max_by fold of k_select, every segment's
-            // fold state (acc, operand a) held uniformly across its 16 lanes; child j's operands
-            // are broadcast within each 16-lane row by DPP row_newbcast (j compile-time)
-            // the draw pairs of children 1 .. K-1 only: buffer loads whose lanes past K (or idle) get an
-            // offset past the resource's range, which returns 0 without a memory access (the noise ring
-            // holds 80 floats per game and simulation, most of them past a root's K). Unconditional
-            // instructions, so all three chunks' loads are in flight together: one round trip (exec-masked
-            // loads in branches get a wait each)
-            float na[3], nb[3];
-            const __amdgpu_buffer_rsrc_t nr = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)noise, (short)0, (int)(t.G * (uint32_t)kNoiseStride * 4u), 0x00020000);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const int j = 16 * c + sl;
-                const uint32_t off = go && j >= 1 && j < K ? (g * (uint32_t)kNoiseStride + 2u * (uint32_t)j) * 4u
-                                                          : 0x80000000u;
-                const auto d = __builtin_amdgcn_raw_buffer_load_b64(nr, (int)off, 0, 0);
-                na[c] = __uint_as_float(d[0]);
-                nb[c] = __uint_as_float(d[1]);
-            }
-            const int Kmax = max(max(__builtin_amdgcn_readlane(K, 0), __builtin_amdgcn_readlane(K, 16)),
-                                 max(__builtin_amdgcn_readlane(K, 32), __builtin_amdgcn_readlane(K, 48)));
-            best = root_fold(K, Kmax, ch, na, nb, sqn, prm, std::make_integer_sequence<int, 39>{});
-        } else {
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const int j = 16 * c + sl;
-                if (go && j < K) {
-                    const double q = ch[c].N ? ch[c].W / (double)ch[c].N : 0.0;
-                    const double sq = sqn / (double)(ch[c].N + 1);
-                    const double u = q + prm.c_puct * ch[c].P * sq;  // mcts_arena.rs:204-207
-                    const int64_t key = total_key(u);
-                    if (key >= bkey) {  // ascending j: the last maximum
-                        bkey = key;
-                        bidx = j;
-                    }
-                }
-            }
-            best = seg_argmax_last(bkey, bidx);
-        }
-        // the chosen child's node from the lane that holds it (chunk best >> 4 of lane best & 15)
+    // one level down: the chosen child of node nd (children in ch[], this segment's best index)
+    auto descend = [&](int best, const NodeRegs (&ch)[3]) {
         const int bc = best >> 4, src = sb + (best & 15);
         NodeRegs c;  // (the walk reads only N, first and misc of the node it descends to)
         c.W = 0.0;
@@ -817,6 +819,95 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
             nd = c;
             go = (node_flags(nd.misc) & 1) && !(node_flags(nd.misc) & 2);
         }
+    };
+    if (WGF && fold_mode) {  // the root level, every thread of the workgroup (uniform: kernel arguments)
+        const int gi = (int)(threadIdx.x >> 4);
+        const int K = go ? node_nch(nd.misc) : 0;
+        if (go && K == 0) {  // reference would panic in select (Q6): stop here, treat as a leaf
+            stuck = true;
+            go = false;
+        }
+        NodeRegs ch[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int j = 16 * c + sl;
+            ch[c].W = 0.0;
+            ch[c].P = 0.0;
+            ch[c].N = 0;
+            ch[c].first = 0;
+            ch[c].misc = 0;
+            if (go && j < K) ch[c] = load_node(na.at(T, nd.first + j));
+        }
+        const double sqn = go ? na.sqrt_n(t, nd.N) : 0.0;
+        float nza[3], nzb[3];
+        root_noise_pairs(t, noise, g, go, K, nza, nzb);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int j = 16 * c + sl;
+            if (go && j < K) {
+                const FoldCh f = fold_chunk(ch[c], nza[c], nzb[c], sqn, prm);
+                wf->kub[j][gi] = __builtin_bit_cast(int64_t, f.kub);
+                wf->q[j][gi] = f.q;
+                wf->base[j][gi] = f.base;
+                wf->sq[j][gi] = f.sq;
+                wf->na[j][gi] = nza[c];
+            }
+        }
+        if (sl == 0) wf->K[gi] = go ? K : 0;
+        __syncthreads();
+        if (threadIdx.x < (unsigned)kWgGames) wg_fold_lane(wf, prm);
+        __syncthreads();
+        descend(go ? wf->best[gi] : 0, ch);
+    }
+    while (__builtin_amdgcn_read_exec() && __ballot(go)) {  // some segment is still walking
+        const int K = go ? node_nch(nd.misc) : 0;
+        if (go && K == 0) {  // reference would panic in select (Q6): stop here, treat as a leaf
+            stuck = true;
+            go = false;
+        }
+        NodeRegs ch[3];
+        int64_t bkey = INT64_MIN;
+        int bidx = sl;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int j = 16 * c + sl;
+            ch[c].W = 0.0;
+            ch[c].P = 0.0;
+            ch[c].N = 0;
+            ch[c].first = 0;
+            ch[c].misc = 0;
+            if (go && j < K) ch[c] = load_node(na.at(T, nd.first + j));
+        }
+        const double sqn = go ? na.sqrt_n(t, nd.N) : 0.0;
+        int best = 0;
+        if (!WGF && depth == 0 && fold_mode) {
+            // root with noise: the sequential Iterator::max_by fold of k_select, every segment's
+            // fold state (acc, operand a) held uniformly across its 16 lanes; child j's operands
+            // are broadcast within each 16-lane row by DPP row_newbcast (j compile-time)
+            float na[3], nb[3];
+            root_noise_pairs(t, noise, g, go, K, na, nb);
+            const int Kmax = max(max(__builtin_amdgcn_readlane(K, 0), __builtin_amdgcn_readlane(K, 16)),
+                                 max(__builtin_amdgcn_readlane(K, 32), __builtin_amdgcn_readlane(K, 48)));
+            best = root_fold(K, Kmax, ch, na, nb, sqn, prm, std::make_integer_sequence<int, 39>{});
+        } else {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int j = 16 * c + sl;
+                if (go && j < K) {
+                    const double q = ch[c].N ? ch[c].W / (double)ch[c].N : 0.0;
+                    const double sq = sqn / (double)(ch[c].N + 1);
+                    const double u = q + prm.c_puct * ch[c].P * sq;  // mcts_arena.rs:204-207
+                    const int64_t key = total_key(u);
+                    if (key >= bkey) {  // ascending j: the last maximum
+                        bkey = key;
+                        bidx = j;
+                    }
+                }
+            }
+            best = seg_argmax_last(bkey, bidx);
+        }
+        // the chosen child's node from the lane that holds it (chunk best >> 4 of lane best & 15)
+        descend(best, ch);
     }
     s.to_move = (uint8_t)color;
     const bool need = leaf_needs_eval(nd.misc, s);
@@ -842,11 +933,16 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
     }
 }
 
+#ifndef OAZ_WG_FOLD
+#define OAZ_WG_FOLD 1  // the workgroup's root noise folds on one wave (WgFold); 0: per segment (A/B build)
+#endif
 // register budget: 80 VGPRs = 6 waves/SIMD (7 waves spill and measured 10 % slower)
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OAZ_TREE_WPE)))
 k_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
              const float* __restrict__ noise, SearchParams prm) {
-    select_seg_body(t, roots, active, noise, prm, seg_game());
+    __shared__ WgFold wf;
+    select_seg_body<NodesGlobalRegs, OAZ_WG_FOLD>(t, roots, active, noise, prm, seg_game(), nullptr, NodesGlobalRegs{},
+                                                  &wf);
 }
 
 template <int N>
@@ -1029,11 +1125,12 @@ k_backup_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8
                     const float* __restrict__ policy, const float* __restrict__ value, const float* __restrict__ noise,
                     SearchParams prm) {
     __shared__ float spol[kWavesPerBlock * 4][52];
+    __shared__ WgFold wf;
     const uint32_t g = seg_game();
-    expand_backup_seg_body(t, roots, active, policy, value, g, spol[threadIdx.x >> 4]);
+    expand_backup_seg_body(t, roots, active, policy, value, g, spol[threadIdx.x >> 4], NodesGlobalRegs{});
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    select_seg_body(t, roots, active, noise, prm, g);
+    select_seg_body<NodesGlobalRegs, OAZ_WG_FOLD>(t, roots, active, noise, prm, g, nullptr, NodesGlobalRegs{}, &wf);
 }
 
 // calculate_priors (mcts_arena.rs:104-124) + best child (87-94) for every root.

@@ -1357,21 +1357,27 @@ static int backward(oaz_trainer* t, int bi) {
                            nullptr, nullptr);
         hipLaunchKernelGGL(k_bn_bwd_apply<kBwdU>, dim3(nwg_bwd), dim3(256), 0, st, t->M[l], t->Z[l], t->mean[l],
                            t->invstd[l], c1, mm, mx, dz, t->bpart[k], R);
-        HIP_TRY(hipEventRecord(t->ev_dz[k], st));
-        HIP_TRY(hipStreamWaitEvent(t->st2, t->ev_dz[k], 0));
-        const float* X = l == 0 ? t->X0 : t->A[l - 1];
-        if (l == 0)
-            hipLaunchKernelGGL(k_wgrad<1>, dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
-        else
-            hipLaunchKernelGGL(k_wgrad<2>, dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
-        const int cin = l == 0 ? kIn : kC;
-        const int nred = 9 * kC * cin;
-        hipLaunchKernelGGL(k_wgrad_reduce, dim3((nred + 255) / 256), dim3(256), 0, t->st2, t->wpart,
-                           l == 0 ? kInPad : kC, cin, G + L.cw[l]);
-        hipLaunchKernelGGL(k_colsum, dim3(1), dim3(1024), 0, t->st2, t->bpart[k], nwg_bwd,
-                           64, 0, 64, G + L.cb[l]);
-        HIP_TRY(hipEventRecord(t->ev_w[k], t->st2));
-        used[k] = true;
+        // the weight gradient of layer l (second stream): it needs dz(l) and the layer's input X only, and runs
+        // beside dgrad(l) (started after dgrad(l) instead, beside the next layer's BN kernels: 0.846 vs 0.764 ms
+        // per step)
+        auto wgrad = [&]() -> int {
+            HIP_TRY(hipEventRecord(t->ev_dz[k], st));
+            HIP_TRY(hipStreamWaitEvent(t->st2, t->ev_dz[k], 0));
+            const float* X = l == 0 ? t->X0 : t->A[l - 1];
+            if (l == 0)
+                hipLaunchKernelGGL(k_wgrad<1>, dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
+            else
+                hipLaunchKernelGGL(k_wgrad<2>, dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
+            const int cin = l == 0 ? kIn : kC;
+            const int nred = 9 * kC * cin;
+            hipLaunchKernelGGL(k_wgrad_reduce, dim3((nred + 255) / 256), dim3(256), 0, t->st2, t->wpart,
+                               l == 0 ? kInPad : kC, cin, G + L.cw[l]);
+            hipLaunchKernelGGL(k_colsum, dim3(1), dim3(1024), 0, t->st2, t->bpart[k], nwg_bwd, 64, 0, 64, G + L.cb[l]);
+            HIP_TRY(hipEventRecord(t->ev_w[k], t->st2));
+            used[k] = true;
+            return 0;
+        };
+        if (int rc = wgrad()) return rc;
         if (l == 0) break;
         ConvArgs a{};
         a.in = dz;

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Same-box A/B of training-step builds (bench.py --mode train, batch 512, 5 blocks): ROUNDS interleaved rounds
+# over onitama_az/libonitama_az_<name>.so for each name in $NAMES; test_train.py on each first (TESTS=1).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
+L=$PWD/onitama-alphazero_amd/onitama_az
+if [ -n "${TESTS:-}" ]; then
+  for n in $NAMES; do
+    OAZ_LIB=$L/libonitama_az_$n.so timeout -k 10 300 python -m pytest tests/test_train.py -x -q -m gpu --timeout 200 \
+        --timeout-method thread 2>&1 | tail -1 | sed "s/^/$n tests: /" || exit 1
+  done
+fi
+for r in $(seq 1 ${ROUNDS:-3}); do
+  for n in $NAMES; do
+    OAZ_LIB=$L/libonitama_az_$n.so timeout -k 10 200 python bench.py --mode train --steps 200 --warmup 20 \
+        --no-cpu-baseline 2>/dev/null | tail -1 | python -c "
+import json, sys
+d = json.loads(sys.stdin.read())
+print(json.dumps({'lib': '$n', 'round': $r, 'ms_per_step': round(d['ms_per_step'], 4)}))" || exit 1
+  done
+done
