@@ -147,9 +147,8 @@ def pmc_traffic(args, cfg):
                          else None)
                     if k:
                         rows[k].append((int(r.get("Dispatch_Id", 0) or 0), float(r["Counter_Value"])))
-            if not rows["nn"]:
-                print(f"bench: PMC pass {ctr} collected no k_nn_ rows", file=sys.stderr)
-                return None
+            if not rows["nn"]:  # C2: the one-launch-per-chunk kernel k_search_grp runs the whole search
+                return pmc_grp_traffic(args, cfg, plies, stagger)
             for k, v in rows.items():  # the last ply's launches only (also if the range was not applied)
                 v.sort()
                 rows[k] = [x for _, x in v[-per_ply:]]
@@ -199,6 +198,45 @@ def pmc_traffic(args, cfg):
             "note": f"rocprofv3 --pmc, separate passes, on the {cfg['sims']} simulation steps of ply {plies + 1} "
                     f"(after {plies} warm-up plies, stagger {stagger}); FETCH_SIZE x2 (gfx950 wide-read "
                     "correction)"}
+
+
+def pmc_grp_traffic(args, cfg, plies, stagger):
+    """The k_search_grp launches' HBM bytes (C2: up to 16 x CU-count games, one launch per 16-simulation noise
+    chunk runs the walks, k_nn_h3's body and the backups of every game): FETCH_SIZE / WRITE_SIZE passes over
+    the launches of the ply after `plies` warm-up plies, as pmc_traffic does for k_nn_h3."""
+    prof = shutil.which("rocprofv3")
+    per_ply = (cfg["sims"] + 15) // 16  # k_search_grp launches per ply
+    first, last = plies * per_ply + 1, (plies + 1) * per_ply
+    kb = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        with tempfile.TemporaryDirectory() as d:
+            cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "k_search_grp",
+                   "--kernel-iteration-range", f"[{first}-{last}]", "--output-format", "csv", "-d", d, "-o", "pmc",
+                   "--", sys.executable, str(Path(__file__).resolve()), "--pmc-child", "--pmc-plies", str(plies),
+                   "--stagger", str(stagger), "--warmup", str(plies), "--config", args.config, "--games", str(cfg["games"]),
+                   "--sims", str(cfg["sims"]), "--fp32-kernel", args.fp32_kernel, "--pmc-parts", "1"]
+            try:
+                subprocess.run(cmd, timeout=600, capture_output=True, check=True)
+            except (subprocess.SubprocessError, OSError) as exc:
+                print(f"bench: PMC pass {ctr} (k_search_grp) failed ({type(exc).__name__})", file=sys.stderr)
+                return None
+            v = []
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                for r in csv.DictReader(open(f)):
+                    if r["Counter_Name"] == ctr and "k_search_grp" in r["Kernel_Name"]:
+                        v.append((int(r.get("Dispatch_Id", 0) or 0), float(r["Counter_Value"])))
+            if not v:
+                print(f"bench: PMC pass {ctr} collected no k_nn_ or k_search_grp rows", file=sys.stderr)
+                return None
+            v.sort()
+            v = [x for _, x in v[-per_ply:]]
+            kb[ctr] = sum(v) / len(v)
+    fetch, write = 2.0 * kb["FETCH_SIZE"] * 1024.0, kb["WRITE_SIZE"] * 1024.0
+    sims_per_launch = cfg["games"] * cfg["sims"] / per_ply
+    return {"kernel": "k_search_grp", "bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+            "bytes_per_sim": (fetch + write) / sims_per_launch, "raw_kb": kb, "launches_profiled": per_ply,
+            "note": f"rocprofv3 --pmc, separate passes, on the {per_ply} k_search_grp launches of ply {plies + 1} "
+                    f"(after {plies} warm-up plies, stagger {stagger}); FETCH_SIZE x2 (gfx950 wide-read correction)"}
 
 
 def pmc_clock(args, cfg):
@@ -956,7 +994,7 @@ def main():
         sims_steps = cfg["sims"]  # simulation steps (select -> NN -> expand launches) per bench step
         nn = nn_step_rate(kt, evals, args.steps * sims_steps, cfg["blocks"])
         parts, positions, achieved = nn["parts"], nn["positions"], nn["achieved"]
-        if traffic and parts != sim_parts(cfg["games"]):
+        if traffic and "game_parts" in traffic and parts != sim_parts(cfg["games"]):
             print(f"bench: PMC passes assumed {sim_parts(cfg['games'])} game parts, the run used {parts}",
                   file=sys.stderr)
         out = {
@@ -1044,7 +1082,7 @@ def main():
             "bound": "mfma", "kernel": NN_KERNEL[cfg["precision"]],
             "achieved": leg["achieved"], "peak": PEAK_TFLOPS[cfg["precision"]], "unit": "TFLOP/s",
             "frac": leg["achieved"] / PEAK_TFLOPS[cfg["precision"]],
-            "traffic": traffic["bytes_per_sim_step"] if traffic else None,
+            "traffic": (traffic or {}).get("bytes_per_sim_step"),
             "measured_on": "the same workload on one stream (oaz_config.parts = 1; 2 warm-up + 2 timed plies, no "
                            "staggered starts), HIP events around the NN launches of every 8th simulation step; "
                            "rocprofv3 kernel trace of the same launches: tools/trace_steady.py (last dispatches)",
@@ -1077,11 +1115,17 @@ def main():
                 "bound": "mfma", "kernel": sk["kernel"], "achieved": sk["achieved_TFLOPs"],
                 "peak": PEAK_TFLOPS[cfg["precision"]], "unit": "TFLOP/s",
                 "frac": sk["achieved_TFLOPs"] / PEAK_TFLOPS[cfg["precision"]],
-                "traffic": None, "flop_per_launch": FLOP_PER_SIM[cfg["blocks"]] * sk["sims_per_launch"],
+                "traffic": (traffic or {}).get("bytes_per_launch"),
+                "flop_per_launch": FLOP_PER_SIM[cfg["blocks"]] * sk["sims_per_launch"],
                 "avg_launch_ms": sk["avg_launch_ms"], "launches": sk["launches"],
                 "measured_on": "the timed region: HIP events around every k_search_grp launch (each covers "
                                "16 simulations of every game, tree work and noise waits included)",
-                "flop_accounting": "SURVEY 8d dense MACs x2 per sim", "nn_kernel_single_stream": nn_leg}
+                "flop_accounting": "SURVEY 8d dense MACs x2 per sim", "nn_kernel_single_stream": nn_leg,
+                # per simulation: the network's state in and policy / value out (24 + 204 B), the tree work
+                # (~1.95 KB at C3 depth and branching), the weights once per 16-game workgroup
+                "algorithmic_bytes_per_launch": sk["sims_per_launch"] * (24 + 204 + 1954)
+                                                + 0.96e6 * (cfg["games"] + 15) // 16 / 256,
+                "traffic_detail": traffic if (traffic or {}).get("kernel") == "k_search_grp" else None}
         bs = (out.get("tree_kernels") or {}).get("backup_select") or {}
         sq = (bs.get("pmc") or {}).get("sq")
         if leg.get("tree_launch_us"):

@@ -62,11 +62,12 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 // ---- gather: create_tensor_from_state (common.rs:26-80) for samples[idx[b]] ----------------------
 // threads [0, R): one input row (square, sample); [R, R + 50B): pi; [R + 50B, R + 51B): z
-__global__ void k_gather(const oaz_sample* samples, const int32_t* idx_all, const int32_t* cur, int B, float* X0,
-                         float* pi, float* z) {
+// bi: the batch number, or -1: the one kept on the device (*cur, advanced by the graph replay)
+__global__ void k_gather(const oaz_sample* samples, const int32_t* idx_all, const int32_t* cur, int bi, int B,
+                         float* X0, float* pi, float* z) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int R = B * 25;
-    const int32_t* idx = idx_all + (size_t)(*cur) * B;  // batch number kept on the device (graph replay)
+    const int32_t* idx = idx_all + (size_t)(bi >= 0 ? bi : *cur) * B;
     if (t >= R) {
         const int u = t - R;
         if (u < B * 50) pi[u] = samples[idx[u / 50]].pi[u % 50];
@@ -1275,8 +1276,7 @@ static int backward(oaz_trainer* t, int bi) {
     const int rg = t->conv_rg, rows_wg = 16 * rg;
     const int nwg_conv = 25 * ((B + rows_wg - 1) / rows_wg);
     const dim3 conv_grid((B + rows_wg - 1) / rows_wg, 25);
-    if (bi >= 0) hipLaunchKernelGGL(k_set_batch, dim3(1), dim3(64), 0, st, t->cur, bi, 0);
-    hipLaunchKernelGGL(k_gather, dim3((R + 51 * B + 255) / 256), dim3(256), 0, st, t->samples, t->idx, t->cur, B,
+    hipLaunchKernelGGL(k_gather, dim3((R + 51 * B + 255) / 256), dim3(256), 0, st, t->samples, t->idx, t->cur, bi, B,
                        t->X0, t->pi, t->z);
     // ---- forward
     for (int l = 0; l < nl; ++l) {
