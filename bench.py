@@ -293,6 +293,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 SIMDS = 1024  # 256 CUs x 4 SIMDs
 VALU_CYC = 2  # issue throughput of a wave64 32-bit VALU instruction on a SIMD-32 (MI355X_MICROARCH.md; f64 ops take more)
 NOMINAL_MHZ = 2400.0  # MI355X_MICROARCH.md: max engine clock (the MFMA peaks are quoted at it)
+XCDS = 8  # MI355X: 8 XCDs, each with its own L2 (written back and invalidated at kernel boundaries)
 XGMI_LINK_GBPS = 153.0  # per direction per link (7 links per GPU), the all-gather's reference rate
 
 
@@ -1078,6 +1079,7 @@ def main():
         # the dominant kernel's roofline, on one stream (single_stream_leg): per-launch HIP events
         leg = single_stream_leg(args, cfg, local, cfg["precision"])
         lp = leg["positions"]
+        nn_blob = float(_abi.load().oaz_nn_device_bytes(cfg["blocks"], getattr(_abi, PREC_ABI[cfg["precision"]])))
         out["roofline"] = {
             "bound": "mfma", "kernel": NN_KERNEL[cfg["precision"]],
             "achieved": leg["achieved"], "peak": PEAK_TFLOPS[cfg["precision"]], "unit": "TFLOP/s",
@@ -1090,7 +1092,16 @@ def main():
             "positions_per_launch": lp, "flop_accounting": "SURVEY 8d dense MACs x2 per sim",
             "achieved_nonzero": leg["nonzero_achieved"],
             "frac_nonzero": leg["nonzero_achieved"] / PEAK_TFLOPS[cfg["precision"]],
-            "algorithmic_bytes_per_launch": 0.96e6 + lp * (24 + 204),  # weights once + states in + outputs
+            # per launch: the packed weight image into each XCD's L2 (a launch starts with cold L2s:
+            # profiles/r05_nn_l2_standalone_pmc.txt) + 24 B state in + 204 B policy / value out per position
+            "algorithmic_bytes_per_launch": XCDS * nn_blob + lp * (24 + 204),
+            "algorithmic_note": f"weights {nn_blob / 1e6:.3f} MB x {XCDS} XCD L2 fills per launch (the L2s do not keep "
+                                "them across launches; the Infinity Cache serves the fills) + 24 B state in + 204 B "
+                                "policy / value out per position; per simulation step the launches of every game part",
+            "algorithmic_bytes_single_weight_copy": nn_blob + lp * (24 + 204),
+            # what `traffic` measures: one simulation step of the timed loop = one launch per game part
+            "algorithmic_bytes_per_sim_step": (traffic or {}).get("game_parts", 1) * XCDS * nn_blob
+                                              + cfg["games"] * (24 + 204),
             "traffic_detail": traffic,
             "peak_note": {"fp32": "F32 MFMA dense peak", "bf16": "BF16 dense MFMA peak",
                           "fp32_split": "BF16 dense MFMA peak / 6 products per fp32 MAC",

@@ -239,6 +239,10 @@ int oaz_device_count(int* n);               /* number of visible HIP devices */
 void oaz_attack_maps(uint32_t out[2 * 16 * 25]);
 /* Number of fp32 values in the canonical weight blob (tch VarStore order). */
 size_t oaz_weight_count(int blocks, int channels, int in_planes);
+/* Bytes of the packed, BN-folded weight image the network kernels read for `precision` (OAZ_FP32 ...
+ * OAZ_FP32_SPLIT16): every launch streams it into each XCD's L2 once (the L2s are written back and
+ * invalidated at kernel boundaries), which is the per-launch weight traffic bench.py's roofline counts. */
+size_t oaz_nn_device_bytes(int blocks, int precision);
 /* Random-init weights in canonical order: conv/linear U(-1/sqrt(fan_in), +1/sqrt(fan_in)),
  * BN gamma 1, beta 0, mean 0, var 1. */
 int oaz_random_weights(uint64_t seed, int blocks, float* out, size_t n);

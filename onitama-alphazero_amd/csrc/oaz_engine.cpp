@@ -81,6 +81,11 @@ extern "C" void oaz_attack_maps(uint32_t out[2 * 16 * 25]) {
     memcpy(out, kAttackHost.m, sizeof(kAttackHost.m));
 }
 
+extern "C" size_t oaz_nn_device_bytes(int blocks, int precision) {
+    if (blocks < 0 || blocks > 64 || precision < OAZ_FP32 || precision > OAZ_FP32_SPLIT16) return 0;
+    return nn_packed_floats(blocks, precision) * sizeof(float);
+}
+
 extern "C" size_t oaz_weight_count(int blocks, int channels, int in_planes) {
     const size_t C = (size_t)channels, I = (size_t)in_planes;
     size_t n = C * I * 9 + C + 4 * C;

@@ -220,6 +220,7 @@ _PROTOS = {
     "oaz_device_count": (C.c_int, [_P(C.c_int)]),
     "oaz_attack_maps": (None, [_VOIDP]),
     "oaz_weight_count": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
+    "oaz_nn_device_bytes": (C.c_size_t, [C.c_int, C.c_int]),
     "oaz_random_weights": (C.c_int, [C.c_uint64, C.c_int, _VOIDP, C.c_size_t]),
     "oaz_deal_deck": (None, [C.c_uint64, C.c_uint64, _VOIDP]),
     "oaz_initial_state": (None, [_VOIDP, _VOIDP]),

@@ -4,7 +4,7 @@ Compares library builds (OAZ_LIB) that differ only in the noise chunk (OAZ_NOISE
 whole ply's noise drawn before the first select, no noise launch shares the CUs with the tree
 kernel, which separates the fold's own cost from that contention. Experiment tool, not a test.
 
-usage: OAZ_LIB=... python tools/tree_noise_probe.py [games] [sims]
+usage: OAZ_LIB=... [OAZ_PROBE_NOISE=1,0] python tools/tree_noise_probe.py [games] [sims]
 """
 import json
 import os
@@ -46,5 +46,6 @@ if __name__ == "__main__":
     G = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     S = int(sys.argv[2]) if len(sys.argv) > 2 else 400
     lib = os.path.basename(os.environ.get("OAZ_LIB", "libonitama_az.so"))
-    for nz in (1, 0):
+    # OAZ_PROBE_NOISE: "1,0" (default), or one of them (a build that is only valid without root noise)
+    for nz in [int(x) for x in os.environ.get("OAZ_PROBE_NOISE", "1,0").split(",")]:
         print(json.dumps({"lib": lib, **probe(G, S, nz)}), flush=True)
