@@ -740,15 +740,12 @@ __device__ __forceinline__ void root_noise_pairs(const TreeView& t, const float*
 // so the folding lanes' reads are bank-conflict free. 46.3 KB: three 8-wave workgroups per CU still fit
 // (the kernels' register budget allows three).
 constexpr int kWgGames = kWavesPerBlock * 4;
-#ifndef OAZ_WGF_CH
-#define OAZ_WGF_CH OAZ_MAX_MOVES  // (a smaller value only for occupancy probes without root noise: A/B builds)
-#endif
 struct WgFold {
-    int64_t kub[OAZ_WGF_CH][kWgGames];  // total_key of operand b (child j with its own draw)
-    double q[OAZ_WGF_CH][kWgGames];     // operand a's parts when child j is the running best
-    double base[OAZ_WGF_CH][kWgGames];
-    double sq[OAZ_WGF_CH][kWgGames];
-    float na[OAZ_WGF_CH][kWgGames];     // operand a's draw of comparison j (x eps in the fold)
+    int64_t kub[OAZ_MAX_MOVES][kWgGames];  // total_key of operand b (child j with its own draw)
+    double q[OAZ_MAX_MOVES][kWgGames];     // operand a's parts when child j is the running best
+    double base[OAZ_MAX_MOVES][kWgGames];
+    double sq[OAZ_MAX_MOVES][kWgGames];
+    float na[OAZ_MAX_MOVES][kWgGames];     // operand a's draw of comparison j (x eps in the fold)
     int32_t K[kWgGames], best[kWgGames];
 };
 // lane = game gi of the workgroup (threadIdx.x < kWgGames): fold_step's comparisons in the same order and
