@@ -24,9 +24,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <algorithm>
-#include <queue>
-#include <type_traits>
 #include <vector>
 
 #include "../../include/onitama_az.h"
@@ -244,229 +241,6 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
         for (int r = 0; r < RG; ++r) v += red[r][k][c];
         a.part[wg * 128 + tid] = v;
     }
-}
-
-// Persistent form of the same conv: one workgroup per CU holds ALL taps' packed weights in LDS (9 x CH x
-// 4 n-tiles x 64 lanes float4 = 147 KB for 64 input channels), loaded once behind one barrier, and its 16
-// waves then run their (square, 16-row group) units with no further barrier: wave w computes n-tile w & 3
-// (16 output channels) of every (w >> 2)-th unit of the workgroup's list, A fragments straight from
-// global memory one tap ahead. The host balances the units (on-board tap counts 4 / 6 / 9) over the
-// workgroups (conv_schedule). BN partials: per wave over its units, then the 4 waves of an n-tile summed
-// in a fixed order -> part[workgroup][2][64].
-__device__ __forceinline__ int onboard_sq(int t, int j) {  // the j-th square (row-major) whose tap t is on the board
-    const int dy = t / 3 - 1, dx = t % 3 - 1, wx = 5 - (dx < 0 ? -dx : dx);
-    return ((dy < 0 ? 1 : 0) + j / wx) * 5 + (dx < 0 ? 1 : 0) + j % wx;
-}
-
-// WGR (input-gradient launches): after its units the workgroup also computes this layer's weight-gradient
-// partial over rows [f0, f1) of one tap (wseg[workgroup] = {tap, f0, f1}; row f = j * B + b over the tap's
-// on-board squares j): D[co][ci] = sum dZ[sq, b][co] * X[nbr(sq, tap), b][ci] on v_mfma_f32_32x32x2_f32, the
-// 16 waves interleaving k-pairs, summed through the LDS the weights held -> wpart[workgroup][64][64].
-template <int MODE, int CH, bool WGR = false>
-__global__ __launch_bounds__(1024) void k_conv_p(ConvArgs a, const int32_t* units, const int32_t* uoff, int nrg, int dbg,
-                                                 const int4* wseg, float* wpart) {
-    __shared__ float4 sw[9 * CH * 256];
-    __shared__ float red[16][2][16];
-    const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, kq = lane >> 4;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nt = wave & 3, co = nt * 16 + i;
-    const int B = a.B, u1 = uoff[blockIdx.x + 1];
-    constexpr int rs = 16 * CH;
-    int ui = uoff[blockIdx.x] + (wave >> 2);
-    float4 av[CH], an[CH];
-    float ep[MODE == CONV_DGRAD ? 3 : 1][4];
-    int sq = 0, b0 = 0, t = 0;
-    // the first unit's first-tap fragments and epilogue operands are requested before the weights
-    auto begin_unit = [&]() {
-        const int unit = units[ui];
-        sq = unit / nrg;
-        b0 = (unit - sq * nrg) * 16;
-        t = 0;
-        while (nbr(sq, t) < 0) ++t;
-        const float* base = a.in + (size_t)(nbr(sq, t) * B + b0 + i) * rs + 4 * kq;
-#pragma unroll
-        for (int g = 0; g < CH; ++g) av[g] = *reinterpret_cast<const float4*>(base + 16 * g);
-        if constexpr (MODE == CONV_DGRAD) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const size_t o = (size_t)(sq * B + b0 + kq * 4 + r) * kC + co;
-                ep[0][r] = a.skip ? a.skip[o] : 0.0f;
-                ep[1][r] = a.act[o];
-                ep[2][r] = a.zprev[o];
-            }
-        }
-    };
-    if (ui < u1) begin_unit();
-    if (dbg & 16) {  // LDS-DMA: each wave's 64 lanes land 1 KB lane-linear per instruction
-        constexpr int n = 9 * CH * 256;
-#pragma unroll
-        for (int k = 0; k < n / 1024; ++k)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.w + k * 1024 + tid),
-                                             (__attribute__((address_space(3))) void*)(sw + k * 1024 + wave * 64), 16, 0, 0);
-        if constexpr (n % 1024 != 0)
-            if (wave < (n % 1024) / 64)
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.w + (n / 1024) * 1024 + tid),
-                                                 (__attribute__((address_space(3))) void*)(sw + (n / 1024) * 1024 + wave * 64), 16, 0, 0);
-    } else if (!(dbg & 1)) {
-        constexpr int n = 9 * CH * 256, per = (n + 1023) / 1024;
-        float4 wv[per];
-#pragma unroll
-        for (int k = 0; k < per; ++k)
-            if (k * 1024 + tid < n) wv[k] = a.w[k * 1024 + tid];
-#pragma unroll
-        for (int k = 0; k < per; ++k)
-            if (k * 1024 + tid < n) sw[k * 1024 + tid] = wv[k];
-    }
-    __syncthreads();
-    float s1 = 0.0f, s2 = 0.0f;
-    const float bb = MODE == CONV_FWD ? a.bias[co] : 0.0f;
-    const float mu = MODE == CONV_DGRAD ? a.mean[co] : 0.0f, is = MODE == CONV_DGRAD ? a.invstd[co] : 0.0f;
-    if (dbg & 2) ui = u1;
-    while (ui < u1) {
-        f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        while (t < 9) {
-            int tn = t + 1;
-            while (tn < 9 && nbr(sq, tn) < 0) ++tn;
-            if (tn < 9 && !(dbg & 8)) {
-                const float* base = a.in + (size_t)(nbr(sq, tn) * B + b0 + i) * rs + 4 * kq;
-#pragma unroll
-                for (int g = 0; g < CH; ++g) an[g] = *reinterpret_cast<const float4*>(base + 16 * g);
-            }
-#pragma unroll
-            for (int g = 0; g < CH; ++g) {
-                const float4 bv = sw[(t * CH + g) * 256 + nt * 64 + lane];
-                if (dbg & 4) { acc[g] += av[g].x * bv.y; continue; }
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].x, bv.x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].y, bv.y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].z, bv.z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g].w, bv.w, acc, 0, 0, 0);
-            }
-            if (!(dbg & 8))
-#pragma unroll
-            for (int g = 0; g < CH; ++g) av[g] = an[g];
-            t = tn;
-        }
-        // C/D layout: reg r of lane l = (row 4*(l>>4) + r, col l&15)
-        const int sq0 = sq, bu = b0;
-        float e[MODE == CONV_DGRAD ? 3 : 1][4];
-#pragma unroll
-        for (int k = 0; k < (MODE == CONV_DGRAD ? 3 : 1); ++k)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) e[k][r] = ep[k][r];
-        ui += 4;
-        if (ui < u1) begin_unit();  // the next unit's loads fly during this epilogue
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const size_t o = (size_t)(sq0 * B + bu + kq * 4 + r) * kC + co;
-            if constexpr (MODE == CONV_FWD) {
-                const float v = acc[r] + bb;
-                a.out[o] = v;
-                s1 += v;
-                s2 += v * v;
-            } else {
-                const float d = acc[r] + e[0][r];
-                const float m = e[1][r] > 0.0f ? d : 0.0f;
-                a.out[o] = m;
-                s1 += m;
-                s2 += m * ((e[2][r] - mu) * is);
-            }
-        }
-    }
-    s1 = wave_sum16(s1);
-    s2 = wave_sum16(s2);
-    if (kq == 0) {
-        red[wave][0][i] = s1;
-        red[wave][1][i] = s2;
-    }
-    __syncthreads();
-    if (tid < 128) {
-        const int k = tid >> 6, c = tid & 63, n = c >> 4, j = c & 15;
-        a.part[(size_t)blockIdx.x * 128 + tid] = ((red[n][k][j] + red[4 + n][k][j]) + red[8 + n][k][j]) + red[12 + n][k][j];
-    }
-    if constexpr (WGR) {
-        const int4 sg = wseg[blockIdx.x];
-        const int tw = sg.x, f0 = sg.y, np = (sg.z - sg.y) >> 1;
-        const int c = lane & 31, h = lane >> 5;
-        typedef float f32x16 __attribute__((ext_vector_type(16)));
-        f32x16 acc2[2][2];
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int n = 0; n < 2; ++n) acc2[m][n] = f32x16{};
-        for (int p0 = wave; p0 < np; p0 += 64) {  // 4 k-pairs per wave per round, all loads issued first
-            float aa[4][2], bb[4][2];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int p = p0 + 16 * u;
-                if (p < np) {
-                    const int f = f0 + 2 * p + h, jj = f / B, b = f - jj * B, s2 = onboard_sq(tw, jj);
-                    const float* pa = a.in + (size_t)(s2 * B + b) * kC + c;
-                    const float* pb = a.act + (size_t)(nbr(s2, tw) * B + b) * kC + c;
-                    aa[u][0] = pa[0];
-                    aa[u][1] = pa[32];
-                    bb[u][0] = pb[0];
-                    bb[u][1] = pb[32];
-                } else {
-                    aa[u][0] = aa[u][1] = bb[u][0] = bb[u][1] = 0.0f;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int m = 0; m < 2; ++m)
-#pragma unroll
-                    for (int n = 0; n < 2; ++n)
-                        acc2[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(aa[u][m], bb[u][n], acc2[m][n], 0, 0, 0);
-        }
-        // D layout: col (ci) = lane&31, row (co) = (reg&3) + 8*(reg>>2) + 4*(lane>>5); 16 tiles -> 8 LDS slots -> 1
-        float* slot = reinterpret_cast<float*>(sw);
-        __syncthreads();  // every wave is past its last weight read
-        if (wave >= 8) {
-#pragma unroll
-            for (int m = 0; m < 2; ++m)
-#pragma unroll
-                for (int n = 0; n < 2; ++n)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        slot[(wave - 8) * 4096 + (32 * m + (r & 3) + 8 * (r >> 2) + 4 * h) * 64 + 32 * n + c] = acc2[m][n][r];
-        }
-        __syncthreads();
-        if (wave < 8) {
-#pragma unroll
-            for (int m = 0; m < 2; ++m)
-#pragma unroll
-                for (int n = 0; n < 2; ++n)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        slot[wave * 4096 + (32 * m + (r & 3) + 8 * (r >> 2) + 4 * h) * 64 + 32 * n + c] += acc2[m][n][r];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int e = tid; e < 4096; e += 1024) {
-            float v = 0.0f;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) v += slot[q * 4096 + e];
-            wpart[(size_t)blockIdx.x * 4096 + e] = v;
-        }
-    }
-}
-
-// grad_w[co][ci][tap] = the sum of the partials of the workgroups [ts[tap], ts[tap + 1]) (k_conv_p<..., WGR>)
-struct TapStart {
-    int s[10];
-};
-__global__ void k_wgrad_reduce_p(const float* part, TapStart ts, float* gw) {
-    const int id = blockIdx.x * blockDim.x + threadIdx.x;
-    if (id >= 9 * 4096) return;
-    const int t = id >> 12, e = id & 4095, co = e >> 6, ci = e & 63;
-    const int w0 = ts.s[t], w1 = ts.s[t + 1];
-    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    int w = w0;
-    for (; w + 4 <= w1; w += 4)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] += part[(size_t)(w + u) * 4096 + e];
-    for (; w < w1; ++w) v[0] += part[(size_t)w * 4096 + e];
-    gw[((size_t)co * kC + ci) * 9 + t] = (v[0] + v[1]) + (v[2] + v[3]);
 }
 
 // ---- BN finalisation (forward): batch mean / biased var, running stats update ----------------------
@@ -687,11 +461,9 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* M, const floa
 #define OAZ_WSPLIT 2
 #endif
 constexpr int kWSplit = OAZ_WSPLIT;  // row splits per (tap, square) (-DOAZ_WSPLIT: A/B variants)
-template <int NNT, bool SMALL = false>  // input-channel tiles of 32 (2 for 64 channels, 1 for the padded 32)
+template <int NNT>  // input-channel tiles of 32 (2 for 64 channels, 1 for the padded 32)
 __global__ __launch_bounds__(256) void k_wgrad(const float* dZ, const float* X, int B, float* part) {
-    // SMALL: the waves' tiles are summed through one 8 KB half tile, wave after wave (fits beside the
-    // persistent conv's 149.5 KB of LDS on one CU)
-    __shared__ float red[SMALL ? 1 : 3][SMALL ? 2048 : 64 * 64];
+    __shared__ float red[3][64 * 64];
     const int sq = blockIdx.x, t = blockIdx.y, zs = blockIdx.z;
     const int nb = nbr(sq, t);
     if (nb < 0) return;
@@ -737,35 +509,6 @@ __global__ __launch_bounds__(256) void k_wgrad(const float* dZ, const float* X, 
         }
     }
     // D layout: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
-    if constexpr (SMALL) {
-        float* out = part + ((size_t)(t * 25 + sq) * kWSplit + zs) * kC * xrs;
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            for (int w = 1; w < 4; ++w) {
-                if (wave == w) {
-#pragma unroll
-                    for (int n = 0; n < NNT; ++n)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            const int o = ((r & 3) + 8 * (r >> 2) + 4 * h) * xrs + 32 * n + c;
-                            red[0][o] = w == 1 ? acc[m][n][r] : red[0][o] + acc[m][n][r];
-                        }
-                }
-                __syncthreads();
-            }
-            if (wave == 0) {
-#pragma unroll
-                for (int n = 0; n < NNT; ++n)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int row = (r & 3) + 8 * (r >> 2) + 4 * h, o = row * xrs + 32 * n + c;
-                        out[(32 * m + row) * xrs + 32 * n + c] = acc[m][n][r] + red[0][o];
-                    }
-            }
-            __syncthreads();
-        }
-        return;
-    }
     if (wave > 0) {
         float* dst = red[wave - 1];
 #pragma unroll
@@ -1274,17 +1017,6 @@ struct oaz_trainer {
     int cfin = -1;     // forward BN finalisation in k_bn_act_cfin (-1: one float4 per thread; A/B build: 0 = the
                        // separate k_bn_fwd_fin + k_bn_act launches, n > 0 = n workgroups)
     int conv_rg = 2;  // 16-row groups per conv workgroup (OAZ_CONV_RG=1|2|4 overrides; tuning knob)
-    int conv_p = 0;   // persistent conv (k_conv_p) for: bit 0 the forward convs, bit 1 the input gradients
-                      // (else k_conv; A/B build: OAZ_CONV_P)
-    int ncu = 0;      // compute units: the persistent conv's grid
-    int convp_dbg = 0;
-    int wgrad_small = 0;  // k_wgrad's 8 KB reduction (co-resident with the persistent dgrad); A/B: OAZ_WGRAD_SMALL=0
-    int32_t *sched_units = nullptr, *sched_off = nullptr;  // conv_schedule() for sched_B
-    int sched_B = 0, sched_grid = 0;
-    int bwd_p = 1;  // input-gradient launches also compute the weight gradient (k_conv_p<1, 4, true>; A/B: OAZ_BWD_P=0)
-    int4* wseg = nullptr;         // [sched_grid] {tap, f0, f1} of that weight-gradient phase
-    float* wpart_p[2] = {};       // [sched_grid][64][64] its partials (double-buffered, as dz)
-    TapStart tap_start{};         // workgroups [s[t], s[t+1]) hold tap t
     size_t nparam = 0;
     std::vector<void*> allocs;
     float *P = nullptr, *G = nullptr, *MOM = nullptr;
@@ -1377,11 +1109,6 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
         if (v == 1 || v == 2 || v == 4) t->conv_rg = v;
     }
     if (const char* e = getenv("OAZ_TRAIN_CFIN")) t->cfin = atoi(e) > 0 ? atoi(e) : 0;
-    if (const char* e = getenv("OAZ_CONV_P")) t->conv_p = atoi(e);
-    if (const char* e = getenv("OAZ_CONVP_DBG")) t->convp_dbg = atoi(e);
-    if (const char* e = getenv("OAZ_CONVP_W")) t->ncu = atoi(e);
-    if (const char* e = getenv("OAZ_WGRAD_SMALL")) t->wgrad_small = atoi(e);
-    if (const char* e = getenv("OAZ_BWD_P")) t->bwd_p = atoi(e);
 #endif
     t->nparam = t->L.total;
     const size_t R = (size_t)t->maxB * 25;
@@ -1397,14 +1124,6 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
         return fail();
     }
     t->st = t->own;
-    if (!t->ncu && (hipDeviceGetAttribute(&t->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || t->ncu < 1)) {
-        oaz_set_err(OAZ_ERR_HIP, "trainer: CU count");
-        return fail();
-    }
-    if (t->alloc(t->sched_units, (size_t)25 * (t->maxB / 16)) || t->alloc(t->sched_off, (size_t)t->ncu + 1) ||
-        t->alloc(t->wseg, (size_t)t->ncu) || t->alloc(t->wpart_p[0], (size_t)t->ncu * 4096) ||
-        t->alloc(t->wpart_p[1], (size_t)t->ncu * 4096))
-        return fail();
     if (t->alloc(t->P, t->nparam) || t->alloc(t->G, t->nparam) || t->alloc(t->MOM, t->nparam) ||
         t->alloc(t->mask, t->nparam))
         return fail();
@@ -1512,72 +1231,6 @@ extern "C" int oaz_trainer_bind_device_samples(oaz_trainer* t, const oaz_sample*
     return 0;
 }
 
-// The persistent conv's work list for batch B: units (square, 16-row group) weighted by the square's
-// on-board taps (4 / 6 / 9), longest first, each to the least-loaded of min(CUs, units) workgroups
-// (ties: lowest index), so every workgroup carries ~1/ncu of the 169 (square, tap) pairs' rows.
-static int conv_schedule(oaz_trainer* t, int B) {
-    if (t->sched_B == B) return 0;
-    const int nrg = B / 16, nunits = 25 * nrg, W = std::min(t->ncu, nunits);
-    auto taps = [](int sq) {
-        const int y = sq / 5, x = sq % 5;
-        return (3 - (y == 0) - (y == 4)) * (3 - (x == 0) - (x == 4));
-    };
-    std::vector<int> order(nunits);
-    for (int u = 0; u < nunits; ++u) order[u] = u;
-    std::stable_sort(order.begin(), order.end(), [&](int p, int q) { return taps(p / nrg) > taps(q / nrg); });
-    std::priority_queue<std::pair<int, int>, std::vector<std::pair<int, int>>, std::greater<>> load;
-    for (int w = 0; w < W; ++w) load.push({0, w});
-    std::vector<std::vector<int32_t>> lists(W);
-    for (int u : order) {
-        auto [l, w] = load.top();
-        load.pop();
-        lists[w].push_back(u);
-        load.push({l + taps(u / nrg), w});
-    }
-    std::vector<int32_t> units, off(W + 1, 0);
-    units.reserve(nunits);
-    for (int w = 0; w < W; ++w) {
-        units.insert(units.end(), lists[w].begin(), lists[w].end());
-        off[w + 1] = (int32_t)units.size();
-    }
-    // the weight-gradient phase (k_conv_p<1, 4, true>): workgroups per tap in proportion to its on-board
-    // squares (16 / 20 / 25 of 169), each a contiguous range of whole 16-row groups of that tap's rows
-    int nt_[9], nsq[9], sum = 0;
-    for (int tp = 0; tp < 9; ++tp) {
-        nsq[tp] = (5 - (tp / 3 != 1)) * (5 - (tp % 3 != 1));
-        nt_[tp] = std::max(1, (int)(W * nsq[tp] / 169.0 + 0.5));
-        sum += nt_[tp];
-    }
-    while (sum != W) {  // the tap with the most (sum > W) / fewest (sum < W) workgroups per square gives / takes one
-        int best = -1;
-        for (int tp = 0; tp < 9; ++tp) {
-            if (sum > W && nt_[tp] == 1) continue;
-            const double r = (double)nt_[tp] / nsq[tp];
-            if (best < 0 || (sum > W ? r > (double)nt_[best] / nsq[best] : r < (double)nt_[best] / nsq[best])) best = tp;
-        }
-        nt_[best] += sum > W ? -1 : 1;
-        sum += sum > W ? -1 : 1;
-    }
-    std::vector<int4> seg(W);
-    int w = 0;
-    for (int tp = 0; tp < 9; ++tp) {
-        t->tap_start.s[tp] = w;
-        const int groups = nsq[tp] * nrg;
-        for (int k = 0; k < nt_[tp]; ++k, ++w)
-            seg[w] = make_int4(tp, 16 * (int)((long long)k * groups / nt_[tp]), 16 * (int)((long long)(k + 1) * groups / nt_[tp]), 0);
-    }
-    t->tap_start.s[9] = w;
-    // on the trainer's stream, waited for (a pageable hipMemcpy may return before its DMA lands, and the
-    // trainer's streams do not synchronise with the null stream)
-    HIP_TRY(hipMemcpyAsync(t->sched_units, units.data(), units.size() * sizeof(int32_t), hipMemcpyHostToDevice, t->st));
-    HIP_TRY(hipMemcpyAsync(t->sched_off, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice, t->st));
-    HIP_TRY(hipMemcpyAsync(t->wseg, seg.data(), seg.size() * sizeof(int4), hipMemcpyHostToDevice, t->st));
-    HIP_TRY(hipStreamSynchronize(t->st));
-    t->sched_B = B;
-    t->sched_grid = W;
-    return 0;
-}
-
 extern "C" int oaz_trainer_set_batches(oaz_trainer* t, const int32_t* idx, int n_batches, int batch) {
     if (!t || !idx || n_batches < 0 || batch < 16 || batch % 16 || batch > t->maxB)
         return oaz_set_err(OAZ_ERR_ARG, "trainer: batch must be a multiple of 16 in [16, %d]", t ? t->maxB : 0);
@@ -1596,7 +1249,6 @@ extern "C" int oaz_trainer_set_batches(oaz_trainer* t, const int32_t* idx, int n
     }
     if (n) HIP_TRY(hipMemcpyAsync(t->idx, idx, n * sizeof(int32_t), hipMemcpyHostToDevice, t->st));
     HIP_TRY(hipStreamSynchronize(t->st));
-    if (int rc = conv_schedule(t, batch)) return rc;
     t->n_batches = n_batches;
     t->batch = batch;
     return 0;
@@ -1622,23 +1274,8 @@ static int backward(oaz_trainer* t, int bi) {
     float* G = t->G;
     const float bn_mom = (float)t->cfg.bn_momentum, eps = (float)t->cfg.bn_eps;
     const int rg = t->conv_rg, rows_wg = 16 * rg;
-    const int nwg_grid = 25 * ((B + rows_wg - 1) / rows_wg);
+    const int nwg_conv = 25 * ((B + rows_wg - 1) / rows_wg);
     const dim3 conv_grid((B + rows_wg - 1) / rows_wg, 25);
-    if (t->conv_p && t->sched_B != B) return oaz_set_err(OAZ_ERR_STATE, "trainer: no conv schedule for batch %d", B);
-    // partial-sum rows a conv launch leaves in t->part (the persistent form: one per workgroup of its schedule)
-    auto conv_nwg = [&](int mode) { return (t->conv_p >> mode) & 1 ? t->sched_grid : nwg_grid; };
-    auto conv = [&](auto mode, int ch, const ConvArgs& a) {
-        constexpr int MODE = decltype(mode)::value;
-        if (!((t->conv_p >> MODE) & 1)) {
-            launch_conv<MODE>(ch, rg, conv_grid, st, a);
-        } else if (ch == 2) {
-            hipLaunchKernelGGL((k_conv_p<MODE, 2>), dim3(t->sched_grid), dim3(1024), 0, st, a, t->sched_units,
-                               t->sched_off, B / 16, t->convp_dbg, nullptr, nullptr);
-        } else {
-            hipLaunchKernelGGL((k_conv_p<MODE, 4>), dim3(t->sched_grid), dim3(1024), 0, st, a, t->sched_units,
-                               t->sched_off, B / 16, t->convp_dbg, nullptr, nullptr);
-        }
-    };
     hipLaunchKernelGGL(k_gather, dim3((R + 51 * B + 255) / 256), dim3(256), 0, st, t->samples, t->idx, t->cur, bi, B,
                        t->X0, t->pi, t->z);
     // ---- forward
@@ -1651,17 +1288,17 @@ static int backward(oaz_trainer* t, int bi) {
         a.part = t->part;
         a.chunks = l == 0 ? 2 : 4;
         a.B = B;
-        conv(std::integral_constant<int, CONV_FWD>{}, l == 0 ? 2 : 4, a);
+        launch_conv<CONV_FWD>(l == 0 ? 2 : 4, rg, conv_grid, st, a);
         const float* skip = (l >= 2 && l % 2 == 0) ? t->A[l - 2] : nullptr;  // block output adds the block input
         const long long n = (long long)R * kC;
         if (t->cfin) {
             const unsigned nwg_act = t->cfin > 0 ? (unsigned)t->cfin : (unsigned)((n / 4 + 1023) / 1024);
-            hipLaunchKernelGGL(k_bn_act_cfin, dim3(nwg_act), dim3(1024), 0, st, t->part, conv_nwg(CONV_FWD), (double)R,
+            hipLaunchKernelGGL(k_bn_act_cfin, dim3(nwg_act), dim3(1024), 0, st, t->part, nwg_conv, (double)R,
                                P + L.brm[l], P + L.brv[l], bn_mom, eps, t->mean[l], t->invstd[l], t->Z[l],
                                P + L.bg[l], P + L.bb[l], skip, t->A[l], n);
             continue;
         }
-        hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->part, conv_nwg(CONV_FWD), 64, 0, 64, (double)R,
+        hipLaunchKernelGGL(k_bn_fwd_fin, dim3(1), dim3(1024), 0, st, t->part, nwg_conv, 64, 0, 64, (double)R,
                            P + L.brm[l], P + L.brv[l], bn_mom, eps, t->mean[l], t->invstd[l], 64, nullptr, nullptr);
         hipLaunchKernelGGL(k_bn_act, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, t->Z[l], t->mean[l],
                            t->invstd[l], P + L.bg[l], P + L.bb[l], skip, t->A[l], n);
@@ -1727,14 +1364,10 @@ static int backward(oaz_trainer* t, int bi) {
             HIP_TRY(hipEventRecord(t->ev_dz[k], st));
             HIP_TRY(hipStreamWaitEvent(t->st2, t->ev_dz[k], 0));
             const float* X = l == 0 ? t->X0 : t->A[l - 1];
-            if (l == 0 && t->wgrad_small)
-                hipLaunchKernelGGL((k_wgrad<1, true>), dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
-            else if (l == 0)
-                hipLaunchKernelGGL((k_wgrad<1, false>), dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
-            else if (t->wgrad_small)
-                hipLaunchKernelGGL((k_wgrad<2, true>), dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
+            if (l == 0)
+                hipLaunchKernelGGL(k_wgrad<1>, dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
             else
-                hipLaunchKernelGGL((k_wgrad<2, false>), dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
+                hipLaunchKernelGGL(k_wgrad<2>, dim3(25, 9, kWSplit), dim3(256), 0, t->st2, dz, X, B, t->wpart);
             const int cin = l == 0 ? kIn : kC;
             const int nred = 9 * kC * cin;
             hipLaunchKernelGGL(k_wgrad_reduce, dim3((nred + 255) / 256), dim3(256), 0, t->st2, t->wpart,
@@ -1744,9 +1377,7 @@ static int backward(oaz_trainer* t, int bi) {
             used[k] = true;
             return 0;
         };
-        const bool fused = l > 0 && t->bwd_p && ((t->conv_p >> CONV_DGRAD) & 1);
-        if (!fused)
-            if (int rc = wgrad()) return rc;
+        if (int rc = wgrad()) return rc;
         if (l == 0) break;
         ConvArgs a{};
         a.in = dz;
@@ -1760,21 +1391,8 @@ static int backward(oaz_trainer* t, int bi) {
         a.skip = (l % 2 == 1) ? t->M[l + 1] : nullptr;  // first conv of a block: add the block-output gradient
         a.chunks = 4;
         a.B = B;
-        if (!fused) {
-            conv(std::integral_constant<int, CONV_DGRAD>{}, 4, a);
-        } else {
-            hipLaunchKernelGGL((k_conv_p<CONV_DGRAD, 4, true>), dim3(t->sched_grid), dim3(1024), 0, st, a,
-                               t->sched_units, t->sched_off, B / 16, t->convp_dbg, t->wseg, t->wpart_p[k]);
-            // the partials' sum and the bias gradient on the second stream, off the critical path
-            HIP_TRY(hipEventRecord(t->ev_dz[k], st));
-            HIP_TRY(hipStreamWaitEvent(t->st2, t->ev_dz[k], 0));
-            hipLaunchKernelGGL(k_wgrad_reduce_p, dim3(9 * 4096 / 256), dim3(256), 0, t->st2, t->wpart_p[k], t->tap_start,
-                               G + L.cw[l]);
-            hipLaunchKernelGGL(k_colsum, dim3(1), dim3(1024), 0, t->st2, t->bpart[k], nwg_bwd, 64, 0, 64, G + L.cb[l]);
-            HIP_TRY(hipEventRecord(t->ev_w[k], t->st2));
-            used[k] = true;
-        }
-        nwg_part = conv_nwg(CONV_DGRAD);
+        launch_conv<CONV_DGRAD>(4, rg, conv_grid, st, a);
+        nwg_part = nwg_conv;
     }
     HIP_TRY(hipEventRecord(t->ev_done, t->st2));
     HIP_TRY(hipStreamWaitEvent(st, t->ev_done, 0));  // every gradient is in G before SGD / all-reduce
