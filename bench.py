@@ -528,6 +528,7 @@ def train_main(args, world, rank, local):
     t0 = time.perf_counter()
     for b in range(args.warmup, nb):
         step(b)
+    t_enq = time.perf_counter() - t0  # the host's enqueue time of the K steps (the device may still be running)
     barrier_sync()
     elapsed = time.perf_counter() - t0
     tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -546,6 +547,7 @@ def train_main(args, world, rank, local):
                "config": {"workload": f"train: {blocks}-block ResNet, global batch {B}, lr 5e-3, momentum 0.9, "
                                       f"wd 1e-4", "parallelism": f"dp{world} (RCCL all-reduce of gradients)"},
                "mean_losses": {"value": v / max(1, k), "policy": p / max(1, k)},
+               "host_enqueue_ms_per_step": 1e3 * t_enq / args.steps,
                "roofline": {"bound": "mfma", "kernel": "whole SGD step (conv fwd/dgrad/wgrad on v_mfma_f32_16x16x4_f32)",
                             "achieved": achieved, "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
                             "frac": achieved / PEAK_TFLOPS["fp32"], "traffic": None,
