@@ -930,13 +930,18 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
     // sqrt((double)n) from the host libm (IEEE correctly rounded), so device PUCT = oracle PUCT
     std::vector<double> tab((size_t)cfg->sims + 2);
     for (size_t i = 0; i < tab.size(); ++i) tab[i] = sqrt((double)i);
-    if (hipMemcpy(e->sqrt_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemset(e->stats, 0, G * GS_COUNT * sizeof(uint64_t)) != hipSuccess ||
-        hipMemset(e->out_count, 0, sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(e->nn_fallback, 0, sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(e->active, 0, G) != hipSuccess || hipMemset(e->need, 0, G) != hipSuccess ||
-        hipMemset(e->slot, 0, G * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(e->cstate, 0, (G + 16) * sizeof(oaz_state)) != hipSuccess) {
+    // on the engine's own stream, waited for: its streams do not synchronise with the null stream, a null-stream
+    // hipMemset returns before it ran and a pageable hipMemcpy before its DMA landed, so the first kernels could
+    // otherwise read these buffers early (seen with several engines created concurrently on one GPU)
+    hipStream_t s0 = e->stream;
+    if (hipMemcpyAsync(e->sqrt_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice, s0) != hipSuccess ||
+        hipMemsetAsync(e->stats, 0, G * GS_COUNT * sizeof(uint64_t), s0) != hipSuccess ||
+        hipMemsetAsync(e->out_count, 0, sizeof(unsigned long long), s0) != hipSuccess ||
+        hipMemsetAsync(e->nn_fallback, 0, sizeof(unsigned long long), s0) != hipSuccess ||
+        hipMemsetAsync(e->active, 0, G, s0) != hipSuccess || hipMemsetAsync(e->need, 0, G, s0) != hipSuccess ||
+        hipMemsetAsync(e->slot, 0, G * sizeof(uint32_t), s0) != hipSuccess ||
+        hipMemsetAsync(e->cstate, 0, (G + 16) * sizeof(oaz_state), s0) != hipSuccess ||
+        hipStreamSynchronize(s0) != hipSuccess) {
         oaz_set_err(OAZ_ERR_HIP, "create: init copies failed");
         return fail();
     }
@@ -1547,7 +1552,8 @@ extern "C" int oaz_selfplay_stats_get(oaz_engine* e, oaz_selfplay_stats* o) {
     uint64_t s[GS_COUNT];
     if (int rc = reduce_stats(e, e->G, s)) return rc;
     unsigned long long cnt = 0;
-    HIP_TRY(hipMemcpy(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
     memset(o, 0, sizeof(*o));
     o->moves = s[GS_MOVES];
     o->games_finished = s[GS_FINISHED];

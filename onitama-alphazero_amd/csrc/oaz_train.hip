@@ -1046,7 +1046,7 @@ struct oaz_trainer {
     int alloc(T*& p, size_t count) {
         void* q = nullptr;
         HIP_TRY(hipMalloc(&q, count * sizeof(T) + 16));
-        HIP_TRY(hipMemset(q, 0, count * sizeof(T) + 16));
+        HIP_TRY(hipMemsetAsync(q, 0, count * sizeof(T) + 16, own));  // ordered before the trainer's work (create syncs)
         allocs.push_back(q);
         p = (T*)q;
         return 0;
@@ -1150,7 +1150,8 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
         for (int c = 0; c < 64; ++c) mask[t->L.brm[l] + c] = mask[t->L.brv[l] + c] = 0;
     mask[t->L.h.vrm] = mask[t->L.h.vrv] = 0;
     mask[t->L.h.prm] = mask[t->L.h.prm + 1] = mask[t->L.h.prv] = mask[t->L.h.prv + 1] = 0;
-    if (hipMemcpy(t->mask, mask.data(), t->nparam, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpyAsync(t->mask, mask.data(), t->nparam, hipMemcpyHostToDevice, t->own) != hipSuccess ||
+        hipStreamSynchronize(t->own) != hipSuccess) {  // the zero fills and the mask landed before any step
         oaz_set_err(OAZ_ERR_HIP, "trainer: mask upload");
         return fail();
     }

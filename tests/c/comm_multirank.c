@@ -6,7 +6,7 @@
  * buffers, alphazero-training/src/train.rs:241-244 (`data_buffer.extend(handle.join())` in worker
  * order = rank order here).
  *
- *   comm_multirank W      (2 <= W <= 4)
+ *   comm_multirank W      (2 <= W <= 8; 8 = the C4 node's rank count)
  *
  * Per rank r: engine A (the exchange) and engine B (the expectation) get the same config (G_r game
  * slots, rank r of W, HASH evaluator, root noise on) and play the same number of plies P_r, ragged
@@ -47,7 +47,7 @@ int hipStreamSynchronize(hipStream_t s);
 uint64_t rccl_stub_ops(void); /* from the stub: proves it served the calls */
 uint64_t rccl_stub_pending_at_return(void); /* ... and that they returned before their operations ran */
 
-#define MAXW 4
+#define MAXW 8
 static int W;
 static oaz_comm_id g_id;
 static oaz_sample* g_expect[MAXW]; /* rank r's samples, sorted (bytewise) */
@@ -80,8 +80,8 @@ static int bar_wait(void) {
 }
 static int g_fail[MAXW];
 
-static const int kGames[MAXW] = {24, 16, 32, 8};
-static const int kPlies[MAXW] = {45, 0, 70, 30};
+static const int kGames[MAXW] = {24, 16, 32, 8, 8, 24, 16, 32};
+static const int kPlies[MAXW] = {45, 0, 70, 30, 45, 30, 70, 45};
 
 static int cmp_sample(const void* a, const void* b) { return memcmp(a, b, sizeof(oaz_sample)); }
 
@@ -126,6 +126,10 @@ static void* rank_main(void* arg) {
     CHECK(oaz_selfplay_step(a, kPlies[rank]) == 0 && oaz_selfplay_step(b, kPlies[rank]) == 0);
     oaz_selfplay_stats sa, sb;
     CHECK(oaz_selfplay_stats_get(a, &sa) == 0 && oaz_selfplay_stats_get(b, &sb) == 0);
+    if (!(sa.samples_ready == sb.samples_ready && sa.samples_dropped == 0))
+        fprintf(stderr, "rank %d: engine A %llu samples (%llu dropped), engine B %llu (%llu dropped)\n", rank,
+                (unsigned long long)sa.samples_ready, (unsigned long long)sa.samples_dropped,
+                (unsigned long long)sb.samples_ready, (unsigned long long)sb.samples_dropped);
     CHECK(sa.samples_ready == sb.samples_ready && sa.samples_dropped == 0);
     g_count[rank] = sb.samples_ready;
     g_expect[rank] = (oaz_sample*)malloc((g_count[rank] + 1) * sizeof(oaz_sample));

@@ -133,10 +133,10 @@ def test_rccl_stub_exports_what_the_product_resolves(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,delay_us", [(2, 0), (3, 0), (4, 0), (3, 3000)])
+@pytest.mark.parametrize("world,delay_us", [(2, 0), (3, 0), (4, 0), (8, 0), (3, 3000), (8, 1000)])
 def test_c_allgather_samples_multirank(tmp_path, world, delay_us):
     """The product exchange (oaz_allgather_samples, oaz_comm_broadcast, oaz_comm_allreduce_sum_f32) at
-    world 2, 3 and 4: ranks are threads of one plain C process on GPU 0 over the RCCL test double
+    world 2, 3, 4 and 8 (the C4 node's rank count): ranks are threads of one plain C process on GPU 0 over the RCCL test double
     (tests/c/rccl_stub.c), which is asynchronous as RCCL is: each collective is enqueued on the caller's
     stream and runs later on a proxy thread, so the results also test the product's stream ordering.
     Ragged counts with a zero-count rank, the capacity error, a local failure on one rank seen by every
