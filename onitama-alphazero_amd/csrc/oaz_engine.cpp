@@ -1484,7 +1484,10 @@ extern "C" int oaz_search(oaz_engine* e, const oaz_state* roots, int G, oaz_move
     HIP_TRY(hipMemcpyAsync(e->s_ply, plies.data(), (size_t)G * 4, hipMemcpyHostToDevice, e->stream));
     e->search_calls++;
     HIP_TRY(launch_tree_reset(t, e->stream));
-    if (int rc = run_sims(e, t, e->s_roots, nullptr, nullptr, e->s_ply)) return rc;
+    if (int rc = run_sims(e, t, e->s_roots, nullptr, nullptr, e->s_ply)) {
+        (void)hipStreamSynchronize(e->stream);  // the plies upload reads this frame's vector
+        return rc;
+    }
     if (int rc = timed(e, 3, (uint32_t)G, [&] { return launch_search_finalize(t, e->s_roots, e->s_move, e->s_pi, e->stream); }))
         return rc;
     if (out_root_value) {  // extra root evaluation (alphazero_mcts/mod.rs:137-141)
