@@ -441,6 +441,70 @@ def train_flop_per_sample(blocks):
     return 3 * fwd - 2 * 25 * 9 * 21 * 64
 
 
+def train_algorithmic_bytes(blocks, B):
+    """HBM-level bytes of one SGD step as the kernels move them (training): every
+    activation-sized tensor (R = 25 B rows x 64 fp32 = S bytes) a kernel reads or writes, the weight-gradient
+    partials (9 x 25 x 2 tiles of 64 x 64 fp32, written and re-read per layer) and the SGD's parameter,
+    gradient and momentum passes. Forward: conv l reads its input (layer 0: 32 of 64 channels) and writes Z,
+    the BN apply reads Z (+ the skip at block outputs) and writes A; heads read A (conv) and A, Z (backward
+    rows) and write M. Backward per layer: the BN-backward apply reads M, Z and writes dZ; the weight gradient
+    reads dZ and the layer input; the input gradient (not for layer 0) reads dZ, the activation, the pre-BN
+    output (+ the skip at a block's first conv) and writes M."""
+    L = 1 + 2 * blocks
+    S = 25 * B * 64 * 4
+    fwd = (0.5 + 1.0) * S + (L - 1) * 2.0 * S + L * 2.0 * S + blocks * S
+    heads = 4.0 * S
+    part = 9 * 25 * 2 * 64 * 64 * 4
+    bwd = L * 3.0 * S + (L - 1) * 2.0 * S + 1.5 * S + (L - 1) * 4.0 * S + blocks * S
+    bwd += (L - 0.5) * 2.0 * part
+    nparam = L * (64 * 64 * 9 + 5 * 64) - 64 * 43 * 9 + 64 + 5 + 64 * 25 + 64 + 64 + 1 + 128 + 10 + 2500 + 50
+    return fwd + heads + bwd + 5.0 * 4 * nparam
+
+
+def pmc_train_traffic(args):
+    """FETCH_SIZE / WRITE_SIZE over every trainer kernel of the timed steps, one counter per rocprofv3 pass
+    (a child bench process; this process has not touched the GPU yet), summed per SGD step (steps end at
+    k_sgd). rocprofv3 serialises the counted dispatches, so the two streams' overlap is gone in these
+    passes; bytes per kernel are unaffected. FETCH_SIZE x2 (gfx950 wide-read correction)."""
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    warm, steps = 3, 4
+    kb = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        with tempfile.TemporaryDirectory() as d:
+            cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "tr::k_", "--output-format", "csv", "-d", d,
+                   "-o", "pmc", "--", sys.executable, str(Path(__file__).resolve()), "--mode", "train", "--pmc-child",
+                   "--no-cpu-baseline", "--steps", str(steps), "--warmup", str(warm),
+                   "--train-blocks", str(args.train_blocks), "--train-batch", str(args.train_batch)]
+            try:
+                subprocess.run(cmd, timeout=600, capture_output=True, check=True)
+            except (subprocess.SubprocessError, OSError) as exc:
+                print(f"bench: train PMC pass {ctr} failed ({type(exc).__name__})", file=sys.stderr)
+                return None
+            rows = []
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                for r in csv.DictReader(open(f)):
+                    if r["Counter_Name"] == ctr:
+                        rows.append((int(r.get("Dispatch_Id", 0) or 0), r["Kernel_Name"], float(r["Counter_Value"])))
+            rows.sort()
+            ends = [i for i, (_, n, _) in enumerate(rows) if "k_sgd" in n]
+            if len(ends) < warm + steps:
+                print(f"bench: train PMC pass {ctr}: {len(ends)} steps collected", file=sys.stderr)
+                return None
+            timed = rows[ends[warm - 1] + 1:ends[warm + steps - 1] + 1]
+            kb[ctr] = sum(v for _, _, v in timed) / steps
+    fetch, write = 2.0 * kb["FETCH_SIZE"] * 1024.0, kb["WRITE_SIZE"] * 1024.0
+    return {"bytes_per_step": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+            "fetch_bytes_uncorrected": kb["FETCH_SIZE"] * 1024.0, "raw_kb": kb,
+            "note": f"rocprofv3 --pmc, separate passes, every tr::k_ dispatch of {steps} SGD steps after {warm} "
+                    "(kernels serialised by the counter collection); FETCH_SIZE x2, the gfx950 correction calibrated "
+                    "for 16-byte-per-lane reads (the convs' operand loads); the BN, reduction and SGD kernels read 4 "
+                    "bytes per lane, for which it is uncalibrated, so fetch_bytes is an upper bound and "
+                    "fetch_bytes_uncorrected a lower one. WRITE_SIZE equals the formula's writes (every intermediate "
+                    "tensor once, the weight-gradient partials, the SGD passes)"}
+
+
 def train_cpu_baseline(blocks, batch, seconds, threads):
     """The reference trains on the CPU through tch (train.rs:163 `Device::Cpu`): the same op graph
     (oracle/train_ref.py) in fp32 ATen on `threads` host threads, batch 512."""
@@ -479,6 +543,9 @@ def train_main(args, world, rank, local):
     from onitama_az.weights import random_weights
     blocks, B = args.train_blocks, args.train_batch
     assert B % world == 0 and (B // world) % 16 == 0, "per-rank batch must be a multiple of 16"
+    traffic = None
+    if not args.pmc_child and not args.no_pmc and world == 1:
+        traffic = pmc_train_traffic(args)  # child processes, before this process touches the GPU
     shard = B // world
     lib = _abi.load()
     n_samples = 65536
@@ -550,7 +617,11 @@ def train_main(args, world, rank, local):
                "host_enqueue_ms_per_step": 1e3 * t_enq / args.steps,
                "roofline": {"bound": "mfma", "kernel": "whole SGD step (conv fwd/dgrad/wgrad on v_mfma_f32_16x16x4_f32)",
                             "achieved": achieved, "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
-                            "frac": achieved / PEAK_TFLOPS["fp32"], "traffic": None,
+                            "frac": achieved / PEAK_TFLOPS["fp32"],
+                            "traffic": traffic["bytes_per_step"] if traffic else None,
+                            "traffic_unit": "HBM-side bytes per SGD step (PMC)",
+                            "algorithmic_bytes_per_step": train_algorithmic_bytes(blocks, shard),
+                            "traffic_detail": traffic,
                             "flop_per_step_per_gpu": fl}}
         if not args.no_cpu_baseline and world == 1:
             try:  # after the timed region: a baseline failure must not lose the measured line
