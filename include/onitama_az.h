@@ -17,7 +17,12 @@
  *     behaviour or an error code.
  *   - An engine is owned by one host thread and bound to one GPU (one process per
  *     GPU, one engine per process in the self-play bench). Distinct engines are
- *     independent.
+ *     independent, also when several threads create and drive engines on one GPU at
+ *     once (creation zeroes and uploads on the engine's own stream and waits for it).
+ *   - Engine, trainer and communicator calls run on their object's device and restore
+ *     the calling thread's current HIP device before returning (so do the pure-MCTS
+ *     search on cfg->device); the stateless rules entry points (oaz_movegen, oaz_step,
+ *     oaz_current_state, oaz_encode) run on the thread's current device.
  *   - Compute entry points need a gfx950 GPU. Without one oaz_create() returns
  *     NULL and the rules entry points return OAZ_ERR_NO_DEVICE; there is no CPU
  *     fallback in this library.

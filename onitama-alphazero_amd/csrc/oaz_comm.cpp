@@ -91,7 +91,7 @@ extern "C" int oaz_comm_unique_id(oaz_comm_id* out) {
 
 extern "C" void oaz_comm_destroy(oaz_comm* c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    DeviceScope dev_scope_(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->nc) (void)g_rccl.comm_destroy(c->nc);
     if (c->d_counts) (void)hipFree(c->d_counts);
@@ -112,7 +112,7 @@ static int comm_init(const oaz_comm_id* id, int rank, int world, int device, oaz
     c->rank = rank;
     c->world = world;
     c->device = device;
-    HIP_TRY(hipSetDevice(device));
+    OAZ_ON_DEVICE(device);
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(hipMalloc((void**)&c->d_counts, (size_t)world * sizeof(uint64_t)));
     for (auto& ev : c->ev) HIP_TRY(hipEventCreate(&ev));
@@ -139,7 +139,7 @@ extern "C" oaz_comm* oaz_comm_init(const oaz_comm_id* id, int rank, int world, i
 
 extern "C" int oaz_comm_sync(oaz_comm* c) {
     if (!c) return oaz_set_err(OAZ_ERR_ARG, "comm_sync: null");
-    HIP_TRY(hipSetDevice(c->device));
+    OAZ_ON_DEVICE(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -171,7 +171,7 @@ extern "C" int oaz_allgather_samples(oaz_engine* eng, oaz_comm* c, oaz_sample* d
         rc_local = oaz_set_err(OAZ_ERR_ARG, "allgather_samples: engine on GPU %d, comm on GPU %d", dev, c->device);
     }
     if (rc_local) why = oaz_last_error();
-    HIP_TRY(hipSetDevice(c->device));
+    OAZ_ON_DEVICE(c->device);
     // 1. counts (every rank joins, also after a local failure)
     const uint64_t mine = rc_local ? kLocalFailure : (uint64_t)n;
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
@@ -226,14 +226,14 @@ extern "C" int oaz_allgather_samples(oaz_engine* eng, oaz_comm* c, oaz_sample* d
 
 extern "C" int oaz_comm_allreduce_sum_f32(oaz_comm* c, float* dev, size_t n, void* stream) {
     if (!c || (!dev && n)) return oaz_set_err(OAZ_ERR_ARG, "allreduce: bad arguments");
-    HIP_TRY(hipSetDevice(c->device));
+    OAZ_ON_DEVICE(c->device);
     NCCL_TRY(g_rccl.all_reduce(dev, dev, n, ncclFloat32, ncclSum, c->nc, stream ? (hipStream_t)stream : c->stream));
     return 0;
 }
 
 extern "C" int oaz_comm_broadcast(oaz_comm* c, void* dev, size_t bytes, int root, void* stream) {
     if (!c || (!dev && bytes) || root < 0 || root >= c->world) return oaz_set_err(OAZ_ERR_ARG, "broadcast: bad arguments");
-    HIP_TRY(hipSetDevice(c->device));
+    OAZ_ON_DEVICE(c->device);
     NCCL_TRY(g_rccl.broadcast(dev, dev, bytes, ncclUint8, root, c->nc, stream ? (hipStream_t)stream : c->stream));
     return 0;
 }

@@ -884,7 +884,8 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         g_err = msg;
         return nullptr;
     };
-    if (hipSetDevice(device) != hipSuccess) {
+    DeviceScope dev_scope_(device);  // the caller's current device is restored on return
+    if (dev_scope_.rc != hipSuccess) {
         oaz_set_err(OAZ_ERR_HIP, "hipSetDevice(%d) failed", device);
         return fail();
     }
@@ -955,7 +956,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
 
 extern "C" void oaz_destroy(oaz_engine* e) {
     if (!e) return;
-    (void)hipSetDevice(e->device);
+    DeviceScope dev_scope_(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->stream2) (void)hipStreamSynchronize(e->stream2);
     for (auto s3 : e->stream3)
@@ -993,7 +994,7 @@ extern "C" int oaz_set_search_params(oaz_engine* e, int sims, double c_puct, int
                            e->sims_cap);
     if (!(c_puct >= 0.0) || !std::isfinite(c_puct)) return oaz_set_err(OAZ_ERR_ARG, "set_search_params: bad c_puct");
     if (train_noise && !e->noise) {  // the engine was made without root noise: its ring comes now
-        HIP_TRY(hipSetDevice(e->device));
+        OAZ_ON_DEVICE(e->device);
         HIP_TRY(hipStreamSynchronize(e->stream));
         if (dalloc(&e->noise, 2 * kNoiseChunk * (size_t)e->G * kNoiseStride)) return OAZ_ERR_HIP;
     }
@@ -1013,7 +1014,7 @@ extern "C" int oaz_set_search_time(oaz_engine* e, int64_t search_time_ns) {
 // The device-budgeted searches leave each game's count on the device; read them once.
 static int fetch_sims_run(oaz_engine* e) {
     if (!e->last_sims_dev) return 0;
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     std::vector<uint32_t> n(e->last_G);
     if (e->last_G) {
         HIP_TRY(hipMemcpyAsync(n.data(), e->sims_run, (size_t)e->last_G * 4, hipMemcpyDeviceToHost, e->stream));
@@ -1057,7 +1058,7 @@ extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
                        e->cfg.blocks);
     std::vector<float> packed;
     if (int rc = pack_weights(blob, e->cfg.blocks, e->cfg.precision, packed)) return rc;
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     HIP_TRY(hipMemcpyAsync(e->weights, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->have_weights = true;
@@ -1066,7 +1067,7 @@ extern "C" int oaz_load_weights(oaz_engine* e, const float* blob, size_t n) {
 
 extern "C" int oaz_sync(oaz_engine* e) {
     if (!e) return oaz_set_err(OAZ_ERR_ARG, "sync: null");
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream2));
     for (auto s3 : e->stream3) HIP_TRY(hipStreamSynchronize(s3));
@@ -1138,7 +1139,7 @@ static int evaluate(oaz_engine* e, const oaz_state* d_states, uint32_t B, float*
 
 extern "C" int oaz_nn_fallbacks(oaz_engine* e, uint64_t* tiles) {
     if (!e || !tiles) return oaz_set_err(OAZ_ERR_ARG, "nn_fallbacks: null");
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     unsigned long long n = 0;
     HIP_TRY(hipMemcpyAsync(&n, e->nn_fallback, sizeof(n), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1150,7 +1151,7 @@ extern "C" int oaz_nn_forward(oaz_engine* e, const oaz_state* s, int B, float* p
     if (!e || !s || B < 0) return oaz_set_err(OAZ_ERR_ARG, "nn_forward: bad arguments");
     if ((uint32_t)B > e->G) return oaz_set_err(OAZ_ERR_CAPACITY, "nn_forward: B=%d > games=%u", B, e->G);
     if (B == 0) return 0;
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     HIP_TRY(hipMemcpyAsync(e->s_roots, s, (size_t)B * sizeof(oaz_state), hipMemcpyHostToDevice, e->stream));
     if (int rc = evaluate(e, e->s_roots, (uint32_t)B, e->s_rootp, e->s_rootv)) return rc;
     if (policy) HIP_TRY(hipMemcpyAsync(policy, e->s_rootp, (size_t)B * 50 * 4, hipMemcpyDeviceToHost, e->stream));
@@ -1476,7 +1477,7 @@ extern "C" int oaz_search(oaz_engine* e, const oaz_state* roots, int G, oaz_move
     if (G == 0) return 0;
     for (int i = 0; i < G; ++i)
         if (roots[i].to_move > 1) return oaz_set_err(OAZ_ERR_ARG, "search: root %d has to_move=%d", i, roots[i].to_move);
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     const TreeView t = tree_view(e, (uint32_t)G);
     HIP_TRY(hipMemcpyAsync(e->s_roots, roots, (size_t)G * sizeof(oaz_state), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipMemsetAsync(e->stats, 0, (size_t)G * GS_COUNT * sizeof(uint64_t), e->stream));
@@ -1508,7 +1509,7 @@ extern "C" int oaz_search(oaz_engine* e, const oaz_state* roots, int G, oaz_move
 
 extern "C" int oaz_tree_dump(oaz_engine* e, int game, oaz_node* out, int cap, int* n_nodes) {
     if (!e || game < 0 || (uint32_t)game >= e->G) return oaz_set_err(OAZ_ERR_ARG, "tree_dump: bad game");
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     uint32_t n = 0;
     HIP_TRY(hipMemcpyAsync(&n, e->n_nodes + game, 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1524,7 +1525,7 @@ extern "C" int oaz_tree_dump(oaz_engine* e, int game, oaz_node* out, int cap, in
 // ---- self-play ----------------------------------------------------------------------------------
 extern "C" int oaz_selfplay_reset(oaz_engine* e) {
     if (!e) return oaz_set_err(OAZ_ERR_ARG, "selfplay_reset: null");
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     const TreeView t = tree_view(e, e->G);
     HIP_TRY(hipMemsetAsync(e->stats, 0, (size_t)e->G * GS_COUNT * sizeof(uint64_t), e->stream));
     HIP_TRY(hipMemsetAsync(e->out_count, 0, sizeof(unsigned long long), e->stream));
@@ -1539,7 +1540,7 @@ extern "C" int oaz_selfplay_step(oaz_engine* e, int moves) {
     if (!e || moves < 0) return oaz_set_err(OAZ_ERR_ARG, "selfplay_step: bad arguments");
     if (!e->selfplay_ready)
         if (int rc = oaz_selfplay_reset(e)) return rc;
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     const TreeView t = tree_view(e, e->G);
     const SlotView sv = slot_view(e);
     for (int m = 0; m < moves; ++m) {
@@ -1551,7 +1552,7 @@ extern "C" int oaz_selfplay_step(oaz_engine* e, int moves) {
 
 extern "C" int oaz_selfplay_stats_get(oaz_engine* e, oaz_selfplay_stats* o) {
     if (!e || !o) return oaz_set_err(OAZ_ERR_ARG, "selfplay_stats: null");
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     uint64_t s[GS_COUNT];
     if (int rc = reduce_stats(e, e->G, s)) return rc;
     unsigned long long cnt = 0;
@@ -1572,7 +1573,7 @@ extern "C" int oaz_selfplay_stats_get(oaz_engine* e, oaz_selfplay_stats* o) {
 }
 
 static int samples_copy(oaz_engine* e, void* dst, size_t cap, size_t* n_out, hipMemcpyKind kind) {
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     unsigned long long cnt = 0;
     HIP_TRY(hipMemcpyAsync(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1594,7 +1595,7 @@ static int samples_copy(oaz_engine* e, void* dst, size_t cap, size_t* n_out, hip
 // Internal (oaz_host.h), for oaz_allgather_samples: the engine's buffered samples as one contiguous
 // device range [*dev, *dev + *n), after the engine's work so far is complete.
 int oaz_engine_samples_peek(oaz_engine* e, const oaz_sample** dev, size_t* n, int* device) {
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     HIP_TRY(hipStreamSynchronize(e->stream2));
     unsigned long long cnt = 0;
     HIP_TRY(hipMemcpyAsync(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
@@ -1608,7 +1609,7 @@ int oaz_engine_samples_peek(oaz_engine* e, const oaz_sample** dev, size_t* n, in
 
 // Drops the first n peeked samples (the caller's copies of them are complete).
 int oaz_engine_samples_consume(oaz_engine* e, size_t n) {
-    HIP_TRY(hipSetDevice(e->device));
+    OAZ_ON_DEVICE(e->device);
     unsigned long long cnt = 0;
     HIP_TRY(hipMemcpyAsync(&cnt, e->out_count, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));

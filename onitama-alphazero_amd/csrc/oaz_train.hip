@@ -1093,7 +1093,8 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
         oaz_set_err(OAZ_ERR_NO_DEVICE, "trainer: no HIP device %d", device);
         return nullptr;
     }
-    if (hipSetDevice(device) != hipSuccess) {
+    DeviceScope dev_scope_(device);  // the caller's current device is restored on return
+    if (dev_scope_.rc != hipSuccess) {
         oaz_set_err(OAZ_ERR_NO_DEVICE, "trainer: hipSetDevice(%d) failed", device);
         return nullptr;
     }
@@ -1160,7 +1161,7 @@ extern "C" oaz_trainer* oaz_trainer_create(const oaz_train_config* cfg, int devi
 
 extern "C" void oaz_trainer_destroy(oaz_trainer* t) {
     if (!t) return;
-    (void)hipSetDevice(t->device);
+    DeviceScope dev_scope_(t->device);
     (void)hipDeviceSynchronize();
     delete t;
 }
@@ -1184,7 +1185,7 @@ static int repack(oaz_trainer* t) {
 
 extern "C" int oaz_trainer_set_weights(oaz_trainer* t, const float* blob, size_t n) {
     if (!t || !blob || n != t->nparam) return oaz_set_err(OAZ_ERR_ARG, "trainer: need %zu floats", t ? t->nparam : 0);
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     HIP_TRY(hipMemcpyAsync(t->P, blob, n * sizeof(float), hipMemcpyHostToDevice, t->st));
     HIP_TRY(hipMemsetAsync(t->MOM, 0, n * sizeof(float), t->st));
     if (int rc = repack(t)) return rc;
@@ -1194,7 +1195,7 @@ extern "C" int oaz_trainer_set_weights(oaz_trainer* t, const float* blob, size_t
 
 extern "C" int oaz_trainer_get_weights(oaz_trainer* t, float* blob, size_t n) {
     if (!t || !blob || n != t->nparam) return oaz_set_err(OAZ_ERR_ARG, "trainer: need %zu floats", t ? t->nparam : 0);
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     HIP_TRY(hipMemcpyAsync(blob, t->P, n * sizeof(float), hipMemcpyDeviceToHost, t->st));
     HIP_TRY(hipStreamSynchronize(t->st));
     return 0;
@@ -1209,7 +1210,7 @@ extern "C" int oaz_trainer_save_ot(oaz_trainer* t, const char* path) {
 
 extern "C" int oaz_trainer_load_samples(oaz_trainer* t, const oaz_sample* s, size_t n) {
     if (!t || (!s && n)) return oaz_set_err(OAZ_ERR_ARG, "trainer: null samples");
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     if (n > t->owned_cap) {
         HIP_TRY(hipStreamSynchronize(t->st));
         if (t->owned_samples) HIP_TRY(hipFree(t->owned_samples));
@@ -1239,7 +1240,7 @@ extern "C" int oaz_trainer_set_batches(oaz_trainer* t, const int32_t* idx, int n
     for (size_t i = 0; i < n; ++i)
         if (idx[i] < 0 || (size_t)idx[i] >= t->n_samples)
             return oaz_set_err(OAZ_ERR_ARG, "trainer: index %d out of range (%zu samples)", idx[i], t->n_samples);
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     if (n > t->idx_cap) {
         HIP_TRY(hipStreamSynchronize(t->st));
         if (t->idx) HIP_TRY(hipFree(t->idx));
@@ -1404,7 +1405,7 @@ static int backward(oaz_trainer* t, int bi) {
 extern "C" int oaz_trainer_backward(oaz_trainer* t, int b) {
     if (!t) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
     if (!t->samples || b < 0 || b >= t->n_batches) return oaz_set_err(OAZ_ERR_STATE, "trainer: batch %d not uploaded", b);
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     return backward(t, b);
 }
 
@@ -1417,7 +1418,7 @@ extern "C" int oaz_trainer_grads(oaz_trainer* t, float** dev, size_t* n) {
 
 extern "C" int oaz_trainer_get_grads(oaz_trainer* t, float* host, size_t n) {
     if (!t || !host || n != t->nparam) return oaz_set_err(OAZ_ERR_ARG, "trainer: need %zu floats", t ? t->nparam : 0);
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     HIP_TRY(hipMemcpyAsync(host, t->G, n * sizeof(float), hipMemcpyDeviceToHost, t->st));
     HIP_TRY(hipStreamSynchronize(t->st));
     return 0;
@@ -1473,7 +1474,7 @@ extern "C" size_t oaz_trainer_bn_stats_count(int blocks) { return (size_t)(1 + 2
 
 extern "C" int oaz_trainer_bn_stats_pack(oaz_trainer* t, float* dev_out) {
     if (!t || !dev_out) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     hipLaunchKernelGGL(k_bn_stats_io, dim3(1), dim3(256), 0, t->st, t->P, dev_out, bn_segs(t), 0, 1.0f);
     HIP_TRY(hipGetLastError());
     return 0;
@@ -1481,7 +1482,7 @@ extern "C" int oaz_trainer_bn_stats_pack(oaz_trainer* t, float* dev_out) {
 
 extern "C" int oaz_trainer_bn_stats_unpack(oaz_trainer* t, const float* dev_in, float scale) {
     if (!t || !dev_in) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     hipLaunchKernelGGL(k_bn_stats_io, dim3(1), dim3(256), 0, t->st, t->P, const_cast<float*>(dev_in), bn_segs(t), 1,
                        scale);
     HIP_TRY(hipGetLastError());
@@ -1490,7 +1491,7 @@ extern "C" int oaz_trainer_bn_stats_unpack(oaz_trainer* t, const float* dev_in, 
 
 extern "C" int oaz_trainer_apply(oaz_trainer* t, float grad_scale) {
     if (!t) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     return apply(t, grad_scale);
 }
 
@@ -1525,7 +1526,7 @@ extern "C" int oaz_trainer_train(oaz_trainer* t, int first, int count) {
     if (!t) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
     if (!t->samples || first < 0 || count < 0 || first + count > t->n_batches)
         return oaz_set_err(OAZ_ERR_STATE, "trainer: batches [%d, %d) not uploaded", first, first + count);
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     if (count == 0) return 0;
     // Plain stream launches by default: on this stack replaying the captured step (~65 kernels on
     // two streams) measured slower (1.06 vs 0.87 ms at batch 512, 5 blocks); OAZ_TRAIN_GRAPH=1
@@ -1551,7 +1552,7 @@ extern "C" int oaz_trainer_train(oaz_trainer* t, int first, int count) {
 
 extern "C" int oaz_trainer_losses(oaz_trainer* t, double out[3]) {
     if (!t || !out) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     HIP_TRY(hipMemcpyAsync(out, t->loss_acc, 3 * sizeof(double), hipMemcpyDeviceToHost, t->st));
     HIP_TRY(hipMemsetAsync(t->loss_acc, 0, 3 * sizeof(double), t->st));
     HIP_TRY(hipStreamSynchronize(t->st));
@@ -1560,7 +1561,7 @@ extern "C" int oaz_trainer_losses(oaz_trainer* t, double out[3]) {
 
 extern "C" int oaz_trainer_sync(oaz_trainer* t) {
     if (!t) return oaz_set_err(OAZ_ERR_ARG, "trainer: null");
-    HIP_TRY(hipSetDevice(t->device));
+    OAZ_ON_DEVICE(t->device);
     HIP_TRY(hipStreamSynchronize(t->st));
     return 0;
 }
