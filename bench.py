@@ -89,7 +89,10 @@ def parse():
     ap.add_argument("--mode", default="selfplay", choices=["selfplay", "train", "pure_mcts", "arena"],
                     help="train: SGD steps of the training loop (SURVEY 8f #2), not the headline metric")
     ap.add_argument("--train-blocks", type=int, default=5, help="train mode: residual blocks (bin/train.rs:60)")
-    ap.add_argument("--pm-games", type=int, default=262144, help="pure_mcts mode: searches per launch")
+    ap.add_argument("--pm-games", type=int, default=1048576,
+                    help="pure_mcts mode: searches per launch (1 M: 933 M playouts/s vs 695 M at 256 k, the "
+                         "divergent rollouts' tail amortised over two rounds of waves; 2 M: 319 M, 134 GB of trees "
+                         "past the TLB's reach; DESIGN.md section 8)")
     ap.add_argument("--arena-games", type=int, default=65536,
                     help="arena mode: games per fight per GPU (the self-play headline's 65 536 slots: a fight lasts as "
                          "long as its longest game, so small fights are tail-bound)")
@@ -639,6 +642,56 @@ def train_main(args, world, rank, local):
 PM_METRIC = "pure-MCTS playouts/sec (random-rollout UCT agent, onitama-game ai/mcts)"
 
 
+def pmc_pure_mcts(args):
+    """k_pure_mcts's VALU issue against the SIMDs' issue peak: one child pass `rocprofv3 --pmc SQ_INSTS_VALU
+    SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace` over one search of the bench's workload (one launch; this process
+    has not touched the GPU yet). achieved = wave64 VALU instructions / the traced duration; peak = 1 024 SIMDs x
+    2.4 GHz / 2 cycles per wave64 instruction (SIMD-32); GRBM_GUI_ACTIVE / 8 XCDs / duration = the clock."""
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        cmd = [prof, "--pmc", "SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE", "--kernel-trace",
+               "--kernel-include-regex", "k_pure_mcts", "--output-format", "csv", "-d", d, "-o", "pm", "--",
+               sys.executable, str(Path(__file__).resolve()), "--mode", "pure_mcts", "--pmc-child", "--no-cpu-baseline",
+               "--steps", "1", "--warmup", "1", "--pm-games", str(args.pm_games), "--pm-playouts", str(args.pm_playouts)]
+        try:
+            subprocess.run(cmd, timeout=600, capture_output=True, check=True)
+        except (subprocess.SubprocessError, OSError) as exc:
+            print(f"bench: pure-MCTS PMC pass failed ({type(exc).__name__})", file=sys.stderr)
+            return None
+        ctr, dur = {}, {}
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if "k_pure_mcts" in r["Kernel_Name"]:
+                    k = (int(r["Dispatch_Id"]), r["Counter_Name"])
+                    ctr[k] = ctr.get(k, 0.0) + float(r["Counter_Value"])
+        for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if "k_pure_mcts" in r["Kernel_Name"]:
+                    dur[int(r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    ids = sorted(set(i for i, _ in ctr) & set(dur))
+    if not ids:
+        print("bench: pure-MCTS PMC pass collected no k_pure_mcts rows", file=sys.stderr)
+        return None
+    i = ids[-1]  # the timed search (after the warm-up one)
+    valu, waves, t = ctr.get((i, "SQ_INSTS_VALU"), 0.0), ctr.get((i, "SQ_WAVES"), 0.0), dur[i]
+    clock = ctr.get((i, "GRBM_GUI_ACTIVE"), 0.0) / XCDS / t / 1e6 if t > 0 else 0.0
+    peak = SIMDS * NOMINAL_MHZ * 1e6 / VALU_CYC
+    achieved = valu / t if t > 0 else 0.0
+    return {"bound": "valu", "kernel": "k_pure_mcts (one thread per search, rollouts: attack-table lookups, popcounts, "
+                                       "Philox draws)",
+            "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "G wave64 VALU instructions/s",
+            "frac": achieved / peak, "traffic": None,
+            "frac_at_measured_clock": achieved / (SIMDS * clock * 1e6 / VALU_CYC) if clock > 0 else None,
+            "measured_clock_mhz": clock, "valu_instructions_per_wave": valu / waves if waves else None,
+            "profiled_launch_ms": t * 1e3,
+            "note": "rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace, one search launch after a "
+                    "warm-up one; instructions are counted per wave, so lanes idled by divergent rollout lengths "
+                    "still count as issued: frac is an upper bound of the lane-level utilisation; traffic is null "
+                    "(the trees and the attack table stay in L2 / LDS; the bound is issue, not memory)"}
+
+
 def pure_mcts_main(args, world, rank, local):
     """One step = one search (max_playouts random-rollout playouts) from each of pm_games seeded
     deals (the arena opponent's config: min_node_visits 5, c 1.41, evaluator.rs:340-345)."""
@@ -647,8 +700,11 @@ def pure_mcts_main(args, world, rank, local):
     from onitama_az import _abi
     from onitama_az.game import initial_state_np
     from onitama_az.pure_mcts import pure_mcts_search
-    lib = _abi.load()
     G, P = args.pm_games, args.pm_playouts
+    roof = None
+    if not args.pmc_child and not args.no_pmc and world == 1:
+        roof = pmc_pure_mcts(args)  # a child process, before this process touches the GPU
+    lib = _abi.load()
     deals = []
     for g in range(G):
         d = (C.c_uint8 * 5)()
@@ -684,7 +740,7 @@ def pure_mcts_main(args, world, rank, local):
                "config": {"workload": f"pure_mcts: {G} searches/GPU x {P} playouts, min_node_visits 5, c 1.41",
                           "parallelism": f"searches sharded x{world}"},
                "searches_per_s": G * args.steps * world / T,
-               "mean_rollout_plies": plies / max(1, G * P * args.steps)}
+               "mean_rollout_plies": plies / max(1, G * P * args.steps), "roofline": roof}
         if not args.no_cpu_baseline and world == 1:
             try:  # after the timed region: a baseline failure must not lose the measured line
                 sys.path.insert(0, str(ROOT / "tests"))
