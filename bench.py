@@ -93,9 +93,9 @@ def parse():
                     help="pure_mcts mode: searches per launch (1 M: 933 M playouts/s vs 695 M at 256 k, the "
                          "divergent rollouts' tail amortised over two rounds of waves; 2 M: 319 M, 134 GB of trees "
                          "past the TLB's reach; DESIGN.md section 8)")
-    ap.add_argument("--arena-games", type=int, default=65536,
-                    help="arena mode: games per fight per GPU (the self-play headline's 65 536 slots: a fight lasts as "
-                         "long as its longest game, so small fights are tail-bound)")
+    ap.add_argument("--arena-games", type=int, default=131072,
+                    help="arena mode: games per fight per GPU (a fight lasts as long as its longest game, so small "
+                         "fights are tail-bound: 65 536 games 4 338 games/s, 131 072 5 112; two engines of ~70 GB)")
     ap.add_argument("--pm-playouts", type=int, default=400, help="pure_mcts mode: playouts per search")
     ap.add_argument("--train-batch", type=int, default=512, help="train mode: global batch (train.rs:142)")
     return ap.parse_args()
