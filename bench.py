@@ -193,6 +193,7 @@ def pmc_traffic(args, cfg):
     for k, v in tree_kb.items():  # per game: a launch covers the game slots of one part
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
             tree[k] = {"fetch_bytes_per_sim": 2.0 * v["FETCH_SIZE"] * 1024.0 * parts / cfg["games"],
+                       "fetch_bytes_per_sim_raw": v["FETCH_SIZE"] * 1024.0 * parts / cfg["games"],
                        "write_bytes_per_sim": v["WRITE_SIZE"] * 1024.0 * parts / cfg["games"]}
     if sq and "backup_select" in tree:
         tree["backup_select"]["sq"] = sq
@@ -352,7 +353,18 @@ def tree_roofline(kt, sims, sim_steps, expansions, depth, branching, cfg, pmc=No
         if pmc and name in pmc:
             out[name]["pmc"] = dict(pmc[name], note="rocprofv3 FETCH/WRITE_SIZE per simulation over the launches "
                                     "of one steady-state ply (after the warm-up plies); writes are small scattered "
-                                    "records (leaf record, counters, path entries), each a whole write transaction")
+                                    "records (leaf record, counters, path entries), each a whole write transaction. "
+                                    "Calibrated (tools/pmc_cal, DESIGN.md section 6): FETCH_SIZE counts 64 B per read "
+                                    "request, a request being up to 64 B for a scattered record or a 64-B segment and "
+                                    "128 B only for contiguous full-line runs, so fetch_bytes_per_sim (x2) is exact for "
+                                    "the runs (a node's children, noise pairs, policy rows) and twice the bytes for the "
+                                    "scattered records, fetch_bytes_per_sim_raw the reverse: the kernel's reads lie "
+                                    "between the two")
+            pm = out[name]["pmc"]
+            if "fetch_bytes_per_sim_raw" in pm and "write_bytes_per_sim" in pm:
+                lo = (pm["fetch_bytes_per_sim_raw"] + pm["write_bytes_per_sim"]) / b
+                hi = (pm["fetch_bytes_per_sim"] + pm["write_bytes_per_sim"]) / b
+                pm["traffic_vs_formula"] = [lo, hi]
             sq = out[name]["pmc"].get("sq")
             if sq:  # the launch time the VALU work alone would take, every SIMD issuing VALU every cycle
                 sq = dict(sq)
