@@ -238,6 +238,7 @@ def pmc_grp_traffic(args, cfg, plies, stagger):
     fetch, write = 2.0 * kb["FETCH_SIZE"] * 1024.0, kb["WRITE_SIZE"] * 1024.0
     sims_per_launch = cfg["games"] * cfg["sims"] / per_ply
     return {"kernel": "k_search_grp", "bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+            "bytes_per_launch_raw": fetch / 2.0 + write,  # FETCH_SIZE x1: exact for scattered records
             "bytes_per_sim": (fetch + write) / sims_per_launch, "raw_kb": kb, "launches_profiled": per_ply,
             "note": f"rocprofv3 --pmc, separate passes, on the {per_ply} k_search_grp launches of ply {plies + 1} "
                     f"(after {plies} warm-up plies, stagger {stagger}); FETCH_SIZE x2 (gfx950 wide-read correction)"}
@@ -1278,6 +1279,11 @@ def main():
                 "algorithmic_bytes_per_launch": sk["sims_per_launch"] * (24 + 204 + 1954)
                                                 + 0.96e6 * (cfg["games"] + 15) // 16 / 256,
                 "traffic_detail": traffic if (traffic or {}).get("kernel") == "k_search_grp" else None}
+            tr = out["roofline"]["traffic_detail"]
+            if tr:  # FETCH_SIZE x1 .. x2 (the tree records are scattered, the weight reads streams)
+                alg = out["roofline"]["algorithmic_bytes_per_launch"]
+                out["roofline"]["traffic_vs_algorithmic"] = [tr["bytes_per_launch_raw"] / alg,
+                                                             tr["bytes_per_launch"] / alg]
         bs = (out.get("tree_kernels") or {}).get("backup_select") or {}
         sq = (bs.get("pmc") or {}).get("sq")
         if leg.get("tree_launch_us"):
