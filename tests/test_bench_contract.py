@@ -93,3 +93,28 @@ def test_extra_modes_parse(bench, monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--mode", "arena", "--arena-games", "128"])
     assert bench.parse().arena_games == 128
     assert "games/sec" in bench.ARENA_METRIC
+
+
+def test_train_byte_formula(bench):
+    """train_algorithmic_bytes: per SGD step every activation-sized tensor the kernels read or write (S = 25 B
+    rows x 64 fp32), the weight-gradient partials written and re-read per layer, and the SGD's five parameter
+    passes; its write side alone (measured exactly by WRITE_SIZE on the GPU) is the
+    intermediate tensors once each plus the partials."""
+    blocks, B = 5, 512
+    L, S = 1 + 2 * blocks, 25 * B * 64 * 4
+    part = 9 * 25 * 2 * 64 * 64 * 4
+    total = bench.train_algorithmic_bytes(blocks, B)
+    assert 600e6 < total < 700e6, total
+    # writes: Z and A per conv (forward), M of the last conv (heads), dZ per conv, M per input gradient,
+    # the partials of L - 0.5 layers (layer 0 has 32 input channels), P and MOM (SGD)
+    nparam = L * (64 * 64 * 9 + 5 * 64) - 64 * 43 * 9 + 64 + 5 + 64 * 25 + 64 + 64 + 1 + 128 + 10 + 2500 + 50
+    writes = 2 * L * S + S + L * S + (L - 1) * S + (L - 0.5) * part + 2 * 4 * nparam
+    assert abs(writes - 226e6) / 226e6 < 0.02, writes  # the GPU's WRITE_SIZE per step (profiles/r05b_train.json)
+
+
+def test_pure_mcts_and_arena_defaults(bench, monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--mode", "pure_mcts"])
+    a = bench.parse()
+    assert a.pm_games == 1 << 20 and a.pm_playouts == 400
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--mode", "arena"])
+    assert bench.parse().arena_games == 131072
