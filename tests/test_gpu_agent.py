@@ -154,3 +154,31 @@ def test_agent_mirror_default_config_one_launch(orc):
         _, v = ev.nn_forward(root)
     assert (mv.used_card_idx, mv.mov.from_, mv.mov.to) == (int(ref["slot"]), int(ref["from_"]), int(ref["to"]))
     assert value == float(v[0])
+
+
+def test_training_mirror_pi_matches_oracle(orc):
+    """TrainingAlphaZeroMcts (the self-play agent, alphazero_mcts/mod.rs:163-214) without training noise:
+    generate_move_tensor's move and pi (the visit distribution it returns for the replay buffer), and the
+    batched generate_move_tensors over 4 roots, equal the oracle's search fed the same network (batch-1 calls
+    of the mirror's precision) at max_playouts."""
+    from onitama_az.game import Deck, GameState, ORIGINAL_CARDS
+    from onitama_az.mcts import AlphaZeroMctsConfig, ConvResNet, ConvResNetConfig, TrainingAlphaZeroMcts
+    model = ConvResNet(ConvResNetConfig(resnet_block_amnt=3), seed=5)
+    cfg = AlphaZeroMctsConfig(exploration_c=5.0, max_playouts=60, train=False)
+    tr = TrainingAlphaZeroMcts(cfg, model)
+    gs = GameState.with_deck(Deck([ORIGINAL_CARDS[i] for i in range(5)]))
+    mv, pi = tr.generate_move_tensor(gs.state, gs.curr_player_color)
+    roots = random_positions(orc, 4, seed=2100)
+    moves, pis = tr.generate_move_tensors(roots)
+    with Engine(games=1, sims=1, blocks=3, precision=_abi.FP32_SPLIT16) as ev:
+        ev.load_weights(model.weights)
+        cb = _gpu_callback(ev)
+        ref, ref_pi, _, _ = orc.search(orc.search_cfg(sims=60, c_puct=5.0, evaluator=orc.EVAL_CALLBACK, fn=cb),
+                                       gs.state.to_np(gs.curr_player_color), tree=False)
+        assert (mv.used_card_idx, mv.mov.from_, mv.mov.to) == (int(ref["slot"]), int(ref["from_"]), int(ref["to"]))
+        assert np.array_equal(np.asarray(pi).reshape(-1), np.asarray(ref_pi).reshape(-1))
+        for g in range(4):
+            rmv, rpi, _, _ = orc.search(orc.search_cfg(sims=60, c_puct=5.0, evaluator=orc.EVAL_CALLBACK, fn=cb),
+                                        roots[g], tree=False)
+            assert _mv(moves[g]) == _mv(rmv)
+            assert np.array_equal(np.asarray(pis[g]).reshape(-1), np.asarray(rpi).reshape(-1))
