@@ -636,7 +636,8 @@ struct oaz_engine {
     hipEvent_t ev_join = nullptr, ev_part[kMaxParts] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t ev_ready[2] = {nullptr, nullptr};
     hipEvent_t ev_consumed[2][kMaxParts] = {};  // noise ring slot done with, per game part
-    float* noise = nullptr;              // [2][kNoiseChunk][G][kNoiseStride]
+    float* noise = nullptr;              // [2][noise_chunk][G][kNoiseStride]
+    uint32_t noise_chunk = 16;           // simulations per noise ring slot (noise_chunk_for)
     uint32_t G = 0, cap = 0, pathcap = 0, hcap = 0, out_cap = 0;
     int32_t sims_cap = 0;                // cfg.sims at creation: trees and paths are sized for it
     // trees
@@ -769,6 +770,16 @@ static hipEvent_t ev_get(oaz_engine* e) {
 #define OAZ_NOISE_CHUNK 16
 #endif
 static constexpr uint32_t kNoiseChunk = OAZ_NOISE_CHUNK;  // simulations of root noise produced per launch
+// The ring slot of an engine whose games fit one round of k_search_grp workgroups (<= 16 x CU count):
+// every chunk is one k_search_grp launch, and the noise launch of the next chunk cannot overlap it (the
+// search holds every CU), so a chunk of up to 512 simulations (a C2 ply in one launch and one noise
+// launch: 46.6-47.1 -> 49.5-50.0 M sims/s) at a 16-simulation minimum; 16 for the
+// rest (the per-step launches, where the noise overlaps). Ring: 2 x chunk x G x 80 floats (<= 1.3 GB).
+static uint32_t noise_chunk_for(uint32_t G, int cus, int32_t sims_cap) {
+    if (G > 16u * (uint32_t)cus) return kNoiseChunk;
+    const uint32_t c = sims_cap < 512 ? (uint32_t)sims_cap : 512u;
+    return c > kNoiseChunk ? c : kNoiseChunk;
+}
 
 static void accumulate(oaz_engine* e, const TimedLaunch& p, float ms) {
     double* acc[7] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms,
@@ -914,6 +925,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         e->cus = 256;
     if (hipDeviceGetAttribute(&e->wall_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess) e->wall_khz = 0;
     const size_t G = e->G;
+    e->noise_chunk = noise_chunk_for(e->G, e->cus, e->sims_cap);
     if (dalloc(&e->nodes, G * e->cap) || dalloc(&e->n_nodes, G) || dalloc(&e->path, G * e->pathcap) ||
         dalloc(&e->depth, G) || dalloc(&e->leaf, G) || dalloc(&e->leaf_state, G) ||
         dalloc(&e->stats, G * GS_COUNT) || dalloc(&e->stats_sum, (size_t)GS_COUNT) ||
@@ -926,7 +938,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         dalloc(&e->game_id, G) || dalloc(&e->active, G) || dalloc(&e->hist, G * e->hcap) ||
         dalloc(&e->out, (size_t)e->out_cap) || dalloc(&e->out_count, (size_t)1) || dalloc(&e->nn_fallback, (size_t)1) ||
         dalloc(&e->deadline, (size_t)1) || dalloc(&e->sims_run, G) ||
-        (cfg->train_noise && dalloc(&e->noise, 2 * kNoiseChunk * G * kNoiseStride)))
+        (cfg->train_noise && dalloc(&e->noise, 2 * (size_t)e->noise_chunk * G * kNoiseStride)))
         return fail();
     // sqrt((double)n) from the host libm (IEEE correctly rounded), so device PUCT = oracle PUCT
     std::vector<double> tab((size_t)cfg->sims + 2);
@@ -996,7 +1008,7 @@ extern "C" int oaz_set_search_params(oaz_engine* e, int sims, double c_puct, int
     if (train_noise && !e->noise) {  // the engine was made without root noise: its ring comes now
         OAZ_ON_DEVICE(e->device);
         HIP_TRY(hipStreamSynchronize(e->stream));
-        if (dalloc(&e->noise, 2 * kNoiseChunk * (size_t)e->G * kNoiseStride)) return OAZ_ERR_HIP;
+        if (dalloc(&e->noise, 2 * (size_t)e->noise_chunk * e->G * kNoiseStride)) return OAZ_ERR_HIP;
     }
     e->cfg.sims = sims;
     e->cfg.c_puct = c_puct;
@@ -1279,8 +1291,9 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
         e->last_sims = sims;  // (with a budget: replaced by the games' largest count when it is asked for)
         return 0;
     }
-    const size_t slot_elems = (size_t)kNoiseChunk * t.G * kNoiseStride;
-    const uint32_t nchunks = (sims + kNoiseChunk - 1) / kNoiseChunk;
+    const uint32_t chunk = e->noise_chunk;
+    const size_t slot_elems = (size_t)chunk * t.G * kNoiseStride;
+    const uint32_t nchunks = (sims + chunk - 1) / chunk;
     // up to one round of 16-game workgroups (k_search_grp): one launch per noise chunk of simulations,
     // each workgroup walking, evaluating and backing up its 16 games without a grid-wide step
     const bool grp = e->cfg.step_kernels == 0 && !compact_leaves(e, t.G) &&
@@ -1297,7 +1310,7 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
         if (c >= 2)
             for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[c & 1][h], 0));
         e->timing_skip = false;  // every noise launch is timed (once per chunk)
-        const uint32_t s0 = c * kNoiseChunk, n = sims - s0 < kNoiseChunk ? sims - s0 : kNoiseChunk;
+        const uint32_t s0 = c * chunk, n = sims - s0 < chunk ? sims - s0 : chunk;
         float* buf = e->noise + (c & 1) * slot_elems;
         if (int rc = timed(e, 4, t.G * n, [&] {
                 return launch_root_noise(roots, active, gids, plies, prm, t.G, s0, n, buf, e->stream2);
@@ -1351,7 +1364,7 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
                 if (int rc = produce(c + 1)) return rc;
             for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(sh[h], e->ev_ready[c & 1], 0));
         }
-        const uint32_t s0 = c * kNoiseChunk, s1 = s0 + kNoiseChunk < sims ? s0 + kNoiseChunk : sims;
+        const uint32_t s0 = c * chunk, s1 = s0 + chunk < sims ? s0 + chunk : sims;
         if (grp) {  // the chunk's simulations in one launch
             const NNView w = nn_view(e, nullptr);
             e->timing_skip = false;

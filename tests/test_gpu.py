@@ -25,6 +25,13 @@ pytestmark = pytest.mark.gpu
 NODE_FIELDS = ("W", "P", "N", "first", "mv", "nch", "flags")
 
 
+def grp_launches(sims):
+    """k_search_grp launches of an engine created with `sims` whose games fit one round of 16-game workgroups:
+    one per root-noise chunk of max(16, min(512, sims)) simulations (oaz_engine.cpp, noise_chunk_for)."""
+    c = max(16, min(512, sims))
+    return (sims + c - 1) // c
+
+
 def _mv(m):
     return tuple(int(m[k]) for k in ("from_", "to", "piece", "slot"))
 
@@ -367,8 +374,8 @@ def test_one_launch_search_equals_step_launches(orc, trained3, evaluator, games,
     (r0, t0, k0), (r1, t1, k1) = out[0], out[1]
     if games <= 256 and not noise:  # k_search_lat: one launch (+ the root value's evaluation)
         assert (k0.backup_select_n, k0.nn_n, k0.select_n, k0.expand_n) == (1, 1, 0, 0)
-    else:  # k_search_grp: one launch per 16-simulation noise chunk, then the last expand / backup
-        assert (k0.backup_select_n, k0.nn_n, k0.select_n, k0.expand_n) == ((sims + 15) // 16, 1, 0, 1)
+    else:  # k_search_grp: one launch per noise chunk (up to 512 simulations), then the last expand / backup
+        assert (k0.backup_select_n, k0.nn_n, k0.select_n, k0.expand_n) == (grp_launches(sims), 1, 0, 1)
     assert k1.select_n == k1.parts and k1.backup_select_n == (sims - 1) * k1.parts
     assert np.array_equal(r0.pi, r1.pi) and r0.moves.tobytes() == r1.moves.tobytes()
     assert np.array_equal(r0.root_value, r1.root_value)

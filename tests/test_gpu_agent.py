@@ -3,7 +3,7 @@ max_playouts 5 000, c = sqrt(2)), through the one-launch searches the drop-in ta
 
 - 5 000 simulations run past k_search_lat's LDS-held path and sqrt(N) table (2 048 entries each,
   csrc/oaz_search_lat.hip), so its global-memory fallbacks execute on every simulation;
-- with root noise the search is k_search_grp, 313 chunk launches;
+- with root noise the search is k_search_grp, 10 launches (512-simulation noise chunks);
 - with a search_time budget the one-launch kernels read the device clock before every simulation
   (mcts_arena.rs:75-81) and the trees equal the oracle's search at the playouts each game ran.
 
@@ -56,7 +56,7 @@ def _gpu_callback(ev):
 @pytest.mark.parametrize("games,noise", [(1, 0), (4, 0), (4, 1)])
 def test_agent_default_playouts_hash_trees_match_oracle(orc, games, noise):
     """5 000 playouts per game with the HASH evaluator: k_search_lat (no noise: one launch, path and sqrt
-    table past their LDS copies) or k_search_grp (noise: a launch per 16-simulation chunk); every node, pi
+    table past their LDS copies) or k_search_grp (noise: a launch per 512-simulation chunk); every node, pi
     and move equal the oracle's (mcts_arena.rs:75-323)."""
     roots = random_positions(orc, games, seed=1700 + games + noise)
     with Engine(games=games, sims=AGENT_PLAYOUTS, c_puct=AGENT_C, train_noise=noise, evaluator=_abi.EVAL_HASH,
@@ -64,7 +64,7 @@ def test_agent_default_playouts_hash_trees_match_oracle(orc, games, noise):
         e.set_timing(1)
         r = e.search(roots)
         k = e.kernel_times()
-        assert k.backup_select_n == (1 if not noise else (AGENT_PLAYOUTS + 15) // 16)
+        assert k.backup_select_n == (1 if not noise else (AGENT_PLAYOUTS + 511) // 512)  # noise chunks of 512
         assert k.select_n == 0
         assert r.stats.sims == AGENT_PLAYOUTS * games
         assert r.stats.max_nodes > 2 * 2048  # trees far past the LDS-held top
