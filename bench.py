@@ -204,12 +204,19 @@ def pmc_traffic(args, cfg):
                     "correction)"}
 
 
+def grp_launches_per_ply(sims):
+    """k_search_grp launches per ply: one per root-noise chunk of max(16, min(512, sims)) simulations
+    (oaz_engine.cpp noise_chunk_for; the engine is created with `sims`), i.e. a C2 ply is one launch."""
+    c = max(16, min(512, sims))
+    return (sims + c - 1) // c
+
+
 def pmc_grp_traffic(args, cfg, plies, stagger):
-    """The k_search_grp launches' HBM bytes (C2: up to 16 x CU-count games, one launch per 16-simulation noise
-    chunk runs the walks, k_nn_h3's body and the backups of every game): FETCH_SIZE / WRITE_SIZE passes over
-    the launches of the ply after `plies` warm-up plies, as pmc_traffic does for k_nn_h3."""
+    """The k_search_grp launches' HBM bytes (C2: up to 16 x CU-count games, one launch per noise chunk runs the
+    walks, k_nn_h3's body and the backups of every game): FETCH_SIZE / WRITE_SIZE passes over the launches of
+    the ply after `plies` warm-up plies, as pmc_traffic does for k_nn_h3."""
     prof = shutil.which("rocprofv3")
-    per_ply = (cfg["sims"] + 15) // 16  # k_search_grp launches per ply
+    per_ply = grp_launches_per_ply(cfg["sims"])  # k_search_grp launches per ply
     first, last = plies * per_ply + 1, (plies + 1) * per_ply
     kb = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -1198,8 +1205,8 @@ def main():
             "checks": checks,
         }
     eng.close()
-    # Up to 16 x CU-count games (C2) the engine runs each 16-simulation noise chunk as ONE launch of
-    # k_search_grp (16 games per workgroup: tree walks, k_nn_h3's body, backups); its launches are then
+    # Up to 16 x CU-count games (C2) the engine runs each root-noise chunk (up to 512 simulations: a C2 ply)
+    # as ONE launch of k_search_grp (16 games per workgroup: tree walks, k_nn_h3's body, backups); its launches are then
     # the timed region's dominant kernel (kernel class backup_select, every launch timed).
     grp_mode = kt.select_n == 0 and kt.nn_n == 0 and kt.backup_select_n > 0
     if rank == 0 and grp_mode:
@@ -1208,8 +1215,8 @@ def main():
         avg_ms = kt.backup_select_ms / kt.backup_select_n
         flops = FLOP_PER_SIM[cfg["blocks"]] * per_launch
         out["search_kernel"] = {
-            "kernel": "k_search_grp (16 games per workgroup: select -> k_nn_h3 body -> expand/backup for a "
-                      "16-simulation noise chunk per launch; oaz_search_lat.hip)",
+            "kernel": "k_search_grp (16 games per workgroup: select -> k_nn_h3 body -> expand/backup for one "
+                      "root-noise chunk of up to 512 simulations per launch; oaz_search_lat.hip)",
             "launches": kt.backup_select_n, "avg_launch_ms": avg_ms, "sims_per_launch": per_launch,
             "achieved_TFLOPs": flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0}
         for k in ("backup_select_fused", "nn"):
@@ -1272,7 +1279,7 @@ def main():
                 "flop_per_launch": FLOP_PER_SIM[cfg["blocks"]] * sk["sims_per_launch"],
                 "avg_launch_ms": sk["avg_launch_ms"], "launches": sk["launches"],
                 "measured_on": "the timed region: HIP events around every k_search_grp launch (each covers "
-                               "16 simulations of every game, tree work and noise waits included)",
+                               "one root-noise chunk, a whole C2 ply, of every game, tree work included)",
                 "flop_accounting": "SURVEY 8d dense MACs x2 per sim", "nn_kernel_single_stream": nn_leg,
                 # per simulation: the network's state in and policy / value out (24 + 204 B), the tree work
                 # (~1.95 KB at C3 depth and branching), the weights once per 16-game workgroup

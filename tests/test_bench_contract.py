@@ -118,3 +118,9 @@ def test_pure_mcts_and_arena_defaults(bench, monkeypatch):
     assert a.pm_games == 1 << 20 and a.pm_playouts == 400
     monkeypatch.setattr(sys, "argv", ["bench.py", "--mode", "arena"])
     assert bench.parse().arena_games == 131072
+
+
+def test_grp_launches_per_ply(bench):
+    """k_search_grp launches per ply follow the engine's root-noise chunk (max(16, min(512, sims))): a C2 ply
+    (100 simulations) is one launch, the Agent default (5 000) ten."""
+    assert [bench.grp_launches_per_ply(s) for s in (8, 16, 100, 512, 1000, 5000)] == [1, 1, 1, 1, 2, 10]
