@@ -1219,6 +1219,11 @@ def main():
                       "root-noise chunk of up to 512 simulations per launch; oaz_search_lat.hip)",
             "launches": kt.backup_select_n, "avg_launch_ms": avg_ms, "sims_per_launch": per_launch,
             "achieved_TFLOPs": flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0}
+        # k_search_grp evaluates every leaf row of its 16-game tile at every simulation (terminal leaves and
+        # slots still waiting for a staggered start included): G positions per simulation step, not the
+        # GS_EVALS count of the evaluations the playouts use
+        out["nn_positions_per_sim"] = cfg["games"] * args.steps * cfg["sims"] / max(1, own_sims)
+        out["nn_leaf_evaluations"] = "every playout (k_search_grp: every leaf row of its 16-game tile)"
         for k in ("backup_select_fused", "nn"):
             out["kernel_ms_per_step"].pop(k, None)
         out["kernel_ms_per_step"]["search_grp"] = kt.backup_select_ms / args.steps
@@ -1251,11 +1256,23 @@ def main():
             # what `traffic` measures: one simulation step of the timed loop = one launch per game part
             "algorithmic_bytes_per_sim_step": (traffic or {}).get("game_parts", 1) * XCDS * nn_blob
                                               + cfg["games"] * (24 + 204),
+            # the SURVEY 8d formula itself: ONE copy of the weight image per simulation step
+            "algorithmic_bytes_per_sim_step_single_copy": nn_blob + cfg["games"] * (24 + 204),
             "traffic_detail": traffic,
             "peak_note": {"fp32": "F32 MFMA dense peak", "bf16": "BF16 dense MFMA peak",
                           "fp32_split": "BF16 dense MFMA peak / 6 products per fp32 MAC",
                           "fp32_split16": "FP16 dense MFMA peak / 3 products per fp32 MAC"}[cfg["precision"]],
             "frac_of_fp32_mfma_peak": leg["achieved"] / PEAK_TFLOPS["fp32"]}
+        rf = out["roofline"]
+        if rf["traffic"]:
+            # measured HBM bytes per simulation step against the single-copy formula (the weights read once,
+            # SURVEY 8d) and against the same formula plus the per-launch refill of every XCD's L2
+            rf["traffic_vs_single_copy"] = rf["traffic"] / rf["algorithmic_bytes_per_sim_step_single_copy"]
+            rf["traffic_vs_with_xcd_refills"] = rf["traffic"] / rf["algorithmic_bytes_per_sim_step"]
+            rf["traffic_note"] = ("traffic / the single-copy formula: the excess is the weight image re-read into "
+                                  f"each of the {XCDS} XCD L2s on every launch (kernel boundaries invalidate the "
+                                  "L2s; profiles/r05_nn_l2_standalone_pmc.txt), a per-launch refill overhead, not "
+                                  "algorithmic bytes")
         if clock:
             # the clock of the measured launches: the kernel's cycles per launch (PMC pass) over the
             # un-profiled HIP-event launch time above; the peak scaled to that clock (2400 MHz nominal)

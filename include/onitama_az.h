@@ -253,6 +253,10 @@ size_t oaz_nn_device_bytes(int blocks, int precision);
 int oaz_random_weights(uint64_t seed, int blocks, float* out, size_t n);
 /* Deck of global game `game_id` under `seed` (random 5 of 16, Fisher-Yates on Philox). */
 void oaz_deal_deck(uint64_t seed, uint64_t game_id, uint8_t out[5]);
+/* Global game ids of the `games` self-play slots of rank `rank` of `world` in their seq-th game:
+ * out[g] = (seq * world + rank) * games + g, the rule the self-play kernel keys deals and root noise with
+ * (replaces the reference's per-worker games, train.rs:218-238: ranks play disjoint game ids). */
+int oaz_slot_game_ids(int rank, int world, int games, uint64_t seq, uint64_t* out);
 /* Start position with `deck`; to_move = colour of the neutral card (game_state.rs:19-24). */
 void oaz_initial_state(const uint8_t deck[5], oaz_state* out);
 /* The HASH test evaluator (identical on host and device; documented in DESIGN.md). */
@@ -350,7 +354,8 @@ int oaz_nn_fallbacks(oaz_engine* eng, uint64_t* tiles);
  * evaluation of the root (Agent::generate_move, mod.rs:137-141). Any output may be NULL. */
 int oaz_search(oaz_engine* eng, const oaz_state* roots, int G, oaz_move* out_move,
                float* out_pi, float* out_root_value, oaz_search_stats* stats);
-/* Tree of `game` left by the last oaz_search: nodes [0, *n_nodes) in reference arena order. */
+/* Tree of `game` left by the last oaz_search, or of slot `game` by the last self-play ply (the tree that
+ * ply's move and pi came from): nodes [0, *n_nodes) in reference arena order. */
 int oaz_tree_dump(oaz_engine* eng, int game, oaz_node* out, int cap, int* n_nodes);
 
 /* ---- self-play (continuous batching over cfg.games slots, device resident) ------ */

@@ -284,6 +284,14 @@ OAZ_HD void deal_deck(uint64_t seed, uint64_t game_id, uint8_t out[5]) {
     for (int i = 0; i < 5; ++i) out[i] = cards[i];
 }
 
+// Global game id of self-play slot g of rank r (of `world` ranks, G slots each) in the slot's seq-th
+// game: (seq * world + r) * G + g. The id keys the deal and the root noise, so
+// ranks play disjoint games and together every id below (seq + 1) * world * G once per sequence;
+// k_selfplay_move's start_game and the host's oaz_slot_game_ids both call this.
+OAZ_HD uint64_t slot_game_id(uint64_t seq, uint32_t world, uint32_t rank, uint32_t G, uint32_t g) {
+    return (seq * (uint64_t)world + (uint64_t)rank) * (uint64_t)G + (uint64_t)g;
+}
+
 OAZ_HD uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -76,6 +76,12 @@ extern "C" int oaz_device_count(int* n) {
     return 0;
 }
 
+static double now_ns() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e9 + (double)ts.tv_nsec;
+}
+
 // ---- host helpers -----------------------------------------------------------------------------
 extern "C" void oaz_attack_maps(uint32_t out[2 * 16 * 25]) {
     memcpy(out, kAttackHost.m, sizeof(kAttackHost.m));
@@ -136,6 +142,13 @@ extern "C" int oaz_random_weights(uint64_t seed, int blocks, float* out, size_t 
 
 extern "C" void oaz_deal_deck(uint64_t seed, uint64_t game_id, uint8_t out[5]) {
     deal_deck(seed, game_id, out);
+}
+
+extern "C" int oaz_slot_game_ids(int rank, int world, int games, uint64_t seq, uint64_t* out) {
+    if (!out || games < 1 || world < 1 || rank < 0 || rank >= world)
+        return oaz_set_err(OAZ_ERR_ARG, "slot_game_ids: rank %d of %d, %d games", rank, world, games);
+    for (int g = 0; g < games; ++g) out[g] = slot_game_id(seq, (uint32_t)world, (uint32_t)rank, (uint32_t)games, (uint32_t)g);
+    return 0;
 }
 
 extern "C" void oaz_initial_state(const uint8_t deck[5], oaz_state* out) {
@@ -522,45 +535,52 @@ struct Scratch {
     }
 };
 
+// One context per device (stream + scratch buffers allocated on that device): the rules entry points run
+// on the calling thread's current device, so calls from threads on different GPUs never share buffers.
 struct RulesCtx {
     std::mutex mu;
     bool init = false;
-    int device = -1;
     hipStream_t stream = nullptr;
     Scratch a, b, c, d;
 };
-static RulesCtx g_rules;
+constexpr int kRulesMaxDevices = 64;
+static RulesCtx g_rules_dev[kRulesMaxDevices];
 
-static int rules_begin() {
+// The current device's context, locked for the caller (lk), its stream created on first use.
+static int rules_begin(RulesCtx** out, std::unique_lock<std::mutex>& lk) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return oaz_set_err(OAZ_ERR_NO_DEVICE, "no HIP device visible (the rules run on the GPU)");
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
-    if (!g_rules.init || g_rules.device != dev) {
-        HIP_TRY(hipStreamCreateWithFlags(&g_rules.stream, hipStreamNonBlocking));
-        g_rules.device = dev;
-        g_rules.init = true;
+    if (dev < 0 || dev >= kRulesMaxDevices) return oaz_set_err(OAZ_ERR_ARG, "rules: device %d unsupported", dev);
+    RulesCtx& r = g_rules_dev[dev];
+    lk = std::unique_lock<std::mutex>(r.mu);
+    if (!r.init) {
+        HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
+        r.init = true;
     }
+    *out = &r;
     return 0;
 }
 
 extern "C" int oaz_movegen(const oaz_state* s, int n, uint32_t* masks, oaz_move* moves, uint8_t* counts) {
     if (!s || n < 0) return oaz_set_err(OAZ_ERR_ARG, "movegen: bad arguments");
     if (n == 0) return 0;
-    std::lock_guard<std::mutex> lk(g_rules.mu);
-    if (int rc = rules_begin()) return rc;
-    hipStream_t st = g_rules.stream;
-    if (int rc = g_rules.a.ensure((size_t)n * sizeof(oaz_state))) return rc;
-    if (int rc = g_rules.b.ensure((size_t)n * 50 * 4)) return rc;
-    if (int rc = g_rules.c.ensure((size_t)n * OAZ_MAX_MOVES * sizeof(oaz_move))) return rc;
-    if (int rc = g_rules.d.ensure((size_t)n)) return rc;
-    HIP_TRY(hipMemcpyAsync(g_rules.a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_movegen((oaz_state*)g_rules.a.p, n, masks ? (uint32_t*)g_rules.b.p : nullptr,
-                           moves ? (oaz_move*)g_rules.c.p : nullptr, counts ? (uint8_t*)g_rules.d.p : nullptr, st));
-    if (masks) HIP_TRY(hipMemcpyAsync(masks, g_rules.b.p, (size_t)n * 50 * 4, hipMemcpyDeviceToHost, st));
-    if (moves) HIP_TRY(hipMemcpyAsync(moves, g_rules.c.p, (size_t)n * OAZ_MAX_MOVES * sizeof(oaz_move), hipMemcpyDeviceToHost, st));
-    if (counts) HIP_TRY(hipMemcpyAsync(counts, g_rules.d.p, (size_t)n, hipMemcpyDeviceToHost, st));
+    RulesCtx* R = nullptr;
+    std::unique_lock<std::mutex> lk;
+    if (int rc = rules_begin(&R, lk)) return rc;
+    hipStream_t st = R->stream;
+    if (int rc = R->a.ensure((size_t)n * sizeof(oaz_state))) return rc;
+    if (int rc = R->b.ensure((size_t)n * 50 * 4)) return rc;
+    if (int rc = R->c.ensure((size_t)n * OAZ_MAX_MOVES * sizeof(oaz_move))) return rc;
+    if (int rc = R->d.ensure((size_t)n)) return rc;
+    HIP_TRY(hipMemcpyAsync(R->a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_movegen((oaz_state*)R->a.p, n, masks ? (uint32_t*)R->b.p : nullptr,
+                           moves ? (oaz_move*)R->c.p : nullptr, counts ? (uint8_t*)R->d.p : nullptr, st));
+    if (masks) HIP_TRY(hipMemcpyAsync(masks, R->b.p, (size_t)n * 50 * 4, hipMemcpyDeviceToHost, st));
+    if (moves) HIP_TRY(hipMemcpyAsync(moves, R->c.p, (size_t)n * OAZ_MAX_MOVES * sizeof(oaz_move), hipMemcpyDeviceToHost, st));
+    if (counts) HIP_TRY(hipMemcpyAsync(counts, R->d.p, (size_t)n, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return 0;
 }
@@ -571,17 +591,18 @@ extern "C" int oaz_step(oaz_state* s, const oaz_move* mv, int n, uint8_t* result
     for (int i = 0; i < n; ++i)
         if (mv[i].from > 24 || mv[i].to > 24 || mv[i].slot > 3 || mv[i].piece > 1)
             return oaz_set_err(OAZ_ERR_ARG, "step: move %d out of range", i);  // deck.rs:88 assert
-    std::lock_guard<std::mutex> lk(g_rules.mu);
-    if (int rc = rules_begin()) return rc;
-    hipStream_t st = g_rules.stream;
-    if (int rc = g_rules.a.ensure((size_t)n * sizeof(oaz_state))) return rc;
-    if (int rc = g_rules.c.ensure((size_t)n * sizeof(oaz_move))) return rc;
-    if (int rc = g_rules.d.ensure((size_t)n)) return rc;
-    HIP_TRY(hipMemcpyAsync(g_rules.a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(g_rules.c.p, mv, (size_t)n * sizeof(oaz_move), hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_step((oaz_state*)g_rules.a.p, (const oaz_move*)g_rules.c.p, n, (uint8_t*)g_rules.d.p, st));
-    HIP_TRY(hipMemcpyAsync(s, g_rules.a.p, (size_t)n * sizeof(oaz_state), hipMemcpyDeviceToHost, st));
-    if (results) HIP_TRY(hipMemcpyAsync(results, g_rules.d.p, (size_t)n, hipMemcpyDeviceToHost, st));
+    RulesCtx* R = nullptr;
+    std::unique_lock<std::mutex> lk;
+    if (int rc = rules_begin(&R, lk)) return rc;
+    hipStream_t st = R->stream;
+    if (int rc = R->a.ensure((size_t)n * sizeof(oaz_state))) return rc;
+    if (int rc = R->c.ensure((size_t)n * sizeof(oaz_move))) return rc;
+    if (int rc = R->d.ensure((size_t)n)) return rc;
+    HIP_TRY(hipMemcpyAsync(R->a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(R->c.p, mv, (size_t)n * sizeof(oaz_move), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_step((oaz_state*)R->a.p, (const oaz_move*)R->c.p, n, (uint8_t*)R->d.p, st));
+    HIP_TRY(hipMemcpyAsync(s, R->a.p, (size_t)n * sizeof(oaz_state), hipMemcpyDeviceToHost, st));
+    if (results) HIP_TRY(hipMemcpyAsync(results, R->d.p, (size_t)n, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return 0;
 }
@@ -589,14 +610,15 @@ extern "C" int oaz_step(oaz_state* s, const oaz_move* mv, int n, uint8_t* result
 extern "C" int oaz_current_state(const oaz_state* s, int n, uint8_t* results) {
     if (!s || !results || n < 0) return oaz_set_err(OAZ_ERR_ARG, "current_state: bad arguments");
     if (n == 0) return 0;
-    std::lock_guard<std::mutex> lk(g_rules.mu);
-    if (int rc = rules_begin()) return rc;
-    hipStream_t st = g_rules.stream;
-    if (int rc = g_rules.a.ensure((size_t)n * sizeof(oaz_state))) return rc;
-    if (int rc = g_rules.d.ensure((size_t)n)) return rc;
-    HIP_TRY(hipMemcpyAsync(g_rules.a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_current_state((const oaz_state*)g_rules.a.p, n, (uint8_t*)g_rules.d.p, st));
-    HIP_TRY(hipMemcpyAsync(results, g_rules.d.p, (size_t)n, hipMemcpyDeviceToHost, st));
+    RulesCtx* R = nullptr;
+    std::unique_lock<std::mutex> lk;
+    if (int rc = rules_begin(&R, lk)) return rc;
+    hipStream_t st = R->stream;
+    if (int rc = R->a.ensure((size_t)n * sizeof(oaz_state))) return rc;
+    if (int rc = R->d.ensure((size_t)n)) return rc;
+    HIP_TRY(hipMemcpyAsync(R->a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_current_state((const oaz_state*)R->a.p, n, (uint8_t*)R->d.p, st));
+    HIP_TRY(hipMemcpyAsync(results, R->d.p, (size_t)n, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return 0;
 }
@@ -604,14 +626,15 @@ extern "C" int oaz_current_state(const oaz_state* s, int n, uint8_t* results) {
 extern "C" int oaz_encode(const oaz_state* s, int n, float* planes) {
     if (!s || !planes || n < 0) return oaz_set_err(OAZ_ERR_ARG, "encode: bad arguments");
     if (n == 0) return 0;
-    std::lock_guard<std::mutex> lk(g_rules.mu);
-    if (int rc = rules_begin()) return rc;
-    hipStream_t st = g_rules.stream;
-    if (int rc = g_rules.a.ensure((size_t)n * sizeof(oaz_state))) return rc;
-    if (int rc = g_rules.b.ensure((size_t)n * 525 * 4)) return rc;
-    HIP_TRY(hipMemcpyAsync(g_rules.a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_encode((const oaz_state*)g_rules.a.p, n, (float*)g_rules.b.p, st));
-    HIP_TRY(hipMemcpyAsync(planes, g_rules.b.p, (size_t)n * 525 * 4, hipMemcpyDeviceToHost, st));
+    RulesCtx* R = nullptr;
+    std::unique_lock<std::mutex> lk;
+    if (int rc = rules_begin(&R, lk)) return rc;
+    hipStream_t st = R->stream;
+    if (int rc = R->a.ensure((size_t)n * sizeof(oaz_state))) return rc;
+    if (int rc = R->b.ensure((size_t)n * 525 * 4)) return rc;
+    HIP_TRY(hipMemcpyAsync(R->a.p, s, (size_t)n * sizeof(oaz_state), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_encode((const oaz_state*)R->a.p, n, (float*)R->b.p, st));
+    HIP_TRY(hipMemcpyAsync(planes, R->b.p, (size_t)n * 525 * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return 0;
 }
@@ -668,6 +691,8 @@ struct oaz_engine {
     uint32_t* sims_run = nullptr;
     int wall_khz = 0;  // hipDeviceAttributeWallClockRate (kHz)
     bool last_sims_dev = false;
+    bool deadline_armed = false;  // begin_budget launched k_deadline_start for the current search / ply
+    double t_search0 = 0.0;       // host clock at the start of the current search / ply (0: no budget)
     uint32_t last_G = 0;
     std::vector<uint32_t> sims_host;  // per-game counts of the last device-budgeted run (empty: all last_sims)
     uint32_t* s_ply = nullptr;
@@ -679,6 +704,8 @@ struct oaz_engine {
     oaz_sample* hist = nullptr;
     oaz_sample* out = nullptr;
     unsigned long long* out_count = nullptr;
+    uint32_t* fin = nullptr;      // SlotView::fin / fin_pos (records of the games that ended in a ply)
+    uint64_t* fin_pos = nullptr;
     unsigned long long out_read = 0;  // samples already handed out
     bool selfplay_ready = false;
     uint64_t quota = 0;
@@ -731,14 +758,17 @@ static SlotView slot_view(oaz_engine* e) {
     s.hist = e->hist;
     s.out = e->out;
     s.out_count = e->out_count;
+    s.fin = e->fin;
+    s.fin_pos = e->fin_pos;
     s.hcap = e->hcap;
     s.out_cap = e->out_cap;
     s.max_plies = e->cfg.max_plies;
     s.fixed_deck = e->cfg.fixed_deck;
     memcpy(s.deck, e->cfg.deck, 5);
     s.seed = e->cfg.seed;
-    s.world_games = e->G * (uint32_t)(e->cfg.world > 0 ? e->cfg.world : 1);
-    s.rank_base = (uint32_t)e->cfg.rank * e->G;
+    s.G = e->G;
+    s.world = (uint32_t)(e->cfg.world > 0 ? e->cfg.world : 1);
+    s.rank = (uint32_t)e->cfg.rank;
     s.quota = e->quota;
     s.stagger = e->quota ? 0u : (uint32_t)(e->cfg.stagger > 0 ? e->cfg.stagger : 0);
     return s;
@@ -770,16 +800,7 @@ static hipEvent_t ev_get(oaz_engine* e) {
 #define OAZ_NOISE_CHUNK 16
 #endif
 static constexpr uint32_t kNoiseChunk = OAZ_NOISE_CHUNK;  // simulations of root noise produced per launch
-// The ring slot of an engine whose games fit one round of k_search_grp workgroups (<= 16 x CU count):
-// every chunk is one k_search_grp launch, and the noise launch of the next chunk cannot overlap it (the
-// search holds every CU), so a chunk of up to 512 simulations (a C2 ply in one launch and one noise
-// launch: 46.6-47.1 -> 49.5-50.0 M sims/s) at a 16-simulation minimum; 16 for the
-// rest (the per-step launches, where the noise overlaps). Ring: 2 x chunk x G x 80 floats (<= 1.3 GB).
-static uint32_t noise_chunk_for(uint32_t G, int cus, int32_t sims_cap) {
-    if (G > 16u * (uint32_t)cus) return kNoiseChunk;
-    const uint32_t c = sims_cap < 512 ? (uint32_t)sims_cap : 512u;
-    return c > kNoiseChunk ? c : kNoiseChunk;
-}
+static uint32_t noise_chunk_for(const oaz_engine* e);  // after grp_search
 
 static void accumulate(oaz_engine* e, const TimedLaunch& p, float ms) {
     double* acc[7] = {&e->times.select_ms, &e->times.nn_ms, &e->times.expand_ms, &e->times.finalize_ms,
@@ -860,7 +881,8 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
     }
     if (cfg->blocks < 0 || cfg->blocks > 64 || cfg->sims < 1 || cfg->sims > 65535 || cfg->games < 1 ||
         cfg->max_plies < 0 || cfg->max_plies > 100000 || cfg->compact < 0 || cfg->compact > 2 || cfg->search_time_ns < 0 ||
-        cfg->step_kernels < 0 || cfg->step_kernels > 1 ||
+        cfg->step_kernels < 0 || cfg->step_kernels > 1 || cfg->world < 0 || cfg->rank < 0 ||
+        cfg->rank >= (cfg->world > 0 ? cfg->world : 1) ||
         (uint64_t)cfg->games * ((uint64_t)cfg->sims + 1) >= (1ull << 32) ||  // 32-bit path offsets (k_select_seg)
         (cfg->parts != 0 && cfg->parts != 1 && cfg->parts != 2 && cfg->parts != 4)) {
         oaz_set_err(OAZ_ERR_ARG, "create: config out of range");
@@ -925,7 +947,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         e->cus = 256;
     if (hipDeviceGetAttribute(&e->wall_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess) e->wall_khz = 0;
     const size_t G = e->G;
-    e->noise_chunk = noise_chunk_for(e->G, e->cus, e->sims_cap);
+    e->noise_chunk = noise_chunk_for(e);
     if (dalloc(&e->nodes, G * e->cap) || dalloc(&e->n_nodes, G) || dalloc(&e->path, G * e->pathcap) ||
         dalloc(&e->depth, G) || dalloc(&e->leaf, G) || dalloc(&e->leaf_state, G) ||
         dalloc(&e->stats, G * GS_COUNT) || dalloc(&e->stats_sum, (size_t)GS_COUNT) ||
@@ -937,7 +959,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         dalloc(&e->root, G) || dalloc(&e->ply, G) || dalloc(&e->seq, G) ||
         dalloc(&e->game_id, G) || dalloc(&e->active, G) || dalloc(&e->hist, G * e->hcap) ||
         dalloc(&e->out, (size_t)e->out_cap) || dalloc(&e->out_count, (size_t)1) || dalloc(&e->nn_fallback, (size_t)1) ||
-        dalloc(&e->deadline, (size_t)1) || dalloc(&e->sims_run, G) ||
+        dalloc(&e->deadline, (size_t)1) || dalloc(&e->sims_run, G) || dalloc(&e->fin, G) || dalloc(&e->fin_pos, G) ||
         (cfg->train_noise && dalloc(&e->noise, 2 * (size_t)e->noise_chunk * G * kNoiseStride)))
         return fail();
     // sqrt((double)n) from the host libm (IEEE correctly rounded), so device PUCT = oracle PUCT
@@ -990,7 +1012,7 @@ extern "C" void oaz_destroy(oaz_engine* e) {
                     e->stats_sum, e->sqrt_tab, e->policy, e->value, e->weights, e->s_roots,
                     e->s_move, e->s_pi, e->s_rootv, e->s_rootp, e->s_ply, e->root, e->ply,
                     e->seq, e->game_id, e->active, e->hist, e->out, e->out_count, e->noise, e->nn_fallback,
-                    e->need, e->slot, e->cstate, e->bcnt, e->deadline, e->sims_run};
+                    e->need, e->slot, e->cstate, e->bcnt, e->deadline, e->sims_run, e->fin, e->fin_pos};
     for (void* p : ptrs) dfree(p);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
@@ -1181,6 +1203,27 @@ static bool compact_leaves(const oaz_engine* e, uint32_t G) {
     return e->cfg.compact == 1 || (e->cfg.compact == 2 && G >= 12u * 16u * (uint32_t)e->cus);
 }
 
+// A search of G games runs as k_search_grp launches (16 games per workgroup, up to one round of workgroups,
+// one launch per root-noise chunk) instead of the per-simulation-step launches. Everything it depends on is
+// fixed at creation except G (any G below a qualifying engine's qualifies as well).
+static bool grp_search(const oaz_engine* e, uint32_t G) {
+    const bool hash = e->cfg.evaluator == OAZ_EVAL_HASH;
+    return e->cfg.step_kernels == 0 && !compact_leaves(e, G) && (G + 15) / 16 <= (uint32_t)e->cus &&
+           (hash || e->cfg.precision == OAZ_FP32_SPLIT16) && tree_seg_kernels();
+}
+
+// Simulations per root-noise ring slot. An engine whose searches run as k_search_grp: every chunk is one
+// launch, and the noise launch of the next chunk cannot overlap it (the search holds every CU), so a chunk of
+// up to 512 simulations (a C2 ply in one launch and one noise launch: 46.6-47.1 -> 49.5-50.0 M sims/s;
+// DESIGN.md section 8) at a 16-simulation minimum. kNoiseChunk (16) for the per-step launches, where the
+// noise overlaps the network and the first select waits for only 16 simulations' draws. Ring: 2 x chunk x
+// G x 80 floats (<= 1.3 GB at 4 096 games).
+static uint32_t noise_chunk_for(const oaz_engine* e) {
+    if (!grp_search(e, e->G)) return kNoiseChunk;
+    const uint32_t c = e->sims_cap < 512 ? (uint32_t)e->sims_cap : 512u;
+    return c > kNoiseChunk ? c : kNoiseChunk;
+}
+
 // All cfg.sims simulations of one move for every game, in lock step: select -> leaf compaction ->
 // evaluate -> expand/backup, where simulation s's expand/backup and simulation s+1's select run as
 // one kernel (k_backup_select_seg; a game's next walk needs only its own backup). Select marks the games whose playout uses its leaf evaluation (all
@@ -1232,10 +1275,27 @@ static int run_sims(oaz_engine* e, const TreeView& t, const oaz_state* roots, co
     return rc;
 }
 
-static double now_ns() {
-    timespec ts;
-    clock_gettime(CLOCK_MONOTONIC, &ts);
-    return (double)ts.tv_sec * 1e9 + (double)ts.tv_nsec;
+
+// Q7: the device deadline = the device clock when k_deadline_start runs on the engine stream + the budget.
+static int arm_deadline(oaz_engine* e) {
+    if (e->wall_khz <= 0) return oaz_set_err(OAZ_ERR_HIP, "search_time: the device reports no wall clock rate");
+    const double ticks = (double)e->cfg.search_time_ns * (double)e->wall_khz * 1e-6;
+    HIP_TRY(launch_deadline_start(e->deadline, ticks < 1.8e19 ? (uint64_t)ticks : (uint64_t)1.8e19, e->stream));
+    e->deadline_armed = true;
+    return 0;
+}
+
+// Q7: a search's budget runs from the start of the search call, as the reference's Instant is taken at the
+// top of search() (mcts_arena.rs:75-78): the host clock now (the per-step loop's reads) and, on the device,
+// the deadline armed before this search's first upload or reset on the engine stream (the one-launch
+// searches' reads), so the roots upload and the tree reset count against the budget on both paths. Work
+// queued on the stream by earlier calls (asynchronous self-play plies) is not part of this search.
+static int begin_budget(oaz_engine* e) {
+    e->deadline_armed = false;
+    e->t_search0 = 0.0;
+    if (e->cfg.search_time_ns <= 0) return 0;
+    e->t_search0 = now_ns();
+    return e->wall_khz > 0 ? arm_deadline(e) : 0;
 }
 
 static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* roots, const uint8_t* active,
@@ -1251,7 +1311,7 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
     // budget: every game then has run the same number of playouts (>= 1). pi / the move come from the
     // visits that ran.
     const double budget_ns = (double)e->cfg.search_time_ns;
-    const double t_start = budget_ns > 0 ? now_ns() : 0.0;
+    const double t_start = budget_ns > 0 ? (e->t_search0 > 0 ? e->t_search0 : now_ns()) : 0.0;
     e->last_sims = 0;
     e->last_sims_dev = false;
     e->sims_host.clear();
@@ -1260,9 +1320,8 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
     // device clock when k_deadline_start runs + the budget in clock ticks
     auto device_budget = [&]() -> int {
         if (budget_ns <= 0) return 0;
-        if (e->wall_khz <= 0) return oaz_set_err(OAZ_ERR_HIP, "search_time: the device reports no wall clock rate");
-        const double ticks = budget_ns * (double)e->wall_khz * 1e-6;
-        HIP_TRY(launch_deadline_start(e->deadline, ticks < 1.8e19 ? (uint64_t)ticks : (uint64_t)1.8e19, e->stream));
+        if (!e->deadline_armed)
+            if (int rc = arm_deadline(e)) return rc;
         HIP_TRY(hipMemsetAsync(e->sims_run, 0, (size_t)t.G * 4, e->stream));
         e->last_sims_dev = true;
         return 0;
@@ -1296,9 +1355,7 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
     const uint32_t nchunks = (sims + chunk - 1) / chunk;
     // up to one round of 16-game workgroups (k_search_grp): one launch per noise chunk of simulations,
     // each workgroup walking, evaluating and backing up its 16 games without a grid-wide step
-    const bool grp = e->cfg.step_kernels == 0 && !compact_leaves(e, t.G) &&
-                     (t.G + 15) / 16 <= (uint32_t)e->cus && (hash || e->cfg.precision == OAZ_FP32_SPLIT16) &&
-                     tree_seg_kernels();
+    const bool grp = grp_search(e, t.G);
     // The games in nh parts, each on its own stream: one part's tree kernels, leaf compaction and NN
     // tail run in the gaps of the others' launches (the NN holds a whole CU per workgroup, so the
     // tree kernels cannot share a CU with it, only fill the CUs it leaves idle). The parts meet only
@@ -1491,6 +1548,7 @@ extern "C" int oaz_search(oaz_engine* e, const oaz_state* roots, int G, oaz_move
     for (int i = 0; i < G; ++i)
         if (roots[i].to_move > 1) return oaz_set_err(OAZ_ERR_ARG, "search: root %d has to_move=%d", i, roots[i].to_move);
     OAZ_ON_DEVICE(e->device);
+    if (int rc = begin_budget(e)) return rc;
     const TreeView t = tree_view(e, (uint32_t)G);
     HIP_TRY(hipMemcpyAsync(e->s_roots, roots, (size_t)G * sizeof(oaz_state), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipMemsetAsync(e->stats, 0, (size_t)G * GS_COUNT * sizeof(uint64_t), e->stream));
@@ -1557,6 +1615,8 @@ extern "C" int oaz_selfplay_step(oaz_engine* e, int moves) {
     const TreeView t = tree_view(e, e->G);
     const SlotView sv = slot_view(e);
     for (int m = 0; m < moves; ++m) {
+        if (int rc = begin_budget(e)) return rc;
+        HIP_TRY(launch_tree_reset(t, e->stream));  // a fresh tree per move (the last ply's stays dumpable)
         if (int rc = run_sims(e, t, e->root, e->active, e->game_id, e->ply)) return rc;
         if (int rc = timed(e, 3, e->G, [&] { return launch_selfplay_move(t, sv, e->stream); })) return rc;
     }

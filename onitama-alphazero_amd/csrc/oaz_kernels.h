@@ -66,14 +66,17 @@ struct SlotView {
     oaz_sample* hist;     // [G][hcap] samples of the running game (z filled at the end)
     oaz_sample* out;      // [out_cap] finished samples
     unsigned long long* out_count;  // appended samples (may exceed out_cap: dropped)
+    uint32_t* fin;        // [G] records of the game that ended in the slot this ply | result << 24 (0: none)
+    uint64_t* fin_pos;    // [G] their first position in out (k_samples_scan)
     uint32_t hcap;
     uint32_t out_cap;
     int32_t max_plies;
     int32_t fixed_deck;
     uint8_t deck[5];
     uint64_t seed;
-    uint32_t world_games;  // games per generation over all ranks (G * world)
-    uint32_t rank_base;    // rank * G
+    uint32_t G;            // slots of this engine
+    uint32_t world;        // ranks (oaz_config.world, >= 1)
+    uint32_t rank;         // this engine's rank (slot_game_id, oaz_device.h)
     uint64_t quota;        // stop starting games at this global index (0 = unlimited)
     uint32_t stagger;      // slot g waits g % stagger plies before its first game (0: none)
 };

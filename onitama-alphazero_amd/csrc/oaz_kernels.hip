@@ -1191,7 +1191,7 @@ __global__ void __launch_bounds__(kBlock) k_search_finalize(TreeView t, const oa
 }
 
 __device__ void start_game(const SlotView& sv, uint32_t g, uint32_t seq, bool lane0) {
-    const uint64_t gid = (uint64_t)seq * sv.world_games + sv.rank_base + g;
+    const uint64_t gid = slot_game_id(seq, sv.world, sv.rank, sv.G, g);
     const bool act = sv.quota == 0 || gid < sv.quota;
     uint8_t deck[5];
     if (sv.fixed_deck) {
@@ -1221,14 +1221,18 @@ __global__ void __launch_bounds__(kBlock) k_selfplay_reset(TreeView t, SlotView 
 
 // One ply of self_play (train.rs:55-80) per slot: record (state, pi, colour), play the most
 // visited move (no temperature, Q9), detect the end (win, or the 152-ply cut of
-// train.rs:74-79), emit z = reward(result, colour) for every sample (train.rs:83-85), deal the
-// next game, and reset the tree (a fresh tree per move, alphazero_mcts/mod.rs:68-77).
+// train.rs:74-79), emit z = reward(result, colour) for every sample (train.rs:83-85) and deal the
+// next game. The tree is reset before the next ply's search (oaz_selfplay_step: k_tree_reset, a fresh
+// tree per move, alphazero_mcts/mod.rs:68-77), so the ply's tree can be dumped in between.
 __global__ void __launch_bounds__(kBlock) k_selfplay_move(TreeView t, SlotView sv) {
     const uint32_t g = wave_game();
     if (g >= t.G) return;
     const uint8_t act = sv.active[g];
     if (act != 1) {  // finished (0) or still waiting for its staggered start (> 1)
-        if (act > 1 && lane_id() == 0) sv.active[g] = act - 1;
+        if (lane_id() == 0) {
+            if (act > 1) sv.active[g] = act - 1;
+            sv.fin[g] = 0u;
+        }
         return;
     }
     const int l = lane_id();
@@ -1263,36 +1267,73 @@ __global__ void __launch_bounds__(kBlock) k_selfplay_move(TreeView t, SlotView s
     const bool over = is_win(res) || (int)nply >= sv.max_plies + 2;
     if (l == 0) st[GS_MOVES] += 1;
     if (over) {
-        // lanes reload history records other lanes of this wave wrote (pi from lanes 0..49, the
-        // state from lane 0): order those global writes before the reads under the memory model
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the game's records go out after the ply, in slot order (k_samples_scan, k_samples_emit): the
+        // history stays until the slot's next game writes its first record in the next ply
         const uint32_t n = nply < sv.hcap ? nply : sv.hcap;
-        unsigned long long base = 0;
-        if (l == 0) base = atomicAdd(sv.out_count, (unsigned long long)n);
-        base = __shfl(base, 0);
-        for (uint32_t i = (uint32_t)l; i < n; i += 64) {
-            oaz_sample smp = hist[i];
-            smp.z = (float)reward(res, smp.state.to_move & 1);
-            if (base + i < sv.out_cap) sv.out[base + i] = smp;
-        }
         if (l == 0) {
+            sv.fin[g] = n | ((uint32_t)res << 24);
             st[GS_FINISHED] += 1;
             if (!is_win(res)) st[GS_CUT] += 1;
             if (res == OAZ_RED_WIN) st[GS_RED] += 1;
             if (res == OAZ_BLUE_WIN) st[GS_BLUE] += 1;
-            if (base + n > sv.out_cap)
-                st[GS_DROPPED] += (base >= sv.out_cap) ? n : (uint32_t)(base + n - sv.out_cap);
         }
         start_game(sv, g, sv.seq[g] + 1, l == 0);
     } else if (l == 0) {
         store_state(&sv.root[g], s);
         sv.ply[g] = nply;
+        sv.fin[g] = 0u;
     }
-    if (l == 0) {
-        store_fresh_node(&T[0], 1.0, 0);
-        t.n_nodes[g] = 1;
+    // the tree stays as searched (oaz_tree_dump after a ply); the next ply starts from k_tree_reset
+}
+
+// The records of the games that ended in this ply, in slot order (the reference appends a worker's
+// games in the order they finish, train.rs:86-97; here a ply's finished games in slot order, so two
+// engines playing the same games hold the same bytes in the same order). One workgroup: each thread
+// sums a run of consecutive slots' record counts, the workgroup scans the runs in LDS, and every slot's
+// first record position (the buffer's count so far + the slots before it) lands in fin_pos; the count
+// grows by the ply's total.
+constexpr int kScanThreads = 1024;
+__global__ void __launch_bounds__(kScanThreads) k_samples_scan(SlotView sv) {
+    const uint32_t per = (sv.G + kScanThreads - 1) / kScanThreads;
+    const uint32_t g0 = threadIdx.x * per, g1 = g0 + per < sv.G ? g0 + per : sv.G;
+    uint64_t sum = 0;
+    for (uint32_t g = g0; g < g1; ++g) sum += sv.fin[g] & 0xFFFFFFu;
+    __shared__ uint64_t run[kScanThreads];
+    run[threadIdx.x] = sum;
+    __syncthreads();
+    for (int d = 1; d < kScanThreads; d <<= 1) {  // inclusive Hillis-Steele scan of the runs
+        const uint64_t v = (int)threadIdx.x >= d ? run[threadIdx.x - d] : 0ull;
+        __syncthreads();
+        run[threadIdx.x] += v;
+        __syncthreads();
     }
+    const unsigned long long base = *sv.out_count;
+    uint64_t pos = base + run[threadIdx.x] - sum;
+    for (uint32_t g = g0; g < g1; ++g) {
+        sv.fin_pos[g] = pos;
+        pos += sv.fin[g] & 0xFFFFFFu;
+    }
+    __syncthreads();  // every thread read the count before it moves
+    if (threadIdx.x == kScanThreads - 1) *sv.out_count = base + run[kScanThreads - 1];
+}
+
+// One wave per slot whose game ended in this ply: its records with z = reward(result, colour)
+// (train.rs:83-85) at fin_pos; the records past the buffer's capacity are counted as dropped.
+__global__ void __launch_bounds__(kBlock) k_samples_emit(TreeView t, SlotView sv) {
+    const uint32_t g = wave_game();
+    if (g >= sv.G) return;
+    const uint32_t f = sv.fin[g], n = f & 0xFFFFFFu;
+    if (n == 0) return;
+    const int res = (int)(f >> 24), l = lane_id();
+    const oaz_sample* hist = sv.hist + (size_t)g * sv.hcap;
+    const uint64_t base = sv.fin_pos[g];
+    for (uint32_t i = (uint32_t)l; i < n; i += 64) {
+        oaz_sample smp = hist[i];
+        smp.z = (float)reward(res, smp.state.to_move & 1);
+        if (base + i < sv.out_cap) sv.out[base + i] = smp;
+    }
+    if (l == 0 && base + n > sv.out_cap)
+        t.stats[(size_t)g * GS_COUNT + GS_DROPPED] += (base >= sv.out_cap) ? n : (uint32_t)(base + n - sv.out_cap);
 }
 
 __global__ void k_stats_reduce(const uint64_t* per_game, uint32_t G, uint64_t* out) {
@@ -1355,10 +1396,15 @@ hipError_t launch_tree_reset(const TreeView& t, hipStream_t st) {
     hipLaunchKernelGGL(k_tree_reset, dim3(thread_grid(t.G, kBlock)), dim3(kBlock), 0, st, t);
     return hipGetLastError();
 }
-// OAZ_TREE_SEG=0 selects the one-game-per-wave kernels (the default is four games per wave)
+// Four games per wave (k_select_seg, k_backup_select_seg). A/B build only: OAZ_TREE_SEG=0 selects the
+// one-game-per-wave kernels (the parity tests' second implementation of the same tree steps).
 static bool tree_seg() {
+#if OAZ_AB
     static const bool v = !(getenv("OAZ_TREE_SEG") && getenv("OAZ_TREE_SEG")[0] == '0');
     return v;
+#else
+    return true;
+#endif
 }
 bool tree_seg_kernels() { return tree_seg(); }
 hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
@@ -1405,6 +1451,8 @@ hipError_t launch_search_finalize(const TreeView& t, const oaz_state* roots, oaz
 }
 hipError_t launch_selfplay_move(const TreeView& t, const SlotView& s, hipStream_t st) {
     hipLaunchKernelGGL(k_selfplay_move, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, s);
+    hipLaunchKernelGGL(k_samples_scan, dim3(1), dim3(kScanThreads), 0, st, s);
+    hipLaunchKernelGGL(k_samples_emit, dim3(wave_grid(t.G)), dim3(kBlock), 0, st, t, s);
     return hipGetLastError();
 }
 hipError_t launch_selfplay_reset(const TreeView& t, const SlotView& s, hipStream_t st) {

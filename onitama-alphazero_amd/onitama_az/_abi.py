@@ -224,6 +224,7 @@ _PROTOS = {
     "oaz_random_weights": (C.c_int, [C.c_uint64, C.c_int, _VOIDP, C.c_size_t]),
     "oaz_deal_deck": (None, [C.c_uint64, C.c_uint64, _VOIDP]),
     "oaz_initial_state": (None, [_VOIDP, _VOIDP]),
+    "oaz_slot_game_ids": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint64, _VOIDP]),
     "oaz_hash_eval": (None, [_VOIDP, _VOIDP, _VOIDP]),
     "oaz_root_noise": (C.c_float, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double, C.c_int]),
     "oaz_movegen": (C.c_int, [_VOIDP, C.c_int, _VOIDP, _VOIDP, _VOIDP]),

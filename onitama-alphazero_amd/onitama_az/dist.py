@@ -22,11 +22,12 @@ from . import _abi
 SAMPLE_BYTES = 228
 
 
-def global_game_ids(rank: int, world: int, games: int, seq: int) -> range:
-    """Global ids of the seq-th game played in each slot of `rank` (matches the kernels:
-    id = (seq * world + rank) * games + slot)."""
-    base = (seq * world + rank) * games
-    return range(base, base + games)
+def global_game_ids(rank: int, world: int, games: int, seq: int) -> np.ndarray:
+    """Global ids of the seq-th game played in each slot of `rank`: oaz_slot_game_ids, the rule the
+    self-play kernel keys deals and root noise with (id = (seq * world + rank) * games + slot)."""
+    out = np.zeros(int(games), dtype=np.uint64)
+    _abi.check(_abi.load().oaz_slot_game_ids(int(rank), int(world), int(games), int(seq), _abi.ptr(out)))
+    return out
 
 
 class Comm:

@@ -6,20 +6,20 @@
  * buffers, alphazero-training/src/train.rs:241-244 (`data_buffer.extend(handle.join())` in worker
  * order = rank order here).
  *
- *   comm_multirank W      (2 <= W <= 8; 8 = the C4 node's rank count)
+ *   comm_multirank W        (2 <= W <= 8; 8 = the C4 node's rank count)
+ *   comm_multirank 8 c4     (the C4 volume: 65,536 slots per rank, > 2^31 bytes gathered into every rank)
  *
  * Per rank r: engine A (the exchange) and engine B (the expectation) get the same config (G_r game
  * slots, rank r of W, HASH evaluator, root noise on) and play the same number of plies P_r, ragged
  * over the ranks and 0 for rank 1 (a rank with no samples). B's samples are fetched to the host;
- * self-play is deterministic, so they are what A holds. Then, on every rank:
+ * self-play is deterministic, records included (a ply's finished games append their records in slot
+ * order), so they are byte for byte what A holds. Then, on every rank:
  *   1. oaz_allgather_samples with cap = total - 1: OAZ_ERR_CAPACITY, *n_total = total, nothing consumed;
  *   2. the last rank passes a NULL engine: it gets OAZ_ERR_ARG, every other rank OAZ_ERR_COMM naming
  *      that rank (the kLocalFailure sentinel through the counts all-gather), nothing consumed;
  *   3. cap = total: counts_out = every rank's count; every rank's device output byte-equal to every
- *      other rank's; block r of it holds exactly rank r's samples (as a set: the engine appends the
- *      samples of games that finish in the same move kernel in atomic order, so two engines playing
- *      the same games may order a ply's samples differently); own buffer drained; stats (ranks,
- *      records, own records);
+ *      other rank's and to the rank-order concatenation of the B engines' fetches; own buffer drained;
+ *      stats (ranks, records, own records);
  *   4. again with every buffer empty: total 0, success;
  *   5. oaz_comm_broadcast from each root in turn (in place, NULL and explicit streams);
  *   6. oaz_comm_allreduce_sum_f32 (exact small sums) on the communicator's and on a caller stream.
@@ -82,8 +82,13 @@ static int g_fail[MAXW];
 
 static const int kGames[MAXW] = {24, 16, 32, 8, 8, 24, 16, 32};
 static const int kPlies[MAXW] = {45, 0, 70, 30, 45, 30, 70, 45};
-
-static int cmp_sample(const void* a, const void* b) { return memcmp(a, b, sizeof(oaz_sample)); }
+/* c4 mode: BASELINE C4's 65,536 slots per rank, 2 simulations, games cut after 20 plies (max_plies 18),
+ * 30 plies on every rank (the zero-count rank is the small mode's): ~1.4 M records = ~0.3 GB per rank, > 2^31
+ * bytes gathered into each of the 8 ranks */
+static int g_c4;
+static const int kC4Games = 65536, kC4Plies = 30;
+static int games_of(int rank) { return g_c4 ? kC4Games : kGames[rank]; }
+static int plies_of(int rank) { return g_c4 ? kC4Plies : kPlies[rank]; }
 
 #define CHECK(c)                                                                                          \
     do {                                                                                                  \
@@ -99,10 +104,11 @@ static oaz_engine* make_engine(int rank) {
     oaz_config_default(&cfg);
     cfg.blocks = 0;
     cfg.evaluator = OAZ_EVAL_HASH;
-    cfg.sims = 12;
-    cfg.games = kGames[rank];
+    cfg.sims = g_c4 ? 2 : 12;
+    cfg.games = games_of(rank);
     cfg.train_noise = 1;
-    cfg.max_plies = 150;
+    cfg.max_plies = g_c4 ? 18 : 150;
+    if (g_c4) cfg.sample_capacity = kC4Games * 32;
     cfg.seed = 20260101ull;
     cfg.rank = rank;
     cfg.world = W;
@@ -123,7 +129,7 @@ static void* rank_main(void* arg) {
     b = make_engine(rank);
     CHECK(a && b);
     CHECK(oaz_selfplay_reset(a) == 0 && oaz_selfplay_reset(b) == 0);
-    CHECK(oaz_selfplay_step(a, kPlies[rank]) == 0 && oaz_selfplay_step(b, kPlies[rank]) == 0);
+    CHECK(oaz_selfplay_step(a, plies_of(rank)) == 0 && oaz_selfplay_step(b, plies_of(rank)) == 0);
     oaz_selfplay_stats sa, sb;
     CHECK(oaz_selfplay_stats_get(a, &sa) == 0 && oaz_selfplay_stats_get(b, &sb) == 0);
     if (!(sa.samples_ready == sb.samples_ready && sa.samples_dropped == 0))
@@ -135,8 +141,9 @@ static void* rank_main(void* arg) {
     g_expect[rank] = (oaz_sample*)malloc((g_count[rank] + 1) * sizeof(oaz_sample));
     size_t got = 0;
     CHECK(oaz_samples_fetch(b, g_expect[rank], g_count[rank], &got) == 0 && got == g_count[rank]);
-    qsort(g_expect[rank], g_count[rank], sizeof(oaz_sample), cmp_sample);
-    CHECK((rank == 1) == (g_count[rank] == 0)); /* rank 1 played no ply: the zero-count rank */
+    oaz_destroy(b); /* (its memory back before the exchange's outputs) */
+    b = NULL;
+    CHECK(g_c4 ? g_count[rank] > 0 : (rank == 1) == (g_count[rank] == 0)); /* rank 1 played no ply: the zero-count rank */
     comm = oaz_comm_init(&g_id, rank, W, 0);
     CHECK(comm != NULL);
     synced = 1;
@@ -169,12 +176,10 @@ static void* rank_main(void* arg) {
     for (int r = 0; r < W; ++r) CHECK(counts[r] == g_count[r]);
     CHECK(hipMemcpy(host, dev, total * sizeof(oaz_sample), 2) == 0);
     size_t off = 0;
-    for (int r = 0; r < W; ++r) {
-        qsort(host + off, g_count[r], sizeof(oaz_sample), cmp_sample); /* sorts the host copy only */
+    for (int r = 0; r < W; ++r) { /* train.rs:241-244: the workers' buffers joined in worker order */
         CHECK(g_count[r] == 0 || memcmp(host + off, g_expect[r], g_count[r] * sizeof(oaz_sample)) == 0);
         off += g_count[r];
     }
-    CHECK(hipMemcpy(host, dev, total * sizeof(oaz_sample), 2) == 0); /* as received again */
     g_out[rank] = host;
     CHECK(bar_wait());
     int same = 1;
@@ -220,8 +225,9 @@ static void* rank_main(void* arg) {
         CHECK(hipMemcpy(fh, dev, nf * sizeof(float), 2) == 0);
         for (size_t i = 0; i < nf; ++i) CHECK(fh[i] == (float)((int)i * W * (W + 1) / 2) + 0.5f * (float)W);
     }
-    printf("OK rank %d: %zu own of %zu records gathered byte-equal; capacity, failure sentinel, empty, "
-           "broadcast x%d, allreduce x2\n", rank, g_count[rank], total, W);
+    if (g_c4) CHECK(total * sizeof(oaz_sample) > ((size_t)1 << 31)); /* the C4 volume: > 2^31 bytes per rank */
+    printf("OK rank %d: %zu own of %zu records (%.3f GB) gathered byte-equal; capacity, failure sentinel, empty, "
+           "broadcast x%d, allreduce x2\n", rank, g_count[rank], total, (double)total * sizeof(oaz_sample) * 1e-9, W);
 done:
     if (!synced) bar_wait(); /* never leave the others waiting at the first barrier */
     if (s) hipStreamDestroy(s);
@@ -237,8 +243,9 @@ done:
 
 int main(int argc, char** argv) {
     W = argc > 1 ? atoi(argv[1]) : 2;
-    if (W < 2 || W > MAXW) {
-        fprintf(stderr, "usage: comm_multirank W (2..%d)\n", MAXW);
+    g_c4 = argc > 2 && strcmp(argv[2], "c4") == 0;
+    if (W < 2 || W > MAXW || (argc > 2 && !g_c4)) {
+        fprintf(stderr, "usage: comm_multirank W [c4]   (2 <= W <= %d)\n", MAXW);
         return 2;
     }
     int ndev = 0;
@@ -257,7 +264,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < W; ++r) fails += g_fail[r];
     for (int r = 0; r < W; ++r) free(g_expect[r]);
     if (fails) return 1;
-    printf("OK multirank %d (%llu stub collectives, %llu calls returned before their collective ran)\n", W,
+    printf("OK multirank %d%s (%llu stub collectives, %llu calls returned before their collective ran)\n", W, g_c4 ? " c4" : "",
            (unsigned long long)rccl_stub_ops(), (unsigned long long)rccl_stub_pending_at_return());
     return 0;
 }

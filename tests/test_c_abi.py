@@ -159,3 +159,24 @@ def test_c_allgather_samples_multirank(tmp_path, world, delay_us):
     if delay_us:  # every operation that moves bytes on a rank: the counts all-gathers, the root's peers' copies
         assert pending >= world * 4, r.stdout
     print(r.stdout)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_c_allgather_samples_c4_volume_world8(tmp_path):
+    """The C4 exchange at its own volume on one GPU: 8 ranks (threads of one C process over the asynchronous
+    RCCL test double), each with BASELINE C4's 65,536 self-play slots (HASH evaluator, 2 simulations, root noise
+    on, games cut after 20 plies, 30 plies). Every rank receives more than 2^31 bytes of (s, pi, z) records
+    (~9.8 M records), and its device output is byte-equal to the rank-order concatenation of the ranks' twin
+    engines' oaz_samples_fetch (train.rs:241-244), so 64-bit offsets and counts hold past 2^31 bytes and
+    2^31 / 228 records."""
+    _, exe, env = _build_multirank(tmp_path)
+    env["RCCL_STUB_DELAY_US"] = "0"
+    r = _run(exe, 8, "c4", env=env, timeout=500)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for rank in range(8):
+        assert f"OK rank {rank}:" in r.stdout, r.stdout
+    assert "OK multirank 8 c4" in r.stdout, r.stdout
+    gb = [float(x) for x in re.findall(r"records \(([0-9.]+) GB\) gathered", r.stdout)]
+    assert len(gb) == 8 and min(gb) > 2 ** 31 * 1e-9, r.stdout
+    print(r.stdout)

@@ -62,7 +62,23 @@ def test_global_game_ids_are_a_partition():
     seen = set()
     for seq in range(3):
         for rank in range(world):
-            ids = set(odist.global_game_ids(rank, world, games, seq))
+            ids = set(int(i) for i in odist.global_game_ids(rank, world, games, seq))
             assert not (ids & seen)
             seen |= ids
     assert seen == set(range(3 * world * games))
+
+
+def test_c4_shard_game_ids_partition_each_sequence():
+    """C4 (65,536 games per GPU x 8 ranks): the product rule (oaz_slot_game_ids, the function the
+    self-play kernel's start_game calls) gives the 8 ranks disjoint id sets whose union is exactly
+    [seq * 8G, (seq + 1) * 8G) for every game sequence, and rank 5's ids are (seq * 8 + 5) * G + slot
+    (the reference's workers, train.rs:218-238, play disjoint games)."""
+    G, W = 65536, 8
+    for seq in (0, 1, 7):
+        ids = np.concatenate([odist.global_game_ids(r, W, G, seq) for r in range(W)])
+        assert ids.dtype == np.uint64 and len(ids) == W * G
+        assert np.array_equal(np.sort(ids), np.arange(seq * W * G, (seq + 1) * W * G, dtype=np.uint64))
+        r5 = odist.global_game_ids(5, W, G, seq)
+        assert np.array_equal(r5, (seq * W + 5) * G + np.arange(G, dtype=np.uint64))
+    with pytest.raises(Exception):
+        odist.global_game_ids(8, W, G, 0)  # rank outside the world

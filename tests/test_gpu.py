@@ -584,8 +584,10 @@ def test_agent_api_mirror(orc):
 
 def test_legacy_one_game_per_wave_tree_kernels_match_oracle(tmp_path):
     """OAZ_TREE_SEG=0 selects the one-game-per-wave k_select / k_expand_backup (the default runs four
-    games per wave). The switch is read once per process, so the check runs in a child process:
-    noise-on searches whose trees must equal the oracle's node for node, as the default path's."""
+    games per wave) in the A/B build (libonitama_az_ab.so, built by __graft_entry__.build(); the product
+    library reads no environment switch). The switch is read once per process, so the check runs in a
+    child process: noise-on searches whose trees must equal the oracle's node for node, as the default
+    path's."""
     import subprocess
     import sys
     from pathlib import Path
@@ -608,7 +610,9 @@ with Engine(games=10, sims=40, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HA
         assert e.tree(g).tobytes() == nodes.tobytes(), g
 print("legacy ok")
 """
-    env = dict(__import__("os").environ, OAZ_TREE_SEG="0")
+    ab = root / "onitama-alphazero_amd" / "onitama_az" / "libonitama_az_ab.so"
+    assert ab.exists(), "build() makes the A/B library"
+    env = dict(__import__("os").environ, OAZ_TREE_SEG="0", OAZ_LIB=str(ab))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "legacy ok" in r.stdout, r.stdout + r.stderr
 

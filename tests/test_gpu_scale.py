@@ -4,6 +4,7 @@ move; full trees on a sample) and against the torch goldens.
 
   C3  65,536 games x 400 sims, fixed deck, root noise on      (HASH evaluator: bit-exact trees)
   C2  4,096 games x 100 sims, 3-block NN (fp16x3 split / fp32) (oracle fed the GPU network)
+  C4  one rank's shard: rank 5 of 8, 65,536 self-play slots x 400 sims (HASH: trees + records)
   C5  65,536 games x 800 sims, 6-block bf16, 16-card deals     (properties + HASH trees)
   NN  B = 65,536 (4,096 workgroups) on the golden positions, every copy against the goldens
 
@@ -160,6 +161,55 @@ def test_c3_selfplay_full_shape_is_valid():
     assert np.all(np.isin(smp["z"], [-1.0, 0.0, 1.0]))
     s = smp["pi"].sum(1)
     assert np.all(np.isclose(s, 1.0, atol=1e-5) | (s == 0))  # 0: a pass position (no legal move)
+
+
+# ---- C4 (one rank's shard) ----------------------------------------------------------------------
+@pytest.mark.timeout(600)
+def test_c4_rank5_of_8_shard_vs_oracle(orc):
+    """C4's per-rank workload on one GPU: the self-play shard of rank 5 of 8 (65,536 slots, 400
+    simulations, fixed deck, root noise on, HASH evaluator so trees compare bit for bit). Every slot
+    plays global game id (seq * 8 + 5) * 65,536 + slot (oaz_slot_game_ids; the deal and the noise are
+    keyed by it, train.rs:218-238 gives each worker its own games). max_plies = 0 cuts every game after
+    two plies (train.rs:74-79), so after ply 1 every slot has emitted its two (s, pi, z) records.
+    Checked against the oracle's games under the same global ids: 64 sampled slots' ply-0 and ply-1
+    trees node for node (oaz_tree_dump after each ply) and pi, their records (state, pi, z = 0) byte-equal
+    at the slot-order positions; the same slots' trees under rank 0's ids differ (another game's noise)."""
+    from onitama_az.dist import global_game_ids
+    G, sims, W, R = 65536, 400, 8, 5
+    deck = [0, 1, 2, 3, 4]
+    gids = global_game_ids(R, W, G, 0)
+    assert int(gids[0]) == 5 * G
+    sample = np.unique(np.concatenate([[0, G - 1], np.random.default_rng(45).integers(0, G, 62)]))
+    cfg = lambda gid, ply=0: orc.search_cfg(sims=sims, c_puct=5.0, evaluator=orc.EVAL_HASH, train_noise=1,
+                                            seed=SEED, game_id=int(gid), ply=ply)
+    ref = {int(g): orc.selfplay_game(cfg(gids[g]), int(gids[g]), max_plies=0, deck=deck)[0] for g in sample}
+    with Engine(games=G, sims=sims, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=SEED,
+                fixed_deck=1, deck=deck, rank=R, world=W, max_plies=0, sample_capacity=2 * G) as e:
+        e.selfplay_reset()
+        for ply in (0, 1):
+            e.selfplay_step(1)
+            for g in sample:
+                root = np.ascontiguousarray(ref[int(g)][ply]["state"]).reshape(1)
+                _, pi, nodes, _ = orc.search(cfg(gids[g], ply), root)
+                _compare_trees(e, int(g), nodes)
+                assert np.array_equal(pi.reshape(-1), ref[int(g)][ply]["pi"].reshape(-1))
+        # the same slots under rank 0's ids are other games (other noise): their ply-1 trees differ
+        differ = 0
+        for g in sample[:8]:
+            root = np.ascontiguousarray(ref[int(g)][1]["state"]).reshape(1)
+            _, _, nodes, _ = orc.search(cfg(g, 1), root)
+            t = e.tree(int(g))
+            differ += int(len(t) != len(nodes) or not np.array_equal(t["N"], nodes["N"]))
+        assert differ >= 6, differ
+        st = e.selfplay_stats()
+        assert (st.moves, st.games_finished, st.games_cut, st.samples_ready, st.samples_dropped) == (2 * G, G, G, 2 * G, 0)
+        assert st.search.sims == 2 * G * sims
+        smp = e.samples_fetch(2 * G)
+    # every game ended in ply 1, and a ply's finished games append their records in slot order: slot g's two
+    # records (state, pi, z = 0) are records 2g and 2g + 1, byte-equal to the oracle's game
+    for g in sample:
+        assert len(ref[int(g)]) == 2 and np.all(ref[int(g)]["z"] == 0.0)
+        assert smp[2 * g: 2 * g + 2].tobytes() == ref[int(g)].tobytes(), g
 
 
 # ---- C2 ----------------------------------------------------------------------------------------
