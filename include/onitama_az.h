@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define OAZ_ABI_VERSION 4
+#define OAZ_ABI_VERSION 5
 
 /* ---- enums mirroring the reference --------------------------------------- */
 enum { OAZ_RED = 0, OAZ_BLUE = 1 };                 /* PlayerColor, player_color.rs:7-10 */
@@ -262,11 +262,11 @@ void oaz_initial_state(const uint8_t deck[5], oaz_state* out);
 /* The HASH test evaluator (identical on host and device; documented in DESIGN.md). */
 void oaz_hash_eval(const oaz_state* s, float policy[50], float* value);
 /* One root-noise draw (replaces the per-comparison Dirichlet(alpha; K) sample of
- * mcts_arena.rs:186-203, marginally Beta(alpha, (K-1) alpha)): draw `draw` (2j + 0 for the
- * running best, 2j + 1 for child j of comparison j) of simulation `sim` at ply `ply` of global
- * game `game_id`. Host computation of the exact f32 value the GPU's root-noise kernel stores. */
-float oaz_root_noise(uint64_t seed, uint64_t game_id, uint32_t ply, uint32_t sim, uint32_t draw, double alpha,
-                     int nchild);
+ * mcts_arena.rs:186-203, marginally Beta(alpha, (K-1) alpha), f64 as the reference's): draw `draw`
+ * (2j + 0 for the running best, 2j + 1 for child j of comparison j) of simulation `sim` at ply `ply`
+ * of global game `game_id`. Host computation of the exact value the GPU's root-noise kernel stores. */
+double oaz_root_noise(uint64_t seed, uint64_t game_id, uint32_t ply, uint32_t sim, uint32_t draw, double alpha,
+                      int nchild);
 
 /* ---- rules on the GPU (bit-exact with the reference) ---------------------------- */
 /* Legal moves of s[i].to_move. masks[i][k][from] = destination mask of own piece on

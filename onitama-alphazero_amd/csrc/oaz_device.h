@@ -209,14 +209,27 @@ OAZ_HD double u01(uint32_t a, uint32_t b) {
 }
 
 // ---- Dirichlet root noise (mcts_arena.rs:186-203) ------------------------------------------
-// The reference draws a fresh Dirichlet(alpha; K) vector for every PUCT evaluation at the root
-// and uses component child.idx-1: marginally Beta(alpha, (K-1) alpha) = X / (X + Y) with
-// X ~ Gamma(alpha), Y ~ Gamma((K-1) alpha) (rand_distr 0.4.3: Marsaglia-Tsang, u^(1/shape) boost
-// for shape < 1). The noise parity with the reference is distributional (its thread_rng is
-// unseedable), so the draws are made in f32 and in the log domain (u^(1/0.03) would underflow in
-// f32) from the same Beta marginal, by Johnk's method (root_noise below). log and exp are the
-// polynomials below (only +, -, *, / and bit operations, no fma contraction): the device and the
-// C oracle compute bit-identical draws.
+// The reference draws a fresh Dirichlet(alpha; K) vector (f64, rand_distr 0.4.3: gamma variates,
+// Marsaglia-Tsang with the u^(1/shape) boost for shape < 1, normalised) for every PUCT evaluation at
+// the root and uses component child.idx-1: marginally Beta(alpha, (K-1) alpha) = X / (X + Y) with
+// X ~ Gamma(alpha), Y ~ Gamma((K-1) alpha). The noise parity with the reference is distributional (its
+// thread_rng is unseedable); the draw here is the same Beta marginal in f64, by Johnk's method in the log
+// domain (U^(1/0.03) underflows even in f64 for U < 1e-9). log and exp are the polynomials below: only
+// IEEE +, -, *, / and explicit fused multiply-adds (correctly rounded on the host, x86 vfmadd / libm fma,
+// and on the device, v_fma_f64) with no compiler contraction, so the device, the host (oaz_root_noise)
+// and the C oracle compute bit-identical draws.
+//
+// OAZ_NOISE_F32 (the A/B build only, a measured option): the previous f32 draw (one 32-bit word per
+// uniform, polynomials in f32), which resolves the law's ends only to f32.
+#ifndef OAZ_NOISE_F32
+#define OAZ_NOISE_F32 0
+#endif
+#if OAZ_NOISE_F32
+typedef float noise_t;
+#else
+typedef double noise_t;
+#endif
+
 OAZ_HD float nz_u(uint32_t x) {  // uniform in (0,1): (2k + 1) 2^-24, k = x >> 9 (exact in f32)
     return (float)(((x >> 9) << 1) | 1u) * (1.0f / 16777216.0f);
 }
@@ -242,15 +255,9 @@ OAZ_HD float nz_exp(float x) {  // e^x (|rel err| < 3e-7); 0 below -87, +inf abo
                                                                                         r * 0.00138888889f)))));
     return q * __builtin_bit_cast(float, (uint32_t)((int)k + 127) << 23);
 }
-// Draw idx (2j + {0: running best, 1: child j}) of comparison j; c2 = ply << 16 | sim.
-// Beta(a, b), a = alpha, b = (K - 1) alpha, by Johnk's method: with U, V uniform, X = U^(1/a),
-// Y = V^(1/b), the pairs with X + Y <= 1 give X / (X + Y) ~ Beta(a, b) exactly (acceptance
-// Gamma(a+1) Gamma(b+1) / Gamma(a+b+1): 0.99 at K = 12, 0.96 at K = 40). In the log domain:
-// lx = log(U) / a, ly = log(V) / b (as products with the rounded reciprocals), accept when
-// exp(lx) + exp(ly) <= 1, eta = 1 / (1 + exp(ly - lx)). Attempt t takes Philox block
-// (game lo, game hi, c2, idx << 12 | t), words 0, 1 and then 2, 3. About 1/6 of the instructions
-// of two Marsaglia-Tsang gamma variates with the small-shape boost (the previous formulation).
-OAZ_HD float root_noise(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx, float alpha, int K) {
+// f32 draw (OAZ_NOISE_F32): idx (2j + {0: running best, 1: child j}) of comparison j; c2 = ply << 16 | sim.
+// Attempt t takes Philox block (game lo, game hi, c2, idx << 12 | t), words 0, 1 and then 2, 3.
+OAZ_HD float root_noise_f32(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx, float alpha, int K) {
     const float ia = 1.0f / alpha, ib = 1.0f / (alpha * (float)(K - 1));
     for (uint32_t t = 0; t < 1024u; ++t) {
         const u32x4 r = philox(seed, (uint32_t)game, (uint32_t)(game >> 32), c2, (idx << 12) | t);
@@ -260,6 +267,85 @@ OAZ_HD float root_noise(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx,
         if (nz_exp(lx2) + nz_exp(ly2) <= 1.0f) return 1.0f / (1.0f + nz_exp(ly2 - lx2));
     }
     return 1.0f / (float)K;  // (never reached: 2048 rejections in a row)
+}
+
+// ln 2 split: kLn2Hi has 21 trailing zero bits (k * kLn2Hi is exact for |k| < 2^21), kLn2Lo the rest.
+constexpr double kLn2Hi = 6.93147180369123816490e-01, kLn2Lo = 1.90821492927058770002e-10;
+OAZ_HD double nz_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+// natural log for normal x > 0: x = 2^e m, m in [sqrt(1/2), sqrt(2)), t = (m - 1) / (m + 1), log m =
+// 2 atanh(t) = 2 (t + t^3 / 3 + ... + t^21 / 21) (|t| <= 0.1716: the next term is < 1e-18 relative).
+OAZ_HD double nz_log64(double x) {
+    uint64_t b = __builtin_bit_cast(uint64_t, x);
+    int e = (int)((b >> 52) & 0x7FF) - 1023;
+    double m = __builtin_bit_cast(double, (b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    if (m > 1.4142135623730951) {
+        m = m * 0.5;
+        e += 1;
+    }
+    const double t = (m - 1.0) / (m + 1.0), t2 = t * t;
+    double p = 2.0 / 21.0;
+    p = nz_fma(p, t2, 2.0 / 19.0);
+    p = nz_fma(p, t2, 2.0 / 17.0);
+    p = nz_fma(p, t2, 2.0 / 15.0);
+    p = nz_fma(p, t2, 2.0 / 13.0);
+    p = nz_fma(p, t2, 2.0 / 11.0);
+    p = nz_fma(p, t2, 2.0 / 9.0);
+    p = nz_fma(p, t2, 2.0 / 7.0);
+    p = nz_fma(p, t2, 2.0 / 5.0);
+    p = nz_fma(p, t2, 2.0 / 3.0);
+    p = nz_fma(p * t2, t, 2.0 * t);  // t (2 + t2 p)
+    const double de = (double)e;
+    return nz_fma(de, kLn2Hi, nz_fma(de, kLn2Lo, p));
+}
+// e^x: x = k ln2 + r, |r| <= ln2 / 2, Taylor to r^13 (the remainder is < 5e-18 relative); 0 below -708
+// (the normal range), +inf above 709.
+OAZ_HD double nz_exp64(double x) {
+    if (x < -708.0) return 0.0;
+    if (x > 709.0) return __builtin_bit_cast(double, 0x7FF0000000000000ull);
+    const double k = (double)(int)(x * 1.4426950408889634 + (x >= 0.0 ? 0.5 : -0.5));
+    const double r = (x - k * kLn2Hi) - k * kLn2Lo;
+    double q = 1.0 / 6227020800.0;  // 1 / 13!
+    q = nz_fma(q, r, 1.0 / 479001600.0);
+    q = nz_fma(q, r, 1.0 / 39916800.0);
+    q = nz_fma(q, r, 1.0 / 3628800.0);
+    q = nz_fma(q, r, 1.0 / 362880.0);
+    q = nz_fma(q, r, 1.0 / 40320.0);
+    q = nz_fma(q, r, 1.0 / 5040.0);
+    q = nz_fma(q, r, 1.0 / 720.0);
+    q = nz_fma(q, r, 1.0 / 120.0);
+    q = nz_fma(q, r, 1.0 / 24.0);
+    q = nz_fma(q, r, 1.0 / 6.0);
+    q = nz_fma(q, r, 0.5);
+    q = nz_fma(q, r, 1.0);
+    q = nz_fma(q, r, 1.0);
+    return q * __builtin_bit_cast(double, (uint64_t)((int64_t)k + 1023) << 52);
+}
+// Draw idx (2j + {0: running best, 1: child j}) of comparison j; c2 = ply << 16 | sim.
+// Beta(a, b), a = alpha, b = (K - 1) alpha, by Johnk's method: with U, V uniform, X = U^(1/a),
+// Y = V^(1/b), the pairs with X + Y <= 1 give X / (X + Y) ~ Beta(a, b) exactly (acceptance
+// Gamma(a+1) Gamma(b+1) / Gamma(a+b+1): 0.99 at K = 12, 0.96 at K = 40). In the log domain:
+// lx = log(U) / a, ly = log(V) / b (as products with the rounded reciprocals), X = exp(lx), Y = exp(ly),
+// accept when X + Y <= 1, eta = X / (X + Y) when both are normal, else (one of them below e^-708) in the
+// log domain, eta = 1 / (1 + exp(ly - lx)). Attempt t takes Philox block (game lo, game hi, c2,
+// idx << 12 | t): U from words 0, 1 and V from words 2, 3 (53-bit uniforms, u01).
+// Resolution: eta is 1.0 exactly when Y / X < 2^-53, as the reference's X / (X + Y) in f64 is.
+OAZ_HD double root_noise_f64(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx, double alpha, int K) {
+    const double ia = 1.0 / alpha, ib = 1.0 / (alpha * (double)(K - 1));
+    for (uint32_t t = 0; t < 2048u; ++t) {
+        const u32x4 r = philox(seed, (uint32_t)game, (uint32_t)(game >> 32), c2, (idx << 12) | t);
+        const double lx = nz_log64(u01(r.x, r.y)) * ia, ly = nz_log64(u01(r.z, r.w)) * ib;
+        const double x = nz_exp64(lx), y = nz_exp64(ly), sum = x + y;
+        if (sum <= 1.0) return (x > 0.0 && y > 0.0) ? x / sum : 1.0 / (1.0 + nz_exp64(ly - lx));
+    }
+    return 1.0 / (double)K;  // (never reached: 2048 rejections in a row)
+}
+// The engine's draw (k_root_noise, oaz_root_noise): f64, or f32 in an OAZ_NOISE_F32 build.
+OAZ_HD noise_t root_noise(uint64_t seed, uint64_t game, uint32_t c2, uint32_t idx, double alpha, int K) {
+#if OAZ_NOISE_F32
+    return root_noise_f32(seed, game, c2, idx, (float)alpha, K);
+#else
+    return root_noise_f64(seed, game, c2, idx, alpha, K);
+#endif
 }
 
 // Deck::default (deck.rs:139-151): random 5 of the 16 cards; Fisher-Yates driven by

@@ -156,9 +156,9 @@ extern "C" void oaz_initial_state(const uint8_t deck[5], oaz_state* out) {
     initial_state(deck, *out);
 }
 
-extern "C" float oaz_root_noise(uint64_t seed, uint64_t game_id, uint32_t ply, uint32_t sim, uint32_t draw,
+extern "C" double oaz_root_noise(uint64_t seed, uint64_t game_id, uint32_t ply, uint32_t sim, uint32_t draw,
                                 double alpha, int nchild) {
-    return root_noise(seed, game_id, (ply << 16) | (sim & 0xFFFFu), draw, (float)alpha, nchild);
+    return (double)root_noise(seed, game_id, (ply << 16) | (sim & 0xFFFFu), draw, alpha, nchild);
 }
 
 extern "C" void oaz_hash_eval(const oaz_state* s, float policy[50], float* value) {
@@ -659,7 +659,7 @@ struct oaz_engine {
     hipEvent_t ev_join = nullptr, ev_part[kMaxParts] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t ev_ready[2] = {nullptr, nullptr};
     hipEvent_t ev_consumed[2][kMaxParts] = {};  // noise ring slot done with, per game part
-    float* noise = nullptr;              // [2][noise_chunk][G][kNoiseStride]
+    noise_t* noise = nullptr;            // [2][noise_chunk][G][kNoiseStride] (f64 draws; f32 in an OAZ_NOISE_F32 build)
     uint32_t noise_chunk = 16;           // simulations per noise ring slot (noise_chunk_for)
     uint32_t G = 0, cap = 0, pathcap = 0, hcap = 0, out_cap = 0;
     int32_t sims_cap = 0;                // cfg.sims at creation: trees and paths are sized for it
@@ -884,6 +884,7 @@ extern "C" oaz_engine* oaz_create(const oaz_config* cfg, int device) {
         cfg->step_kernels < 0 || cfg->step_kernels > 1 || cfg->world < 0 || cfg->rank < 0 ||
         cfg->rank >= (cfg->world > 0 ? cfg->world : 1) ||
         (uint64_t)cfg->games * ((uint64_t)cfg->sims + 1) >= (1ull << 32) ||  // 32-bit path offsets (k_select_seg)
+        (uint64_t)cfg->games * kNoiseStride * sizeof(noise_t) >= (1ull << 31) ||  // 32-bit noise offsets (root_noise_pairs)
         (cfg->parts != 0 && cfg->parts != 1 && cfg->parts != 2 && cfg->parts != 4)) {
         oaz_set_err(OAZ_ERR_ARG, "create: config out of range");
         return nullptr;
@@ -1368,7 +1369,7 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
             for (int h = 0; h < nh; ++h) HIP_TRY(hipStreamWaitEvent(e->stream2, e->ev_consumed[c & 1][h], 0));
         e->timing_skip = false;  // every noise launch is timed (once per chunk)
         const uint32_t s0 = c * chunk, n = sims - s0 < chunk ? sims - s0 : chunk;
-        float* buf = e->noise + (c & 1) * slot_elems;
+        noise_t* buf = e->noise + (c & 1) * slot_elems;
         if (int rc = timed(e, 4, t.G * n, [&] {
                 return launch_root_noise(roots, active, gids, plies, prm, t.G, s0, n, buf, e->stream2);
             }, e->stream2))
@@ -1425,7 +1426,7 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
         if (grp) {  // the chunk's simulations in one launch
             const NNView w = nn_view(e, nullptr);
             e->timing_skip = false;
-            const float* nz = noise ? e->noise + (c & 1) * slot_elems : nullptr;
+            const noise_t* nz = noise ? e->noise + (c & 1) * slot_elems : nullptr;
             if (int rc = timed(e, 6, t.G * (s1 - s0), [&] {
                     return launch_search_grp(tv[0], roots, active, prm, (int)s0, (int)s1, nz, hash ? nullptr : &w,
                                              e->policy, e->value, dl, sr, sh[0]);
@@ -1458,7 +1459,7 @@ static int run_sims_body(oaz_engine* e, const TreeView& t, const oaz_state* root
                 const uint8_t* ah = active ? active + go : nullptr;  // null in search mode
                 float* pol = e->policy + go * 50;
                 float* val = e->value + go;
-                const float* nz = noise ? e->noise + (c & 1) * slot_elems + ((size_t)(s - s0) * t.G + go) * kNoiseStride
+                const noise_t* nz = noise ? e->noise + (c & 1) * slot_elems + ((size_t)(s - s0) * t.G + go) * kNoiseStride
                                         : nullptr;
                 if (s == 0) {
                     if (int rc = timed(e, 0, th.G, [&] { return launch_select(th, rh, ah, nz, prm, st); }, st))

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/onitama_az.h"
+#include "oaz_device.h"  // noise_t
 
 namespace oaz {
 
@@ -122,17 +123,17 @@ size_t nn_packed_floats(int blocks, int precision);
 
 // MCTS
 hipError_t launch_tree_reset(const TreeView& t, hipStream_t st);
-constexpr int kNoiseStride = 2 * OAZ_MAX_MOVES;  // doubles per (sim, game) in the noise buffer
+constexpr int kNoiseStride = 2 * OAZ_MAX_MOVES;  // noise_t draws per (sim, game) in the noise ring
 hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
-                         const float* noise /* [G][kNoiseStride] or null */, SearchParams p, hipStream_t st);
+                         const noise_t* noise /* [G][kNoiseStride] or null */, SearchParams p, hipStream_t st);
 hipError_t launch_root_noise(const oaz_state* roots, const uint8_t* active, const uint64_t* game_id,
                              const uint32_t* ply, SearchParams p, uint32_t G, uint32_t sim0, uint32_t nsims,
-                             float* out /* [nsims][G][kNoiseStride] */, hipStream_t st);
+                             noise_t* out /* [nsims][G][kNoiseStride] */, hipStream_t st);
 hipError_t launch_expand_backup(const TreeView& t, const oaz_state* roots, const uint8_t* active,
                                 const float* policy, const float* value, hipStream_t st);
 // expand/backup of simulation s, then select of simulation s+1 (noise: its root noise), fused
 hipError_t launch_backup_select(const TreeView& t, const oaz_state* roots, const uint8_t* active, const float* policy,
-                                const float* value, const float* noise, SearchParams p, hipStream_t st);
+                                const float* value, const noise_t* noise, SearchParams p, hipStream_t st);
 hipError_t launch_search_finalize(const TreeView& t, const oaz_state* roots, oaz_move* out_move,
                                   float* out_pi, hipStream_t st);
 // false when OAZ_TREE_SEG=0 selected the one-game-per-wave tree kernels
@@ -149,7 +150,7 @@ hipError_t launch_search_lat(const TreeView& t, const oaz_state* roots, const ui
 // last simulation's expand / backup is the caller's (launch_expand_backup). deadline / sims_run as above, per
 // 16-game group; a group that stopped in an earlier chunk exits at once (sims_run must start at 0).
 hipError_t launch_search_grp(const TreeView& t, const oaz_state* roots, const uint8_t* active, SearchParams p, int s0,
-                             int s1, const float* noise, const NNView* w, float* policy, float* value,
+                             int s1, const noise_t* noise, const NNView* w, float* policy, float* value,
                              const uint64_t* deadline, uint32_t* sims_run, hipStream_t st);
 // *deadline = the device clock (wall_clock64, hipDeviceAttributeWallClockRate) when the kernel runs + ticks
 hipError_t launch_deadline_start(uint64_t* deadline, uint64_t ticks, hipStream_t st);

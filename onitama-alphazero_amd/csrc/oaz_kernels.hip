@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(kBlock) k_root_noise(const oaz_state* __restri
                                                        const uint8_t* __restrict__ active,
                                                        const uint64_t* __restrict__ game_ids,
                                                        const uint32_t* __restrict__ plies, SearchParams prm,
-                                                       uint32_t G, uint32_t sim0, uint32_t nsims, float* out) {
+                                                       uint32_t G, uint32_t sim0, uint32_t nsims, noise_t* out) {
     const uint32_t g = wave_game();
     if (g >= G) return;
     if (active && active[g] != 1) return;
@@ -280,7 +280,7 @@ __global__ void __launch_bounds__(kBlock) k_root_noise(const oaz_state* __restri
         const int k = idx / per_sim, r = idx - k * per_sim;
         const uint32_t d = 2u + (uint32_t)r;  // draw index 2j + which, j = 1 + r/2
         const uint32_t c2 = (ply << 16) | ((sim0 + k) & 0xFFFFu);
-        out[((size_t)k * G + g) * kNoiseStride + d] = root_noise(prm.seed, gid, c2, d, (float)prm.alpha, K);
+        out[((size_t)k * G + g) * kNoiseStride + d] = root_noise(prm.seed, gid, c2, d, prm.alpha, K);
     }
 }
 
@@ -329,7 +329,7 @@ __global__ void __launch_bounds__(kBlock) k_tree_reset(TreeView t) {
 // not terminal; replay each chosen move; mark children whose move wins as terminal.
 __global__ void __launch_bounds__(kBlock) k_select(TreeView t, const oaz_state* __restrict__ roots,
                                                    const uint8_t* __restrict__ active,
-                                                   const float* __restrict__ noise,
+                                                   const noise_t* __restrict__ noise,
                                                    SearchParams prm) {
     const uint32_t g = wave_game();
     if (g >= t.G) return;
@@ -588,7 +588,8 @@ __device__ __forceinline__ double bcast_f64(double v) {
 struct FoldCh {
     double q, base, sq, nae, kub;
 };
-__device__ __forceinline__ FoldCh fold_chunk(const NodeRegs& ch, float na, float nb, double sqn, const SearchParams& prm) {
+__device__ __forceinline__ FoldCh fold_chunk(const NodeRegs& ch, noise_t na, noise_t nb, double sqn,
+                                             const SearchParams& prm) {
     FoldCh f;
     f.q = ch.N ? ch.W / (double)ch.N : 0.0;
     f.sq = sqn / (double)(ch.N + 1);
@@ -603,7 +604,7 @@ __device__ __forceinline__ FoldCh fold_chunk(const NodeRegs& ch, float na, float
 // reaches it (j = 16, 32), so only one chunk's are live at a time.
 template <int J>
 __device__ __forceinline__ void fold_step(int& acc, double& qa, double& ba, double& sa, int K, FoldCh& f,
-                                          const NodeRegs (&ch)[3], const float (&na)[3], const float (&nb)[3],
+                                          const NodeRegs (&ch)[3], const noise_t (&na)[3], const noise_t (&nb)[3],
                                           double sqn, const SearchParams& prm) {
     constexpr int c = J >> 4, n = J & 15;
     if constexpr (n == 0) f = fold_chunk(ch[c], na[c], nb[c], sqn, prm);
@@ -618,8 +619,8 @@ __device__ __forceinline__ void fold_step(int& acc, double& qa, double& ba, doub
     }
 }
 template <int... I>
-__device__ __forceinline__ int root_fold(int K, int Kmax, const NodeRegs (&ch)[3], const float (&na)[3],
-                                         const float (&nb)[3], double sqn, const SearchParams& prm,
+__device__ __forceinline__ int root_fold(int K, int Kmax, const NodeRegs (&ch)[3], const noise_t (&na)[3],
+                                         const noise_t (&nb)[3], double sqn, const SearchParams& prm,
                                          std::integer_sequence<int, I...>) {
     FoldCh f = fold_chunk(ch[0], na[0], nb[0], sqn, prm);
     int acc = 0;
@@ -712,22 +713,30 @@ __device__ __forceinline__ uint32_t lead_max(uint32_t v, uint64_t m) {
 
 // The root's noise draw pairs (operand a, operand b) of this lane's children j = 16c + sl, 1 <= j < K:
 // buffer loads whose lanes past K (or idle) get an offset past the resource's range, which returns 0
-// without a memory access (the noise ring holds 80 floats per game and simulation, most of them past a
+// without a memory access (the noise ring holds 80 draws per game and simulation, most of them past a
 // root's K). Unconditional instructions, so all three chunks' loads are in flight together: one round
-// trip (exec-masked loads in branches get a wait each).
-__device__ __forceinline__ void root_noise_pairs(const TreeView& t, const float* noise, uint32_t g, bool go, int K,
-                                                 float (&na)[3], float (&nb)[3]) {
+// trip (exec-masked loads in branches get a wait each). Byte offsets are 32-bit: G * 80 * sizeof(noise_t)
+// < 2^31 (oaz_create bounds G).
+__device__ __forceinline__ void root_noise_pairs(const TreeView& t, const noise_t* noise, uint32_t g, bool go, int K,
+                                                 noise_t (&na)[3], noise_t (&nb)[3]) {
     const int sl = seg_lane();
+    constexpr uint32_t kB = (uint32_t)sizeof(noise_t);
     const __amdgpu_buffer_rsrc_t nr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)noise, (short)0, (int)(t.G * (uint32_t)kNoiseStride * 4u), 0x00020000);
+        (void*)noise, (short)0, (int)(t.G * (uint32_t)kNoiseStride * kB), 0x00020000);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const int j = 16 * c + sl;
         const uint32_t off =
-            go && j >= 1 && j < K ? (g * (uint32_t)kNoiseStride + 2u * (uint32_t)j) * 4u : 0x80000000u;
+            go && j >= 1 && j < K ? (g * (uint32_t)kNoiseStride + 2u * (uint32_t)j) * kB : 0x80000000u;
+#if OAZ_NOISE_F32
         const auto d = __builtin_amdgcn_raw_buffer_load_b64(nr, (int)off, 0, 0);
         na[c] = __uint_as_float(d[0]);
         nb[c] = __uint_as_float(d[1]);
+#else
+        const auto d = __builtin_amdgcn_raw_buffer_load_b128(nr, (int)off, 0, 0);
+        na[c] = __builtin_bit_cast(double, ((uint64_t)d[1] << 32) | d[0]);
+        nb[c] = __builtin_bit_cast(double, ((uint64_t)d[3] << 32) | d[2]);
+#endif
     }
 }
 
@@ -737,7 +746,7 @@ __device__ __forceinline__ void root_noise_pairs(const TreeView& t, const float*
 // its 4 games, Kmax - 1 times; here every segment stages its children's fold operands (everything that
 // does not depend on the running best, computed in parallel per child as before) in LDS, and ONE wave folds
 // all 32 games at once: ~1/6 of the fold's instructions per workgroup. Structure of arrays [child][game],
-// so the folding lanes' reads are bank-conflict free. 46.3 KB: three 8-wave workgroups per CU still fit
+// so the folding lanes' reads are bank-conflict free. 51.4 KB (f64 draws): three 8-wave workgroups per CU still fit
 // (the kernels' register budget allows three).
 constexpr int kWgGames = kWavesPerBlock * 4;
 struct WgFold {
@@ -745,7 +754,7 @@ struct WgFold {
     double q[OAZ_MAX_MOVES][kWgGames];     // operand a's parts when child j is the running best
     double base[OAZ_MAX_MOVES][kWgGames];
     double sq[OAZ_MAX_MOVES][kWgGames];
-    float na[OAZ_MAX_MOVES][kWgGames];     // operand a's draw of comparison j (x eps in the fold)
+    noise_t na[OAZ_MAX_MOVES][kWgGames];   // operand a's draw of comparison j (x eps in the fold)
     int32_t K[kWgGames], best[kWgGames];
 };
 // lane = game gi of the workgroup (threadIdx.x < kWgGames): fold_step's comparisons in the same order and
@@ -775,9 +784,9 @@ __device__ __forceinline__ void wg_fold_lane(WgFold* wf, const SearchParams& prm
 // WGF (k_select_seg / k_backup_select_seg: every thread of the workgroup calls this body): the root's noise
 // fold for the workgroup's games at once in wf (WgFold), the root level peeled off the walk so that every
 // wave reaches its two barriers; otherwise each segment folds its own game (16 lanes, DPP broadcasts).
-template <class NA = NodesGlobal, bool WGF = false>
+template <class NA = NodesGlobal, bool WGF = false, bool WF_ALIASED = false>
 __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_state* __restrict__ roots,
-                                                const uint8_t* __restrict__ active, const float* __restrict__ noise,
+                                                const uint8_t* __restrict__ active, const noise_t* __restrict__ noise,
                                                 const SearchParams& prm, uint32_t g, oaz_state* leaf_lds = nullptr,
                                                 const NA& na = NA{}, WgFold* wf = nullptr) {
     const int sl = seg_lane(), sb = seg_base();
@@ -839,8 +848,11 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
             if (go && j < K) ch[c] = load_node(na.at(T, nd.first + j));
         }
         const double sqn = go ? na.sqrt_n(t, nd.N) : 0.0;
-        float nza[3], nzb[3];
+        noise_t nza[3], nzb[3];
         root_noise_pairs(t, noise, g, go, K, nza, nzb);
+        // wf overlays the expand/backup's policy rows (k_backup_select_seg): every wave is past its backup
+        // before any writes the fold operands (the operand loads above are already in flight)
+        if constexpr (WF_ALIASED) __syncthreads();
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const int j = 16 * c + sl;
@@ -884,7 +896,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
             // root with noise: the sequential Iterator::max_by fold of k_select, every segment's
             // fold state (acc, operand a) held uniformly across its 16 lanes; child j's operands
             // are broadcast within each 16-lane row by DPP row_newbcast (j compile-time)
-            float na[3], nb[3];
+            noise_t na[3], nb[3];
             root_noise_pairs(t, noise, g, go, K, na, nb);
             const int Kmax = max(max(__builtin_amdgcn_readlane(K, 0), __builtin_amdgcn_readlane(K, 16)),
                                  max(__builtin_amdgcn_readlane(K, 32), __builtin_amdgcn_readlane(K, 48)));
@@ -939,7 +951,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
 // register budget: 80 VGPRs = 6 waves/SIMD (7 waves spill and measured 10 % slower)
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OAZ_TREE_WPE)))
 k_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
-             const float* __restrict__ noise, SearchParams prm) {
+             const noise_t* __restrict__ noise, SearchParams prm) {
     __shared__ WgFold wf;
     select_seg_body<NodesGlobalRegs, OAZ_WG_FOLD>(t, roots, active, noise, prm, seg_game(), nullptr, NodesGlobalRegs{},
                                                   &wf);
@@ -1122,15 +1134,21 @@ __global__ void __launch_bounds__(kBlock) k_expand_backup_seg(TreeView t, const 
 // grid; one launch and one grid ramp per simulation step fewer.
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OAZ_TREE_WPE)))
 k_backup_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
-                    const float* __restrict__ policy, const float* __restrict__ value, const float* __restrict__ noise,
+                    const float* __restrict__ policy, const float* __restrict__ value, const noise_t* __restrict__ noise,
                     SearchParams prm) {
-    __shared__ float spol[kWavesPerBlock * 4][52];
-    __shared__ WgFold wf;
+    // the backup's policy rows and the select's fold operands share the LDS (51.5 KB: three 8-wave
+    // workgroups per CU, 6 waves per SIMD; side by side they would be 58 KB and two)
+    union BackupSelectLds {
+        float spol[kWavesPerBlock * 4][52];
+        WgFold wf;
+    };
+    __shared__ BackupSelectLds lds;
     const uint32_t g = seg_game();
-    expand_backup_seg_body(t, roots, active, policy, value, g, spol[threadIdx.x >> 4], NodesGlobalRegs{});
+    expand_backup_seg_body(t, roots, active, policy, value, g, lds.spol[threadIdx.x >> 4], NodesGlobalRegs{});
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    select_seg_body<NodesGlobalRegs, OAZ_WG_FOLD>(t, roots, active, noise, prm, g, nullptr, NodesGlobalRegs{}, &wf);
+    select_seg_body<NodesGlobalRegs, OAZ_WG_FOLD, true>(t, roots, active, noise, prm, g, nullptr, NodesGlobalRegs{},
+                                                        &lds.wf);
 }
 
 // calculate_priors (mcts_arena.rs:104-124) + best child (87-94) for every root.
@@ -1408,7 +1426,7 @@ static bool tree_seg() {
 }
 bool tree_seg_kernels() { return tree_seg(); }
 hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
-                         const float* noise, SearchParams p, hipStream_t st) {
+                         const noise_t* noise, SearchParams p, hipStream_t st) {
     if (tree_seg())
         hipLaunchKernelGGL(k_select_seg, dim3(wave_grid((t.G + 3) / 4)), dim3(kBlock), 0, st, t, roots, active, noise,
                            p);
@@ -1418,7 +1436,7 @@ hipError_t launch_select(const TreeView& t, const oaz_state* roots, const uint8_
 }
 hipError_t launch_root_noise(const oaz_state* roots, const uint8_t* active, const uint64_t* game_id,
                              const uint32_t* ply, SearchParams p, uint32_t G, uint32_t sim0, uint32_t nsims,
-                             float* out, hipStream_t st) {
+                             noise_t* out, hipStream_t st) {
     hipLaunchKernelGGL(k_root_noise, dim3(wave_grid(G)), dim3(kBlock), 0, st, roots, active, game_id, ply, p, G,
                        sim0, nsims, out);
     return hipGetLastError();
@@ -1434,7 +1452,7 @@ hipError_t launch_expand_backup(const TreeView& t, const oaz_state* roots, const
     return hipGetLastError();
 }
 hipError_t launch_backup_select(const TreeView& t, const oaz_state* roots, const uint8_t* active, const float* policy,
-                                const float* value, const float* noise, SearchParams p, hipStream_t st) {
+                                const float* value, const noise_t* noise, SearchParams p, hipStream_t st) {
     if (!tree_seg()) {  // the one-game-per-wave kernels, one after the other
         if (hipError_t err = launch_expand_backup(t, roots, active, policy, value, st)) return err;
         return launch_select(t, roots, active, noise, p, st);

@@ -404,7 +404,7 @@ __device__ __noinline__ void grp_backup(const TreeView& t, const oaz_state* root
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 __device__ __noinline__ void grp_select(const TreeView& t, const oaz_state* roots, const uint8_t* active,
-                                        const float* noise, const SearchParams& prm, uint32_t gs) {
+                                        const noise_t* noise, const SearchParams& prm, uint32_t gs) {
     select_seg_body(t, roots, active, noise, prm, gs, nullptr, NodesGlobalRegs{});
 }
 
@@ -415,7 +415,7 @@ __device__ __noinline__ void grp_select(const TreeView& t, const oaz_state* root
 template <class C, int DBG = 0>
 __global__ void __launch_bounds__(kLatThreads) k_search_grp(TreeView t, const oaz_state* __restrict__ roots,
                                                             const uint8_t* __restrict__ active, SearchParams prm,
-                                                            int s0, int s1, const float* __restrict__ noise,
+                                                            int s0, int s1, const noise_t* __restrict__ noise,
                                                             int hash_eval, const float* __restrict__ blob, int blocks,
                                                             const float* __restrict__ xblob,
                                                             unsigned long long* __restrict__ fallback, float* policy,
@@ -501,7 +501,7 @@ __global__ void __launch_bounds__(kLatThreads) k_search_grp(TreeView t, const oa
 }
 
 hipError_t launch_search_grp(const TreeView& t, const oaz_state* roots, const uint8_t* active, SearchParams p, int s0,
-                             int s1, const float* noise, const NNView* w, float* policy, float* value,
+                             int s1, const noise_t* noise, const NNView* w, float* policy, float* value,
                              const uint64_t* deadline, uint32_t* sims_run, hipStream_t st) {
     if (deadline && !sims_run) return hipErrorInvalidValue;
     if (t.G == 0 || s1 <= s0) return hipSuccess;

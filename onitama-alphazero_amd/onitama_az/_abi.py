@@ -22,7 +22,7 @@ FP32, BF16, FP32_SPLIT, FP32_SPLIT16 = 0, 1, 2, 3  # OAZ_FP32 / OAZ_BF16 / OAZ_F
 ERR_RANGE = -7  # OAZ_ERR_RANGE (ABI 1 only; ABI 2 recomputes fp16-range tiles, oaz_nn_fallbacks)
 ERR_CAPACITY = -4
 ERR_COMM = -8
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_MOVES = 40
 
 
@@ -226,7 +226,7 @@ _PROTOS = {
     "oaz_initial_state": (None, [_VOIDP, _VOIDP]),
     "oaz_slot_game_ids": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint64, _VOIDP]),
     "oaz_hash_eval": (None, [_VOIDP, _VOIDP, _VOIDP]),
-    "oaz_root_noise": (C.c_float, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double, C.c_int]),
+    "oaz_root_noise": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double, C.c_int]),
     "oaz_movegen": (C.c_int, [_VOIDP, C.c_int, _VOIDP, _VOIDP, _VOIDP]),
     "oaz_step": (C.c_int, [_VOIDP, _VOIDP, C.c_int, _VOIDP]),
     "oaz_current_state": (C.c_int, [_VOIDP, C.c_int, _VOIDP]),

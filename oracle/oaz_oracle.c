@@ -488,63 +488,92 @@ static inline int64_t tkey(double x) {
 }
 
 /* --- Dirichlet root noise (mcts_arena.rs:186-203). Each PUCT evaluation at the root draws
- * a fresh Dirichlet(alpha; K) vector and uses component child.idx-1, i.e. a
+ * a fresh Dirichlet(alpha; K) vector (f64) and uses component child.idx-1, i.e. a
  * Beta(alpha, (K-1)alpha) variate X/(X+Y) from two gamma variates (rand_distr 0.4.3 Gamma:
  * Marsaglia-Tsang, small-shape boost u^(1/shape)). The reference's thread_rng is unseedable, so
- * noise parity is distributional; this restates the engine's f32 log-domain formulation
- * (oaz_device.h root_noise) op for op so that the engine's draws can be checked bit for bit:
- * the same Beta marginal by Johnk's method, with polynomial log/exp (+, -, *, / and bit
- * operations only; built with -ffp-contract=off). */
+ * noise parity is distributional; this restates the engine's f64 log-domain formulation
+ * (oaz_device.h root_noise_f64) op for op so that the engine's draws can be checked bit for bit:
+ * the same Beta marginal by Johnk's method, with polynomial log/exp (+, -, *, /, explicit fma and
+ * bit operations only; built with -ffp-contract=off). */
 typedef struct {
     uint64_t seed, game;
     uint32_t c2;
 } noise_key;
 
-static float f_from_u(uint32_t b) { float f; memcpy(&f, &b, 4); return f; }
-static uint32_t u_from_f(float f) { uint32_t b; memcpy(&b, &f, 4); return b; }
+static double d_from_u(uint64_t b) { double d; memcpy(&d, &b, 8); return d; }
+static uint64_t u_from_d(double d) { uint64_t b; memcpy(&b, &d, 8); return b; }
 
-static float nz_u(uint32_t x) { return (float)(((x >> 9) << 1) | 1u) * (1.0f / 16777216.0f); }
-
-static float nz_log(float x) {
-    uint32_t b = u_from_f(x);
-    int e = (int)((b >> 23) & 0xFF) - 127;
-    float m = f_from_u((b & 0x007FFFFFu) | 0x3F800000u);
-    if (m > 1.41421356f) {
-        m = m * 0.5f;
-        e += 1;
-    }
-    const float t = (m - 1.0f) / (m + 1.0f), t2 = t * t;
-    const float p = t * (2.0f + t2 * (0.666666667f + t2 * (0.4f + t2 * (0.285714286f + t2 * 0.222222222f))));
-    return (float)e * 0.693147182f + p;
+/* 53-bit uniform in (0, 1) from two Philox words (oaz_device.h u01) */
+static double nz_u01(uint32_t a, uint32_t b) {
+    const uint64_t m = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+    return ((double)m + 0.5) * (1.0 / 9007199254740992.0);
 }
 
-static float nz_exp(float x) {
-    if (x < -87.0f) return 0.0f;
-    if (x > 88.0f) return f_from_u(0x7F800000u);
-    const float k = (float)(int)(x * 1.44269504f + (x >= 0.0f ? 0.5f : -0.5f));
-    const float r = (x - k * 0.693145752f) - k * 1.42860677e-6f;
-    const float q = 1.0f + r * (1.0f + r * (0.5f + r * (0.166666667f + r * (0.0416666667f + r * (0.00833333333f +
-                                                                                        r * 0.00138888889f)))));
-    return q * f_from_u((uint32_t)((int)k + 127) << 23);
+static const double kLn2Hi = 6.93147180369123816490e-01, kLn2Lo = 1.90821492927058770002e-10;
+
+/* log x for normal x > 0: x = 2^e m, m in [sqrt(1/2), sqrt(2)), 2 atanh((m-1)/(m+1)) to t^21 */
+static double nz_log64(double x) {
+    const uint64_t b = u_from_d(x);
+    int e = (int)((b >> 52) & 0x7FF) - 1023;
+    double m = d_from_u((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    if (m > 1.4142135623730951) {
+        m = m * 0.5;
+        e += 1;
+    }
+    const double t = (m - 1.0) / (m + 1.0), t2 = t * t;
+    double p = 2.0 / 21.0;
+    p = fma(p, t2, 2.0 / 19.0);
+    p = fma(p, t2, 2.0 / 17.0);
+    p = fma(p, t2, 2.0 / 15.0);
+    p = fma(p, t2, 2.0 / 13.0);
+    p = fma(p, t2, 2.0 / 11.0);
+    p = fma(p, t2, 2.0 / 9.0);
+    p = fma(p, t2, 2.0 / 7.0);
+    p = fma(p, t2, 2.0 / 5.0);
+    p = fma(p, t2, 2.0 / 3.0);
+    p = fma(p * t2, t, 2.0 * t);
+    const double de = (double)e;
+    return fma(de, kLn2Hi, fma(de, kLn2Lo, p));
+}
+
+/* e^x: x = k ln2 + r, Taylor to r^13; 0 below -708, +inf above 709 */
+static double nz_exp64(double x) {
+    if (x < -708.0) return 0.0;
+    if (x > 709.0) return d_from_u(0x7FF0000000000000ull);
+    const double k = (double)(int)(x * 1.4426950408889634 + (x >= 0.0 ? 0.5 : -0.5));
+    const double r = (x - k * kLn2Hi) - k * kLn2Lo;
+    double q = 1.0 / 6227020800.0;
+    q = fma(q, r, 1.0 / 479001600.0);
+    q = fma(q, r, 1.0 / 39916800.0);
+    q = fma(q, r, 1.0 / 3628800.0);
+    q = fma(q, r, 1.0 / 362880.0);
+    q = fma(q, r, 1.0 / 40320.0);
+    q = fma(q, r, 1.0 / 5040.0);
+    q = fma(q, r, 1.0 / 720.0);
+    q = fma(q, r, 1.0 / 120.0);
+    q = fma(q, r, 1.0 / 24.0);
+    q = fma(q, r, 1.0 / 6.0);
+    q = fma(q, r, 0.5);
+    q = fma(q, r, 1.0);
+    q = fma(q, r, 1.0);
+    return q * d_from_u((uint64_t)((int64_t)k + 1023) << 52);
 }
 
 /* Beta(a, b), a = alpha, b = (K-1) alpha, by Johnk's method (exact): X = U^(1/a), Y = V^(1/b),
- * accept X + Y <= 1, eta = X / (X + Y); in the log domain with products by the rounded
- * reciprocals; attempt t uses Philox block (game lo, game hi, c2, idx << 12 | t), words 0, 1 then
- * 2, 3 (oaz_device.h root_noise, op for op). */
+ * accept X + Y <= 1, eta = X / (X + Y) (when X or Y is below e^-708: 1 / (1 + exp(ly - lx))); in the
+ * log domain with products by the rounded reciprocals; attempt t uses Philox block (game lo, game hi, c2,
+ * idx << 12 | t): U from words 0, 1, V from words 2, 3 (oaz_device.h root_noise_f64, op for op). */
 static double beta_noise(const noise_key* k, uint32_t idx, double alpha, int nchild) {
-    const float a = (float)alpha;
-    const float ia = 1.0f / a, ib = 1.0f / (a * (float)(nchild - 1));
-    for (uint32_t t = 0; t < 1024u; t++) {
+    const double ia = 1.0 / alpha, ib = 1.0 / (alpha * (double)(nchild - 1));
+    for (uint32_t t = 0; t < 2048u; t++) {
         uint32_t r[4];
         const uint32_t ctr[4] = {(uint32_t)k->game, (uint32_t)(k->game >> 32), k->c2, (idx << 12) | t};
         orc_philox(k->seed, ctr, r);
-        const float lx = nz_log(nz_u(r[0])) * ia, ly = nz_log(nz_u(r[1])) * ib;
-        if (nz_exp(lx) + nz_exp(ly) <= 1.0f) return (double)(1.0f / (1.0f + nz_exp(ly - lx)));
-        const float lx2 = nz_log(nz_u(r[2])) * ia, ly2 = nz_log(nz_u(r[3])) * ib;
-        if (nz_exp(lx2) + nz_exp(ly2) <= 1.0f) return (double)(1.0f / (1.0f + nz_exp(ly2 - lx2)));
+        const double lx = nz_log64(nz_u01(r[0], r[1])) * ia, ly = nz_log64(nz_u01(r[2], r[3])) * ib;
+        const double x = nz_exp64(lx), y = nz_exp64(ly), sum = x + y;
+        if (sum <= 1.0) return (x > 0.0 && y > 0.0) ? x / sum : 1.0 / (1.0 + nz_exp64(ly - lx));
     }
-    return (double)(1.0f / (float)nchild);
+    return 1.0 / (double)nchild;
 }
 
 double orc_root_noise(uint64_t seed, uint64_t game_id, uint32_t c2, uint32_t draw, double alpha, int nchild) {

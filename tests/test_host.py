@@ -30,7 +30,7 @@ def test_header_functions_exported(lib):
 
 
 def test_abi_version_and_structs(lib):
-    assert lib.oaz_abi_version() == _abi.ABI_VERSION == 4
+    assert lib.oaz_abi_version() == _abi.ABI_VERSION == 5
     assert C.sizeof(_abi.oaz_config) == 120 and _abi.oaz_config.search_time_ns.offset == 104
     assert C.sizeof(_abi.oaz_comm_stats) == 56
 
@@ -280,8 +280,8 @@ def test_display_kat(kats):  # state.rs:397-417 (State::display is host-side for
 
 
 def test_root_noise_host_matches_oracle_and_distribution():
-    """The engine's root-noise draw (f32 log-domain Beta(alpha, (K-1) alpha), the marginal of the
-    reference's per-comparison Dirichlet sample, mcts_arena.rs:186-203) equals the oracle's
+    """The engine's root-noise draw (f64 log-domain Beta(alpha, (K-1) alpha), the marginal of the
+    reference's per-comparison f64 Dirichlet sample, mcts_arena.rs:186-203) equals the oracle's
     restatement bit for bit, and its sample mean is 1/K (Beta(a, b) mean a / (a + b))."""
     import oracle_ffi as orc
     lib = _abi.load()
@@ -292,7 +292,7 @@ def test_root_noise_host_matches_oracle_and_distribution():
         ply, sim, draw, K = int(rng.integers(0, 152)), int(rng.integers(0, 800)), int(rng.integers(2, 80)), int(rng.integers(2, 41))
         a = lib.oaz_root_noise(seed, gid, ply, sim, draw, 0.03, K)
         b = olib.orc_root_noise(seed, gid, (ply << 16) | sim, draw, 0.03, K)
-        assert np.float32(a) == np.float32(b)
+        assert a == b  # the same f64 value (exact double equality)
         assert 0.0 <= a <= 1.0
     for K in (2, 12, 40):
         xs = np.array([lib.oaz_root_noise(7, g, 0, s, 3, 0.03, K) for g in range(40) for s in range(100)])
@@ -304,37 +304,42 @@ def test_root_noise_host_matches_oracle_and_distribution():
 
 def test_root_noise_distribution_ks():
     """The root-noise draw against its target law, Beta(alpha, (K - 1) alpha) — the marginal of one
-    component of the reference's Dirichlet(alpha; K) sample (rand_distr 0.4.3, mcts_arena.rs:190-203)
+    component of the reference's f64 Dirichlet(alpha; K) sample (rand_distr 0.4.3, mcts_arena.rs:190-203)
     — with 2 * 10^5 host draws per K (bit-identical to the device's, test above and the noise-on tree
-    tests): a Kolmogorov-Smirnov distance and the mass at quantiles 1 % ... 99 %.
-    An f32 draw cannot resolve the law's two ends at alpha = 0.03: below ~6e-39 (e^-88, where the
-    sampler's exp(ly - lx) overflows) the draw is 0, and within ~6e-8 of 1 (f32's spacing there) it
-    is 1.0 — at K = 2 that is 4 % and 30 % of the mass. Each end's mass is compared as a whole
-    (P(X <= x0), P(X >= x1) against their binomial spread), and the KS sup runs over x0 < x < x1
-    (a sup over a subset: the full-sample Kolmogorov null is conservative for it)."""
+    tests): a Kolmogorov-Smirnov distance and the mass at quantiles 1 % ... 99 % and in the tails.
+    The draw is f64, so the law is resolved to within f64's spacing of 1: a draw is 1.0 exactly only
+    when 1 - eta < 2^-53 (Y / X below f64's epsilon, where the reference's X / (X + Y) in f64 is 1.0 as
+    well: ~16 % of the mass at K = 2; the previous f32 draw collapsed everything within 6e-8 of 1, 30 %).
+    The masses between 1 - 1e-7 and 1 - 1e-15, which an f32 draw cannot resolve, are compared one decade
+    at a time, the mass at exactly 1.0 as a whole, and the KS sup runs over x < 1 - 2^-52 (a sup over a
+    subset: the full-sample Kolmogorov null is conservative for it). Below 1e-300 the mass is < 1e-9."""
     from scipy import stats
     lib = _abi.load()
-    x0, x1, n = 1e-37, 1.0 - 1e-6, 200_000
+    x1, n = 1.0 - 2.0 ** -52, 200_000
     for K in (2, 14, 40):
-        law = stats.beta(0.03, 0.03 * (K - 1))
+        a, b = 0.03, 0.03 * (K - 1)
+        law, flip = stats.beta(a, b), stats.beta(b, a)  # flip: 1 - eta, for the tail near 1
         xs = np.sort(np.array([lib.oaz_root_noise(11, g, 0, s, 5, 0.03, K) for g in range(2000) for s in range(100)]))
-        f0, m0 = law.cdf(x0), float(np.mean(xs <= x0))  # the two ends, as masses
-        f1, m1 = law.sf(x1), float(np.mean(xs >= x1))
-        assert abs(m0 - f0) < 5 * np.sqrt(f0 * (1 - f0) / n), (K, m0, f0)
+        assert xs.dtype == np.float64 and xs.min() >= 0.0 and xs.max() <= 1.0
+        assert np.mean(xs <= 1e-300) < 1e-4
+        f1, m1 = flip.cdf(1.0 - x1), float(np.mean(xs >= x1))  # the draws that are 1.0 (or 1 - 2^-53)
         assert abs(m1 - f1) < 5 * np.sqrt(max(f1 * (1 - f1), 1.0 / n) / n), (K, m1, f1)
-        mid = xs[(xs > x0) & (xs < x1)]  # KS distance over x0 < x < x1
+        for lo, hi in ((1e-15, 1e-13), (1e-13, 1e-11), (1e-11, 1e-9), (1e-9, 1e-7)):  # 1 - eta in [lo, hi)
+            p = flip.cdf(hi) - flip.cdf(lo)
+            m = float(np.mean((1.0 - xs >= lo) & (1.0 - xs < hi)))
+            assert abs(m - p) < 5 * np.sqrt(max(p * (1 - p), 1.0 / n) / n), (K, lo, hi, m, p)
+        mid = xs[xs < x1]  # KS distance over x < 1 - 2^-52
         lo = np.searchsorted(xs, mid, side="left") / n  # ECDF just below each value
         hi = np.searchsorted(xs, mid, side="right") / n  # ECDF at each value
         F = law.cdf(mid)
         d = float(max(np.max(hi - F), np.max(F - lo)))
         p = float(stats.kstwo(n).sf(d))
-        print(f"K={K}: mass <= 1e-37 {m0:.4f} (law {f0:.4f}), >= 1-1e-6 {m1:.4f} (law {f1:.4f}); "
-              f"KS D={d:.5f} p={p:.3f}")
+        print(f"K={K}: mass at 1.0 {m1:.4f} (law {f1:.4f}); KS D={d:.5f} p={p:.3f}")
         assert p > 1e-3, (K, d, p)
         for q in (0.01, 0.05, 0.25, 0.5, 0.75, 0.95, 0.99):
             xq = law.ppf(q)
-            if not x0 < xq < x1:
-                continue  # inside an end's mass, checked above
+            if not xq < x1:
+                continue  # inside the mass at 1.0, checked above
             frac = float(np.mean(xs <= xq))
             assert abs(frac - q) < 5 * np.sqrt(q * (1 - q) / n), (K, q, frac)
 
