@@ -799,7 +799,10 @@ def arena_main(args, world, rank, local):
     opts = Options(precision=_abi.FP32_SPLIT16, device=local)
     net = ConvResNetConfig(resnet_block_amnt=3)
     new, best = ConvResNet(net, opts, seed=0), ConvResNet(net, opts, seed=1)
-    cfg = AlphaZeroMctsConfig(search_time=0.4, exploration_c=5.0, max_playouts=sims, train=False)
+    # exactly `sims` playouts per move (a 131 072-game batch would pass the reference's 400 ms per-agent budget,
+    # which is a per-game clock in the reference, as one batch clock)
+    cfg = AlphaZeroMctsConfig(search_time=0.4, exploration_c=5.0, max_playouts=sims, train=False,
+                              enforce_search_time=False)
     agent, opponent = AlphaZeroAgent(cfg, new), AlphaZeroAgent(cfg, best)
     fight(EvaluatorConfig(game_amnt=n, max_plies=1, seed=20260101 + rank), agent, opponent)  # warm-up: 3 plies
     if world > 1:

@@ -20,15 +20,17 @@ from .weights import ot_blob, random_weights
 
 @dataclass
 class AlphaZeroMctsConfig:  # alphazero_mcts/mod.rs:26-43
-    search_time: float = 0.4          # seconds; honoured only with enforce_search_time (Q7)
+    search_time: float = 0.4          # seconds (Q7)
     exploration_c: float = math.sqrt(2.0)
     max_playouts: int = 5000
     train: bool = False
-    # Q7: False (default, the parity mode) runs exactly max_playouts playouts per search; True stops each
-    # game's search at the first playout that ends past search_time, as the reference's loop
-    # `while playouts < max_playouts && elapsed < search_time` (mcts_arena.rs:78) does (on the device
-    # clock inside the one-launch search; a batch of more than 16 x CU-count games stops together)
-    enforce_search_time: bool = False
+    # Q7: True (default, the reference's semantics) stops each game's search at the first playout that ends
+    # past search_time, as the reference's loop `while playouts < max_playouts && elapsed < search_time`
+    # (mcts_arena.rs:78) does: on the device clock inside the one-launch searches (every game, or 16-game
+    # group, on its own clock read); a batch of more than 16 x CU-count games stops together after the
+    # simulation step that passes the budget. False runs exactly max_playouts playouts per search (the
+    # parity and throughput mode: bench.py's arena line, the engine-level self-play)
+    enforce_search_time: bool = True
 
 
 def reward(move_result: MoveResult, reward_color: PlayerColor) -> float:  # mod.rs:45-53

@@ -719,17 +719,18 @@ def test_search_time_budget_groups_stop_independently(orc):
 
 
 def test_search_time_through_agent_config():
-    """AlphaZeroMctsConfig.enforce_search_time applies search_time to the engine; without it the
-    search runs max_playouts exactly (Q7 default)."""
+    """AlphaZeroMctsConfig applies search_time to the engine by default, as the reference always does
+    (mcts_arena.rs:78); with enforce_search_time=False the search runs max_playouts exactly."""
     from onitama_az.mcts import AlphaZeroMcts, AlphaZeroMctsConfig, ConvResNet, ConvResNetConfig
     model = ConvResNet(ConvResNetConfig(resnet_block_amnt=3), seed=0)
     gs = GameState.with_deck(Deck([ORIGINAL_CARDS[i] for i in range(5)]))
-    timed = AlphaZeroMcts(AlphaZeroMctsConfig(search_time=0.02, exploration_c=5.0, max_playouts=20000,
-                                              enforce_search_time=True), model)
+    assert AlphaZeroMctsConfig().enforce_search_time  # the reference's semantics by default
+    timed = AlphaZeroMcts(AlphaZeroMctsConfig(search_time=0.02, exploration_c=5.0, max_playouts=20000), model)
     mv, _ = timed.generate_move(gs)
     eng = model.__dict__["_search"]["engine"]
     assert 1 <= eng.last_sims() < 20000
     assert (mv.used_card_idx, mv.mov) in gs.state.generate_all_legal_moves(gs.curr_player_color)
-    plain = AlphaZeroMcts(AlphaZeroMctsConfig(search_time=0.02, exploration_c=5.0, max_playouts=300), model)
+    plain = AlphaZeroMcts(AlphaZeroMctsConfig(search_time=0.02, exploration_c=5.0, max_playouts=300,
+                                              enforce_search_time=False), model)
     plain.generate_move(gs)
     assert eng.last_sims() == 300

@@ -139,7 +139,7 @@ def test_agent_mirror_default_config_one_launch(orc):
     from onitama_az.game import Deck, GameState, ORIGINAL_CARDS
     from onitama_az.mcts import AlphaZeroMcts, AlphaZeroMctsConfig, ConvResNet, ConvResNetConfig
     model = ConvResNet(ConvResNetConfig(resnet_block_amnt=3), seed=3)
-    agent = AlphaZeroMcts(AlphaZeroMctsConfig(enforce_search_time=True), model)
+    agent = AlphaZeroMcts(AlphaZeroMctsConfig(), model)  # the reference default: 400 ms, 5 000 playouts, c = sqrt(2)
     gs = GameState.with_deck(Deck([ORIGINAL_CARDS[i] for i in range(5)]))
     mv, value = agent.generate_move(gs)
     eng = model.__dict__["_search"]["engine"]

@@ -89,6 +89,37 @@ def test_search_statistics_vs_oracle_fp32_network(orc, precision, move_agree, pi
     assert agree >= move_agree and l1 <= pi_l1, (agree, l1)
 
 
+@pytest.mark.timeout(300)
+def test_default_precision_search_equals_exact_fp32_on_clear_moves(orc):
+    """The default config's network arithmetic is the fp16x3 split (oaz_config_default, Options), not the
+    exact-fp32 MFMA kernel a caller gets with OAZ_FP32 (the ABI-4 behaviour change). Pinned:
+    256 roots x 200 simulations with the reference's trained 3-block network, no noise, one search with the
+    default config and one with OAZ_FP32: wherever the exact-fp32 search's most visited child leads the
+    runner-up by more than 2 % of the simulations, the default's move is the same; over all roots the
+    moves agree on >= 97 % and pi differs by <= 0.02 in mean L1 (near-ties may flip: both are fp32-level)."""
+    from conftest import random_positions
+    w = np.load(GOLDEN / "weights_3block_trained.npy", allow_pickle=False)
+    roots = random_positions(orc, 256, seed=4711)
+    sims = 200
+    cfg = _abi.default_config()
+    assert cfg.precision == _abi.FP32_SPLIT16
+    out = {}
+    for name, prec in (("default", None), ("fp32", _abi.FP32)):
+        kw = dict(games=256, sims=sims, blocks=3, c_puct=5.0, train_noise=0, evaluator=_abi.EVAL_NN)
+        if prec is not None:
+            kw["precision"] = prec
+        with Engine(**kw) as e:
+            e.load_weights(w)
+            out[name] = e.search(roots)
+    d, f = out["default"], out["fp32"]
+    pf = f.pi.reshape(-1, 50)
+    top2 = np.sort(pf, axis=1)[:, -2:]
+    clear = (top2[:, 1] - top2[:, 0]) > 0.02
+    same = np.array([d.moves[i].tobytes() == f.moves[i].tobytes() for i in range(len(roots))])
+    assert clear.sum() >= 128 and same[clear].all(), (int(clear.sum()), int((~same[clear]).sum()))
+    assert same.mean() >= 0.97 and np.abs(d.pi.reshape(-1, 50) - pf).sum(1).mean() <= 0.02
+
+
 @pytest.mark.timeout(120)
 def test_allgather_samples_c_abi_world1_equals_fetch():
     """oaz_allgather_samples at world 1 (RCCL communicator over one GPU): the gathered records are
