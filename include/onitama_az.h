@@ -522,6 +522,10 @@ size_t oaz_pure_mcts_tree_capacity(const oaz_pure_mcts_config* cfg);
  * HIP device is restored before the call returns. */
 int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pure_mcts_config* cfg, oaz_move* out_move,
                          float* out_value, oaz_pure_mcts_stats* stats, oaz_pure_node* tree_out, size_t tree_cap);
+/* A search's device buffers are one allocation (G x oaz_pure_mcts_tree_capacity nodes + ~100 B per root), and the
+ * last one of each device is kept for the next search (a 1 M-search launch's trees are 64 GB); this frees a
+ * device's kept buffer (OAZ_ERR_STATE while a search uses it). */
+int oaz_pure_mcts_release_workspace(int device);
 
 #ifdef __cplusplus
 }

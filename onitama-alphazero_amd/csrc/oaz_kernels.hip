@@ -1315,7 +1315,8 @@ __global__ void __launch_bounds__(kScanThreads) k_samples_scan(SlotView sv) {
     const uint32_t per = (sv.G + kScanThreads - 1) / kScanThreads;
     const uint32_t g0 = threadIdx.x * per, g1 = g0 + per < sv.G ? g0 + per : sv.G;
     uint64_t sum = 0;
-    for (uint32_t g = g0; g < g1; ++g) sum += sv.fin[g] & 0xFFFFFFu;
+#pragma unroll 16
+    for (uint32_t g = g0; g < g1; ++g) sum += sv.fin[g] & 0xFFFFFFu;  // (unrolled: the loads in flight together)
     __shared__ uint64_t run[kScanThreads];
     run[threadIdx.x] = sum;
     __syncthreads();
@@ -1327,6 +1328,7 @@ __global__ void __launch_bounds__(kScanThreads) k_samples_scan(SlotView sv) {
     }
     const unsigned long long base = *sv.out_count;
     uint64_t pos = base + run[threadIdx.x] - sum;
+#pragma unroll 16
     for (uint32_t g = g0; g < g1; ++g) {
         sv.fin_pos[g] = pos;
         pos += sv.fin[g] & 0xFFFFFFu;

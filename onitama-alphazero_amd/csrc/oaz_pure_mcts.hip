@@ -19,6 +19,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <mutex>
 #include <vector>
 
 #include "../../include/onitama_az.h"
@@ -253,6 +254,69 @@ extern "C" size_t oaz_pure_mcts_tree_capacity(const oaz_pure_mcts_config* c) {
     return 1 + 40 * exp;
 }
 
+// The search's device buffers as one allocation, and the last one of each device kept for the next call: a
+// 1 M-search launch's trees take 64 GB, and allocating and freeing that per call cost 0.02-1.9 s on top of a
+// 0.42 s search depending on the box (bench.py --mode pure_mcts). A call finding the kept buffer in use (a
+// concurrent search on the same device) allocates its own and frees it on return.
+// oaz_pure_mcts_release_workspace returns a device's kept buffer.
+namespace {
+struct PureWorkspace {
+    std::mutex mu;
+    void* p = nullptr;
+    size_t n = 0;
+    bool busy = false;
+};
+constexpr int kPureMaxDevices = 64;
+PureWorkspace g_pure_ws[kPureMaxDevices];
+
+// (on the calling thread's current device, which is `dev`)
+hipError_t ws_acquire(int dev, size_t bytes, void** out, bool* kept) {
+    PureWorkspace& w = g_pure_ws[dev];
+    {
+        std::lock_guard<std::mutex> lk(w.mu);
+        if (!w.busy) {
+            if (w.n < bytes) {
+                if (w.p) (void)hipFree(w.p);
+                w.p = nullptr;
+                w.n = 0;
+                if (hipError_t e = hipMalloc(&w.p, bytes)) return e;
+                w.n = bytes;
+            }
+            w.busy = true;
+            *out = w.p;
+            *kept = true;
+            return hipSuccess;
+        }
+    }
+    *kept = false;
+    return hipMalloc(out, bytes);
+}
+void ws_release(int dev, void* p, bool kept) {
+    if (!p) return;
+    if (!kept) {
+        (void)hipFree(p);
+        return;
+    }
+    std::lock_guard<std::mutex> lk(g_pure_ws[dev].mu);
+    g_pure_ws[dev].busy = false;
+}
+size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
+}  // namespace
+
+extern "C" int oaz_pure_mcts_release_workspace(int device) {
+    if (device < 0 || device >= kPureMaxDevices) return oaz_set_err(OAZ_ERR_ARG, "pure_mcts: device %d", device);
+    PureWorkspace& w = g_pure_ws[device];
+    std::lock_guard<std::mutex> lk(w.mu);
+    if (w.busy) return oaz_set_err(OAZ_ERR_STATE, "pure_mcts: the workspace of device %d is in use", device);
+    if (w.p) {
+        DeviceScope dev_scope_(device);
+        (void)hipFree(w.p);
+    }
+    w.p = nullptr;
+    w.n = 0;
+    return 0;
+}
+
 extern "C" int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pure_mcts_config* cfg,
                                     oaz_move* out_move, float* out_value, oaz_pure_mcts_stats* stats,
                                     oaz_pure_node* tree_out, size_t tree_cap) {
@@ -282,6 +346,13 @@ extern "C" int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pur
     oaz_pure_node* d_nodes = nullptr;
     oaz_move* d_mv = nullptr;
     uint64_t* d_st = nullptr;
+    void* ws = nullptr;
+    bool ws_kept = false;
+    // the workspace: roots, ln table, values, moves, statistics, trees (256-byte aligned sections)
+    const size_t o_ln = align256(sizeof(oaz_state) * G), o_val = o_ln + align256(sizeof(float) * ln.size());
+    const size_t o_mv = o_val + align256(sizeof(float) * G), o_st = o_mv + align256(sizeof(oaz_move) * G);
+    const size_t o_nodes = o_st + align256(sizeof(uint64_t) * 8 * G);
+    const size_t ws_bytes = o_nodes + sizeof(oaz_pure_node) * cap * G;
     int rc = 0;
     auto fail = [&](hipError_t e, const char* what) {
         rc = oaz_set_err(OAZ_ERR_HIP, "pure_mcts: %s: %s", what, hipGetErrorString(e));
@@ -294,12 +365,17 @@ extern "C" int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pur
     if ((e = hipGetDevice(&prev_dev)) != hipSuccess) prev_dev = -1;
     if ((e = hipSetDevice(cfg->device)) != hipSuccess) fail(e, "set device");
     else if ((e = hipStreamCreateWithFlags(&sm, hipStreamNonBlocking)) != hipSuccess) fail(e, "stream");
-    else if ((e = hipMalloc(&d_roots, sizeof(oaz_state) * G)) != hipSuccess) fail(e, "alloc");
-    else if ((e = hipMalloc(&d_ln, sizeof(float) * ln.size())) != hipSuccess) fail(e, "alloc");
-    else if ((e = hipMalloc(&d_val, sizeof(float) * G)) != hipSuccess) fail(e, "alloc");
-    else if ((e = hipMalloc(&d_mv, sizeof(oaz_move) * G)) != hipSuccess) fail(e, "alloc");
-    else if ((e = hipMalloc(&d_st, sizeof(uint64_t) * 8 * G)) != hipSuccess) fail(e, "alloc");
-    else if ((e = hipMalloc(&d_nodes, sizeof(oaz_pure_node) * cap * G)) != hipSuccess) fail(e, "alloc tree");
+    else if (cfg->device >= kPureMaxDevices) rc = oaz_set_err(OAZ_ERR_ARG, "pure_mcts: device %d unsupported", cfg->device);
+    else if ((e = ws_acquire(cfg->device, ws_bytes, &ws, &ws_kept)) != hipSuccess) fail(e, "alloc");
+    if (!rc) {
+        char* b = static_cast<char*>(ws);
+        d_roots = reinterpret_cast<oaz_state*>(b);
+        d_ln = reinterpret_cast<float*>(b + o_ln);
+        d_val = reinterpret_cast<float*>(b + o_val);
+        d_mv = reinterpret_cast<oaz_move*>(b + o_mv);
+        d_st = reinterpret_cast<uint64_t*>(b + o_st);
+        d_nodes = reinterpret_cast<oaz_pure_node*>(b + o_nodes);
+    }
     if (!rc) {
         (void)hipMemcpyAsync(d_roots, roots, sizeof(oaz_state) * G, hipMemcpyHostToDevice, sm);
         (void)hipMemcpyAsync(d_ln, ln.data(), sizeof(float) * ln.size(), hipMemcpyHostToDevice, sm);
@@ -331,12 +407,7 @@ extern "C" int oaz_pure_mcts_search(const oaz_state* roots, int G, const oaz_pur
         }
     }
     if (sm) (void)hipStreamSynchronize(sm);
-    if (d_roots) (void)hipFree(d_roots);
-    if (d_ln) (void)hipFree(d_ln);
-    if (d_val) (void)hipFree(d_val);
-    if (d_mv) (void)hipFree(d_mv);
-    if (d_st) (void)hipFree(d_st);
-    if (d_nodes) (void)hipFree(d_nodes);
+    if (ws) ws_release(cfg->device, ws, ws_kept);
     if (sm) (void)hipStreamDestroy(sm);
     if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
     return rc;

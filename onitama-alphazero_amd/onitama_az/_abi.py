@@ -273,6 +273,7 @@ _PROTOS = {
     "oaz_pure_mcts_tree_capacity": (C.c_size_t, [_P(oaz_pure_mcts_config)]),
     "oaz_pure_mcts_search": (C.c_int, [_VOIDP, C.c_int, _P(oaz_pure_mcts_config), _VOIDP, _VOIDP,
                                        _P(oaz_pure_mcts_stats), _VOIDP, C.c_size_t]),
+    "oaz_pure_mcts_release_workspace": (C.c_int, [C.c_int]),
     "oaz_train_config_default": (None, [_P(oaz_train_config)]),
     "oaz_trainer_create": (_VOIDP, [_P(oaz_train_config), C.c_int]),
     "oaz_trainer_destroy": (None, [_VOIDP]),

@@ -51,6 +51,11 @@ def pure_mcts_search(roots: np.ndarray, max_playouts: int = 5000, min_node_visit
     return PureSearchResult(moves, values, st, trees)
 
 
+def release_workspace(device: int = 0) -> None:
+    """Free the device buffer the searches on `device` keep between calls (oaz_pure_mcts_release_workspace)."""
+    _abi.check(_abi.load().oaz_pure_mcts_release_workspace(int(device)))
+
+
 @dataclass
 class Mcts:  # ai/mcts/mod.rs:13-30 (search_time is not used: searches run exactly max_playouts)
     search_time: float = 1.0

@@ -80,6 +80,43 @@ def test_gpu_trees_bitexact_vs_oracle(orc):
 
 
 @pytest.mark.gpu
+def test_gpu_workspace_kept_reused_concurrent_and_released(orc):
+    """The device workspace kept between searches (oaz_pure_mcts_release_workspace): a smaller search after a
+    larger one reuses it, threads searching at once on the same device (one of them on its own allocation)
+    and a search after the release all give the oracle's trees."""
+    import threading
+    from onitama_az.pure_mcts import pure_mcts_search, release_workspace
+    roots = random_positions(orc, 16, seed=78)
+    ref = [orc.pure_mcts(_cfg(120, 5, 1.41, 7), 500 + g, roots[g])[2] for g in range(len(roots))]
+
+    def check(r):
+        for g in range(len(roots)):
+            assert r.trees[g][: len(ref[g])].tobytes() == ref[g].tobytes(), g
+
+    big = np.concatenate([roots] * 64)  # a larger search first: the kept buffer grows to it
+    pure_mcts_search(big, 120, 5, 1.41, seed=7, game_id0=500)
+    check(pure_mcts_search(roots, 120, 5, 1.41, seed=7, game_id0=500, with_trees=True))
+    out, errs = [None] * 4, []
+
+    def run(k):
+        try:
+            out[k] = pure_mcts_search(roots, 120, 5, 1.41, seed=7, game_id0=500, with_trees=True)
+        except Exception as ex:  # noqa: BLE001
+            errs.append(ex)
+    th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for r in out:
+        check(r)
+    release_workspace(0)
+    release_workspace(0)  # nothing kept: fine
+    check(pure_mcts_search(roots, 120, 5, 1.41, seed=7, game_id0=500, with_trees=True))
+
+
+@pytest.mark.gpu
 def test_gpu_reference_tactics(kats):
     from onitama_az.pure_mcts import pure_mcts_search
     for case, (mv, c, po) in _tactics(kats):
