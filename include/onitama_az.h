@@ -271,7 +271,8 @@ double oaz_root_noise(uint64_t seed, uint64_t game_id, uint32_t ply, uint32_t si
 /* ---- rules on the GPU (bit-exact with the reference) ---------------------------- */
 /* Legal moves of s[i].to_move. masks[i][k][from] = destination mask of own piece on
  * `from` with the mover's k-th card (slot 0/1 for Red, 2/3 for Blue), 0 if no own piece.
- * moves[i][*] in reference order (slot, from, to ascending); counts[i] = #moves.
+ * moves[i][*] in reference order (slot, from, to ascending), the entries past counts[i] zero;
+ * counts[i] = #moves.
  * Any output pointer may be NULL. Host pointers. */
 int oaz_movegen(const oaz_state* s, int n, uint32_t* masks /* n*2*25 */,
                 oaz_move* moves /* n*40 */, uint8_t* counts /* n */);

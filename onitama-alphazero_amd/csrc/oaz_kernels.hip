@@ -155,6 +155,8 @@ __global__ void __launch_bounds__(kBlock) k_movegen(const oaz_state* __restrict_
             }
             ++o;
         }
+        // the entries past the count are zero (the whole output is defined, whatever the buffer held)
+        if (l < OAZ_MAX_MOVES && (uint32_t)l >= total) moves[(size_t)g * OAZ_MAX_MOVES + l] = oaz_move{0, 0, 0, 0};
     }
     if (counts && l == 0) counts[g] = (uint8_t)total;
 }

@@ -71,7 +71,41 @@ def test_movegen_bitexact_vs_oracle(orc):
         ref = orc.movegen(pos[i])
         assert counts[i] == len(ref)
         assert moves[i, : len(ref)].tobytes() == ref.tobytes()
+        assert not moves[i, len(ref):].tobytes().strip(b"\0")  # the entries past the count are zero
         assert np.array_equal(masks[i], orc.movegen_masks(pos[i]))
+
+
+def test_rules_entry_points_from_concurrent_threads(orc):
+    """oaz_movegen / oaz_step / oaz_encode from 6 threads at once, every thread with its own batch size (the
+    per-device rules context grows its scratch under its lock): each thread's results equal the serial ones."""
+    import threading
+    pos = random_positions(orc, 3000, seed=111)
+    sizes = [3000, 17, 1000, 1, 2500, 640]
+    ref = {}
+    for n in set(sizes):
+        sub = np.ascontiguousarray(pos[:n])
+        mv, ct = movegen_batch(sub)
+        ref[n] = (mv.copy(), ct.copy(), encode_batch(sub).copy())
+    errs = []
+
+    def run(n):
+        try:
+            sub = np.ascontiguousarray(pos[:n])
+            for _ in range(5):
+                mv, ct = movegen_batch(sub)
+                pl = encode_batch(sub)
+                assert np.array_equal(mv, ref[n][0]) and np.array_equal(ct, ref[n][1]), n
+                assert np.array_equal(pl, ref[n][2]), n
+                keep = ct > 0
+                step_batch(np.ascontiguousarray(sub[keep]), np.ascontiguousarray(mv[keep, 0]))
+        except Exception as ex:  # noqa: BLE001
+            errs.append(ex)
+    th = [threading.Thread(target=run, args=(n,)) for n in sizes]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
 
 
 def test_step_and_terminal_bitexact_vs_oracle(orc):
