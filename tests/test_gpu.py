@@ -500,9 +500,9 @@ def test_empty_and_single_inputs(orc):
 
 
 def test_search_root_noise_matches_oracle(orc):
-    """Noise on: both sides draw the same Philox streams and run the same f32 log-domain
-    gamma/Beta algorithm with polynomial log/exp (no libm), so the draws and the trees are
-    bit-identical."""
+    """Noise on: both sides draw the same Philox streams and run the same f64 log-domain
+    Beta algorithm (Johnk) with polynomial log/exp by explicit fused multiply-adds (no libm), so the
+    draws and the trees are bit-identical."""
     roots = random_positions(orc, 24, seed=1010)
     sims = 48
     with Engine(games=24, sims=sims, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=77) as e:
