@@ -24,7 +24,7 @@ __constant__ AttackTable c_attack = make_attack_table();
 
 constexpr int kWave = 64;
 #ifndef OAZ_TREE_WPE
-#define OAZ_TREE_WPE 6  // waves per SIMD the segmented tree kernels are register-budgeted for (80 VGPRs)
+#define OAZ_TREE_WPE 8  // waves per SIMD the segmented tree kernels are register-budgeted for (64 VGPRs)
 #endif
 #ifndef OAZ_TREE_WPB
 #define OAZ_TREE_WPB 8
@@ -719,6 +719,8 @@ __device__ __forceinline__ uint32_t lead_max(uint32_t v, uint64_t m) {
 // root's K). Unconditional instructions, so all three chunks' loads are in flight together: one round
 // trip (exec-masked loads in branches get a wait each). Byte offsets are 32-bit: G * 80 * sizeof(noise_t)
 // < 2^31 (oaz_create bounds G).
+// C0 .. C1 - 1: the chunks loaded (the workgroup fold loads chunk 2 only for its rare second pass).
+template <int C0 = 0, int C1 = 3>
 __device__ __forceinline__ void root_noise_pairs(const TreeView& t, const noise_t* noise, uint32_t g, bool go, int K,
                                                  noise_t (&na)[3], noise_t (&nb)[3]) {
     const int sl = seg_lane();
@@ -726,7 +728,7 @@ __device__ __forceinline__ void root_noise_pairs(const TreeView& t, const noise_
     const __amdgpu_buffer_rsrc_t nr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)noise, (short)0, (int)(t.G * (uint32_t)kNoiseStride * kB), 0x00020000);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
+    for (int c = C0; c < C1; ++c) {
         const int j = 16 * c + sl;
         const uint32_t off =
             go && j >= 1 && j < K ? (g * (uint32_t)kNoiseStride + 2u * (uint32_t)j) * kB : 0x80000000u;
@@ -748,37 +750,45 @@ __device__ __forceinline__ void root_noise_pairs(const TreeView& t, const noise_
 // its 4 games, Kmax - 1 times; here every segment stages its children's fold operands (everything that
 // does not depend on the running best, computed in parallel per child as before) in LDS, and ONE wave folds
 // all 32 games at once: ~1/6 of the fold's instructions per workgroup. Structure of arrays [child][game],
-// so the folding lanes' reads are bank-conflict free. 51.4 KB (f64 draws): three 8-wave workgroups per CU still fit
-// (the kernels' register budget allows three).
+// so the folding lanes' reads are bank-conflict free. The arrays hold 32 children (two 16-lane chunks):
+// a game with more (K <= 40, rare at a root) is folded in a second pass over children 32 .. K - 1 in the same
+// rows. Row 0's kub is never a fold operand (the fold starts with child 0 as the running best), so it
+// carries K in and the chosen child out. 40 KB (f64 draws): four 8-wave workgroups per CU, 8 waves per SIMD.
 constexpr int kWgGames = kWavesPerBlock * 4;
+constexpr int kFoldRows = 32;
 struct WgFold {
-    int64_t kub[OAZ_MAX_MOVES][kWgGames];  // total_key of operand b (child j with its own draw)
-    double q[OAZ_MAX_MOVES][kWgGames];     // operand a's parts when child j is the running best
-    double base[OAZ_MAX_MOVES][kWgGames];
-    double sq[OAZ_MAX_MOVES][kWgGames];
-    noise_t na[OAZ_MAX_MOVES][kWgGames];   // operand a's draw of comparison j (x eps in the fold)
-    int32_t K[kWgGames], best[kWgGames];
+    int64_t kub[kFoldRows][kWgGames];  // total_key of operand b (child j with its own draw); row 0: K, then best
+    double q[kFoldRows][kWgGames];     // operand a's parts when child j is the running best
+    double base[kFoldRows][kWgGames];
+    double sq[kFoldRows][kWgGames];
+    noise_t na[kFoldRows][kWgGames];   // operand a's draw of comparison j (x eps in the fold)
+};
+static_assert(sizeof(WgFold) <= 40960, "four workgroups' fold operands per CU");
+// The running best of a lane's fold across its passes (registers of the folding lane).
+struct FoldAcc {
+    int K, acc;
+    double qa, ba, sa;
 };
 // lane = game gi of the workgroup (threadIdx.x < kWgGames): fold_step's comparisons in the same order and
-// with the same operands and expressions, so the same best child
-__device__ __forceinline__ void wg_fold_lane(WgFold* wf, const SearchParams& prm) {
+// with the same operands and expressions, so the same best child. Pass 0 starts the fold from row 0 (child 0)
+// and compares children 1 .. min(K, 32) - 1; pass 1 compares children 32 .. K - 1 from rows 0 .. K - 33.
+__device__ __forceinline__ void wg_fold_pass(const WgFold* wf, const SearchParams& prm, FoldAcc& f, int pass) {
     const int gi = (int)threadIdx.x;
-    const int K = wf->K[gi];
-    int acc = 0;
-    double qa = wf->q[0][gi], ba = wf->base[0][gi], sa = wf->sq[0][gi];
-    for (int j = 1; __ballot(j < K) != 0; ++j) {  // uniform: until every game's K is passed
-        const double nae = (double)wf->na[j][gi] * prm.eps;
-        const int64_t kb = wf->kub[j][gi];
-        const double qj = wf->q[j][gi], bj = wf->base[j][gi], sj = wf->sq[j][gi];
-        const double ua = qa + prm.c_puct * (ba + nae) * sa;
-        if (j < K && !(total_key(ua) > kb)) {
-            acc = j;
-            qa = qj;
-            ba = bj;
-            sa = sj;
+    const int j0 = pass ? kFoldRows : 1;
+    const int jend = pass ? f.K : (f.K < kFoldRows ? f.K : kFoldRows);
+    for (int j = j0; __ballot(j < jend) != 0; ++j) {  // uniform: until every game's bound is passed
+        const int r = j - (pass ? kFoldRows : 0);
+        const double nae = (double)wf->na[r][gi] * prm.eps;
+        const int64_t kb = wf->kub[r][gi];
+        const double qj = wf->q[r][gi], bj = wf->base[r][gi], sj = wf->sq[r][gi];
+        const double ua = f.qa + prm.c_puct * (f.ba + nae) * f.sa;
+        if (j < jend && !(total_key(ua) > kb)) {
+            f.acc = j;
+            f.qa = qj;
+            f.ba = bj;
+            f.sa = sj;
         }
     }
-    wf->best[gi] = acc;
 }
 
 // g: this segment's game (>= t.G: an idle segment); leaf_lds: also store the leaf position there (LDS of
@@ -851,27 +861,51 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
         }
         const double sqn = go ? na.sqrt_n(t, nd.N) : 0.0;
         noise_t nza[3], nzb[3];
-        root_noise_pairs(t, noise, g, go, K, nza, nzb);
+        root_noise_pairs<0, 2>(t, noise, g, go, K, nza, nzb);
         // wf overlays the expand/backup's policy rows (k_backup_select_seg): every wave is past its backup
         // before any writes the fold operands (the operand loads above are already in flight)
         if constexpr (WF_ALIASED) __syncthreads();
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
+        auto stage = [&](int c, int r0) {  // chunk c's operands into rows j - r0
             const int j = 16 * c + sl;
             if (go && j < K) {
                 const FoldCh f = fold_chunk(ch[c], nza[c], nzb[c], sqn, prm);
-                wf->kub[j][gi] = __builtin_bit_cast(int64_t, f.kub);
-                wf->q[j][gi] = f.q;
-                wf->base[j][gi] = f.base;
-                wf->sq[j][gi] = f.sq;
-                wf->na[j][gi] = nza[c];
+                if (j != 0) wf->kub[j - r0][gi] = __builtin_bit_cast(int64_t, f.kub);  // (child 0's row: K)
+                wf->q[j - r0][gi] = f.q;
+                wf->base[j - r0][gi] = f.base;
+                wf->sq[j - r0][gi] = f.sq;
+                wf->na[j - r0][gi] = nza[c];
             }
+        };
+        stage(0, 0);
+        stage(1, 0);
+        if (sl == 0) wf->kub[0][gi] = go ? K : 0;
+        __syncthreads();
+        FoldAcc fa;
+        if (threadIdx.x < (unsigned)kWgGames) {
+            fa.K = (int)wf->kub[0][threadIdx.x];
+            fa.acc = 0;
+            fa.qa = wf->q[0][threadIdx.x];
+            fa.ba = wf->base[0][threadIdx.x];
+            fa.sa = wf->sq[0][threadIdx.x];
+            wg_fold_pass(wf, prm, fa, 0);
+            // whether any game has children 32 .. K - 1, for every wave: the last row (free after this
+            // pass's reads; a second pass fills rows 0 .. 7), not __syncthreads_or, whose LDS word would
+            // make the workgroup 256 B too large for four per CU
+            const bool more = __ballot(fa.K > kFoldRows) != 0;
+            if (threadIdx.x == 0) wf->kub[kFoldRows - 1][0] = more ? 1 : 0;
         }
-        if (sl == 0) wf->K[gi] = go ? K : 0;
         __syncthreads();
-        if (threadIdx.x < (unsigned)kWgGames) wg_fold_lane(wf, prm);
+        // children 32 .. K - 1 of any game: a second pass in the same rows, after the first pass's reads
+        if (wf->kub[kFoldRows - 1][0] != 0) {
+            root_noise_pairs<2, 3>(t, noise, g, go, K, nza, nzb);
+            stage(2, kFoldRows);
+            __syncthreads();
+            if (threadIdx.x < (unsigned)kWgGames) wg_fold_pass(wf, prm, fa, 1);
+            __syncthreads();
+        }
+        if (threadIdx.x < (unsigned)kWgGames) wf->kub[0][threadIdx.x] = fa.acc;
         __syncthreads();
-        descend(go ? wf->best[gi] : 0, ch);
+        descend(go ? (int)wf->kub[0][gi] : 0, ch);
     }
     while (__builtin_amdgcn_read_exec() && __ballot(go)) {  // some segment is still walking
         const int K = go ? node_nch(nd.misc) : 0;
@@ -950,7 +984,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
 #ifndef OAZ_WG_FOLD
 #define OAZ_WG_FOLD 1  // the workgroup's root noise folds on one wave (WgFold); 0: per segment (A/B build)
 #endif
-// register budget: 80 VGPRs = 6 waves/SIMD (7 waves spill and measured 10 % slower)
+// register budget: 64 VGPRs = 8 waves/SIMD, no spill (the fold operands 40 KB: four workgroups per CU)
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OAZ_TREE_WPE)))
 k_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
              const noise_t* __restrict__ noise, SearchParams prm) {
@@ -1138,8 +1172,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OAZ
 k_backup_select_seg(TreeView t, const oaz_state* __restrict__ roots, const uint8_t* __restrict__ active,
                     const float* __restrict__ policy, const float* __restrict__ value, const noise_t* __restrict__ noise,
                     SearchParams prm) {
-    // the backup's policy rows and the select's fold operands share the LDS (51.5 KB: three 8-wave
-    // workgroups per CU, 6 waves per SIMD; side by side they would be 58 KB and two)
+    // the backup's policy rows and the select's fold operands share the LDS (40 KB: four 8-wave
+    // workgroups per CU, 8 waves per SIMD; side by side they would be 47 KB and three)
     union BackupSelectLds {
         float spol[kWavesPerBlock * 4][52];
         WgFold wf;

@@ -516,6 +516,57 @@ def test_search_root_noise_matches_oracle(orc):
     assert same == 24, same
 
 
+def _wide_roots(orc, n, seed):
+    """Seeded positions whose mover has more than 32 legal moves (placed pieces, random cards): random play
+    never reached one in 1 200 positions (max 26), so these are built to reach the workgroup fold's second
+    pass (children 32 .. K - 1)."""
+    import random
+    rng = random.Random(seed)
+    base = random_positions(orc, 1, seed=1)
+    bit = lambda q: 1 << (31 - q)
+    out = []
+    while len(out) < n:
+        color = rng.randint(0, 1)
+        sq = rng.sample(range(25), 10)
+        mine, opp = sq[:5], sq[5:5 + rng.randint(1, 5)]
+        s = base.copy()
+        k, p = [0, 0], [0, 0]
+        k[color], p[color] = bit(mine[0]), sum(bit(q) for q in mine[1:])
+        k[1 - color], p[1 - color] = bit(opp[0]), sum(bit(q) for q in opp[1:])
+        s["kings"][0], s["pawns"][0] = k, p
+        s["cards"][0] = rng.sample(range(16), 5)
+        s["to_move"][0] = color
+        if len(orc.movegen(s)) > 32:
+            out.append(s)
+    return np.concatenate(out)
+
+
+@pytest.mark.parametrize("step_kernels", [0, 1])
+def test_search_root_noise_wide_roots_match_oracle(orc, step_kernels):
+    """Roots with 33-40 children and root noise: the per-step kernels' workgroup fold stages 32 children
+    per pass, so a workgroup holding such a root folds its games in two passes (workgroup 0 mixes 3 wide
+    roots with ordinary ones, workgroup 1 is all wide roots); step_kernels 0 is the one-launch search's
+    per-segment fold over three chunks. Every tree equals the oracle's node for node."""
+    roots = random_positions(orc, 64, seed=2024)
+    wide = _wide_roots(orc, 35, seed=31)
+    for slot, w in zip((3, 17, 30), wide[:3]):
+        roots[slot] = w
+    roots[32:] = wide[3:35]
+    sims = 40
+    with Engine(games=64, sims=sims, c_puct=5.0, train_noise=1, evaluator=_abi.EVAL_HASH, blocks=0, seed=91,
+                step_kernels=step_kernels) as e:
+        e.search(roots)
+        bad = []
+        for g in range(64):
+            cfg = orc.search_cfg(sims=sims, c_puct=5.0, evaluator=orc.EVAL_HASH, train_noise=1, seed=91, game_id=g, ply=0)
+            _, _, nodes, _ = orc.search(cfg, roots[g])
+            t = e.tree(g)
+            if not (len(t) == len(nodes) and t.tobytes() == nodes.tobytes()):
+                bad.append(g)
+    assert not bad, bad
+    assert all(len(orc.movegen(roots[g:g + 1])) > 32 for g in (3, 17, 30, 32, 63))
+
+
 def test_search_finds_win_in_one(kats):
     case = kats["tactics"][0]  # onitama-game/src/ai/mcts/mcts_arena.rs:459-483
     root = kat_state(case["state"], case["color"])
