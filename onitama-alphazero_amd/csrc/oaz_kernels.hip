@@ -761,7 +761,7 @@ struct WgFold {
     double q[kFoldRows][kWgGames];     // operand a's parts when child j is the running best
     double base[kFoldRows][kWgGames];
     double sq[kFoldRows][kWgGames];
-    noise_t na[kFoldRows][kWgGames];   // operand a's draw of comparison j (x eps in the fold)
+    double nae[kFoldRows][kWgGames];   // operand a's draw of comparison j x eps
 };
 static_assert(sizeof(WgFold) <= 40960, "four workgroups' fold operands per CU");
 // The running best of a lane's fold across its passes (registers of the folding lane).
@@ -772,22 +772,29 @@ struct FoldAcc {
 // lane = game gi of the workgroup (threadIdx.x < kWgGames): fold_step's comparisons in the same order and
 // with the same operands and expressions, so the same best child. Pass 0 starts the fold from row 0 (child 0)
 // and compares children 1 .. min(K, 32) - 1; pass 1 compares children 32 .. K - 1 from rows 0 .. K - 33.
+// Comparison j's operands are read one comparison ahead (the LDS latency off the sequential chain; the row
+// read past the game's last comparison is never used), child j's q / base / sq at the start of comparison j,
+// so a takeover is four selects, not a dependent read.
 __device__ __forceinline__ void wg_fold_pass(const WgFold* wf, const SearchParams& prm, FoldAcc& f, int pass) {
     const int gi = (int)threadIdx.x;
+    const int off = pass ? kFoldRows : 0;
     const int j0 = pass ? kFoldRows : 1;
     const int jend = pass ? f.K : (f.K < kFoldRows ? f.K : kFoldRows);
+    double nae = wf->nae[j0 - off][gi];
+    int64_t kb = wf->kub[j0 - off][gi];
     for (int j = j0; __ballot(j < jend) != 0; ++j) {  // uniform: until every game's bound is passed
-        const int r = j - (pass ? kFoldRows : 0);
-        const double nae = (double)wf->na[r][gi] * prm.eps;
-        const int64_t kb = wf->kub[r][gi];
-        const double qj = wf->q[r][gi], bj = wf->base[r][gi], sj = wf->sq[r][gi];
+        const int r = j - off, rn = r + 1 < kFoldRows ? r + 1 : kFoldRows - 1;
+        const double qj = wf->q[r][gi], bj = wf->base[r][gi], sj = wf->sq[r][gi];  // used after the chain
+        const double nae_n = wf->nae[rn][gi];
+        const int64_t kb_n = wf->kub[rn][gi];
         const double ua = f.qa + prm.c_puct * (f.ba + nae) * f.sa;
-        if (j < jend && !(total_key(ua) > kb)) {
-            f.acc = j;
-            f.qa = qj;
-            f.ba = bj;
-            f.sa = sj;
-        }
+        const bool take = j < jend && !(total_key(ua) > kb);
+        f.acc = take ? j : f.acc;
+        f.qa = take ? qj : f.qa;
+        f.ba = take ? bj : f.ba;
+        f.sa = take ? sj : f.sa;
+        nae = nae_n;
+        kb = kb_n;
     }
 }
 
@@ -873,7 +880,7 @@ __device__ __forceinline__ void select_seg_body(const TreeView& t, const oaz_sta
                 wf->q[j - r0][gi] = f.q;
                 wf->base[j - r0][gi] = f.base;
                 wf->sq[j - r0][gi] = f.sq;
-                wf->na[j - r0][gi] = nza[c];
+                wf->nae[j - r0][gi] = f.nae;
             }
         };
         stage(0, 0);
