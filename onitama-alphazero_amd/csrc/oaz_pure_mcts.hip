@@ -50,13 +50,15 @@ struct Rng {  // draw d of (game, playout): Philox(seed; game, playout, kTag, d 
 
 // generate_all_legal_moves order (state.rs:301-378): card slot, from square, to square.
 // Returns the number of moves; with k >= 0 also the k-th move (packed).
+// (The state's colour- and slot-indexed fields are read through selects (state_card, make_move_regs): a
+// runtime index into the struct put the whole state in scratch memory.)
 __device__ __forceinline__ int movegen_kth(const oaz_state& s, int color, const uint32_t (*att)[25], int k,
                                           uint32_t* kth) {
-    const uint32_t P = s.pawns[color], K = s.kings[color], occ = P | K;
+    const uint32_t P = color ? s.pawns[1] : s.pawns[0], K = color ? s.kings[1] : s.kings[0], occ = P | K;
     const int s0 = color ? 2 : 0;
     int n = 0;
     for (int si = 0; si < 2; ++si) {
-        const int card = s.cards[s0 + si] & 15;
+        const int card = state_card(s, s0 + si) & 15;
         uint32_t pieces = occ;
         while (pieces) {
             const int from = __clz(pieces);
@@ -71,6 +73,54 @@ __device__ __forceinline__ int movegen_kth(const oaz_state& s, int color, const 
             n += c;
         }
     }
+    return n;
+}
+
+// A rollout ply's random move (mcts_arena.rs:190-230): the same move movegen_kth(s, color, att, k) returns for
+// k = rng.below(n), n = the move count, from one pass over the mover's pieces (the masks of both cards kept in
+// registers, then k located by the two cards' counts), not a counting pass and a second search pass. Returns n
+// (0: no legal move; no draw is taken then, as before).
+__device__ __forceinline__ int rollout_pick(const oaz_state& s, int color, const uint32_t (*att)[25], Rng& rng,
+                                            uint32_t* mv) {
+    const uint32_t P = color ? s.pawns[1] : s.pawns[0], K = color ? s.kings[1] : s.kings[0], occ = P | K;
+    const int s0 = color ? 2 : 0;
+    const uint32_t (*a0)[25] = att + (state_card(s, s0) & 15), (*a1)[25] = att + (state_card(s, s0 + 1) & 15);
+    uint32_t m0[5], m1[5];
+    int fr[5];
+    int n0 = 0, n1 = 0;
+    uint32_t pieces = occ;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {  // at most 5 pieces, in square order (generate_all_legal_moves)
+        const int from = pieces ? __clz(pieces) : 0;
+        fr[i] = from;
+        m0[i] = pieces ? (*a0)[from] & ~occ : 0u;
+        m1[i] = pieces ? (*a1)[from] & ~occ : 0u;
+        n0 += __popc(m0[i]);
+        n1 += __popc(m1[i]);
+        pieces &= pieces ? ~sq_bit(from) : ~0u;
+    }
+    const int n = n0 + n1;
+    if (n == 0) return 0;
+    int k = (int)rng.below((uint32_t)n);
+    const bool second = k >= n0;
+    k -= second ? n0 : 0;
+    uint32_t map = 0;
+    int from = 0;
+    bool found = false;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t m = second ? m1[i] : m0[i];
+        const int c = __popc(m);
+        if (!found && k < c) {
+            map = m;
+            from = fr[i];
+            found = true;
+        } else if (!found) {
+            k -= c;
+        }
+    }
+    for (; k > 0; --k) map &= ~sq_bit(__clz(map));
+    *mv = pack_move(from, __clz(map), s0 + (second ? 1 : 0), (P & sq_bit(from)) ? OAZ_PAWN : OAZ_KING);
     return n;
 }
 
@@ -91,7 +141,14 @@ struct Params {
     uint32_t cap;
 };
 
-__global__ __launch_bounds__(64) void k_pure_mcts(const oaz_state* roots, int G, Params p, const float* ln_tab,
+#ifndef OAZ_PM_SELB
+#define OAZ_PM_SELB 4
+#endif
+constexpr int kSelBatch = OAZ_PM_SELB;
+#ifndef OAZ_PM_WPE
+#define OAZ_PM_WPE 6
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OAZ_PM_WPE))) void k_pure_mcts(const oaz_state* roots, int G, Params p, const float* ln_tab,
                                                   oaz_pure_node* nodes, oaz_move* out_move, float* out_value,
                                                   uint64_t* stats /* [G][8] */) {
     __shared__ uint32_t att_s[2][16][25];
@@ -100,13 +157,19 @@ __global__ __launch_bounds__(64) void k_pure_mcts(const oaz_state* roots, int G,
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
     oaz_pure_node* T = nodes + (size_t)g * p.cap;
-    const oaz_state root = roots[g];
-    const int root_color = root.to_move & 1;
+    const int root_color = roots[g].to_move & 1;
     T[0] = oaz_pure_node{0u, 0.0f, 0.0f, 0u, 0xFFFFFFFFu, 0, 0, 0};
     uint32_t n_nodes = 1;
-    uint64_t st_exp = 0, st_plies = 0, st_pass = 0, st_capped = 0, st_over = 0;
+    // the search's counters in LDS (the thread's own slots), out of the registers the walk and rollout need
+    __shared__ uint64_t stl[5][64];
+    uint64_t& st_plies = stl[0][threadIdx.x];
+    uint64_t& st_pass = stl[1][threadIdx.x];
+    uint64_t& st_exp = stl[2][threadIdx.x];
+    uint64_t& st_capped = stl[3][threadIdx.x];
+    uint64_t& st_over = stl[4][threadIdx.x];
+    st_plies = st_pass = st_exp = st_capped = st_over = 0;
     for (int po = 0; po < p.playouts; ++po) {
-        oaz_state s = root;
+        oaz_state s = roots[g];  // (reloaded per playout: an L2 hit, six registers fewer)
         uint32_t idx = 0;
         // 1. selection (mcts_arena.rs:100-116)
         while ((T[idx].flags & kExpanded) && !(T[idx].flags & kTerminal) && T[idx].nch) {
@@ -114,17 +177,31 @@ __global__ __launch_bounds__(64) void k_pure_mcts(const oaz_state* roots, int G,
             const uint32_t first = T[idx].first, nch = T[idx].nch;
             uint32_t best = first;
             int32_t bk = INT32_MIN;
-            for (uint32_t c = first; c < first + nch; ++c) {
-                const float u = T[c].winrate + p.c * sqrtf(lnN / (float)T[c].visits);
-                const int32_t k = total_key(u);
-                if (k >= bk) {  // max_by: the last maximum wins
-                    bk = k;
-                    best = c;
-                }
+            // the children's (visits, winrate) kSelBatch at a time, all loads in flight before the fold (the
+            // fold itself stays sequential in child order)
+            for (uint32_t c0 = 0; c0 < nch; c0 += kSelBatch) {
+                uint32_t vis[kSelBatch];
+                float wr[kSelBatch];
+#pragma unroll
+                for (int j = 0; j < kSelBatch; ++j)
+                    if (c0 + j < nch) {
+                        vis[j] = T[first + c0 + j].visits;
+                        wr[j] = T[first + c0 + j].winrate;
+                    }
+#pragma unroll
+                for (int j = 0; j < kSelBatch; ++j)
+                    if (c0 + j < nch) {
+                        const float u = wr[j] + p.c * sqrtf(lnN / (float)vis[j]);
+                        const int32_t k = total_key(u);
+                        if (k >= bk) {  // max_by: the last maximum wins
+                            bk = k;
+                            best = first + c0 + j;
+                        }
+                    }
             }
             const uint32_t m = T[best].mv;
             const int color = s.to_move & 1;
-            const int res = make_move(s, mv_from(m), mv_to(m), mv_piece(m), mv_slot(m), color);
+            const int res = make_move_regs(s, mv_from(m), mv_to(m), mv_piece(m), mv_slot(m), color);
             s.to_move ^= 1;
             if (is_win(res)) T[best].flags |= kTerminal;
             idx = best;
@@ -163,20 +240,16 @@ __global__ __launch_bounds__(64) void k_pure_mcts(const oaz_state* roots, int G,
                     capped = true;
                     break;
                 }
-                const int n = movegen_kth(s, color, att_s[color], -1, nullptr);
+                uint32_t m = 0;
+                const int n = rollout_pick(s, color, att_s[color], rng, &m);
                 if (n == 0) {  // pass with a random own card (state.rs:139-142)
-                    const int slot = (color ? 2 : 0) + (int)rng.below(2);
-                    const uint8_t t = s.cards[slot];
-                    s.cards[slot] = s.cards[4];
-                    s.cards[4] = t;
+                    state_rotate(s, (color ? 2 : 0) + (int)rng.below(2));
                     color ^= 1;
                     ++st_pass;
                     ++plies;
                     continue;
                 }
-                uint32_t m = 0;
-                movegen_kth(s, color, att_s[color], (int)rng.below((uint32_t)n), &m);
-                mr = make_move(s, mv_from(m), mv_to(m), mv_piece(m), mv_slot(m), color);
+                mr = make_move_regs(s, mv_from(m), mv_to(m), mv_piece(m), mv_slot(m), color);
                 color ^= 1;
                 ++plies;
             }
